@@ -1,0 +1,107 @@
+/*
+ * tspgpu — MI355X (gfx950) exact TSP block search behind a C ABI.
+ *
+ * Drop-in for the reference's per-block solver
+ *     BlockSolution tsp(vector<City> cities)        (assignment2.h:56, tsp.cpp:405-509)
+ * and its helper computeDistanceMatrix               (assignment2.h:184-200).
+ * Results are bit-identical to the reference: the same FP64 optimal cost and
+ * the same tour (the reference's first-strict-minimum tie rule, tsp.cpp:457-470,
+ * 484-498).  Plain C types only; no HIP or torch types cross this boundary
+ * (HIP streams are passed as void*).  See INTEGRATION.md for the C++/ctypes
+ * bindings a maintainer of the reference would add.
+ *
+ * Return codes: 0 on success, otherwise a negative errno value
+ *   -EINVAL  bad argument (n outside [2, TSPGPU_MAX_CITIES] (strict: 16), nblocks < 0,
+ *            NULL pointer, non-finite or negative distance)
+ *   -ERANGE  n * max(d) >= INT_MAX: the reference's INT_MAX sentinel
+ *            (tsp.cpp:411,453) would leave its tour undefined
+ *   -ENODEV  no HIP device / device ordinal out of range
+ *   -ENOMEM  device allocation failed
+ *   -EIO     a HIP runtime call or kernel launch failed
+ */
+#ifndef TSPGPU_H
+#define TSPGPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TSPGPU_VERSION 100          /* 1.0.0 */
+#define TSPGPU_MAX_CITIES 20        /* extension limit (N = n-1 <= 19) */
+#define TSPGPU_REFERENCE_MAX_CITIES 16 /* tsp.cpp:289 rejects more */
+
+/* Memory layout identical to the reference's City (assignment2.h:13-18):
+ * int id at offset 0, double x at 8, double y at 16; 24 bytes. */
+typedef struct
+{
+    int32_t id;
+    double x;
+    double y;
+} tspgpu_city;
+
+typedef struct
+{
+    int device;      /* HIP device ordinal; -1 = the calling thread's current device */
+    int strict;      /* 1: accept n <= 16 only (the reference's cap, tsp.cpp:289) */
+    int slots;       /* resident DP workspaces (persistent grid size); 0 = auto */
+    int reserved[5]; /* must be zero */
+} tspgpu_opts;
+
+typedef struct tspgpu_ctx tspgpu_ctx;
+
+int tspgpu_version(void);
+const char *tspgpu_strerror(int code);
+
+/* Length of the tour written per block: n+1 (0, t1..tN, 0), except the
+ * reference's n==2 quirk [1,0] (tsp.cpp:483-502 with one inner city). */
+int tspgpu_tour_length(int n);
+
+/* computeDistanceMatrix (assignment2.h:184-200) on the host with glibc pow/sqrt,
+ * bit-exact with the reference.  dist: nblocks*n*n row-major. */
+int tspgpu_distance_matrix(const tspgpu_city *cities, int n, int nblocks, double *dist);
+
+/* Host-side validation applied by the host-pointer entry points. */
+int tspgpu_validate(const double *dist, int n, int nblocks, int strict);
+
+int tspgpu_ctx_create(const tspgpu_opts *opts, tspgpu_ctx **out);
+int tspgpu_ctx_destroy(tspgpu_ctx *ctx);
+
+/* Batched replacement for tsp() on host buffers; synchronous.
+ *   dist     nblocks*n*n doubles (host), from tspgpu_distance_matrix
+ *   cost_out nblocks doubles: the block's tour cost (BlockSolution.cost)
+ *   tour_out nblocks*(n+1) int32: local city indices of BlockSolution.path
+ *            (tspgpu_tour_length(n) valid entries; the rest is -1) */
+int tspgpu_solve_blocks(tspgpu_ctx *ctx, const double *dist, int n, int nblocks, double *cost_out,
+                        int32_t *tour_out);
+
+/* Same, from cities (distance matrix computed on the host, then solved). */
+int tspgpu_solve_cities(tspgpu_ctx *ctx, const tspgpu_city *cities, int n, int nblocks, double *cost_out,
+                        int32_t *tour_out);
+
+/* Device-pointer form, asynchronous on `hip_stream` (hipStream_t, NULL = default).
+ * The caller guarantees the data satisfy tspgpu_validate (not re-checked).
+ * d_dist/d_cost/d_tour are device pointers on the context's device. */
+int tspgpu_solve_blocks_device(tspgpu_ctx *ctx, const double *d_dist, int n, int nblocks, double *d_cost,
+                               int32_t *d_tour, void *hip_stream);
+
+/* Context-free convenience form (uses a per-thread default context on the
+ * current device, created on first use). */
+int tspgpu_solve(const double *dist, int n, int nblocks, double *cost_out, int32_t *tour_out,
+                 const tspgpu_opts *opts);
+
+/* Device-side information for measurement: number of persistent workgroups
+ * the last launch used and the DP relaxations per block for n cities,
+ * N(N-1)2^(N-2) with N = n-1 (tsp.cpp:442-471). */
+int tspgpu_last_grid(const tspgpu_ctx *ctx);
+double tspgpu_relaxations_per_block(int n);
+/* Algorithmic table bytes per block: every DP entry written once and read
+ * once, 2 * 8 * N * 2^(N-1). */
+double tspgpu_table_bytes_per_block(int n);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

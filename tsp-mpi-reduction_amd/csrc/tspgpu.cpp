@@ -1,0 +1,369 @@
+// C-ABI of libtspgpu (include/tspgpu.h): context, validation, host<->device
+// staging, launch of the K1 Held-Karp kernels (heldkarp.hip).
+//
+// Replaces the reference's `BlockSolution tsp(vector<City>)` (tsp.cpp:405-509)
+// for a whole batch of blocks in one call.  The distance matrix stays on the
+// host (computeDistanceMatrix, assignment2.h:184-200) because glibc pow(x,2)
+// differs from x*x in ~0.08% of inputs; the device never recomputes it.
+#include "tspgpu.h"
+
+#include <hip/hip_runtime.h>
+
+#include <cerrno>
+#include <climits>
+#include <cmath>
+#include <cstdlib>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <vector>
+
+#include "heldkarp.h"
+
+namespace tspgpu {
+
+static int binom_host(int a, int b)
+{
+    if (b < 0 || b > a) return 0;
+    long long r = 1;
+    for (int i = 1; i <= b; ++i) r = r * (a - b + i) / i;
+    return (int)r;
+}
+
+size_t table_doubles(int N) { return (size_t)N << (N - 1); }
+
+void host_layer_info(int N, LayerInfo *info)
+{
+    std::memset(info, 0, sizeof(*info));
+    for (int a = 0; a < kBinomRows; ++a)
+        for (int b = 0; b < kBinomCols; ++b) info->binom[a * kBinomCols + b] = binom_host(a, b);
+    int off = 0, moff = 0;
+    for (int t = 0; t <= N + 1 && t < 24; ++t) {
+        info->count[t] = binom_host(N, t);
+        info->moff[t] = moff;
+        moff += info->count[t];
+        if (t >= 1) {
+            info->off[t] = off;
+            off += info->count[t] * t;
+        }
+    }
+}
+
+}  // namespace tspgpu
+
+using namespace tspgpu;
+
+struct tspgpu_ctx {
+    int device = 0;
+    int strict = 0;
+    int slots_opt = 0;
+    int cu_count = 256;
+    hipStream_t stream = nullptr;
+    uint32_t *d_masks[kMaxN + 1] = {};
+    LayerInfo *d_info[kMaxN + 1] = {};
+    double *d_slots = nullptr;
+    size_t slots_bytes = 0;
+    double *d_dist = nullptr;
+    size_t dist_bytes = 0;
+    double *d_cost = nullptr;
+    size_t cost_bytes = 0;
+    int32_t *d_tour = nullptr;
+    size_t tour_bytes = 0;
+    int last_grid = 0;
+    std::mutex mu;
+};
+
+namespace {
+
+int hip_err(hipError_t e)
+{
+    if (e == hipSuccess) return 0;
+    if (e == hipErrorOutOfMemory) return -ENOMEM;
+    if (e == hipErrorNoDevice || e == hipErrorInvalidDevice) return -ENODEV;
+    return -EIO;
+}
+
+template <typename T>
+int ensure(T **p, size_t *have, size_t need)
+{
+    if (*have >= need && *p) return 0;
+    if (*p) (void)hipFree(*p);
+    *p = nullptr;
+    *have = 0;
+    size_t alloc = need < 256 ? 256 : need;
+    hipError_t e = hipMalloc((void **)p, alloc);
+    if (e != hipSuccess) {
+        *p = nullptr;
+        return hip_err(e);
+    }
+    *have = alloc;
+    return 0;
+}
+
+int ensure_tables(tspgpu_ctx *c, int N)
+{
+    if (c->d_info[N]) return 0;
+    LayerInfo info;
+    host_layer_info(N, &info);
+    std::vector<uint32_t> masks;
+    masks.reserve((size_t)1 << N);
+    for (int t = 0; t <= N; ++t)
+        for (uint32_t m = 0; m < (1u << N); ++m)
+            if (__builtin_popcount(m) == t) masks.push_back(m);
+    hipError_t e = hipMalloc((void **)&c->d_info[N], sizeof(LayerInfo));
+    if (e == hipSuccess) e = hipMalloc((void **)&c->d_masks[N], masks.size() * sizeof(uint32_t));
+    if (e == hipSuccess) e = hipMemcpy(c->d_info[N], &info, sizeof(info), hipMemcpyHostToDevice);
+    if (e == hipSuccess)
+        e = hipMemcpy(c->d_masks[N], masks.data(), masks.size() * sizeof(uint32_t), hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+        if (c->d_info[N]) (void)hipFree(c->d_info[N]);
+        if (c->d_masks[N]) (void)hipFree(c->d_masks[N]);
+        c->d_info[N] = nullptr;
+        c->d_masks[N] = nullptr;
+        return hip_err(e);
+    }
+    return 0;
+}
+
+int check_n(int n, int strict)
+{
+    if (n < 2) return -EINVAL;
+    if (n > (strict ? TSPGPU_REFERENCE_MAX_CITIES : TSPGPU_MAX_CITIES)) return -EINVAL;
+    return 0;
+}
+
+int solve_device_locked(tspgpu_ctx *c, const double *d_dist, int n, int nblocks, double *d_cost,
+                        int32_t *d_tour, hipStream_t stream)
+{
+    int rc = check_n(n, c->strict);
+    if (rc) return rc;
+    if (nblocks < 0 || (nblocks > 0 && (!d_dist || !d_cost || !d_tour))) return -EINVAL;
+    if (nblocks == 0) return 0;
+    if (hipSetDevice(c->device) != hipSuccess) return -ENODEV;
+    const int N = n - 1;
+    LaunchArgs a{};
+    a.dist = d_dist;
+    a.n = n;
+    a.nblocks = nblocks;
+    a.cost = d_cost;
+    a.tour = d_tour;
+    a.stream = stream;
+    int grid = nblocks;
+    if (N >= 2) {
+        rc = ensure_tables(c, N);
+        if (rc) return rc;
+        a.masks = c->d_masks[N];
+        a.info = c->d_info[N];
+        a.use_lds = N <= kLdsTableMaxN;
+        if (a.use_lds) {
+            int cap = c->cu_count * 16;
+            grid = nblocks < cap ? nblocks : cap;
+        } else {
+            int slots = c->slots_opt > 0 ? c->slots_opt : c->cu_count * 2;
+            // keep the workspace under ~8 GiB for the largest extension sizes
+            const size_t per = table_doubles(N) * sizeof(double);
+            const size_t budget = (size_t)8 << 30;
+            if ((size_t)slots * per > budget) slots = (int)(budget / per);
+            if (slots < 1) slots = 1;
+            grid = nblocks < slots ? nblocks : slots;
+            a.slot_doubles = table_doubles(N);
+            rc = ensure(&c->d_slots, &c->slots_bytes, (size_t)grid * per);
+            if (rc) return rc;
+            a.slots = c->d_slots;
+        }
+    }
+    c->last_grid = grid;
+    return hip_err(launch_heldkarp(a, grid));
+}
+
+thread_local std::unique_ptr<tspgpu_ctx, int (*)(tspgpu_ctx *)> t_default(nullptr, tspgpu_ctx_destroy);
+
+}  // namespace
+
+extern "C" {
+
+int tspgpu_version(void) { return TSPGPU_VERSION; }
+
+const char *tspgpu_strerror(int code)
+{
+    switch (code) {
+    case 0: return "success";
+    case -EINVAL: return "invalid argument";
+    case -ERANGE: return "tour costs reach INT_MAX (reference behaviour undefined)";
+    case -ENODEV: return "no usable HIP device";
+    case -ENOMEM: return "device allocation failed";
+    case -EIO: return "HIP runtime or kernel launch failure";
+    default: return "unknown error";
+    }
+}
+
+int tspgpu_tour_length(int n) { return n == 2 ? 2 : n + 1; }
+
+double tspgpu_relaxations_per_block(int n)
+{
+    const double N = n - 1;
+    return N * (N - 1) * std::ldexp(1.0, n - 3);
+}
+
+double tspgpu_table_bytes_per_block(int n)
+{
+    const int N = n - 1;
+    return 2.0 * 8.0 * N * std::ldexp(1.0, N - 1);
+}
+
+int tspgpu_distance_matrix(const tspgpu_city *cities, int n, int nblocks, double *dist)
+{
+    // assignment2.h:196: sqrt(pow(dx, 2) + pow(dy, 2)), glibc pow really called
+    // (a volatile pointer keeps the compiler from folding pow(x,2) to x*x).
+    static double (*volatile pow_fn)(double, double) = ::pow;
+    static double (*volatile sqrt_fn)(double) = ::sqrt;
+    if (n < 1 || nblocks < 0 || (nblocks > 0 && (!cities || !dist))) return -EINVAL;
+    for (int b = 0; b < nblocks; ++b) {
+        const tspgpu_city *c = cities + (size_t)b * n;
+        double *d = dist + (size_t)b * n * n;
+        for (int i = 0; i < n; ++i)
+            for (int j = 0; j < n; ++j) {
+                const double dx = pow_fn(c[i].x - c[j].x, 2);
+                const double dy = pow_fn(c[i].y - c[j].y, 2);
+                d[i * n + j] = sqrt_fn(dx + dy);
+            }
+    }
+    return 0;
+}
+
+int tspgpu_validate(const double *dist, int n, int nblocks, int strict)
+{
+    int rc = check_n(n, strict);
+    if (rc) return rc;
+    if (nblocks < 0 || (nblocks > 0 && !dist)) return -EINVAL;
+    for (int b = 0; b < nblocks; ++b) {
+        const double *d = dist + (size_t)b * n * n;
+        double mx = 0.0;
+        for (int i = 0; i < n * n; ++i) {
+            const double v = d[i];
+            if (!(v >= 0.0) || !std::isfinite(v)) return -EINVAL;
+            if (v > mx) mx = v;
+        }
+        // Every partial tour has at most n edges: below INT_MAX the reference's
+        // sentinel (tsp.cpp:411,453) never wins a comparison.
+        if ((double)n * mx >= (double)INT_MAX) return -ERANGE;
+    }
+    return 0;
+}
+
+int tspgpu_ctx_create(const tspgpu_opts *opts, tspgpu_ctx **out)
+{
+    if (!out) return -EINVAL;
+    *out = nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return -ENODEV;
+    auto *c = new (std::nothrow) tspgpu_ctx();
+    if (!c) return -ENOMEM;
+    int dev = opts ? opts->device : -1;
+    if (dev < 0) {
+        if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+    }
+    if (dev >= ndev) {
+        delete c;
+        return -ENODEV;
+    }
+    c->device = dev;
+    c->strict = opts ? opts->strict : 0;
+    c->slots_opt = opts ? opts->slots : 0;
+    if (hipSetDevice(dev) != hipSuccess) {
+        delete c;
+        return -ENODEV;
+    }
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, dev) == hipSuccess && prop.multiProcessorCount > 0)
+        c->cu_count = prop.multiProcessorCount;
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        return -EIO;
+    }
+    *out = c;
+    return 0;
+}
+
+int tspgpu_ctx_destroy(tspgpu_ctx *c)
+{
+    if (!c) return 0;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    for (int i = 0; i <= kMaxN; ++i) {
+        if (c->d_masks[i]) (void)hipFree(c->d_masks[i]);
+        if (c->d_info[i]) (void)hipFree(c->d_info[i]);
+    }
+    if (c->d_slots) (void)hipFree(c->d_slots);
+    if (c->d_dist) (void)hipFree(c->d_dist);
+    if (c->d_cost) (void)hipFree(c->d_cost);
+    if (c->d_tour) (void)hipFree(c->d_tour);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+    return 0;
+}
+
+int tspgpu_solve_blocks_device(tspgpu_ctx *c, const double *d_dist, int n, int nblocks, double *d_cost,
+                               int32_t *d_tour, void *hip_stream)
+{
+    if (!c) return -EINVAL;
+    std::lock_guard<std::mutex> g(c->mu);
+    return solve_device_locked(c, d_dist, n, nblocks, d_cost, d_tour, (hipStream_t)hip_stream);
+}
+
+int tspgpu_solve_blocks(tspgpu_ctx *c, const double *dist, int n, int nblocks, double *cost_out,
+                        int32_t *tour_out)
+{
+    if (!c) return -EINVAL;
+    int rc = tspgpu_validate(dist, n, nblocks, c->strict);
+    if (rc) return rc;
+    if (nblocks > 0 && (!cost_out || !tour_out)) return -EINVAL;
+    if (nblocks == 0) return 0;
+    std::lock_guard<std::mutex> g(c->mu);
+    if (hipSetDevice(c->device) != hipSuccess) return -ENODEV;
+    const size_t db = (size_t)nblocks * n * n * sizeof(double);
+    const size_t cb = (size_t)nblocks * sizeof(double);
+    const size_t tb = (size_t)nblocks * (n + 1) * sizeof(int32_t);
+    if ((rc = ensure(&c->d_dist, &c->dist_bytes, db))) return rc;
+    if ((rc = ensure(&c->d_cost, &c->cost_bytes, cb))) return rc;
+    if ((rc = ensure(&c->d_tour, &c->tour_bytes, tb))) return rc;
+    hipError_t e = hipMemcpyAsync(c->d_dist, dist, db, hipMemcpyHostToDevice, c->stream);
+    if (e == hipSuccess) e = hipMemsetAsync(c->d_tour, 0xff, tb, c->stream);
+    if (e != hipSuccess) return hip_err(e);
+    rc = solve_device_locked(c, c->d_dist, n, nblocks, c->d_cost, c->d_tour, c->stream);
+    if (rc) return rc;
+    e = hipMemcpyAsync(cost_out, c->d_cost, cb, hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(tour_out, c->d_tour, tb, hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    if (e != hipSuccess) return hip_err(e);
+    for (int b = 0; b < nblocks; ++b)
+        if (cost_out[b] < 0.0) return -EIO;  // backtracking found no predecessor
+    return 0;
+}
+
+int tspgpu_solve_cities(tspgpu_ctx *c, const tspgpu_city *cities, int n, int nblocks, double *cost_out,
+                        int32_t *tour_out)
+{
+    if (n < 2 || nblocks < 0) return -EINVAL;
+    std::vector<double> dist((size_t)nblocks * n * n);
+    int rc = tspgpu_distance_matrix(cities, n, nblocks, dist.data());
+    if (rc) return rc;
+    return tspgpu_solve_blocks(c, dist.data(), n, nblocks, cost_out, tour_out);
+}
+
+int tspgpu_solve(const double *dist, int n, int nblocks, double *cost_out, int32_t *tour_out,
+                 const tspgpu_opts *opts)
+{
+    if (!t_default) {
+        tspgpu_ctx *c = nullptr;
+        int rc = tspgpu_ctx_create(opts, &c);
+        if (rc) return rc;
+        t_default.reset(c);
+    }
+    t_default->strict = opts ? opts->strict : 0;
+    return tspgpu_solve_blocks(t_default.get(), dist, n, nblocks, cost_out, tour_out);
+}
+
+int tspgpu_last_grid(const tspgpu_ctx *c) { return c ? c->last_grid : 0; }
+
+}  // extern "C"
