@@ -1,0 +1,290 @@
+#!/usr/bin/env python3
+"""Benchmark of the hot path: exact 16-city block search on MI355X.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--n 16] [--blocks-per-gpu B]
+
+One STEP = one launch of the K1 Held-Karp kernel over this rank's shard of B
+blocks (inputs already resident in HBM).  Ranks (torchrun, one per GPU) each
+own a contiguous shard of the instance `./tsp n B*N 1000 1000` (the
+reference's own generator, srand(0)); there is no data-path collective, so
+scaling is weak.  A gloo process group provides the barriers and the
+max-over-ranks of the timed region (measurement only).
+
+`value` = DP relaxations (the search nodes of Held-Karp: one (S,k,m) extension
+G[S\\k][m] + d[m][k] with its min, tsp.cpp:457-470; N(N-1)2^(N-2) per block) of
+all ranks / max wall time.  Rank 0 prints ONE JSON line.
+
+The GPU is driven only through libtspgpu's C ABI (device buffers, stream and
+HIP-event timer included), so the HIP events sit on the stream the kernel runs
+on.  torch is used only for torch.distributed (gloo) when WORLD_SIZE > 1.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import shutil
+import statistics
+import subprocess
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, "tsp-mpi-reduction_amd")
+sys.path.insert(0, PKG)
+import tspgpu  # noqa: E402
+
+METRIC = "search nodes/sec (whole node) + time-to-optimal tour, 16-city, 1/2/4/8 GPU"
+HBM_PEAK = 8.0e12  # B/s, MI355X_MICROARCH.md chip table (spec)
+DOMINANT_KERNEL = "heldkarp_kernel"
+
+
+def host_lib():
+    import ctypes
+
+    L = ctypes.CDLL(tspgpu.HOST_LIB_PATH)
+    L.tsphost_generate.argtypes = [ctypes.c_int] * 4 + [ctypes.POINTER(tspgpu.City)]
+    return L
+
+
+class Shard:
+    """Cities of `./tsp n blocks_total grid grid` (tsp.cpp:373-403), blocks [lo, hi),
+    kept as the C array the ABI takes."""
+
+    def __init__(self, n, blocks_total, lo, hi, grid=1000):
+        L = host_lib()
+        full = (tspgpu.City * (n * blocks_total))()
+        L.tsphost_generate(n, blocks_total, grid, grid, full)
+        self.n, self.B = n, hi - lo
+        self.arr = (tspgpu.City * (n * self.B)).from_buffer_copy(
+            memoryview(full).cast("B")[lo * n * 24:hi * n * 24])
+
+    def block(self, b):
+        return [(self.arr[b * self.n + j].id, self.arr[b * self.n + j].x, self.arr[b * self.n + j].y)
+                for j in range(self.n)]
+
+    def distances(self):
+        """Host libm distance matrices, bit-exact with computeDistanceMatrix."""
+        return tspgpu.distance_matrix_array(self.arr, self.n, self.B)
+
+
+def cpu_baseline(n, seconds_budget=20.0):
+    """The reference's own tsp() (oracle/_ref, built from /root/reference at -O0)
+    timed on this host: P parallel processes, one block each, like
+    `mpirun -np P ./tsp n P ...` minus MPI startup.  Falls back to the C
+    oracle port when the reference binary is absent."""
+    ref = os.path.join(ROOT, "oracle", "_ref", "ref_harness")
+    cores = max(1, min(8, len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()))
+    relax = tspgpu.relaxations_per_block(n)
+    if os.path.exists(ref):
+        try:
+            t0 = time.perf_counter()
+            procs = [subprocess.Popen([ref, "timeone", str(n), str(cores), "1000", "1000", str(i)],
+                                      stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, text=True)
+                     for i in range(cores)]
+            outs = [p.communicate(timeout=seconds_budget * 6)[0] for p in procs]
+            wall = time.perf_counter() - t0
+            per = [float(ln.split()[2]) for o in outs for ln in o.splitlines() if ln.startswith("T ")]
+            if len(per) == cores and all(p.returncode == 0 for p in procs):
+                return {"value": cores * relax / wall, "unit": "search nodes/s", "cores": cores, "kind": "reference",
+                        "sample": f"{cores} blocks x {n} cities of `./tsp {n} {cores} 1000 1000`, reference tsp() "
+                                  f"(-O0, std::map Held-Karp) one block per process on {cores} cores; "
+                                  f"{wall:.1f} s wall, median block {statistics.median(per):.2f} s",
+                        "blocks_per_s": cores / wall}
+        except Exception as e:  # reference binary unusable here: fall back to the port
+            sys.stderr.write(f"cpu_baseline: reference run failed ({e}); using the oracle port\n")
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_py as O
+
+    shard = Shard(n, 64, 0, 64)
+    d = shard.distances()
+    t0 = time.perf_counter()
+    k = 0
+    while k < shard.B and time.perf_counter() - t0 < seconds_budget:
+        O.solve_block(d[k])
+        k += 1
+    wall = time.perf_counter() - t0
+    return {"value": k * relax / wall, "unit": "search nodes/s", "cores": 1, "kind": "port",
+            "sample": f"{k} blocks x {n} cities, oracle array Held-Karp (-O2), 1 core, {wall:.1f} s",
+            "blocks_per_s": k / wall}
+
+
+def pmc_traffic(n, blocks, timeout=90):
+    """HBM bytes per launch of the dominant kernel from rocprofv3 PMC counters,
+    one counter group per pass (MI355X_MICROARCH.md §HBM / rocprofv3 PMC slots):
+    FETCH_SIZE and WRITE_SIZE (KiB) in separate passes; FETCH_SIZE is doubled
+    because gfx950 tallies 128-B requests at 64 B."""
+    rocprof = shutil.which("rocprofv3")
+    if not rocprof:
+        return None, "rocprofv3 not found"
+    out = {}
+    for counter in ("FETCH_SIZE", "WRITE_SIZE"):
+        d = os.path.join(ROOT, "gpurun_out", f"pmc_{counter}")
+        shutil.rmtree(d, ignore_errors=True)
+        cmd = ["timeout", "-s", "KILL", str(timeout), rocprof, "--pmc", counter, "--output-format", "csv",
+               "-d", d, "-o", "pmc", "--", sys.executable, os.path.abspath(__file__), "--pmc-child",
+               "--n", str(n), "--blocks-per-gpu", str(blocks)]
+        p = subprocess.run(cmd, capture_output=True, text=True, cwd="/tmp")
+        vals = []
+        for root, _, files in os.walk(d):
+            for f in files:
+                if f.endswith("counter_collection.csv"):
+                    import csv
+
+                    with open(os.path.join(root, f)) as fh:
+                        for row in csv.DictReader(fh):
+                            if DOMINANT_KERNEL in row.get("Kernel_Name", "") and row.get("Counter_Name") == counter:
+                                vals.append(float(row["Counter_Value"]))
+        if p.returncode != 0 or not vals:
+            return None, f"{counter}: rc={p.returncode} {p.stderr[-300:]}"
+        out[counter] = statistics.median(vals) * 1024.0  # KiB -> B per launch
+    fetch = out["FETCH_SIZE"] * 2.0
+    return fetch + out["WRITE_SIZE"], {"fetch_size_bytes_raw": out["FETCH_SIZE"], "write_size_bytes": out["WRITE_SIZE"],
+                                       "fetch_corrected_x2": fetch}
+
+
+def pmc_child(args):
+    ctx = tspgpu.Context(device=0)
+    shard = Shard(args.n, args.blocks_per_gpu, 0, args.blocks_per_gpu)
+    d = shard.distances()
+    B, n = shard.B, args.n
+    dd, dc, dt = ctx.upload(d), ctx.alloc(B * 8), ctx.alloc(B * (n + 1) * 4)
+    for _ in range(3):
+        ctx.solve_device(dd, n, B, dc, dt, ctx.stream)
+    ctx.synchronize()
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--n", type=int, default=16, help="cities per block (config 3: 16)")
+    ap.add_argument("--blocks-per-gpu", type=int, default=16384)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-pmc", action="store_true")
+    ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
+    args = ap.parse_args()
+    if args.pmc_child:
+        return pmc_child(args)
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.init_process_group("gloo")
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    def allmax(x):
+        if dist is None:
+            return x
+        import torch
+
+        t = torch.tensor([x], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    n, Bp = args.n, args.blocks_per_gpu
+    ctx = tspgpu.Context(device=local_rank, strict=False)
+    cu, devname = ctx.device_info()
+    shard = Shard(n, Bp * world, rank * Bp, (rank + 1) * Bp)
+    d = shard.distances()
+    dd, dc, dt = ctx.upload(d), ctx.alloc(Bp * 8), ctx.alloc(Bp * (n + 1) * 4)
+    stream = ctx.stream
+
+    for _ in range(args.warmup):
+        ctx.solve_device(dd, n, Bp, dc, dt, stream)
+    ctx.synchronize()
+    barrier()
+    ctx.synchronize()
+    t0 = time.perf_counter()
+    ctx.timer_start()
+    for _ in range(args.steps):
+        ctx.solve_device(dd, n, Bp, dc, dt, stream)
+    kernel_ms = ctx.timer_stop() / args.steps  # HIP events on the kernel's stream
+    ctx.synchronize()
+    barrier()
+    wall = time.perf_counter() - t0
+    wall_max = allmax(wall)
+
+    # correctness of what was timed: every tour's left fold equals its cost
+    cost = ctx.download(dc, (Bp,), np.float64)
+    tour = ctx.download(dt, (Bp, n + 1), np.int32)
+    for b in range(0, Bp, max(1, Bp // 64)):
+        acc = 0.0
+        for i in range(n):
+            acc = acc + d[b, tour[b, i], tour[b, i + 1]]
+        assert acc == cost[b], "timed result failed the left-fold check"
+
+    relax = tspgpu.relaxations_per_block(n)
+    total_blocks = Bp * world * args.steps
+    value = total_blocks * relax / wall_max
+
+    # time-to-optimal: one block, host libm distances + copy + kernel + copy back
+    tto = []
+    one = [shard.block(0)]
+    for _ in range(10):
+        t = time.perf_counter()
+        ctx.solve_cities(one)
+        tto.append((time.perf_counter() - t) * 1e3)
+    d1, c1, t1 = ctx.upload(d[:1]), ctx.alloc(8), ctx.alloc((n + 1) * 4)
+    ctx.timer_start()
+    for _ in range(10):
+        ctx.solve_device(d1, n, 1, c1, t1, stream)
+    one_kernel_ms = ctx.timer_stop() / 10
+
+    if rank != 0:
+        return
+    alg_bytes = tspgpu.table_bytes_per_block(n) * Bp
+    achieved = alg_bytes / (kernel_ms * 1e-3)
+    traffic, traffic_note = (None, "skipped")
+    if world == 1 and not args.no_pmc:
+        traffic, traffic_note = pmc_traffic(n, min(Bp, 4096))
+        if traffic is not None:
+            traffic = traffic * (Bp / min(Bp, 4096))  # per launch of this run's size (same per-block bytes)
+    cpu = None
+    if world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(n)
+    line = {
+        "metric": METRIC,
+        "value": value,
+        "unit": "search nodes/s (Held-Karp DP relaxations)",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": wall_max / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic: the reference's own generator (srand(0), ./tsp n B 1000 1000), no dataset",
+        "config": {"workload": f"{n}-city blocks, exact Held-Karp per block (config 3 cities/block; "
+                               f"./tsp {n} {Bp * world} 1000 1000 instance)",
+                   "n": n, "blocks_per_gpu": Bp, "global_blocks": Bp * world,
+                   "parallelism": f"blocks sharded over {world} rank(s), no data-path collective"},
+        "blocks_per_s": total_blocks / wall_max,
+        "time_to_optimal_ms": {"one_block_end_to_end_median": statistics.median(tto),
+                               "one_block_kernel": one_kernel_ms},
+        "kernel_ms_per_launch": kernel_ms,
+        "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK, "traffic": traffic,
+                     "note": f"{DOMINANT_KERNEL}<15,false>: algorithmic bytes = 2*8*N*2^(N-1) per block "
+                             f"(each DP entry written once, read once) x {Bp} blocks per launch / HIP-event "
+                             f"launch time; traffic = PMC HBM bytes per launch ({traffic_note})"},
+        "cpu_baseline": cpu,
+        "device": devname,
+        "cus": cu,
+    }
+    print(json.dumps(line), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -92,6 +92,22 @@ int tspgpu_solve_blocks_device(tspgpu_ctx *ctx, const double *d_dist, int n, int
 int tspgpu_solve(const double *dist, int n, int nblocks, double *cost_out, int32_t *tour_out,
                  const tspgpu_opts *opts);
 
+/* Device memory, stream and timing helpers for callers that have no HIP
+ * runtime of their own (ctypes / cgo / JNI users, bench.py): everything on the
+ * context's device; copies are synchronous; the timer is a pair of HIP events
+ * recorded on the context's stream (the stream the kernels run on when
+ * hip_stream == tspgpu_stream(ctx)). */
+int tspgpu_device_alloc(tspgpu_ctx *ctx, size_t bytes, void **ptr);
+int tspgpu_device_free(tspgpu_ctx *ctx, void *ptr);
+int tspgpu_memcpy_htod(tspgpu_ctx *ctx, void *dst, const void *src, size_t bytes);
+int tspgpu_memcpy_dtoh(tspgpu_ctx *ctx, void *dst, const void *src, size_t bytes);
+void *tspgpu_stream(tspgpu_ctx *ctx);
+int tspgpu_synchronize(tspgpu_ctx *ctx);
+int tspgpu_timer_start(tspgpu_ctx *ctx);
+int tspgpu_timer_stop(tspgpu_ctx *ctx, float *elapsed_ms);
+/* CU count and device name of the context's device. */
+int tspgpu_device_info(const tspgpu_ctx *ctx, int *cu_count, char *name, int namecap);
+
 /* Device-side information for measurement: number of persistent workgroups
  * the last launch used and the DP relaxations per block for n cities,
  * N(N-1)2^(N-2) with N = n-1 (tsp.cpp:442-471). */

@@ -14,6 +14,7 @@
 //   dist  n B X Y      computeDistanceMatrix (assignment2.h:184-200)
 //   fold  n B X Y      sequential mergeBlocks fold (tsp.cpp:202-269, 348-352)
 //   time  n B X Y      wall time of tsp() per block (CPU baseline)
+//   timeone n B X Y i  wall time of tsp() on block i only
 // Output lines start with a tag so the generator's own printf
 // ("%i blocks in X %i in Y", tsp.cpp:377) can be skipped by the reader.
 #include <map>
@@ -77,8 +78,14 @@ int main(int argc, char **argv)
 {
     if (argc < 3)
     {
-        fprintf(stderr, "usage: ref_harness gen|solve|dist|fold|time n B X Y | solvefile FILE\n");
+        fprintf(stderr, "usage: ref_harness gen|solve|dist|fold|time n B X Y | timeone n B X Y i | solvefile FILE\n");
         return 1;
+    }
+    int only = -1;
+    if (string(argv[1]) == "timeone" && argc == 7)
+    {
+        only = atoi(argv[6]);
+        argc = 6;
     }
     procNum = 0;
     string cmd = argv[1];
@@ -126,10 +133,12 @@ int main(int argc, char **argv)
             print_solution("F", (int)b, acc);
         }
     }
-    else if (cmd == "time")
+    else if (cmd == "time" || cmd == "timeone")
     {
         for (size_t b = 0; b < blocks.size(); b++)
         {
+            if (only >= 0 && (int)b != only)
+                continue;
             auto t0 = std::chrono::steady_clock::now();
             BlockSolution s = tsp(blocks[b]);
             auto t1 = std::chrono::steady_clock::now();

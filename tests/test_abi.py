@@ -1,0 +1,82 @@
+"""C-ABI checks that need no GPU: the libraries load, every function that
+include/tspgpu.h declares is exported, and the pure host entry points
+(distance matrix, validation) behave.  No kernel is launched here."""
+import ctypes
+import errno
+import os
+import re
+
+import numpy as np
+import pytest
+
+import oracle_py as O
+import tspgpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "tspgpu.h")
+
+
+def declared(header):
+    src = open(header).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(tspgpu_[a-z_0-9]+)\s*\(", src)))
+
+
+def test_every_declared_symbol_is_exported():
+    L = ctypes.CDLL(tspgpu.LIB_PATH)
+    names = declared(HEADER)
+    assert len(names) >= 20
+    missing = [nm for nm in names if not hasattr(L, nm)]
+    assert not missing
+    assert set(names) == set(tspgpu.EXPORTED_SYMBOLS)
+
+
+def test_host_library_exports():
+    L = ctypes.CDLL(tspgpu.HOST_LIB_PATH)
+    names = declared(os.path.join(tspgpu.PKG_DIR, "include", "tsp_host.h"))
+    names = [n for n in re.findall(r"\b(tsphost_[a-z_]+)\s*\(", open(os.path.join(tspgpu.PKG_DIR, "include", "tsp_host.h")).read())]
+    assert names and all(hasattr(L, n) for n in names)
+
+
+def test_version_and_tour_length():
+    assert tspgpu.lib().tspgpu_version() == 100
+    assert tspgpu.tour_length(2) == 2 and tspgpu.tour_length(16) == 17
+    assert tspgpu.relaxations_per_block(16) == 1720320
+    assert tspgpu.relaxations_per_block(14) == 319488 and tspgpu.relaxations_per_block(12) == 56320
+    assert tspgpu.table_bytes_per_block(16) == 2 * 8 * 15 * 2 ** 14
+
+
+def test_distance_matrix_matches_reference_bits():
+    for case in O.load_golden("seed0_dist.json"):
+        blocks = O.generate(case["n"], case["B"], case["X"], case["Y"])
+        d = tspgpu.distance_matrix(blocks)
+        ref = np.array([[[O.hexf(v) for v in row] for row in blk] for blk in case["dist_hex"]])
+        assert np.array_equal(d, ref)
+
+
+def test_validation_host_side():
+    ok = np.zeros((2, 5, 5))
+    assert tspgpu.validate(ok) == 0
+    bad = ok.copy()
+    bad[1, 2, 3] = np.nan
+    assert tspgpu.validate(bad) == -errno.EINVAL
+    bad = ok.copy()
+    bad[0, 1, 1] = -1.0
+    assert tspgpu.validate(bad) == -errno.EINVAL
+    big = np.full((1, 5, 5), 2147483647.0 / 5)
+    assert tspgpu.validate(big) == -errno.ERANGE
+    assert tspgpu.validate(np.zeros((1, 1, 1))) == -errno.EINVAL
+    assert tspgpu.validate(np.zeros((1, 17, 17)), strict=True) == -errno.EINVAL
+    assert tspgpu.validate(np.zeros((1, 17, 17)), strict=False) == 0
+    assert tspgpu.validate(np.zeros((1, 21, 21)), strict=False) == -errno.EINVAL
+
+
+def test_no_device_fails_loudly():
+    """Without a GPU the product refuses (no CPU fallback)."""
+    try:
+        ctx = tspgpu.Context(device=0)
+    except tspgpu.TspGpuError as e:
+        assert e.code == -errno.ENODEV
+        return
+    ctx.close()
+    pytest.skip("a GPU is present")

@@ -125,20 +125,61 @@ def test_validation_errors(gpu_ctx):
     assert c.shape == (0,)
 
 
-def test_device_pointer_entry_with_torch_stream(gpu_ctx):
-    torch = pytest.importorskip("torch")
+def test_device_resident_entry_and_timer(gpu_ctx):
+    """Device-pointer entry on the context's own stream (what bench.py times)."""
     rng = np.random.default_rng(9)
     n, B = 16, 256
     xy = rng.uniform(0, 1000, size=(B, n, 2))
     blocks = [[(i, p[0], p[1]) for i, p in enumerate(xy[b])] for b in range(B)]
     d = tspgpu.distance_matrix(blocks)
     ref_c, ref_t = gpu_ctx.solve_blocks(d)
-    dd = torch.from_numpy(d).cuda()
-    dc = torch.empty(B, dtype=torch.float64, device="cuda")
-    dt = torch.full((B, n + 1), -1, dtype=torch.int32, device="cuda")
-    s = torch.cuda.Stream()
-    with torch.cuda.stream(s):
-        gpu_ctx.solve_device(dd.data_ptr(), n, B, dc.data_ptr(), dt.data_ptr(), s.cuda_stream)
-    s.synchronize()
-    assert np.array_equal(dc.cpu().numpy(), ref_c)
-    assert np.array_equal(dt.cpu().numpy(), ref_t)
+    dd = gpu_ctx.upload(d)
+    dc = gpu_ctx.alloc(B * 8)
+    dt = gpu_ctx.alloc(B * (n + 1) * 4)
+    try:
+        gpu_ctx.timer_start()
+        gpu_ctx.solve_device(dd, n, B, dc, dt, gpu_ctx.stream)
+        ms = gpu_ctx.timer_stop()
+        assert ms > 0
+        assert np.array_equal(gpu_ctx.download(dc, (B,), np.float64), ref_c)
+        got_t = gpu_ctx.download(dt, (B, n + 1), np.int32)
+        assert np.array_equal(got_t, ref_t)
+    finally:
+        for p in (dd, dc, dt):
+            gpu_ctx.free(p)
+
+
+TORCH_INTEROP = r"""
+import sys, numpy as np, torch
+torch.cuda.init()                       # torch's HIP runtime first: libtspgpu binds to it
+sys.path.insert(0, sys.argv[1])
+import tspgpu
+rng = np.random.default_rng(9)
+n, B = 16, 64
+xy = rng.uniform(0, 1000, size=(B, n, 2))
+d = tspgpu.distance_matrix([[(i, p[0], p[1]) for i, p in enumerate(xy[b])] for b in range(B)])
+ctx = tspgpu.Context(device=0)
+ref_c, ref_t = ctx.solve_blocks(d)
+dd = torch.from_numpy(d).cuda()
+dc = torch.empty(B, dtype=torch.float64, device="cuda")
+dt = torch.full((B, n + 1), -1, dtype=torch.int32, device="cuda")
+s = torch.cuda.Stream()
+ctx.solve_device(dd.data_ptr(), n, B, dc.data_ptr(), dt.data_ptr(), s.cuda_stream)
+s.synchronize()
+assert np.array_equal(dc.cpu().numpy(), ref_c)
+assert np.array_equal(dt.cpu().numpy(), ref_t)
+print("OK")
+"""
+
+
+def test_torch_tensors_and_stream_interop():
+    """torch-owned device tensors and a torch stream through the C ABI.  torch
+    ships its own HIP runtime, so this runs in a fresh process that initialises
+    torch first (libtspgpu then binds to the already-loaded runtime)."""
+    import subprocess
+    import sys
+
+    pytest.importorskip("torch")
+    p = subprocess.run([sys.executable, "-c", TORCH_INTEROP, tspgpu.PKG_DIR], capture_output=True, text=True,
+                       timeout=300)
+    assert p.returncode == 0 and "OK" in p.stdout, p.stderr[-2000:]

@@ -30,11 +30,13 @@ struct LaunchArgs {
     double *cost;
     int32_t *tour;
     bool use_lds;
+    int threads;            // 256 / 512 / 1024 threads per workgroup (global-table kernels)
     hipStream_t stream;
 };
 
 void host_layer_info(int N, LayerInfo *info);
 size_t table_doubles(int N);
 hipError_t launch_heldkarp(const LaunchArgs &a, int grid);
+size_t lds_bytes_for(int N, bool lds_table);
 
 }  // namespace tspgpu

@@ -240,6 +240,14 @@ static hipError_t launch_n(const LaunchArgs &a, int grid)
     return hipGetLastError();
 }
 
+size_t lds_bytes_for(int N, bool lds_table)
+{
+    const int n = N + 1;
+    size_t lds = kBinomBytesPadded + (((size_t)n * dist_stride(N) * 8 + 15) & ~(size_t)15);
+    if (lds_table) lds += table_doubles(N) * 8;
+    return lds;
+}
+
 hipError_t launch_heldkarp(const LaunchArgs &a, int grid)
 {
     if (a.nblocks <= 0) return hipSuccess;

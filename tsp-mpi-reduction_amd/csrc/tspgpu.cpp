@@ -12,6 +12,7 @@
 #include <cerrno>
 #include <climits>
 #include <cmath>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <memory>
@@ -70,6 +71,10 @@ struct tspgpu_ctx {
     int32_t *d_tour = nullptr;
     size_t tour_bytes = 0;
     int last_grid = 0;
+    int threads = 256;   // workgroup size of the global-table kernels
+    int wg_per_cu = 2;   // resident slots per CU (auto grid)
+    hipEvent_t ev_start = nullptr, ev_stop = nullptr;
+    char name[256] = {0};
     std::mutex mu;
 };
 
@@ -155,11 +160,14 @@ int solve_device_locked(tspgpu_ctx *c, const double *d_dist, int n, int nblocks,
         a.masks = c->d_masks[N];
         a.info = c->d_info[N];
         a.use_lds = N <= kLdsTableMaxN;
+        a.threads = c->threads;
         if (a.use_lds) {
-            int cap = c->cu_count * 16;
+            // as many resident workgroups as the LDS allows, then persistent
+            const int per_cu = (int)(160 * 1024 / lds_bytes_for(N, true));
+            const int cap = c->cu_count * (per_cu > 0 ? per_cu : 1);
             grid = nblocks < cap ? nblocks : cap;
         } else {
-            int slots = c->slots_opt > 0 ? c->slots_opt : c->cu_count * 2;
+            int slots = c->slots_opt > 0 ? c->slots_opt : c->cu_count * c->wg_per_cu;
             // keep the workspace under ~8 GiB for the largest extension sizes
             const size_t per = table_doubles(N) * sizeof(double);
             const size_t budget = (size_t)8 << 30;
@@ -275,8 +283,13 @@ int tspgpu_ctx_create(const tspgpu_opts *opts, tspgpu_ctx **out)
         return -ENODEV;
     }
     hipDeviceProp_t prop;
-    if (hipGetDeviceProperties(&prop, dev) == hipSuccess && prop.multiProcessorCount > 0)
-        c->cu_count = prop.multiProcessorCount;
+    if (hipGetDeviceProperties(&prop, dev) == hipSuccess) {
+        if (prop.multiProcessorCount > 0) c->cu_count = prop.multiProcessorCount;
+        std::snprintf(c->name, sizeof c->name, "%s (%s)", prop.name, prop.gcnArchName);
+    }
+    // tuning overrides for experiments (defaults are the measured best)
+    if (const char *e = std::getenv("TSPGPU_THREADS")) c->threads = std::atoi(e);
+    if (const char *e = std::getenv("TSPGPU_WG_PER_CU")) c->wg_per_cu = std::atoi(e) > 0 ? std::atoi(e) : 2;
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
         delete c;
         return -EIO;
@@ -298,6 +311,8 @@ int tspgpu_ctx_destroy(tspgpu_ctx *c)
     if (c->d_dist) (void)hipFree(c->d_dist);
     if (c->d_cost) (void)hipFree(c->d_cost);
     if (c->d_tour) (void)hipFree(c->d_tour);
+    if (c->ev_start) (void)hipEventDestroy(c->ev_start);
+    if (c->ev_stop) (void)hipEventDestroy(c->ev_stop);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
     return 0;
@@ -365,5 +380,80 @@ int tspgpu_solve(const double *dist, int n, int nblocks, double *cost_out, int32
 }
 
 int tspgpu_last_grid(const tspgpu_ctx *c) { return c ? c->last_grid : 0; }
+
+int tspgpu_device_alloc(tspgpu_ctx *c, size_t bytes, void **ptr)
+{
+    if (!c || !ptr) return -EINVAL;
+    *ptr = nullptr;
+    if (hipSetDevice(c->device) != hipSuccess) return -ENODEV;
+    return hip_err(hipMalloc(ptr, bytes ? bytes : 1));
+}
+
+int tspgpu_device_free(tspgpu_ctx *c, void *ptr)
+{
+    if (!c) return -EINVAL;
+    if (!ptr) return 0;
+    if (hipSetDevice(c->device) != hipSuccess) return -ENODEV;
+    return hip_err(hipFree(ptr));
+}
+
+static int copy_sync(tspgpu_ctx *c, void *dst, const void *src, size_t bytes, hipMemcpyKind kind)
+{
+    if (!c || (bytes && (!dst || !src))) return -EINVAL;
+    if (!bytes) return 0;
+    std::lock_guard<std::mutex> g(c->mu);
+    if (hipSetDevice(c->device) != hipSuccess) return -ENODEV;
+    hipError_t e = hipMemcpyAsync(dst, src, bytes, kind, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    return hip_err(e);
+}
+
+int tspgpu_memcpy_htod(tspgpu_ctx *c, void *dst, const void *src, size_t bytes)
+{
+    return copy_sync(c, dst, src, bytes, hipMemcpyHostToDevice);
+}
+
+int tspgpu_memcpy_dtoh(tspgpu_ctx *c, void *dst, const void *src, size_t bytes)
+{
+    return copy_sync(c, dst, src, bytes, hipMemcpyDeviceToHost);
+}
+
+void *tspgpu_stream(tspgpu_ctx *c) { return c ? (void *)c->stream : nullptr; }
+
+int tspgpu_synchronize(tspgpu_ctx *c)
+{
+    if (!c) return -EINVAL;
+    if (hipSetDevice(c->device) != hipSuccess) return -ENODEV;
+    return hip_err(hipStreamSynchronize(c->stream));
+}
+
+int tspgpu_timer_start(tspgpu_ctx *c)
+{
+    if (!c) return -EINVAL;
+    if (hipSetDevice(c->device) != hipSuccess) return -ENODEV;
+    hipError_t e = hipSuccess;
+    if (!c->ev_start) e = hipEventCreate(&c->ev_start);
+    if (e == hipSuccess && !c->ev_stop) e = hipEventCreate(&c->ev_stop);
+    if (e == hipSuccess) e = hipEventRecord(c->ev_start, c->stream);
+    return hip_err(e);
+}
+
+int tspgpu_timer_stop(tspgpu_ctx *c, float *ms)
+{
+    if (!c || !ms || !c->ev_start) return -EINVAL;
+    if (hipSetDevice(c->device) != hipSuccess) return -ENODEV;
+    hipError_t e = hipEventRecord(c->ev_stop, c->stream);
+    if (e == hipSuccess) e = hipEventSynchronize(c->ev_stop);
+    if (e == hipSuccess) e = hipEventElapsedTime(ms, c->ev_start, c->ev_stop);
+    return hip_err(e);
+}
+
+int tspgpu_device_info(const tspgpu_ctx *c, int *cu_count, char *name, int namecap)
+{
+    if (!c) return -EINVAL;
+    if (cu_count) *cu_count = c->cu_count;
+    if (name && namecap > 0) std::snprintf(name, (size_t)namecap, "%s", c->name);
+    return 0;
+}
 
 }  // extern "C"

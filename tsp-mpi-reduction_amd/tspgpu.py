@@ -21,7 +21,9 @@ EXPORTED_SYMBOLS = (
     "tspgpu_version", "tspgpu_strerror", "tspgpu_tour_length", "tspgpu_distance_matrix", "tspgpu_validate",
     "tspgpu_ctx_create", "tspgpu_ctx_destroy", "tspgpu_solve_blocks", "tspgpu_solve_cities",
     "tspgpu_solve_blocks_device", "tspgpu_solve", "tspgpu_last_grid", "tspgpu_relaxations_per_block",
-    "tspgpu_table_bytes_per_block",
+    "tspgpu_table_bytes_per_block", "tspgpu_device_alloc", "tspgpu_device_free", "tspgpu_memcpy_htod",
+    "tspgpu_memcpy_dtoh", "tspgpu_stream", "tspgpu_synchronize", "tspgpu_timer_start", "tspgpu_timer_stop",
+    "tspgpu_device_info",
 )
 
 
@@ -70,6 +72,16 @@ def lib():
         L.tspgpu_relaxations_per_block.restype = ctypes.c_double
         L.tspgpu_table_bytes_per_block.argtypes = [ctypes.c_int]
         L.tspgpu_table_bytes_per_block.restype = ctypes.c_double
+        L.tspgpu_device_alloc.argtypes = [vp, ctypes.c_size_t, ctypes.POINTER(vp)]
+        L.tspgpu_device_free.argtypes = [vp, vp]
+        L.tspgpu_memcpy_htod.argtypes = [vp, vp, vp, ctypes.c_size_t]
+        L.tspgpu_memcpy_dtoh.argtypes = [vp, vp, vp, ctypes.c_size_t]
+        L.tspgpu_stream.argtypes = [vp]
+        L.tspgpu_stream.restype = vp
+        L.tspgpu_synchronize.argtypes = [vp]
+        L.tspgpu_timer_start.argtypes = [vp]
+        L.tspgpu_timer_stop.argtypes = [vp, ctypes.POINTER(ctypes.c_float)]
+        L.tspgpu_device_info.argtypes = [vp, ctypes.POINTER(ctypes.c_int), ctypes.c_char_p, ctypes.c_int]
         _lib = L
     return _lib
 
@@ -110,6 +122,15 @@ def cities_array(blocks):
 def distance_matrix(blocks) -> np.ndarray:
     """Host libm distances, bit-exact with computeDistanceMatrix (assignment2.h:184-200)."""
     arr, n, B = cities_array(blocks)
+    d = np.zeros((B, n, n), dtype=np.float64)
+    rc = lib().tspgpu_distance_matrix(arr, n, B, _dp(d))
+    if rc:
+        raise TspGpuError(rc, "tspgpu_distance_matrix")
+    return d
+
+
+def distance_matrix_array(arr, n: int, B: int) -> np.ndarray:
+    """Same, from a ctypes City array of B*n cities."""
     d = np.zeros((B, n, n), dtype=np.float64)
     rc = lib().tspgpu_distance_matrix(arr, n, B, _dp(d))
     if rc:
@@ -180,6 +201,50 @@ class Context:
 
     def last_grid(self) -> int:
         return lib().tspgpu_last_grid(self.handle)
+
+    def _check(self, rc, what):
+        if rc:
+            raise TspGpuError(rc, what)
+
+    def alloc(self, nbytes: int) -> int:
+        p = ctypes.c_void_p()
+        self._check(lib().tspgpu_device_alloc(self.handle, nbytes, ctypes.byref(p)), "tspgpu_device_alloc")
+        return p.value
+
+    def free(self, ptr: int):
+        self._check(lib().tspgpu_device_free(self.handle, ptr), "tspgpu_device_free")
+
+    def upload(self, arr: np.ndarray) -> int:
+        arr = np.ascontiguousarray(arr)
+        p = self.alloc(arr.nbytes)
+        self._check(lib().tspgpu_memcpy_htod(self.handle, p, arr.ctypes.data, arr.nbytes), "tspgpu_memcpy_htod")
+        return p
+
+    def download(self, ptr: int, shape, dtype) -> np.ndarray:
+        out = np.empty(shape, dtype=dtype)
+        self._check(lib().tspgpu_memcpy_dtoh(self.handle, out.ctypes.data, ptr, out.nbytes), "tspgpu_memcpy_dtoh")
+        return out
+
+    @property
+    def stream(self) -> int:
+        return lib().tspgpu_stream(self.handle) or 0
+
+    def synchronize(self):
+        self._check(lib().tspgpu_synchronize(self.handle), "tspgpu_synchronize")
+
+    def timer_start(self):
+        self._check(lib().tspgpu_timer_start(self.handle), "tspgpu_timer_start")
+
+    def timer_stop(self) -> float:
+        ms = ctypes.c_float()
+        self._check(lib().tspgpu_timer_stop(self.handle, ctypes.byref(ms)), "tspgpu_timer_stop")
+        return ms.value
+
+    def device_info(self):
+        cu = ctypes.c_int()
+        name = ctypes.create_string_buffer(256)
+        self._check(lib().tspgpu_device_info(self.handle, ctypes.byref(cu), name, 256), "tspgpu_device_info")
+        return cu.value, name.value.decode()
 
 
 def errno_name(code: int) -> str:
