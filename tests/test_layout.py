@@ -1,5 +1,6 @@
 """CPU check of the K1 kernel's table layout and index arithmetic
-(tsp-mpi-reduction_amd/csrc/heldkarp.hip), emulated step by step in Python:
+(tsp-mpi-reduction_amd/csrc/heldkarp.hip: position-major layers,
+G[S][k] at off(t) + pos(k in S) * C(N,t) + colexrank(S)), emulated step by step in Python:
 colex ranks, layer offsets, the prefix/suffix destination-rank update and the
 backtracking addresses.  Verifies that every table slot is written exactly
 once, every read hits a written slot, no index leaves its layer, and the
@@ -52,14 +53,14 @@ def emulate(d):
     tab = np.full(total, np.nan)
     writes = np.zeros(total, dtype=np.int64)
     for i in range(N):
-        tab[off[1] + i] = d[0, i + 1]
+        tab[off[1] + i] = d[0, i + 1]  # rank i, position 0
         writes[off[1] + i] += 1
     for t in range(1, N):
         s = t + 1
         for r in range(count[t]):
             T = masks[moff[t] + r]
             assert bin(T).count("1") == t and colex_rank(T) == r
-            row = [tab[off[t] + r * t + j] for j in range(t)]
+            row = [tab[off[t] + j * count[t] + r] for j in range(t)]
             assert not any(np.isnan(row))
             members = [k + 1 for k in range(N) if T >> k & 1]
             acc = [INT_MAX] * N
@@ -81,14 +82,14 @@ def emulate(d):
                 else:
                     rank = low + C(k, p + 1) + high
                     assert rank == colex_rank(T | (1 << k)) and rank < count[s]
-                    a = off[s] + rank * s + p
+                    a = off[s] + p * count[s] + rank
                     assert off[s] <= a < off[s] + count[s] * s
                     tab[a] = acc[k]
                     writes[a] += 1
     assert (writes == 1).all()
     # closing + backtracking exactly as the kernel's wave does it
     full = (1 << N) - 1
-    cands = [tab[off[N] + m - 1] + d[m, 0] for m in range(1, N + 1)]
+    cands = [tab[off[N] + (m - 1) * count[N] + 0] + d[m, 0] for m in range(1, N + 1)]
     best = min(min(cands), INT_MAX)
     bestM = next(m for m in range(1, N + 1) if cands[m - 1] == best)
     tour = [0] * (n + 1)
@@ -97,11 +98,11 @@ def emulate(d):
     while bin(S).count("1") >= 2:
         T = S & ~(1 << (k - 1))
         tt, ss = bin(T).count("1"), bin(T).count("1") + 1
-        target = tab[off[ss] + colex_rank(S) * ss + bin(S & ((1 << (k - 1)) - 1)).count("1")]
+        target = tab[off[ss] + bin(S & ((1 << (k - 1)) - 1)).count("1") * count[ss] + colex_rank(S)]
         pick = None
         for m in range(1, N + 1):
             if T >> (m - 1) & 1:
-                c = tab[off[tt] + colex_rank(T) * tt + bin(T & ((1 << (m - 1)) - 1)).count("1")] + d[m, k]
+                c = tab[off[tt] + bin(T & ((1 << (m - 1)) - 1)).count("1") * count[tt] + colex_rank(T)] + d[m, k]
                 if c == target:
                     pick = m
                     break

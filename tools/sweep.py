@@ -1,0 +1,52 @@
+"""Kernel tuning sweep (development aid): K1 launch time per configuration.
+
+    python tools/sweep.py [n ...]
+Each configuration is a fresh context created under TSPGPU_THREADS /
+TSPGPU_WG_PER_CU; all configurations run interleaved in one process.
+"""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "tsp-mpi-reduction_amd"))
+sys.path.insert(0, ROOT)
+import numpy as np  # noqa: E402
+
+import tspgpu  # noqa: E402
+from bench import Shard  # noqa: E402
+
+ns = [int(a) for a in sys.argv[1:]] or [16, 14, 12]
+configs = [(256, 2), (256, 3), (256, 4), (512, 1), (512, 2), (1024, 1)]
+for n in ns:
+    B = {16: 8192, 15: 16384, 14: 16384, 13: 32768, 12: 65536}.get(n, 65536)
+    shard = Shard(n, B, 0, B)
+    d = shard.distances()
+    rows = []
+    ctxs = []
+    for th, wg in configs:
+        os.environ["TSPGPU_THREADS"] = str(th)
+        os.environ["TSPGPU_WG_PER_CU"] = str(wg)
+        ctx = tspgpu.Context(device=0)
+        ctxs.append((th, wg, ctx, ctx.upload(d), ctx.alloc(B * 8), ctx.alloc(B * (n + 1) * 4)))
+    ref = None
+    for rep in range(2):
+        for th, wg, ctx, dd, dc, dt in ctxs:
+            ctx.solve_device(dd, n, B, dc, dt, ctx.stream)
+            ctx.timer_start()
+            for _ in range(3):
+                ctx.solve_device(dd, n, B, dc, dt, ctx.stream)
+            ms = ctx.timer_stop() / 3
+            c = ctx.download(dc, (B,), np.float64)
+            if ref is None:
+                ref = c
+            ok = np.array_equal(c, ref)
+            if rep == 1:
+                relax = tspgpu.relaxations_per_block(n) * B
+                tb = tspgpu.table_bytes_per_block(n) * B
+                print(f"n={n} B={B} threads={th} wg/cu={wg} grid={ctx.last_grid()} {ms:.3f} ms "
+                      f"{B / ms * 1e3:.3e} blocks/s {relax / ms / 1e9:.3f} Trelax/s {tb / ms / 1e9:.0f} GB/s alg "
+                      f"{'ok' if ok else 'MISMATCH'}", flush=True)
+    for *_, ctx, dd, dc, dt in ctxs:
+        for p in (dd, dc, dt):
+            ctx.free(p)
+        ctx.close()

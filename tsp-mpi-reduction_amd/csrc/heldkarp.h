@@ -37,6 +37,7 @@ struct LaunchArgs {
 void host_layer_info(int N, LayerInfo *info);
 size_t table_doubles(int N);
 hipError_t launch_heldkarp(const LaunchArgs &a, int grid);
-size_t lds_bytes_for(int N, bool lds_table);
+size_t lds_bytes_for(int N, bool lds_table, int threads);
+int threads_for(int N, bool lds_table, int requested);
 
 }  // namespace tspgpu

@@ -1,211 +1,14 @@
-// K1 — batched exact Held-Karp for gfx950 (MI355X).
-//
-// Replaces the hot loop of the reference's per-block solver
-// `BlockSolution tsp(vector<City>)` (tsp.cpp:405-509): the std::map subset DP
-// with per-state path vectors becomes a dense, colex-ranked FP64 table that one
-// workgroup sweeps layer by layer.
-//
-// Semantics kept bit-exact:
-//   layer 1   G[{i}][i]  = d[0][i]
-//   layer s   G[S][k]    = min_{m in S\k} G[S\k][m] + d[m][k]      (s >= 2)
-//             layer 2 = d[0][i] + d[i][k], the reference's init (tsp.cpp:435;
-//             IEEE add commutes); layers >= 3 start from INT_MAX like
-//             tsp.cpp:453 (the host guarantees every candidate < INT_MAX).
-//   closing   OPT = first strict min over m ascending of G[full][m] + d[m][0]
-//   tour      backtracking with the SMALLEST m whose candidate equals the
-//             state value == the reference's first strict-< argmin path.
-// Only IEEE adds and min/compare touch the values: no FMA, no reassociation,
-// distances come from the host (glibc pow), never recomputed here.
-//
-// Table layout per block (one slot per resident workgroup):
-//   layer t (|S| = t) at doubles [off[t], off[t] + C(N,t)*t),
-//   row = colex rank of S among t-subsets, column = position of k in S.
-// Every entry is written once and read once: 2*8*N*2^(N-1) bytes per block.
-//
-// Work split: layer t -> t+1 is one pass over the C(N,t) SOURCE rows T.  A
-// thread loads its row G[T][.] once (contiguous), streams the d-row of each
-// member m from LDS (stride 18 doubles => conflict-free ds_read_b128 across
-// distinct m) and keeps the N running minima acc[k] in VGPRs; it then stores
-// acc[k] for every k not in T to G[T+k][k] (its unique writer).  The k loop is
-// fully unrolled over all N cities (members masked on store) so no register
-// array is ever indexed dynamically.
-#include <hip/hip_runtime.h>
-#include <stdint.h>
-
-#include "heldkarp.h"
+// K1 dispatch: picks the per-N instantiation (hk_n*.hip) and the n == 2 kernel.
+// Kernel design and the bit-exactness argument: heldkarp_impl.h.
+#include "heldkarp_impl.h"
 
 namespace tspgpu {
 
-constexpr int kThreads = 256;
-constexpr int kBinomStride = kBinomCols;   // ints per binomial row, C(a,b) a<=20, b<=21
-constexpr int kBinomBytesPadded = 2048;    // 21*24*4 = 2016 rounded to 16
-
-__host__ __device__ constexpr int dist_stride(int N) { return ((N + 2) & ~1) + 2; }
-
-template <int N>
-__device__ __forceinline__ int colex_rank(uint32_t mask, const int *binom)
-{
-    int rank = 0, j = 0;
-    while (mask) {
-        const int b = __builtin_ctz(mask);
-        rank += binom[b * kBinomStride + j + 1];
-        ++j;
-        mask &= mask - 1u;
-    }
-    return rank;
-}
-
-__device__ __forceinline__ double wave_min(double v)
-{
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) v = fmin(v, __shfl_xor(v, off));
-    return v;
-}
-
-// One workgroup solves blocks blockIdx.x, blockIdx.x + gridDim.x, ...
-// LDS_TABLE: the whole compact table lives in LDS (N <= 11), else in the
-// workgroup's global slot.
-template <int N, bool LDS_TABLE>
-__global__ __launch_bounds__(kThreads) void heldkarp_kernel(const double *__restrict__ dist, int nblocks,
-                                                            double *__restrict__ slots, size_t slot_doubles,
-                                                            const uint32_t *__restrict__ masks,
-                                                            const LayerInfo *__restrict__ info,
-                                                            double *__restrict__ cost_out,
-                                                            int32_t *__restrict__ tour_out)
-{
-    constexpr int n = N + 1;
-    constexpr int DS = dist_stride(N);
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    int *binom = reinterpret_cast<int *>(smem);
-    double *dl = reinterpret_cast<double *>(smem + kBinomBytesPadded);
-    const int tid = threadIdx.x;
-
-    for (int i = tid; i < kBinomRows * kBinomStride; i += kThreads) binom[i] = info->binom[i];
-
-    double *tab;
-    if constexpr (LDS_TABLE) {
-        constexpr int dl_bytes = ((n * DS * 8) + 15) & ~15;
-        tab = reinterpret_cast<double *>(smem + kBinomBytesPadded + dl_bytes);
-    } else {
-        tab = slots + (size_t)blockIdx.x * slot_doubles;
-    }
-
-    for (int blk = blockIdx.x; blk < nblocks; blk += gridDim.x) {
-        const double *dsrc = dist + (size_t)blk * n * n;
-        for (int i = tid; i < n * n; i += kThreads) dl[(i / n) * DS + (i % n)] = dsrc[i];
-        __syncthreads();
-
-        // layer 1: G[{i}][i] = d[0][i]; colex rank of {i} is i-1
-        if (tid < N) tab[info->off[1] + tid] = dl[tid + 1];
-        __syncthreads();
-
-        for (int t = 1; t < N; ++t) {
-            const int s = t + 1;
-            const int rows = info->count[t];
-            const double *src = tab + info->off[t];
-            double *dst = tab + info->off[s];
-            const uint32_t *mt = masks + info->moff[t];
-            for (int r = tid; r < rows; r += kThreads) {
-                const uint32_t T = mt[r];
-                double acc[N];
-#pragma unroll
-                for (int k = 0; k < N; ++k) acc[k] = 2147483647.0;  // INT_MAX, tsp.cpp:453
-                // the whole source row in VGPRs first (index clamped to the row:
-                // no branch, no read past it), then the member sweep
-                const double *row = src + (size_t)r * t;
-                double g[N];
-#pragma unroll
-                for (int j = 0; j < N; ++j) g[j] = row[j < t ? j : t - 1];
-                uint32_t bits = T;
-#pragma unroll
-                for (int j = 0; j < N; ++j) {
-                    if (j < t) {  // wave-uniform: t is the layer
-                        const int m = __builtin_ctz(bits) + 1;
-                        bits &= bits - 1u;
-                        const double2 *drow = reinterpret_cast<const double2 *>(dl + m * DS);
-                        double2 dv[(N + 2) / 2];
-#pragma unroll
-                        for (int q = 0; q < (N + 2) / 2; ++q) dv[q] = drow[q];
-#pragma unroll
-                        for (int k = 0; k < N; ++k) {
-                            const double dk = ((k + 1) & 1) ? dv[(k + 1) >> 1].y : dv[(k + 1) >> 1].x;
-                            acc[k] = fmin(acc[k], g[j] + dk);
-                        }
-                    }
-                }
-                // destination rank of T+{k} from prefix/suffix colex sums
-                int high = 0;
-                {
-                    int idx = 0;
-#pragma unroll
-                    for (int k = 0; k < N; ++k)
-                        if (T & (1u << k)) {
-                            high += binom[k * kBinomStride + idx + 2];
-                            ++idx;
-                        }
-                }
-                int low = 0, p = 0;
-#pragma unroll
-                for (int k = 0; k < N; ++k) {
-                    if (T & (1u << k)) {
-                        low += binom[k * kBinomStride + p + 1];
-                        high -= binom[k * kBinomStride + p + 2];
-                        ++p;
-                    } else {
-                        const int rank = low + binom[k * kBinomStride + p + 1] + high;
-                        dst[(size_t)rank * s + p] = acc[k];
-                    }
-                }
-            }
-            __syncthreads();
-        }
-
-        // closing min (tsp.cpp:483-499) and backtracking, one wave
-        if (tid < 64) {
-            const int lane = tid;
-            const int m = lane + 1;
-            const uint32_t full = (1u << N) - 1u;
-            const double *last = tab + info->off[N];
-            const bool valid = m <= N;
-            const double cand = valid ? last[m - 1] + dl[m * DS + 0] : 1.0e300;
-            const double best = fmin(wave_min(cand), 2147483647.0);
-            const unsigned long long hit = __ballot(valid && cand == best && cand < 2147483647.0);
-            const int bestM = hit ? __ffsll(hit) : 0;
-            int32_t *tour = tour_out + (size_t)blk * (n + 1);
-            uint32_t S = full;
-            int k = bestM;
-            int pos = n - 2;
-            bool ok = bestM != 0;
-            while (ok && __builtin_popcount(S) >= 2) {
-                const uint32_t T = S & ~(1u << (k - 1));
-                const int tt = __builtin_popcount(T);
-                const int ss = tt + 1;
-                const int rS = colex_rank<N>(S, binom);
-                const int rT = colex_rank<N>(T, binom);
-                const double target =
-                    tab[info->off[ss] + rS * ss + __builtin_popcount(S & ((1u << (k - 1)) - 1u))];
-                const bool inT = valid && ((T >> (m - 1)) & 1u);
-                double c = 0.0;
-                if (inT) c = tab[info->off[tt] + rT * tt + __builtin_popcount(T & ((1u << (m - 1)) - 1u))] +
-                             dl[m * DS + k];
-                const unsigned long long bb = __ballot(inT && c == target);
-                const int pick = bb ? __ffsll(bb) : 0;
-                ok = pick != 0;
-                if (lane == 0) tour[pos] = pick;
-                --pos;
-                S = T;
-                k = pick;
-            }
-            if (lane == 0) {
-                tour[0] = 0;
-                tour[n - 1] = bestM;
-                tour[n] = 0;
-                cost_out[blk] = ok ? best : -1.0;  // -1: no predecessor matched (never expected)
-            }
-        }
-        __syncthreads();
-    }
-}
+#define TSPGPU_EXTERN(NN) extern template hipError_t launch_threads<NN>(const LaunchArgs &, int);
+TSPGPU_EXTERN(2) TSPGPU_EXTERN(3) TSPGPU_EXTERN(4) TSPGPU_EXTERN(5) TSPGPU_EXTERN(6) TSPGPU_EXTERN(7)
+TSPGPU_EXTERN(8) TSPGPU_EXTERN(9) TSPGPU_EXTERN(10) TSPGPU_EXTERN(11) TSPGPU_EXTERN(12) TSPGPU_EXTERN(13)
+TSPGPU_EXTERN(14) TSPGPU_EXTERN(15) TSPGPU_EXTERN(16) TSPGPU_EXTERN(17) TSPGPU_EXTERN(18) TSPGPU_EXTERN(19)
+#undef TSPGPU_EXTERN
 
 // n == 2: tsp.cpp:483-502 with cityNums = {1}: key(empty,1) is default-inserted
 // with cost 0, so cost = 0 + d[1][0] and the path is [1, 0].
@@ -220,32 +23,16 @@ __global__ void two_city_kernel(const double *__restrict__ dist, int nblocks, do
     tour_out[(size_t)b * 3 + 2] = -1;
 }
 
-template <int N, bool LDS>
-static hipError_t launch_n(const LaunchArgs &a, int grid)
+int threads_for(int N, bool lds_table, int requested)
 {
-    constexpr int n = N + 1;
-    size_t lds = kBinomBytesPadded + (((size_t)n * dist_stride(N) * 8 + 15) & ~(size_t)15);
-    if constexpr (LDS) lds += table_doubles(N) * 8;
-    if (lds > 64 * 1024) {
-        static bool raised = false;  // once per instantiation
-        if (!raised) {
-            hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&heldkarp_kernel<N, LDS>),
-                                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-            if (e != hipSuccess) return e;
-            raised = true;
-        }
-    }
-    hipLaunchKernelGGL((heldkarp_kernel<N, LDS>), dim3(grid), dim3(kThreads), lds, a.stream, a.dist, a.nblocks,
-                       a.slots, a.slot_doubles, a.masks, a.info, a.cost, a.tour);
-    return hipGetLastError();
+    if (lds_table) return lds_table_threads(N);
+    if (N >= 12 && N <= 15 && (requested == 512 || requested == 1024)) return requested;
+    return 256;
 }
 
-size_t lds_bytes_for(int N, bool lds_table)
+size_t lds_bytes_for(int N, bool lds_table, int threads)
 {
-    const int n = N + 1;
-    size_t lds = kBinomBytesPadded + (((size_t)n * dist_stride(N) * 8 + 15) & ~(size_t)15);
-    if (lds_table) lds += table_doubles(N) * 8;
-    return lds;
+    return N >= 2 && N <= kMaxN ? lds_bytes(N, lds_table, threads) : 0;
 }
 
 hipError_t launch_heldkarp(const LaunchArgs &a, int grid)
@@ -258,30 +45,24 @@ hipError_t launch_heldkarp(const LaunchArgs &a, int grid)
         return hipGetLastError();
     }
     switch (N) {
-#define TSPGPU_CASE_LDS(NN) \
-    case NN: return a.use_lds ? launch_n<NN, true>(a, grid) : launch_n<NN, false>(a, grid);
-#define TSPGPU_CASE_GLB(NN) \
-    case NN: return launch_n<NN, false>(a, grid);
-        TSPGPU_CASE_LDS(2)
-        TSPGPU_CASE_LDS(3)
-        TSPGPU_CASE_LDS(4)
-        TSPGPU_CASE_LDS(5)
-        TSPGPU_CASE_LDS(6)
-        TSPGPU_CASE_LDS(7)
-        TSPGPU_CASE_LDS(8)
-        TSPGPU_CASE_LDS(9)
-        TSPGPU_CASE_LDS(10)
-        TSPGPU_CASE_LDS(11)
-        TSPGPU_CASE_GLB(12)
-        TSPGPU_CASE_GLB(13)
-        TSPGPU_CASE_GLB(14)
-        TSPGPU_CASE_GLB(15)
-        TSPGPU_CASE_GLB(16)
-        TSPGPU_CASE_GLB(17)
-        TSPGPU_CASE_GLB(18)
-        TSPGPU_CASE_GLB(19)
-#undef TSPGPU_CASE_LDS
-#undef TSPGPU_CASE_GLB
+    case 2: return launch_threads<2>(a, grid);
+    case 3: return launch_threads<3>(a, grid);
+    case 4: return launch_threads<4>(a, grid);
+    case 5: return launch_threads<5>(a, grid);
+    case 6: return launch_threads<6>(a, grid);
+    case 7: return launch_threads<7>(a, grid);
+    case 8: return launch_threads<8>(a, grid);
+    case 9: return launch_threads<9>(a, grid);
+    case 10: return launch_threads<10>(a, grid);
+    case 11: return launch_threads<11>(a, grid);
+    case 12: return launch_threads<12>(a, grid);
+    case 13: return launch_threads<13>(a, grid);
+    case 14: return launch_threads<14>(a, grid);
+    case 15: return launch_threads<15>(a, grid);
+    case 16: return launch_threads<16>(a, grid);
+    case 17: return launch_threads<17>(a, grid);
+    case 18: return launch_threads<18>(a, grid);
+    case 19: return launch_threads<19>(a, grid);
     default: return hipErrorInvalidValue;
     }
 }

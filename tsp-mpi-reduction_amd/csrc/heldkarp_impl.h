@@ -1,0 +1,393 @@
+// Templates of the K1 Held-Karp kernels; instantiated per N in hk_n*.hip so the
+// instantiations compile in parallel (see heldkarp.hip for the dispatch).
+#pragma once
+// K1 — batched exact Held-Karp for gfx950 (MI355X): kernel templates.
+//
+// Replaces the hot loop of the reference's per-block solver
+// `BlockSolution tsp(vector<City>)` (tsp.cpp:405-509): the std::map subset DP
+// with per-state path vectors becomes a dense, colex-ranked FP64 table that one
+// workgroup sweeps layer by layer.
+//
+// Semantics kept bit-exact:
+//   layer 1   G[{i}][i]  = d[0][i]
+//   layer s   G[S][k]    = min_{m in S\k} G[S\k][m] + d[m][k]      (s >= 2)
+//             layer 2 = d[0][i] + d[i][k], the reference's init (tsp.cpp:435;
+//             IEEE add commutes); layers >= 3 start from INT_MAX like
+//             tsp.cpp:453 (the host guarantees every candidate < INT_MAX).
+//   closing   OPT = first strict min over m ascending of G[full][m] + d[m][0]
+//   tour      backtracking with the SMALLEST m whose candidate equals the
+//             state value == the reference's first strict-< argmin path.
+// Only IEEE adds and min/compare touch the values: no FMA, no reassociation,
+// distances come from the host (glibc pow), never recomputed here.
+//
+// Table layout per block, position-major ("SoA") inside each layer:
+//   G[S][k], |S| = t, at  off(t) + pos(k in S) * C(N,t) + colexrank(S)
+// so a wave that sweeps 64 consecutive source rows reads each position as one
+// contiguous 512-B segment, and its scattered destination writes land ~4x
+// denser in 64-B sectors than with row-major rows (tools/layout_sim.py).
+// Every entry is written once and read once: 2*8*N*2^(N-1) bytes per block.
+//
+// Work split: layer t -> t+1 is one pass over the C(N,t) SOURCE rows T,
+// compiled separately for every t (offsets, counts, row length are constants).
+// A thread issues the t loads of its next row early (software pipelining into
+// VGPRs), parks the current row in a thread-private LDS slot, sweeps the
+// members m of T (d-row of m from LDS, N running minima acc[k] in VGPRs) and
+// stores acc[k] for every k not in T to G[T+k][k] (its unique writer).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <type_traits>
+
+#include "heldkarp.h"
+
+namespace tspgpu {
+
+constexpr int kBinomStride = kBinomCols;   // ints per binomial row, C(a,b) a<=20, b<=23
+constexpr int kBinomBytesPadded = 2048;    // 21*24*4 = 2016 rounded to 16
+constexpr double kIntMax = 2147483647.0;   // the reference's sentinel (tsp.cpp:411,453)
+
+__host__ __device__ constexpr int cbinom(int a, int b)
+{
+    if (b < 0 || b > a) return 0;
+    long long r = 1;
+    for (int i = 1; i <= b; ++i) r = r * (a - b + i) / i;
+    return (int)r;
+}
+__host__ __device__ constexpr int layer_off(int N, int t)
+{
+    int o = 0;
+    for (int u = 1; u < t; ++u) o += cbinom(N, u) * u;
+    return o;
+}
+__host__ __device__ constexpr int mask_off(int N, int t)
+{
+    int o = 0;
+    for (int u = 0; u < t; ++u) o += cbinom(N, u);
+    return o;
+}
+// d row stride in doubles: >= N+1, even (16-B rows), and 2 mod 4 in 8-B units
+// so distinct rows start on distinct 16-B bank groups (ds_read_b128).
+__host__ __device__ constexpr int dist_stride(int N) { return ((N + 2) & ~1) + 2; }
+__host__ __device__ constexpr size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
+__host__ __device__ constexpr size_t dl_bytes(int N) { return align16((size_t)(N + 1) * dist_stride(N) * 8); }
+// LDS: binomials | distance rows | table (LDS_TABLE) or per-thread row slots
+__host__ __device__ constexpr size_t lds_bytes(int N, bool lds_table, int threads)
+{
+    return kBinomBytesPadded + dl_bytes(N) +
+           (lds_table ? ((size_t)N << (N - 1)) * 8 : (size_t)(N - 1) * threads * 8);
+}
+
+__device__ __forceinline__ int colex_rank(uint32_t mask, const int *binom)
+{
+    int rank = 0, j = 0;
+    while (mask) {
+        const int b = __builtin_ctz(mask);
+        rank += binom[b * kBinomStride + j + 1];
+        ++j;
+        mask &= mask - 1u;
+    }
+    return rank;
+}
+
+__device__ __forceinline__ double wave_min(double v)
+{
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v = fmin(v, __shfl_xor(v, off));
+    return v;
+}
+
+// dl row m holds d[m][1..N] at [0, N) and d[m][0] at N: the N values a row
+// sweep needs start 16-B aligned.
+template <int N>
+__device__ __forceinline__ double dget(const double *dl, int m, int k)
+{
+    return dl[m * dist_stride(N) + (k == 0 ? N : k - 1)];
+}
+
+// Global table access through a buffer resource (SRSRC): 32-bit offsets in
+// one VGPR instead of 64-bit pointers, and the hardware range check turns
+// any out-of-slot index into a dropped access instead of a fault.
+struct GlobalTable {
+    __amdgpu_buffer_rsrc_t rs;
+    __device__ __forceinline__ double load(uint32_t idx) const
+    {
+        return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, (int)(idx * 8u), 0, 0));
+    }
+    __device__ __forceinline__ void store(uint32_t idx, double v) const
+    {
+        using u2 = decltype(__builtin_amdgcn_raw_buffer_load_b64(rs, 0, 0, 0));
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2, v), rs, (int)(idx * 8u), 0, 0);
+    }
+};
+struct LdsTable {
+    double *p;
+    __device__ __forceinline__ double load(uint32_t idx) const { return p[idx]; }
+    __device__ __forceinline__ void store(uint32_t idx, double v) const { p[idx] = v; }
+};
+
+// acc[k] = min(acc[k], g + d[m][k+1]) for all k: one member of the source row.
+template <int N>
+__device__ __forceinline__ void relax_member(double (&acc)[N], const double *dl, int m, double g)
+{
+    const double2 *drow = reinterpret_cast<const double2 *>(__builtin_assume_aligned(dl + m * dist_stride(N), 16));
+#pragma unroll
+    for (int q = 0; q < N / 2; ++q) {
+        const double2 v = drow[q];
+        acc[2 * q] = fmin(acc[2 * q], g + v.x);
+        acc[2 * q + 1] = fmin(acc[2 * q + 1], g + v.y);
+    }
+    if constexpr (N & 1) acc[N - 1] = fmin(acc[N - 1], g + dl[m * dist_stride(N) + N - 1]);
+}
+
+// Store acc[k] for every k not in Tm at G[Tm+k][k] of layer S = T+1.
+// colex rank of T+{k}: members below k keep their index, those above shift by
+// one: rank = sum_{i<p} C(e_i,i+1) + C(k,p+1) + sum_{i>=p} C(e_i,i+2).
+template <int N, int S, typename Tab>
+__device__ __forceinline__ void scatter_row(const Tab &tab, const double (&acc)[N], uint32_t Tm, const int *binom)
+{
+    constexpr int ROWS_S = cbinom(N, S);
+    constexpr uint32_t DST = layer_off(N, S);
+    int high = 0;
+    {
+        int idx = 0;
+#pragma unroll
+        for (int k = 0; k < N; ++k)
+            if (Tm & (1u << k)) {
+                high += binom[k * kBinomStride + idx + 2];
+                ++idx;
+            }
+    }
+    int low = 0, p = 0;
+#pragma unroll
+    for (int k = 0; k < N; ++k) {
+        if (Tm & (1u << k)) {
+            low += binom[k * kBinomStride + p + 1];
+            high -= binom[k * kBinomStride + p + 2];
+            ++p;
+        } else {
+            const int rank = low + binom[k * kBinomStride + p + 1] + high;
+            tab.store(DST + (uint32_t)(p * ROWS_S + rank), acc[k]);
+        }
+    }
+}
+
+// Global table: layer T -> T+1, rows r = tid, tid+THREADS, ...; the next row's
+// t loads are in flight while the current row is swept.
+template <int N, int T, int THREADS>
+__device__ __forceinline__ void layer_pass_global(const GlobalTable &tab, const double *__restrict__ dl,
+                                                  const int *__restrict__ binom, double *__restrict__ slot,
+                                                  const uint32_t *__restrict__ masks, uint32_t tid)
+{
+    constexpr int S = T + 1;
+    constexpr uint32_t ROWS = cbinom(N, T);
+    constexpr uint32_t SRC = layer_off(N, T);
+    const uint32_t *mt = masks + mask_off(N, T);
+    uint32_t r = tid;
+    if (r >= ROWS) return;
+    double nxt[T];
+    uint32_t nmask = mt[r];
+#pragma unroll
+    for (int j = 0; j < T; ++j) nxt[j] = tab.load(SRC + j * ROWS + r);
+    for (; r < ROWS; r += THREADS) {
+        const uint32_t Tm = nmask;
+#pragma unroll
+        for (int j = 0; j < T; ++j) slot[j * THREADS] = nxt[j];
+        const uint32_t rn = r + THREADS;
+        if (rn < ROWS) {
+            nmask = mt[rn];
+#pragma unroll
+            for (int j = 0; j < T; ++j) nxt[j] = tab.load(SRC + j * ROWS + rn);
+        }
+        double acc[N];
+#pragma unroll
+        for (int k = 0; k < N; ++k) acc[k] = kIntMax;
+        uint32_t bits = Tm;
+#pragma unroll 2
+        for (int j = 0; j < T; ++j) {
+            const int m = __builtin_ctz(bits) + 1;
+            bits &= bits - 1u;
+            relax_member<N>(acc, dl, m, slot[j * THREADS]);
+        }
+        scatter_row<N, S>(tab, acc, Tm, binom);
+    }
+}
+
+// LDS table: the source row is read straight from the table.
+template <int N, int T, int THREADS>
+__device__ __forceinline__ void layer_pass_lds(const LdsTable &tab, const double *__restrict__ dl,
+                                               const int *__restrict__ binom, const uint32_t *__restrict__ masks,
+                                               uint32_t tid)
+{
+    constexpr int S = T + 1;
+    constexpr uint32_t ROWS = cbinom(N, T);
+    constexpr uint32_t SRC = layer_off(N, T);
+    const uint32_t *mt = masks + mask_off(N, T);
+    for (uint32_t r = tid; r < ROWS; r += THREADS) {
+        const uint32_t Tm = mt[r];
+        double acc[N];
+#pragma unroll
+        for (int k = 0; k < N; ++k) acc[k] = kIntMax;
+        uint32_t bits = Tm;
+#pragma unroll 2
+        for (int j = 0; j < T; ++j) {
+            const int m = __builtin_ctz(bits) + 1;
+            bits &= bits - 1u;
+            relax_member<N>(acc, dl, m, tab.load(SRC + j * ROWS + r));
+        }
+        scatter_row<N, S>(tab, acc, Tm, binom);
+    }
+}
+
+template <int N, int T, int THREADS, typename Tab>
+__device__ __forceinline__ void all_layers(const Tab &tab, const double *dl, const int *binom, double *slot,
+                                           const uint32_t *masks, uint32_t tid)
+{
+    if constexpr (T < N) {
+        if constexpr (std::is_same<Tab, LdsTable>::value)
+            layer_pass_lds<N, T, THREADS>(tab, dl, binom, masks, tid);
+        else
+            layer_pass_global<N, T, THREADS>(tab, dl, binom, slot, masks, tid);
+        __syncthreads();
+        all_layers<N, T + 1, THREADS>(tab, dl, binom, slot, masks, tid);
+    }
+}
+
+// One workgroup solves blocks blockIdx.x, blockIdx.x + gridDim.x, ...
+// LDS_TABLE: the whole compact table lives in LDS (N <= 11), else in the
+// workgroup's global slot.
+// Occupancy target: 4 waves per SIMD (16 per CU), i.e. <= 128 VGPRs, for the
+// reference's sizes; 2 waves per SIMD for the n > 16 extension kernels.
+__host__ __device__ constexpr int min_waves(int N) { return N <= 15 ? 4 : 2; }
+template <int N, bool LDS_TABLE, int THREADS>
+__global__ __launch_bounds__(THREADS, min_waves(N)) void heldkarp_kernel(const double *__restrict__ dist, int nblocks,
+                                                           double *__restrict__ slots, size_t slot_doubles,
+                                                           const uint32_t *__restrict__ masks,
+                                                           const LayerInfo *__restrict__ info,
+                                                           double *__restrict__ cost_out,
+                                                           int32_t *__restrict__ tour_out)
+{
+    constexpr int n = N + 1;
+    constexpr int DS = dist_stride(N);
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    int *binom = reinterpret_cast<int *>(smem);
+    double *dl = reinterpret_cast<double *>(smem + kBinomBytesPadded);
+    double *lds_rest = reinterpret_cast<double *>(smem + kBinomBytesPadded + dl_bytes(N));
+    const int tid = threadIdx.x;
+
+    for (int i = tid; i < kBinomRows * kBinomStride; i += THREADS) binom[i] = info->binom[i];
+
+    double *tab;
+    if constexpr (LDS_TABLE)
+        tab = lds_rest;
+    else
+        tab = slots + (size_t)blockIdx.x * slot_doubles;
+    using Tab = typename std::conditional<LDS_TABLE, LdsTable, GlobalTable>::type;
+    Tab th;
+    if constexpr (LDS_TABLE)
+        th.p = tab;
+    else
+        th.rs = __builtin_amdgcn_make_buffer_rsrc(tab, 0, (int)(slot_doubles * 8), 0x00020000);
+
+    for (int blk = blockIdx.x; blk < nblocks; blk += gridDim.x) {
+        const double *dsrc = dist + (size_t)blk * n * n;
+        for (int i = tid; i < n * n; i += THREADS) {
+            const int row = i / n, col = i % n;
+            dl[row * DS + (col == 0 ? N : col - 1)] = dsrc[i];
+        }
+        __syncthreads();
+
+        // layer 1: G[{i}][i] = d[0][i]; colex rank of {i} is i-1, position 0
+        if (tid < N) tab[tid] = dget<N>(dl, 0, tid + 1);
+        __syncthreads();
+
+        // Opaque per-block copies: keeps the compiler from hoisting every
+        // layer's per-thread addresses out of the block loop (that LICM alone
+        // costs ~200 VGPRs of 64-bit pointers).
+        int tid_b = tid;
+        asm volatile("" : "+v"(tid_b));
+        all_layers<N, 1, THREADS>(th, dl, binom, lds_rest + tid_b, masks, (uint32_t)tid_b);
+
+        // closing min (tsp.cpp:483-499) and backtracking, one wave
+        if (tid < 64) {
+            const int lane = tid;
+            const int m = lane + 1;
+            const uint32_t full = (1u << N) - 1u;
+            const double *last = tab + layer_off(N, N);  // one row: position m-1 at m-1
+            const bool valid = m <= N;
+            const double cand = valid ? last[m - 1] + dget<N>(dl, m, 0) : 1.0e300;
+            const double best = fmin(wave_min(cand), kIntMax);
+            const unsigned long long hit = __ballot(valid && cand == best && cand < kIntMax);
+            const int bestM = hit ? __ffsll(hit) : 0;
+            int32_t *tour = tour_out + (size_t)blk * (n + 1);
+            uint32_t S = full;
+            int k = bestM;
+            int pos = n - 2;
+            bool ok = bestM != 0;
+            while (ok && __builtin_popcount(S) >= 2) {
+                const uint32_t T = S & ~(1u << (k - 1));
+                const int tt = __builtin_popcount(T);
+                const int ss = tt + 1;
+                const int rS = colex_rank(S, binom);
+                const int rT = colex_rank(T, binom);
+                const double target = tab[info->off[ss] +
+                                          __builtin_popcount(S & ((1u << (k - 1)) - 1u)) * info->count[ss] + rS];
+                const bool inT = valid && ((T >> (m - 1)) & 1u);
+                double c = 0.0;
+                if (inT)
+                    c = tab[info->off[tt] + __builtin_popcount(T & ((1u << (m - 1)) - 1u)) * info->count[tt] + rT] +
+                        dget<N>(dl, m, k);
+                const unsigned long long bb = __ballot(inT && c == target);
+                const int pick = bb ? __ffsll(bb) : 0;
+                ok = pick != 0;
+                if (lane == 0) tour[pos] = pick;
+                --pos;
+                S = T;
+                k = pick;
+            }
+            if (lane == 0) {
+                tour[0] = 0;
+                tour[n - 1] = bestM;
+                tour[n] = 0;
+                cost_out[blk] = ok ? best : -1.0;  // -1: no predecessor matched (never expected)
+            }
+        }
+        __syncthreads();
+    }
+}
+
+template <int N, bool LDS, int THREADS>
+hipError_t launch_n(const LaunchArgs &a, int grid)
+{
+    const size_t lds = lds_bytes(N, LDS, THREADS);
+    if (lds > 64 * 1024) {
+        static bool raised = false;  // once per instantiation
+        if (!raised) {
+            hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&heldkarp_kernel<N, LDS, THREADS>),
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+            if (e != hipSuccess) return e;
+            raised = true;
+        }
+    }
+    hipLaunchKernelGGL((heldkarp_kernel<N, LDS, THREADS>), dim3(grid), dim3(THREADS), lds, a.stream, a.dist,
+                       a.nblocks, a.slots, a.slot_doubles, a.masks, a.info, a.cost, a.tour);
+    return hipGetLastError();
+}
+
+// Workgroup size of the LDS-table kernels: the whole table of N=11 (88 KiB)
+// admits one workgroup per CU, so it gets 1024 threads (4 waves per SIMD).
+__host__ __device__ constexpr int lds_table_threads(int N) { return N >= 11 ? 1024 : 256; }
+
+template <int N>
+hipError_t launch_threads(const LaunchArgs &a, int grid)
+{
+    if constexpr (N <= kLdsTableMaxN) {
+        if (a.use_lds) return launch_n<N, true, lds_table_threads(N)>(a, grid);
+    }
+    if constexpr (N >= 12 && N <= 15) {
+        if (a.threads == 512) return launch_n<N, false, 512>(a, grid);
+        if (a.threads == 1024) return launch_n<N, false, 1024>(a, grid);
+    }
+    return launch_n<N, false, 256>(a, grid);
+}
+
+}  // namespace tspgpu
