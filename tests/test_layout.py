@@ -67,25 +67,23 @@ def emulate(d):
             for j, m in enumerate(members):
                 for k in range(N):
                     acc[k] = min(acc[k], row[j] + d[m, k + 1])
-            high = 0
-            idx = 0
-            for k in range(N):
-                if T >> k & 1:
-                    high += C(k, idx + 2)
-                    idx += 1
-            low = p = 0
-            for k in range(N):
-                if T >> k & 1:
-                    low += C(k, p + 1)
-                    high -= C(k, p + 2)
-                    p += 1
-                else:
-                    rank = low + C(k, p + 1) + high
+            # descending k with suffix sums (heldkarp_impl.h scatter_row)
+            q = s1 = s2 = 0
+            for k in range(N - 1, -1, -1):
+                inn = T >> k & 1
+                p = t - q - inn
+                c1, c2 = C(k, p + 1), C(k, p + 2)
+                if not inn:
+                    rank = r - s1 + c1 + s2
                     assert rank == colex_rank(T | (1 << k)) and rank < count[s]
                     a = off[s] + p * count[s] + rank
                     assert off[s] <= a < off[s] + count[s] * s
                     tab[a] = acc[k]
                     writes[a] += 1
+                else:
+                    s1 += c1
+                    s2 += c2
+                    q += 1
     assert (writes == 1).all()
     # closing + backtracking exactly as the kernel's wave does it
     full = (1 << N) - 1

@@ -113,16 +113,22 @@ struct GlobalTable {
     {
         return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, (int)(idx * 8u), 0, 0));
     }
-    __device__ __forceinline__ void store(uint32_t idx, double v) const
+    // a store at an offset past num_records is dropped by the buffer range
+    // check: predication without a branch
+    __device__ __forceinline__ void store_if(bool pred, uint32_t idx, double v) const
     {
         using u2 = decltype(__builtin_amdgcn_raw_buffer_load_b64(rs, 0, 0, 0));
-        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2, v), rs, (int)(idx * 8u), 0, 0);
+        const int off = pred ? (int)(idx * 8u) : 0x7ffffff0;
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2, v), rs, off, 0, 0);
     }
 };
 struct LdsTable {
     double *p;
     __device__ __forceinline__ double load(uint32_t idx) const { return p[idx]; }
-    __device__ __forceinline__ void store(uint32_t idx, double v) const { p[idx] = v; }
+    __device__ __forceinline__ void store_if(bool pred, uint32_t idx, double v) const
+    {
+        if (pred) p[idx] = v;
+    }
 };
 
 // acc[k] = min(acc[k], g + d[m][k+1]) for all k: one member of the source row.
@@ -140,34 +146,30 @@ __device__ __forceinline__ void relax_member(double (&acc)[N], const double *dl,
 }
 
 // Store acc[k] for every k not in Tm at G[Tm+k][k] of layer S = T+1.
-// colex rank of T+{k}: members below k keep their index, those above shift by
-// one: rank = sum_{i<p} C(e_i,i+1) + C(k,p+1) + sum_{i>=p} C(e_i,i+2).
+// colex rank of T+{k} (e_i = members ascending, p = #members below k):
+//   sum_{i<p} C(e_i,i+1) + C(k,p+1) + sum_{i>=p} C(e_i,i+2)
+//   = r - s1 + C(k,p+1) + s2, with s1/s2 the suffix sums of C(e_i,i+1) /
+// C(e_i,i+2) over the members above k, built while k runs downwards.
+// Branch-free: two binomial lookups per k and a predicated store.
 template <int N, int S, typename Tab>
-__device__ __forceinline__ void scatter_row(const Tab &tab, const double (&acc)[N], uint32_t Tm, const int *binom)
+__device__ __forceinline__ void scatter_row(const Tab &tab, const double (&acc)[N], uint32_t Tm, uint32_t r,
+                                            const int *binom)
 {
-    constexpr int ROWS_S = cbinom(N, S);
+    constexpr int T = S - 1;
+    constexpr uint32_t ROWS_S = cbinom(N, S);
     constexpr uint32_t DST = layer_off(N, S);
-    int high = 0;
-    {
-        int idx = 0;
+    int q = 0, s1 = 0, s2 = 0;
 #pragma unroll
-        for (int k = 0; k < N; ++k)
-            if (Tm & (1u << k)) {
-                high += binom[k * kBinomStride + idx + 2];
-                ++idx;
-            }
-    }
-    int low = 0, p = 0;
-#pragma unroll
-    for (int k = 0; k < N; ++k) {
-        if (Tm & (1u << k)) {
-            low += binom[k * kBinomStride + p + 1];
-            high -= binom[k * kBinomStride + p + 2];
-            ++p;
-        } else {
-            const int rank = low + binom[k * kBinomStride + p + 1] + high;
-            tab.store(DST + (uint32_t)(p * ROWS_S + rank), acc[k]);
-        }
+    for (int k = N - 1; k >= 0; --k) {
+        const int in = (Tm >> k) & 1u;
+        const int p = T - q - in;
+        const int c1 = binom[k * kBinomStride + p + 1];
+        const int c2 = binom[k * kBinomStride + p + 2];
+        const uint32_t rank = r - (uint32_t)s1 + (uint32_t)c1 + (uint32_t)s2;
+        tab.store_if(!in, DST + (uint32_t)p * ROWS_S + rank, acc[k]);
+        s1 += in ? c1 : 0;
+        s2 += in ? c2 : 0;
+        q += in;
     }
 }
 
@@ -208,7 +210,7 @@ __device__ __forceinline__ void layer_pass_global(const GlobalTable &tab, const 
             bits &= bits - 1u;
             relax_member<N>(acc, dl, m, slot[j * THREADS]);
         }
-        scatter_row<N, S>(tab, acc, Tm, binom);
+        scatter_row<N, S>(tab, acc, Tm, r, binom);
     }
 }
 
@@ -234,7 +236,7 @@ __device__ __forceinline__ void layer_pass_lds(const LdsTable &tab, const double
             bits &= bits - 1u;
             relax_member<N>(acc, dl, m, tab.load(SRC + j * ROWS + r));
         }
-        scatter_row<N, S>(tab, acc, Tm, binom);
+        scatter_row<N, S>(tab, acc, Tm, r, binom);
     }
 }
 
@@ -283,10 +285,18 @@ __global__ __launch_bounds__(THREADS, min_waves(N)) void heldkarp_kernel(const d
         tab = slots + (size_t)blockIdx.x * slot_doubles;
     using Tab = typename std::conditional<LDS_TABLE, LdsTable, GlobalTable>::type;
     Tab th;
-    if constexpr (LDS_TABLE)
+    if constexpr (LDS_TABLE) {
         th.p = tab;
-    else
-        th.rs = __builtin_amdgcn_make_buffer_rsrc(tab, 0, (int)(slot_doubles * 8), 0x00020000);
+    } else {
+        // descriptor inputs made provably wave-uniform (readfirstlane), else
+        // hipcc wraps every buffer op in a waterfall loop (guide T20)
+        const uint64_t base = reinterpret_cast<uint64_t>(tab);
+        const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)base);
+        const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(base >> 32));
+        const int bytes = __builtin_amdgcn_readfirstlane((int)(slot_doubles * 8));
+        th.rs = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void *>(((uint64_t)hi << 32) | lo), 0, bytes,
+                                                  0x00020000);
+    }
 
     for (int blk = blockIdx.x; blk < nblocks; blk += gridDim.x) {
         const double *dsrc = dist + (size_t)blk * n * n;

@@ -71,8 +71,8 @@ struct tspgpu_ctx {
     int32_t *d_tour = nullptr;
     size_t tour_bytes = 0;
     int last_grid = 0;
-    int threads = 256;   // workgroup size of the global-table kernels
-    int wg_per_cu = 4;   // resident slots per CU (auto grid); 4 x 256 threads measured best at n=14,16
+    int threads = 512;   // workgroup size of the global-table kernels (profiles/r01/*sweep*)
+    int wg_per_cu = 2;   // resident slots per CU (auto grid): 2 x 512 threads = 16 waves/CU
     hipEvent_t ev_start = nullptr, ev_stop = nullptr;
     char name[256] = {0};
     std::mutex mu;
@@ -291,7 +291,7 @@ int tspgpu_ctx_create(const tspgpu_opts *opts, tspgpu_ctx **out)
     }
     // tuning overrides for experiments (defaults are the measured best)
     if (const char *e = std::getenv("TSPGPU_THREADS")) c->threads = std::atoi(e);
-    if (const char *e = std::getenv("TSPGPU_WG_PER_CU")) c->wg_per_cu = std::atoi(e) > 0 ? std::atoi(e) : 4;
+    if (const char *e = std::getenv("TSPGPU_WG_PER_CU")) c->wg_per_cu = std::atoi(e) > 0 ? std::atoi(e) : 2;
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
         delete c;
         return -EIO;
