@@ -70,6 +70,69 @@ class Shard:
         return tspgpu.distance_matrix_array(self.arr, self.n, self.B)
 
 
+def shard_bounds(rank, world, per_rank):
+    """Contiguous shard of the global instance owned by `rank` (weak scaling)."""
+    return rank * per_rank, (rank + 1) * per_rank
+
+
+class Group:
+    """Barrier + max-over-ranks for the timed region (gloo; measurement only,
+    the data path has no collective)."""
+
+    def __init__(self, world):
+        self.dist = None
+        if world > 1:
+            import torch.distributed as dist
+
+            if not dist.is_initialized():
+                dist.init_process_group("gloo")
+            self.dist = dist
+
+    def barrier(self):
+        if self.dist is not None:
+            self.dist.barrier()
+
+    def allmax(self, x):
+        if self.dist is None:
+            return x
+        import torch
+
+        t = torch.tensor([x], dtype=torch.float64)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def allsum(self, x):
+        if self.dist is None:
+            return x
+        import torch
+
+        t = torch.tensor([x], dtype=torch.float64)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM)
+        return float(t.item())
+
+
+def timed_steps(step, sync, group, warmup, steps, begin=None, end=None):
+    """W untimed steps, then exactly K steps bracketed by barrier + device sync
+    on both sides; `begin`/`end` run right inside the timed region (the HIP
+    event pair).  Returns (max-over-ranks wall seconds, local wall seconds)."""
+    for _ in range(warmup):
+        step()
+    sync()
+    group.barrier()
+    sync()
+    t0 = time.perf_counter()
+    if begin:
+        begin()
+    for _ in range(steps):
+        step()
+    if end:
+        end()
+    sync()
+    group.barrier()
+    wall = time.perf_counter() - t0
+    return group.allmax(wall), wall
+
+
 def cpu_baseline(n, seconds_budget=20.0):
     """The reference's own tsp() (oracle/_ref, built from /root/reference at -O0)
     timed on this host: P parallel processes, one block each, like
@@ -165,6 +228,7 @@ def main():
     ap.add_argument("--blocks-per-gpu", type=int, default=16384)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pmc", action="store_true")
+    ap.add_argument("--no-tto", action="store_true", help="skip the one-block time-to-optimal probe")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
     if args.pmc_child:
@@ -173,47 +237,28 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-
-        dist.init_process_group("gloo")
-
-    def barrier():
-        if dist is not None:
-            dist.barrier()
-
-    def allmax(x):
-        if dist is None:
-            return x
-        import torch
-
-        t = torch.tensor([x], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        return float(t.item())
+    group = Group(world)
 
     n, Bp = args.n, args.blocks_per_gpu
     ctx = tspgpu.Context(device=local_rank, strict=False)
     cu, devname = ctx.device_info()
-    shard = Shard(n, Bp * world, rank * Bp, (rank + 1) * Bp)
+    lo, hi = shard_bounds(rank, world, Bp)
+    shard = Shard(n, Bp * world, lo, hi)
     d = shard.distances()
     dd, dc, dt = ctx.upload(d), ctx.alloc(Bp * 8), ctx.alloc(Bp * (n + 1) * 4)
     stream = ctx.stream
 
-    for _ in range(args.warmup):
+    ev = {}
+
+    def step():
         ctx.solve_device(dd, n, Bp, dc, dt, stream)
-    ctx.synchronize()
-    barrier()
-    ctx.synchronize()
-    t0 = time.perf_counter()
-    ctx.timer_start()
-    for _ in range(args.steps):
-        ctx.solve_device(dd, n, Bp, dc, dt, stream)
-    kernel_ms = ctx.timer_stop() / args.steps  # HIP events on the kernel's stream
-    ctx.synchronize()
-    barrier()
-    wall = time.perf_counter() - t0
-    wall_max = allmax(wall)
+
+    def stop_events():
+        ev["ms"] = ctx.timer_stop()  # HIP events on the kernel's stream
+
+    wall_max, _ = timed_steps(step, ctx.synchronize, group, args.warmup, args.steps, begin=ctx.timer_start,
+                              end=stop_events)
+    kernel_ms = ev["ms"] / args.steps
 
     # correctness of what was timed: every tour's left fold equals its cost
     cost = ctx.download(dc, (Bp,), np.float64)
@@ -229,17 +274,19 @@ def main():
     value = total_blocks * relax / wall_max
 
     # time-to-optimal: one block, host libm distances + copy + kernel + copy back
-    tto = []
-    one = [shard.block(0)]
-    for _ in range(10):
-        t = time.perf_counter()
-        ctx.solve_cities(one)
-        tto.append((time.perf_counter() - t) * 1e3)
-    d1, c1, t1 = ctx.upload(d[:1]), ctx.alloc(8), ctx.alloc((n + 1) * 4)
-    ctx.timer_start()
-    for _ in range(10):
-        ctx.solve_device(d1, n, 1, c1, t1, stream)
-    one_kernel_ms = ctx.timer_stop() / 10
+    tto, one_kernel_ms = [float("nan")], float("nan")
+    if not args.no_tto:
+        tto = []
+        one = [shard.block(0)]
+        for _ in range(10):
+            t = time.perf_counter()
+            ctx.solve_cities(one)
+            tto.append((time.perf_counter() - t) * 1e3)
+        d1, c1, t1 = ctx.upload(d[:1]), ctx.alloc(8), ctx.alloc((n + 1) * 4)
+        ctx.timer_start()
+        for _ in range(10):
+            ctx.solve_device(d1, n, 1, c1, t1, stream)
+        one_kernel_ms = ctx.timer_stop() / 10
 
     if rank != 0:
         return

@@ -35,7 +35,7 @@ for s in $STEPS; do
     prof)
         rm -rf $OUT/prof_$TAG
         run prof 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_$TAG -o run -- \
-            python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-pmc ;;
+            python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-pmc --no-tto ;;
     esac
 done
 exit 0

@@ -287,7 +287,10 @@ int tspgpu_ctx_create(const tspgpu_opts *opts, tspgpu_ctx **out)
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, dev) == hipSuccess) {
         if (prop.multiProcessorCount > 0) c->cu_count = prop.multiProcessorCount;
-        std::snprintf(c->name, sizeof c->name, "%s (%s)", prop.name, prop.gcnArchName);
+        char nm[128] = {0};
+        if (hipDeviceGetName(nm, sizeof nm, dev) != hipSuccess || !nm[0]) std::snprintf(nm, sizeof nm, "%s", prop.name);
+        std::snprintf(c->name, sizeof c->name, "%s (%s, %d CUs)", nm[0] ? nm : "AMD GPU", prop.gcnArchName,
+                      prop.multiProcessorCount);
     }
     // tuning overrides for experiments (defaults are the measured best)
     if (const char *e = std::getenv("TSPGPU_THREADS")) c->threads = std::atoi(e);
