@@ -16,21 +16,25 @@ import tspgpu  # noqa: E402
 from bench import Shard  # noqa: E402
 
 ns = [int(a) for a in sys.argv[1:]] or [16, 14, 12]
-configs = [(256, 2), (256, 3), (256, 4), (512, 1), (512, 2), (1024, 1)]
+# (K1 variant, threads, workgroups per CU); SWEEP="v,t,w;v,t,w" overrides
+configs = [(0, 512, 2), (1, 256, 4), (1, 256, 8), (1, 512, 2), (1, 512, 4), (1, 1024, 2)]
+if os.environ.get("SWEEP"):
+    configs = [tuple(int(x) for x in c.split(",")) for c in os.environ["SWEEP"].split(";")]
 for n in ns:
     B = {16: 8192, 15: 16384, 14: 16384, 13: 32768, 12: 65536}.get(n, 65536)
     shard = Shard(n, B, 0, B)
     d = shard.distances()
     rows = []
     ctxs = []
-    for th, wg in configs:
+    for v, th, wg in configs:
+        os.environ["TSPGPU_K1"] = str(v)
         os.environ["TSPGPU_THREADS"] = str(th)
         os.environ["TSPGPU_WG_PER_CU"] = str(wg)
         ctx = tspgpu.Context(device=0)
-        ctxs.append((th, wg, ctx, ctx.upload(d), ctx.alloc(B * 8), ctx.alloc(B * (n + 1) * 4)))
+        ctxs.append((v, th, wg, ctx, ctx.upload(d), ctx.alloc(B * 8), ctx.alloc(B * (n + 1) * 4)))
     ref = None
     for rep in range(2):
-        for th, wg, ctx, dd, dc, dt in ctxs:
+        for v, th, wg, ctx, dd, dc, dt in ctxs:
             ctx.solve_device(dd, n, B, dc, dt, ctx.stream)
             ctx.timer_start()
             for _ in range(3):
@@ -43,7 +47,7 @@ for n in ns:
             if rep == 1:
                 relax = tspgpu.relaxations_per_block(n) * B
                 tb = tspgpu.table_bytes_per_block(n) * B
-                print(f"n={n} B={B} threads={th} wg/cu={wg} grid={ctx.last_grid()} {ms:.3f} ms "
+                print(f"n={n} B={B} k1={v} threads={th} wg/cu={wg} grid={ctx.last_grid()} {ms:.3f} ms "
                       f"{B / ms * 1e3:.3e} blocks/s {relax / ms / 1e9:.3f} Trelax/s {tb / ms / 1e9:.0f} GB/s alg "
                       f"{'ok' if ok else 'MISMATCH'}", flush=True)
     for *_, ctx, dd, dc, dt in ctxs:

@@ -30,9 +30,9 @@ int threads_for(int N, bool lds_table, int requested)
     return 256;
 }
 
-size_t lds_bytes_for(int N, bool lds_table, int threads)
+size_t lds_bytes_for(int N, bool lds_table, int threads, bool compact)
 {
-    return N >= 2 && N <= kMaxN ? lds_bytes(N, lds_table, threads) : 0;
+    return N >= 2 && N <= kMaxN ? lds_bytes(N, lds_table, threads, compact) : 0;
 }
 
 hipError_t launch_heldkarp(const LaunchArgs &a, int grid)

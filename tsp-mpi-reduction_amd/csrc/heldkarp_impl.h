@@ -70,11 +70,29 @@ __host__ __device__ constexpr int mask_off(int N, int t)
 __host__ __device__ constexpr int dist_stride(int N) { return ((N + 2) & ~1) + 2; }
 __host__ __device__ constexpr size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
 __host__ __device__ constexpr size_t dl_bytes(int N) { return align16((size_t)(N + 1) * dist_stride(N) * 8); }
-// LDS: binomials | distance rows | table (LDS_TABLE) or per-thread row slots
-__host__ __device__ constexpr size_t lds_bytes(int N, bool lds_table, int threads)
+// only the digit groups N needs are staged in LDS
+__host__ __device__ constexpr int rank_lut_ints(int N)
 {
-    return kBinomBytesPadded + dl_bytes(N) +
-           (lds_table ? ((size_t)N << (N - 1)) * 8 : (size_t)(N - 1) * threads * 8);
+    return N <= 7 ? kRankR1 : (N <= 14 ? kRankR1 + kRankR2 : kRankLutInts);
+}
+__host__ __device__ constexpr int rank_lut_bytes(int N) { return (rank_lut_ints(N) * 4 + 15) & ~15; }
+// LDS: binomials | distance rows | rank LUT | table (LDS_TABLE) or per-thread
+// row slots (member-sweep global kernels only)
+__host__ __device__ constexpr size_t lds_bytes(int N, bool lds_table, int threads, bool compact)
+{
+    return kBinomBytesPadded + dl_bytes(N) + rank_lut_bytes(N) +
+           (lds_table ? ((size_t)N << (N - 1)) * 8 : (compact ? 0 : (size_t)(N - 1) * threads * 8));
+}
+
+// colex rank through the three-digit LUT (heldkarp.h)
+template <int N>
+__device__ __forceinline__ uint32_t lut_rank(uint32_t mask, const int *rl)
+{
+    const uint32_t lo = mask & 127u;
+    int r = rl[lo];
+    if constexpr (N > 7) r += rl[kRankR1 + ((mask >> 7) & 127u) * 8 + __builtin_popcount(lo)];
+    if constexpr (N > 14) r += rl[kRankR1 + kRankR2 + (mask >> 14) * 15 + __builtin_popcount(mask & 0x3fffu)];
+    return (uint32_t)r;
 }
 
 __device__ __forceinline__ int colex_rank(uint32_t mask, const int *binom)
@@ -121,6 +139,11 @@ struct GlobalTable {
         const int off = pred ? (int)(idx * 8u) : 0x7ffffff0;
         __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2, v), rs, off, 0, 0);
     }
+    __device__ __forceinline__ void store(uint32_t idx, double v) const
+    {
+        using u2 = decltype(__builtin_amdgcn_raw_buffer_load_b64(rs, 0, 0, 0));
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2, v), rs, (int)(idx * 8u), 0, 0);
+    }
 };
 struct LdsTable {
     double *p;
@@ -129,6 +152,7 @@ struct LdsTable {
     {
         if (pred) p[idx] = v;
     }
+    __device__ __forceinline__ void store(uint32_t idx, double v) const { p[idx] = v; }
 };
 
 // acc[k] = min(acc[k], g + d[m][k+1]) for all k: one member of the source row.
@@ -240,6 +264,73 @@ __device__ __forceinline__ void layer_pass_lds(const LdsTable &tab, const double
     }
 }
 
+// Compact pass, layer T -> T+1: a thread owns source rows r = tid, tid+THREADS,
+// ... and relaxes ONLY the Q = N-T destinations k not in T (every row of a
+// layer has exactly Q of them, so the loops have static trip counts):
+//   acc[q] = min_j g[j] + d[m_j][k_q]           (m_j: j-th member, k_q: q-th non-member)
+//   G[T+k_q][k_q] = acc[q]  at  DST + (k_q - q) * C(N,T+1) + colexrank(T + k_q)
+// (k_q - q = number of members below k_q = position of k_q in T+k_q).
+// t*(N-t) relaxations per row instead of t*N for the member sweep: no lane
+// computes a value that is thrown away.  Registers: t + 2(N-t) + O(1) per
+// thread, so the kernel runs at 8 waves/SIMD without spilling.
+template <int N, int T, int THREADS, typename Tab>
+__device__ __forceinline__ void layer_pass_compact(const Tab &tab, const double *__restrict__ dl,
+                                                   const int *__restrict__ rl, const uint32_t *__restrict__ masks,
+                                                   uint32_t tid)
+{
+    constexpr int S = T + 1;
+    constexpr int Q = N - T;
+    constexpr int DS = dist_stride(N);
+    constexpr uint32_t ROWS = cbinom(N, T);
+    constexpr uint32_t ROWS_S = cbinom(N, S);
+    constexpr uint32_t SRC = layer_off(N, T);
+    constexpr uint32_t DST = layer_off(N, S);
+    constexpr uint32_t FULL = (1u << N) - 1u;
+    const uint32_t *mt = masks + mask_off(N, T);
+    for (uint32_t r = tid; r < ROWS; r += THREADS) {
+        const uint32_t Tm = mt[r];
+        double g[T];
+#pragma unroll
+        for (int j = 0; j < T; ++j) g[j] = tab.load(SRC + j * ROWS + r);
+        uint32_t kb[Q];
+        uint32_t nb = ~Tm & FULL;
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+            kb[q] = __builtin_ctz(nb);
+            nb &= nb - 1u;
+        }
+        double acc[Q];
+#pragma unroll
+        for (int q = 0; q < Q; ++q) acc[q] = kIntMax;
+        uint32_t bits = Tm;
+#pragma unroll
+        for (int j = 0; j < T; ++j) {
+            const int m = __builtin_ctz(bits) + 1;
+            bits &= bits - 1u;
+            const double *drow = dl + m * DS;
+#pragma unroll
+            for (int q = 0; q < Q; ++q) acc[q] = fmin(acc[q], g[j] + drow[kb[q]]);
+        }
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+            const uint32_t k = kb[q];
+            const uint32_t rank = lut_rank<N>(Tm | (1u << k), rl);
+            tab.store(DST + (k - (uint32_t)q) * ROWS_S + rank, acc[q]);
+        }
+    }
+}
+
+template <int N, int T, int THREADS, typename Tab>
+__device__ __forceinline__ void all_layers_compact(const Tab &tab, const double *dl, const int *rl,
+                                                   const uint32_t *masks, uint32_t tid)
+{
+    if constexpr (T < N) {
+        layer_pass_compact<N, T, THREADS>(tab, dl, rl, masks, tid);
+        __syncthreads();
+        all_layers_compact<N, T + 1, THREADS>(tab, dl, rl, masks, tid);
+    }
+}
+
 template <int N, int T, int THREADS, typename Tab>
 __device__ __forceinline__ void all_layers(const Tab &tab, const double *dl, const int *binom, double *slot,
                                            const uint32_t *masks, uint32_t tid)
@@ -256,27 +347,31 @@ __device__ __forceinline__ void all_layers(const Tab &tab, const double *dl, con
 
 // One workgroup solves blocks blockIdx.x, blockIdx.x + gridDim.x, ...
 // LDS_TABLE: the whole compact table lives in LDS (N <= 11), else in the
-// workgroup's global slot.
-// Occupancy target: 4 waves per SIMD (16 per CU), i.e. <= 128 VGPRs, for the
-// reference's sizes; 2 waves per SIMD for the n > 16 extension kernels.
-__host__ __device__ constexpr int min_waves(int N) { return N <= 15 ? 4 : 2; }
-template <int N, bool LDS_TABLE, int THREADS>
-__global__ __launch_bounds__(THREADS, min_waves(N)) void heldkarp_kernel(const double *__restrict__ dist, int nblocks,
-                                                           double *__restrict__ slots, size_t slot_doubles,
-                                                           const uint32_t *__restrict__ masks,
-                                                           const LayerInfo *__restrict__ info,
-                                                           double *__restrict__ cost_out,
-                                                           int32_t *__restrict__ tour_out)
+// workgroup's global slot.  COMPACT selects the layer pass (see above).
+// Occupancy target (waves per SIMD): the member sweep holds N running minima
+// plus a prefetched row (<= 128 VGPRs, 4 waves); the compact pass needs about
+// half of that (<= 64 VGPRs, 8 waves) at the reference's sizes.
+__host__ __device__ constexpr int min_waves(int N, bool compact)
+{
+    return compact ? (N <= 15 ? 8 : 4) : (N <= 15 ? 4 : 2);
+}
+template <int N, bool LDS_TABLE, int THREADS, bool COMPACT>
+__global__ __launch_bounds__(THREADS, min_waves(N, COMPACT)) void heldkarp_kernel(
+    const double *__restrict__ dist, int nblocks, double *__restrict__ slots, size_t slot_doubles,
+    const uint32_t *__restrict__ masks, const LayerInfo *__restrict__ info, double *__restrict__ cost_out,
+    int32_t *__restrict__ tour_out)
 {
     constexpr int n = N + 1;
     constexpr int DS = dist_stride(N);
     extern __shared__ __attribute__((aligned(16))) char smem[];
     int *binom = reinterpret_cast<int *>(smem);
     double *dl = reinterpret_cast<double *>(smem + kBinomBytesPadded);
-    double *lds_rest = reinterpret_cast<double *>(smem + kBinomBytesPadded + dl_bytes(N));
+    int *rl = reinterpret_cast<int *>(smem + kBinomBytesPadded + dl_bytes(N));
+    double *lds_rest = reinterpret_cast<double *>(smem + kBinomBytesPadded + dl_bytes(N) + rank_lut_bytes(N));
     const int tid = threadIdx.x;
 
     for (int i = tid; i < kBinomRows * kBinomStride; i += THREADS) binom[i] = info->binom[i];
+    for (int i = tid; i < rank_lut_ints(N); i += THREADS) rl[i] = info->rlut[i];
 
     double *tab;
     if constexpr (LDS_TABLE)
@@ -315,16 +410,22 @@ __global__ __launch_bounds__(THREADS, min_waves(N)) void heldkarp_kernel(const d
         // costs ~200 VGPRs of 64-bit pointers).
         int tid_b = tid;
         asm volatile("" : "+v"(tid_b));
-        all_layers<N, 1, THREADS>(th, dl, binom, lds_rest + tid_b, masks, (uint32_t)tid_b);
+        if constexpr (COMPACT)
+            all_layers_compact<N, 1, THREADS>(th, dl, rl, masks, (uint32_t)tid_b);
+        else
+            all_layers<N, 1, THREADS>(th, dl, binom, lds_rest + tid_b, masks, (uint32_t)tid_b);
 
-        // closing min (tsp.cpp:483-499) and backtracking, one wave
+        // closing min (tsp.cpp:483-499) and backtracking, one wave: lane m-1
+        // holds candidate m.  The state value of the next step is the g value
+        // the picked lane loaded, so each step costs one dependent load.
         if (tid < 64) {
             const int lane = tid;
             const int m = lane + 1;
             const uint32_t full = (1u << N) - 1u;
             const double *last = tab + layer_off(N, N);  // one row: position m-1 at m-1
             const bool valid = m <= N;
-            const double cand = valid ? last[m - 1] + dget<N>(dl, m, 0) : 1.0e300;
+            const double glast = valid ? last[m - 1] : 0.0;
+            const double cand = valid ? glast + dget<N>(dl, m, 0) : 1.0e300;
             const double best = fmin(wave_min(cand), kIntMax);
             const unsigned long long hit = __ballot(valid && cand == best && cand < kIntMax);
             const int bestM = hit ? __ffsll(hit) : 0;
@@ -333,23 +434,22 @@ __global__ __launch_bounds__(THREADS, min_waves(N)) void heldkarp_kernel(const d
             int k = bestM;
             int pos = n - 2;
             bool ok = bestM != 0;
+            double target = __shfl(glast, ok ? bestM - 1 : 0);
             while (ok && __builtin_popcount(S) >= 2) {
                 const uint32_t T = S & ~(1u << (k - 1));
                 const int tt = __builtin_popcount(T);
-                const int ss = tt + 1;
-                const int rS = colex_rank(S, binom);
-                const int rT = colex_rank(T, binom);
-                const double target = tab[info->off[ss] +
-                                          __builtin_popcount(S & ((1u << (k - 1)) - 1u)) * info->count[ss] + rS];
+                const uint32_t rT = lut_rank<N>(T, rl);
                 const bool inT = valid && ((T >> (m - 1)) & 1u);
-                double c = 0.0;
-                if (inT)
-                    c = tab[info->off[tt] + __builtin_popcount(T & ((1u << (m - 1)) - 1u)) * info->count[tt] + rT] +
-                        dget<N>(dl, m, k);
+                double gv = 0.0, c = 0.0;
+                if (inT) {
+                    gv = tab[info->off[tt] + __builtin_popcount(T & ((1u << (m - 1)) - 1u)) * info->count[tt] + rT];
+                    c = gv + dget<N>(dl, m, k);
+                }
                 const unsigned long long bb = __ballot(inT && c == target);
                 const int pick = bb ? __ffsll(bb) : 0;
                 ok = pick != 0;
                 if (lane == 0) tour[pos] = pick;
+                target = __shfl(gv, ok ? pick - 1 : 0);
                 --pos;
                 S = T;
                 k = pick;
@@ -365,20 +465,21 @@ __global__ __launch_bounds__(THREADS, min_waves(N)) void heldkarp_kernel(const d
     }
 }
 
-template <int N, bool LDS, int THREADS>
+template <int N, bool LDS, int THREADS, bool COMPACT>
 hipError_t launch_n(const LaunchArgs &a, int grid)
 {
-    const size_t lds = lds_bytes(N, LDS, THREADS);
+    const size_t lds = lds_bytes(N, LDS, THREADS, COMPACT);
     if (lds > 64 * 1024) {
         static bool raised = false;  // once per instantiation
         if (!raised) {
-            hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&heldkarp_kernel<N, LDS, THREADS>),
-                                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+            hipError_t e = hipFuncSetAttribute(
+                reinterpret_cast<const void *>(&heldkarp_kernel<N, LDS, THREADS, COMPACT>),
+                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
             if (e != hipSuccess) return e;
             raised = true;
         }
     }
-    hipLaunchKernelGGL((heldkarp_kernel<N, LDS, THREADS>), dim3(grid), dim3(THREADS), lds, a.stream, a.dist,
+    hipLaunchKernelGGL((heldkarp_kernel<N, LDS, THREADS, COMPACT>), dim3(grid), dim3(THREADS), lds, a.stream, a.dist,
                        a.nblocks, a.slots, a.slot_doubles, a.masks, a.info, a.cost, a.tour);
     return hipGetLastError();
 }
@@ -387,17 +488,23 @@ hipError_t launch_n(const LaunchArgs &a, int grid)
 // admits one workgroup per CU, so it gets 1024 threads (4 waves per SIMD).
 __host__ __device__ constexpr int lds_table_threads(int N) { return N >= 11 ? 1024 : 256; }
 
+template <int N, bool COMPACT>
+hipError_t launch_threads_v(const LaunchArgs &a, int grid)
+{
+    if constexpr (N <= kLdsTableMaxN) {
+        if (a.use_lds) return launch_n<N, true, lds_table_threads(N), COMPACT>(a, grid);
+    }
+    if constexpr (N >= 12 && N <= 15) {
+        if (a.threads == 512) return launch_n<N, false, 512, COMPACT>(a, grid);
+        if (a.threads == 1024) return launch_n<N, false, 1024, COMPACT>(a, grid);
+    }
+    return launch_n<N, false, 256, COMPACT>(a, grid);
+}
+
 template <int N>
 hipError_t launch_threads(const LaunchArgs &a, int grid)
 {
-    if constexpr (N <= kLdsTableMaxN) {
-        if (a.use_lds) return launch_n<N, true, lds_table_threads(N)>(a, grid);
-    }
-    if constexpr (N >= 12 && N <= 15) {
-        if (a.threads == 512) return launch_n<N, false, 512>(a, grid);
-        if (a.threads == 1024) return launch_n<N, false, 1024>(a, grid);
-    }
-    return launch_n<N, false, 256>(a, grid);
+    return a.variant == 1 ? launch_threads_v<N, true>(a, grid) : launch_threads_v<N, false>(a, grid);
 }
 
 }  // namespace tspgpu

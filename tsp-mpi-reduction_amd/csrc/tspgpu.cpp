@@ -38,6 +38,28 @@ void host_layer_info(int N, LayerInfo *info)
     std::memset(info, 0, sizeof(*info));
     for (int a = 0; a < kBinomRows; ++a)
         for (int b = 0; b < kBinomCols; ++b) info->binom[a * kBinomCols + b] = binom_host(a, b);
+    // colex rank = sum over members e_i (ascending) of C(e_i, i+1), split in
+    // three 7-bit digit groups whose contribution depends on the member count below
+    for (int lo = 0; lo < 128; ++lo) {
+        int r = 0, i = 0;
+        for (int b = 0; b < 7; ++b)
+            if (lo >> b & 1) r += binom_host(b, ++i);
+        info->rlut[lo] = r;
+    }
+    for (int mid = 0; mid < 128; ++mid)
+        for (int c = 0; c < 8; ++c) {
+            int r = 0, i = c;
+            for (int b = 0; b < 7; ++b)
+                if (mid >> b & 1) r += binom_host(b + 7, ++i);
+            info->rlut[kRankR1 + mid * 8 + c] = r;
+        }
+    for (int hi = 0; hi < 64; ++hi)
+        for (int c = 0; c < 15; ++c) {
+            int r = 0, i = c;
+            for (int b = 0; b < 6; ++b)
+                if (hi >> b & 1) r += binom_host(b + 14, ++i);
+            info->rlut[kRankR1 + kRankR2 + hi * 15 + c] = r;
+        }
     int off = 0, moff = 0;
     for (int t = 0; t <= N + 1 && t < 24; ++t) {
         info->count[t] = binom_host(N, t);
@@ -71,8 +93,10 @@ struct tspgpu_ctx {
     int32_t *d_tour = nullptr;
     size_t tour_bytes = 0;
     int last_grid = 0;
-    int threads = 512;   // workgroup size of the global-table kernels (profiles/r01/*sweep*)
-    int wg_per_cu = 2;   // resident slots per CU (auto grid): 2 x 512 threads = 16 waves/CU
+    int threads = 0;     // workgroup size of the global-table kernels; 0 = per-N default
+    int wg_per_cu = 0;   // resident slots per CU (auto grid); 0 = per-N default
+    int lds_table_max_n = kLdsTableDefaultMaxN;  // largest N whose whole table stays in LDS
+    int variant = 1;     // K1 layer pass: 1 = compact (non-member destinations only), 0 = member sweep
     hipEvent_t ev_start = nullptr, ev_stop = nullptr;
     char name[256] = {0};
     std::mutex mu;
@@ -159,16 +183,22 @@ int solve_device_locked(tspgpu_ctx *c, const double *d_dist, int n, int nblocks,
         if (rc) return rc;
         a.masks = c->d_masks[N];
         a.info = c->d_info[N];
-        a.use_lds = N <= kLdsTableMaxN;
-        a.threads = c->threads;
+        a.use_lds = N <= c->lds_table_max_n;
+        // per-N defaults measured on MI355X (profiles/r01/sweep_*.log): small
+        // tables want many blocks in flight, n = 13..16 two 512-thread slots per CU
+        const int def_threads = N <= 11 ? 256 : (N <= 15 ? 512 : 256);
+        const int def_wg = N <= 11 ? 8 : 2;
+        a.threads = c->threads > 0 ? c->threads : def_threads;
+        a.variant = c->variant;
         if (a.use_lds) {
             // as many resident workgroups as the LDS allows, then persistent
-            const int per_cu = (int)(160 * 1024 / lds_bytes_for(N, true, threads_for(N, true, 0)));
+            const int per_cu = (int)(160 * 1024 / lds_bytes_for(N, true, threads_for(N, true, 0), c->variant == 1));
             const int cap = c->cu_count * (per_cu > 0 ? per_cu : 1);
             grid = nblocks < cap ? nblocks : cap;
         } else {
             // extension sizes (N >= 16) run at 2 waves/SIMD: two workgroups per CU
-            const int per_cu = N >= 16 ? (c->wg_per_cu < 2 ? c->wg_per_cu : 2) : c->wg_per_cu;
+            const int wg = c->wg_per_cu > 0 ? c->wg_per_cu : def_wg;
+            const int per_cu = N >= 16 ? (wg < 2 ? wg : 2) : wg;
             int slots = c->slots_opt > 0 ? c->slots_opt : c->cu_count * per_cu;
             // keep the workspace under ~8 GiB for the largest extension sizes
             const size_t per = table_doubles(N) * sizeof(double);
@@ -294,7 +324,12 @@ int tspgpu_ctx_create(const tspgpu_opts *opts, tspgpu_ctx **out)
     }
     // tuning overrides for experiments (defaults are the measured best)
     if (const char *e = std::getenv("TSPGPU_THREADS")) c->threads = std::atoi(e);
-    if (const char *e = std::getenv("TSPGPU_WG_PER_CU")) c->wg_per_cu = std::atoi(e) > 0 ? std::atoi(e) : 2;
+    if (const char *e = std::getenv("TSPGPU_LDS_TABLE_MAX_N")) {
+        const int v = std::atoi(e);
+        c->lds_table_max_n = v < kLdsTableMaxN ? v : kLdsTableMaxN;
+    }
+    if (const char *e = std::getenv("TSPGPU_K1")) c->variant = std::atoi(e) == 0 ? 0 : 1;
+    if (const char *e = std::getenv("TSPGPU_WG_PER_CU")) c->wg_per_cu = std::atoi(e) > 0 ? std::atoi(e) : 0;
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
         delete c;
         return -EIO;
