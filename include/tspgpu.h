@@ -117,6 +117,92 @@ double tspgpu_relaxations_per_block(int n);
  * once, 2 * 8 * N * 2^(N-1). */
 double tspgpu_table_bytes_per_block(int n);
 
+/* ---------------------------------------------------------------------------
+ * K2: exact search of ONE instance, prefix-parallel branch and bound over the
+ * whole GPU (one instance per call instead of one block per workgroup), the
+ * north_star's search shape for the reference's per-block problem
+ * (tsp.cpp:405-509).  Same answer as tsp()/K1: the optimal left-fold cost and
+ * the DP's tie-broken tour (see tspgpu_select_tour), for n <= 32 cities.
+ * Distances: f64 (the reference's computeDistanceMatrix output) or i32 (the
+ * integer-matrix extension: d >= 0, n * max(d) < 2^30).
+ * ------------------------------------------------------------------------- */
+#define TSPGPU_SEARCH_MAX_CITIES 32
+#define TSPGPU_F64 0
+#define TSPGPU_I32 1
+
+/* One recorded complete tour: cost (IEEE bits of the f64 cost, or the
+ * integer cost) and the inner cities t1..tN (N = n-1) in visiting order. */
+typedef struct
+{
+    uint64_t cost;
+    uint8_t city[32];
+} tspgpu_tour_record;
+
+typedef struct
+{
+    uint64_t nodes;         /* search nodes: child extensions cost + d[last][next] with their bound test */
+    uint64_t records;       /* complete tours recorded at cost <= incumbent (last phase) */
+    uint64_t optimal_tours; /* |O|: tours whose cost equals the optimum */
+    uint64_t items;         /* prefixes (work items) N!/(N-D)! */
+    int depth;              /* prefix depth D */
+    int phases;             /* 1, or 2 when the record buffer overflowed (second search, bound = optimum) */
+    int fallback;           /* 1: |O| too large to enumerate, the answer came from K1 (n <= 20) */
+    int rounds;             /* search rounds of the last phase (items split and re-queued between rounds) */
+    double kernel_ms;       /* device time of the search launches */
+} tspgpu_search_stats;
+
+typedef struct tspgpu_search tspgpu_search; /* one instance (or one shard of it) on one context */
+
+/* One-shot: whole instance on the context's GPU.  cost_out: the optimal cost
+ * (an integer value for TSPGPU_I32); tour_out: n+1 entries 0,t1..tN,0.
+ * When more tours tie for the optimum than can be enumerated (coincident
+ * cities), n <= 20 is answered by K1 (stats->fallback = 1), larger n return
+ * -EOVERFLOW. */
+int tspgpu_search_solve(tspgpu_ctx *ctx, const void *dist, int dtype, int n, double *cost_out,
+                        int32_t *tour_out, tspgpu_search_stats *stats);
+
+/* Sharded form for multi-GPU drivers (one process or thread per GPU): shard s
+ * of S seeds the depth-D prefixes p with p mod S == s (static interleave).
+ * Inside the GPU the work runs in rounds: lanes take items from a device
+ * queue, and an item that exceeds its iteration budget is split into the
+ * untried siblings of each level of its stack, re-queued for the next round.
+ * A driver calls start, then step until pending == 0, exchanging the
+ * incumbent word between steps (e.g. RCCL all-reduce MIN of the u64 read with
+ * tspgpu_search_counters, written back with tspgpu_search_set_bound); at the
+ * end it all-reduces the incumbent, gathers the records whose cost equals it
+ * from every shard and calls tspgpu_select_tour.  depth 0 = automatic. */
+int tspgpu_search_create(tspgpu_ctx *ctx, const void *dist, int dtype, int n, int shard, int nshards, int depth,
+                         tspgpu_search **out);
+int tspgpu_search_destroy(tspgpu_search *s);
+int tspgpu_search_info(const tspgpu_search *s, int *depth, uint64_t *items, uint64_t *local_items);
+/* initial incumbent (a real tour's cost, e.g. tspgpu_heuristic_tour) */
+int tspgpu_search_set_bound(tspgpu_search *s, double bound);
+/* seed this shard's live prefixes (synchronous) */
+int tspgpu_search_start(tspgpu_search *s);
+/* one round over the pending items (synchronous); *pending = items left for the next round */
+int tspgpu_search_step(tspgpu_search *s, uint64_t *pending);
+/* start + steps until nothing is pending */
+int tspgpu_search_run_all(tspgpu_search *s);
+/* device time of all seed/round launches so far, and the rounds run */
+int tspgpu_search_timing(const tspgpu_search *s, double *kernel_ms, int *rounds);
+/* device address of the 64-bit incumbent word (f64 bits or integer cost) */
+void *tspgpu_search_incumbent_device(tspgpu_search *s);
+int tspgpu_search_counters(tspgpu_search *s, uint64_t *incumbent_bits, uint64_t *nodes, uint64_t *records);
+/* forget the records (and grow the buffer to `capacity` if larger) */
+int tspgpu_search_reset_records(tspgpu_search *s, unsigned int capacity);
+/* the recorded tours whose cost bits equal cost_bits; -EOVERFLOW if records
+ * were lost (rerun with the optimum as the bound), -ENOSPC if cap is short */
+int tspgpu_search_records(tspgpu_search *s, uint64_t cost_bits, tspgpu_tour_record *out, int cap, int *count);
+
+/* Host helpers.  A nearest-neighbour + 2-opt tour and its left-fold cost (an
+ * upper bound); and the DP's tie rule applied to the optimal set O: walking
+ * from the last city backwards, take the smallest m that ends a tour of O with
+ * the chosen suffix and whose best prefix fold + d[m][next] equals the state
+ * value (tsp.cpp:457-470, 483-499) — the tour tsp() returns. */
+int tspgpu_heuristic_tour(const void *dist, int dtype, int n, double *cost_out, int32_t *tour_out);
+int tspgpu_select_tour(const void *dist, int dtype, int n, const tspgpu_tour_record *records, int count,
+                       uint64_t cost_bits, int32_t *tour_out);
+
 #ifdef __cplusplus
 }
 #endif

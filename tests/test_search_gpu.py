@@ -1,0 +1,184 @@
+"""K2 (prefix-parallel exact search of one instance, csrc/search.hip) on the
+GPU through the C ABI: the same cost bits and the same tour as the reference's
+tsp() (goldens) and the pinned oracle, f64 and the integer-matrix extension,
+one GPU and sharded.
+
+Run on an MI355X:  python -m pytest tests -m gpu
+"""
+import numpy as np
+import pytest
+
+import oracle_py as O
+import search_dist
+import tspgpu
+
+pytestmark = pytest.mark.gpu
+
+
+def _cities(case_cities):
+    return [(c[0], O.hexf(c[1]), O.hexf(c[2])) for c in case_cities]
+
+
+def test_seed0_fixtures(gpu_ctx):
+    """The reference's own instances (./tsp n B 1000 1000, n = 3..16): golden cost and tour."""
+    for case in O.load_golden("seed0_blocks.json"):
+        if case["n"] < 3:
+            continue
+        for blk, sol in zip(case["cities"], case["solutions"]):
+            cities = _cities(blk)
+            d = tspgpu.distance_matrix([cities])[0]
+            cost, tour, st = tspgpu.search_solve(gpu_ctx, d)
+            assert cost == O.hexf(sol["cost_hex"]), (case["n"], st)
+            assert [cities[t][0] for t in tour] == sol["ids"], (case["n"], st)
+
+
+@pytest.mark.parametrize("name", ["tie_blocks.json", "random_blocks.json"])
+def test_file_fixtures(gpu_ctx, name):
+    """Tie-heavy (collinear, lattice, coincident cities) and random goldens."""
+    for inst in O.load_golden(name):
+        cities = _cities(inst["cities"])
+        if len(cities) < 3:
+            continue
+        d = tspgpu.distance_matrix([cities])[0]
+        cost, tour, st = tspgpu.search_solve(gpu_ctx, d)
+        assert cost == O.hexf(inst["solution"]["cost_hex"]), (name, len(cities), st)
+        assert [cities[t][0] for t in tour] == inst["solution"]["ids"], (name, len(cities), st)
+
+
+@pytest.mark.parametrize("n", [3, 4, 5, 7, 9, 11, 13, 15, 16, 17, 18])
+def test_f64_against_oracle(gpu_ctx, n):
+    rng = np.random.default_rng(4000 + n)
+    for k in range(6 if n <= 14 else 2):
+        if k % 3 == 1:
+            xy = rng.integers(0, 4, size=(n, 2)).astype(np.float64)  # lattice ties
+        else:
+            xy = rng.uniform(0, 1000, size=(n, 2))
+        d = O.distance_matrix([(i, xy[i, 0], xy[i, 1]) for i in range(n)])
+        cost, tour, st = tspgpu.search_solve(gpu_ctx, d)
+        oc, ot = O.solve_block(d)
+        assert cost == oc, (n, k, st)
+        assert tour.tolist() == ot, (n, k, st)
+
+
+@pytest.mark.parametrize("n", [4, 8, 12, 14, 16])
+def test_i32_against_oracle(gpu_ctx, n):
+    """Integer-matrix extension (configs 1 and 4): symmetric and asymmetric."""
+    rng = np.random.default_rng(7000 + n)
+    for k in range(6 if n <= 12 else 2):
+        hi = 1000 if k % 2 == 0 else 8
+        m = rng.integers(1, hi, size=(n, n)).astype(np.int32)
+        if k % 3 != 2:
+            m = np.minimum(m, m.T)
+        np.fill_diagonal(m, 0)
+        cost, tour, st = tspgpu.search_solve(gpu_ctx, m)
+        oc, ot = O.solve_block(m.astype(np.float64))
+        assert cost == int(oc), (n, k, st)
+        assert tour.tolist() == ot, (n, k, st)
+
+
+def test_clustered_16(gpu_ctx):
+    """Config-4 stand-in: 4 Gaussian clusters (pruning imbalance across prefixes)."""
+    rng = np.random.default_rng(44)
+    for seed in range(3):
+        centers = rng.uniform(100, 900, size=(4, 2))
+        xy = np.concatenate([centers[i] + rng.normal(0, 50, size=(4, 2)) for i in range(4)])
+        d = O.distance_matrix([(i, xy[i, 0], xy[i, 1]) for i in range(16)])
+        cost, tour, st = tspgpu.search_solve(gpu_ctx, d)
+        oc, ot = O.solve_block(d)
+        assert (cost, tour.tolist()) == (oc, ot), st
+
+
+def test_k2_matches_k1(gpu_ctx):
+    """Both GPU paths, same inputs: identical bits and tours (n = 12..16)."""
+    rng = np.random.default_rng(99)
+    for n in (12, 14, 16):
+        xy = rng.uniform(0, 1000, size=(4, n, 2))
+        blocks = [[(b * n + i, xy[b, i, 0], xy[b, i, 1]) for i in range(n)] for b in range(4)]
+        d = tspgpu.distance_matrix(blocks)
+        c1, t1 = gpu_ctx.solve_blocks(d)
+        for b in range(4):
+            c2, t2, _ = tspgpu.search_solve(gpu_ctx, d[b])
+            assert c2 == c1[b] and t2.tolist() == t1[b].tolist()
+
+
+@pytest.mark.parametrize("budget", ["1", "64"])
+def test_tiny_budget_splits_everything(gpu_ctx, monkeypatch, budget):
+    """Budgets of 1 and 64 iterations: nearly every item is cut and re-queued
+    many times; the answer must not change."""
+    monkeypatch.setenv("TSPGPU_SEARCH_BUDGET", budget)
+    rng = np.random.default_rng(int(budget))
+    for n in (9, 12):
+        xy = rng.uniform(0, 1000, size=(n, 2))
+        d = O.distance_matrix([(i, xy[i, 0], xy[i, 1]) for i in range(n)])
+        cost, tour, st = tspgpu.search_solve(gpu_ctx, d)
+        oc, ot = O.solve_block(d)
+        assert (cost, tour.tolist()) == (oc, ot), st
+        if n == 12 and budget == "1":
+            assert st["rounds"] > 2, st
+
+
+@pytest.mark.parametrize("nshards", [2, 3, 5])
+def test_sharded_on_one_gpu(gpu_ctx, nshards):
+    """The multi-GPU decomposition, run shard by shard on one device: min of
+    the shards' incumbents + union of their optimal records -> same answer."""
+    rng = np.random.default_rng(nshards)
+    n = 13
+    xy = rng.integers(0, 5, size=(n, 2)).astype(np.float64)
+    d = O.distance_matrix([(i, xy[i, 0], xy[i, 1]) for i in range(n)])
+    shards = [tspgpu.Search(gpu_ctx, d, shard=s, nshards=nshards) for s in range(nshards)]
+    ub, _ = tspgpu.heuristic_tour(d)
+    for S in shards:
+        S.set_bound(ub)
+        S.run_all()
+    opt = min(S.counters()[0] for S in shards)
+    recs = [r for S in shards for r in S.records(opt)]
+    cost = tspgpu.bits_cost(opt, tspgpu.F64)
+    tour = tspgpu.select_tour(d, recs, cost)
+    oc, ot = O.solve_block(d)
+    assert cost == oc and tour.tolist() == ot
+    for S in shards:
+        S.close()
+
+
+def test_solve_sharded_single_process(gpu_ctx):
+    """search_dist's round driver with one rank (exchange is a no-op)."""
+    rng = np.random.default_rng(5)
+    xy = rng.uniform(0, 1000, size=(15, 2))
+    d = O.distance_matrix([(i, xy[i, 0], xy[i, 1]) for i in range(15)])
+    cost, tour, st = search_dist.solve_sharded(gpu_ctx, d)
+    oc, ot = O.solve_block(d)
+    assert cost == oc and tour.tolist() == ot, st
+    assert st["exchanges"] == st["rounds"] >= 1
+
+
+def test_overflow_falls_back_to_second_phase(gpu_ctx):
+    """All-equal distances: every tour is optimal.  7! = 5040 fit the record
+    buffer; 9! = 362880 at n = 10 do not, so the search runs a second phase
+    with the optimum as the bound and a buffer of the needed size."""
+    d = np.full((8, 8), 7, dtype=np.int32)
+    np.fill_diagonal(d, 0)
+    cost, tour, st = tspgpu.search_solve(gpu_ctx, d)  # 7! = 5040 optimal tours: fits
+    oc, ot = O.solve_block(d.astype(np.float64))
+    assert cost == int(oc) and tour.tolist() == ot and st["optimal_tours"] == 5040
+    d = np.full((10, 10), 7, dtype=np.int32)
+    np.fill_diagonal(d, 0)
+    cost, tour, st = tspgpu.search_solve(gpu_ctx, d)
+    oc, ot = O.solve_block(d.astype(np.float64))
+    assert cost == int(oc) and tour.tolist() == ot and st["phases"] == 2 and st["optimal_tours"] == 362880
+
+
+def test_forced_second_phase_and_k1_fallback(gpu_ctx, monkeypatch):
+    """A tiny record buffer forces the second phase on an ordinary lattice
+    instance; coincident cities (12! optimal tours) fall back to K1."""
+    rng = np.random.default_rng(11)
+    xy = rng.integers(0, 3, size=(11, 2)).astype(np.float64)
+    d = O.distance_matrix([(i, xy[i, 0], xy[i, 1]) for i in range(11)])
+    monkeypatch.setenv("TSPGPU_SEARCH_RECORD_CAP", "2")
+    cost, tour, st = tspgpu.search_solve(gpu_ctx, d)
+    monkeypatch.delenv("TSPGPU_SEARCH_RECORD_CAP")
+    oc, ot = O.solve_block(d)
+    assert (cost, tour.tolist()) == (oc, ot) and st["phases"] == 2, st
+    d = np.zeros((13, 13))
+    cost, tour, st = tspgpu.search_solve(gpu_ctx, d)
+    oc, ot = O.solve_block(d)
+    assert (cost, tour.tolist()) == (oc, ot) and st["fallback"] == 1, st

@@ -1,0 +1,124 @@
+"""K2 host logic, no GPU: the DP tie rule applied to the optimal set O
+(tspgpu_select_tour) against the pinned CPU oracle, with O enumerated by brute
+force; and the 2-opt upper bound.  Exercised through libtspgpu's C ABI (host
+functions only; nothing here launches a kernel).
+"""
+import itertools
+
+import numpy as np
+import pytest
+
+import oracle_py as O
+import tspgpu
+
+
+def left_fold(d, t):
+    """tsp.cpp's cost of the closed tour 0, t1..tN, 0 (IEEE double / int)."""
+    c = d.dtype.type(0)
+    prev = 0
+    for x in t:
+        c = c + d[prev, x]
+        prev = x
+    return c + d[prev, 0]
+
+
+def optimal_set(d):
+    """All tours whose left fold equals the optimum (brute force)."""
+    n = d.shape[0]
+    costs = {}
+    for p in itertools.permutations(range(1, n)):
+        costs[p] = left_fold(d, p)
+    opt = min(costs.values())
+    return opt, [p for p, c in costs.items() if c == opt]
+
+
+def records(opt_set, cost, dtype):
+    out = []
+    for p in opt_set:
+        r = tspgpu.TourRecord()
+        r.cost = tspgpu.cost_bits(cost, dtype)
+        for i, x in enumerate(p):
+            r.city[i] = x
+        out.append(r)
+    return out
+
+
+def instances(rng, n, count):
+    for k in range(count):
+        kind = k % 4
+        if kind == 0:
+            xy = rng.uniform(0, 1000, size=(n, 2))
+        elif kind == 1:
+            xy = rng.integers(0, 3, size=(n, 2)).astype(np.float64)  # lattice: heavy ties
+        elif kind == 2:
+            xy = np.stack([rng.integers(0, 6, size=n), np.zeros(n)], 1).astype(np.float64)  # collinear
+        else:
+            xy = rng.integers(0, 1000, size=(n, 2)).astype(np.float64)
+        cities = [(i, xy[i, 0], xy[i, 1]) for i in range(n)]
+        yield O.distance_matrix(cities)
+
+
+@pytest.mark.parametrize("n", [3, 4, 5, 6, 7, 8])
+def test_select_tour_f64_matches_dp(n):
+    rng = np.random.default_rng(500 + n)
+    for d in instances(rng, n, 24 if n <= 7 else 8):
+        opt, oset = optimal_set(d)
+        oc, ot = O.solve_block(d)
+        assert opt == oc
+        tour = tspgpu.select_tour(d, records(oset, opt, tspgpu.F64), opt)
+        assert tour.tolist() == ot, (n, len(oset))
+
+
+@pytest.mark.parametrize("n", [4, 6, 8])
+def test_select_tour_i32_matches_dp(n):
+    """Integer-matrix extension: symmetric and asymmetric small integers (many
+    ties); the oracle runs on the same values as doubles (exact)."""
+    rng = np.random.default_rng(900 + n)
+    for k in range(16 if n < 8 else 6):
+        m = rng.integers(1, 6, size=(n, n)).astype(np.int32)
+        if k % 2 == 0:
+            m = np.minimum(m, m.T)
+        np.fill_diagonal(m, 0)
+        opt, oset = optimal_set(m)
+        oc, ot = O.solve_block(m.astype(np.float64))
+        assert float(opt) == oc
+        tour = tspgpu.select_tour(m, records(oset, int(opt), tspgpu.I32), int(opt))
+        assert tour.tolist() == ot, (n, k, len(oset))
+
+
+def test_select_tour_ignores_non_optimal_and_needs_optimal():
+    rng = np.random.default_rng(3)
+    d = next(instances(rng, 6, 1))
+    opt, oset = optimal_set(d)
+    worse = [p for p in itertools.permutations(range(1, 6)) if left_fold(d, p) > opt][:5]
+    recs = records(oset, opt, tspgpu.F64) + records(worse, opt, tspgpu.F64)  # wrong-cost stragglers
+    assert tspgpu.select_tour(d, recs, opt).tolist() == O.solve_block(d)[1]
+    with pytest.raises(tspgpu.TspGpuError):
+        tspgpu.select_tour(d, records(worse, opt, tspgpu.F64), opt)
+
+
+@pytest.mark.parametrize("n", [5, 9, 16, 24, 32])
+def test_heuristic_is_an_upper_bound(n):
+    rng = np.random.default_rng(n)
+    xy = rng.uniform(0, 1000, size=(n, 2))
+    d = O.distance_matrix([(i, xy[i, 0], xy[i, 1]) for i in range(n)])
+    cost, tour = tspgpu.heuristic_tour(d)
+    assert tour[0] == 0 and tour[-1] == 0 and sorted(tour[1:-1].tolist()) == list(range(1, n))
+    assert cost == left_fold(d, tour[1:-1])
+    if n <= 16:
+        assert cost >= O.solve_block(d)[0]
+
+
+def test_search_validation():
+    """Host-side argument checks of the K2 entry points (no device needed)."""
+    with pytest.raises(tspgpu.TspGpuError):
+        tspgpu.heuristic_tour(np.zeros((2, 2)))          # n < 3
+    with pytest.raises(tspgpu.TspGpuError):
+        tspgpu.heuristic_tour(np.zeros((33, 33)))        # n > 32
+    bad = np.ones((5, 5))
+    bad[1, 2] = -1.0
+    with pytest.raises(tspgpu.TspGpuError):
+        tspgpu.heuristic_tour(bad)
+    big = np.full((5, 5), 1 << 28, dtype=np.int32)
+    with pytest.raises(tspgpu.TspGpuError):
+        tspgpu.heuristic_tour(big)                       # n * max(d) >= 2^30

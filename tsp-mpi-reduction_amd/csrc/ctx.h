@@ -1,0 +1,36 @@
+// Internal definition of the opaque tspgpu_ctx (include/tspgpu.h): one HIP
+// device, one stream, the K1 tables/workspaces and the K2 search state cache.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <mutex>
+
+#include "heldkarp.h"
+#include "tspgpu.h"
+
+struct tspgpu_ctx {
+    // (members are used by tspgpu.cpp for K1 and search_abi.cpp for K2)
+    int device = 0;
+    int strict = 0;
+    int slots_opt = 0;
+    int cu_count = 256;
+    hipStream_t stream = nullptr;
+    uint32_t *d_masks[tspgpu::kMaxN + 1] = {};
+    tspgpu::LayerInfo *d_info[tspgpu::kMaxN + 1] = {};
+    double *d_slots = nullptr;
+    size_t slots_bytes = 0;
+    double *d_dist = nullptr;
+    size_t dist_bytes = 0;
+    double *d_cost = nullptr;
+    size_t cost_bytes = 0;
+    int32_t *d_tour = nullptr;
+    size_t tour_bytes = 0;
+    int last_grid = 0;
+    int threads = 0;     // workgroup size of the global-table kernels; 0 = per-N default
+    int wg_per_cu = 0;   // resident slots per CU (auto grid); 0 = per-N default
+    int lds_table_max_n = tspgpu::kLdsTableDefaultMaxN;  // largest N whose whole table stays in LDS
+    int variant = 1;     // K1 layer pass: 1 = compact (non-member destinations only), 0 = member sweep
+    hipEvent_t ev_start = nullptr, ev_stop = nullptr;
+    char name[256] = {0};
+    std::mutex mu;
+};

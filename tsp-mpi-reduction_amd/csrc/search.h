@@ -1,0 +1,57 @@
+// Internal launch interface of K2, the prefix-parallel exact search
+// (search.hip).  Public entry points: include/tspgpu.h, "K2".
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+namespace tspgpu {
+
+constexpr int kSearchMaxN = 32;     // cities, city 0 included (tour bits 1..31 of a u32)
+constexpr int kSearchThreads = 256; // workgroup size of the search kernels
+
+// One recorded complete tour: cost (IEEE bits of the f64 fold, or the integer
+// cost) and the inner cities t1..tN in visiting order (tsp.cpp's path minus
+// the two 0s).
+struct SearchRecord {
+    uint64_t cost;
+    uint8_t city[kSearchMaxN];
+};
+
+// One unit of search work: the subtrees below the path city[0..len-1]
+// (city[0] = 0) whose next city is >= `from`.  Seeds are whole prefixes
+// (from = 1); a lane that spends its budget on an item hands back, per level
+// of its stack, the siblings it has not tried yet as new items.
+struct SearchItem {
+    uint8_t city[kSearchMaxN];
+    uint8_t len;
+    uint8_t from;
+    uint8_t pad[2];
+};
+
+struct SearchArgs {
+    const void *dist;          // n*n row-major, f64 or i32 (device)
+    const void *amin;          // n: cheapest edge entering each city (device), f64 on a 2^-20 grid or i32
+    int n;
+    int depth;                 // seed prefix depth D (1 <= D <= n-2)
+    uint32_t items;            // global prefix count N!/(N-D)!
+    uint32_t shard, nshards;   // this shard seeds prefixes p = i*nshards + shard
+    uint32_t budget;           // DFS iterations per item before its rest is handed back
+    const SearchItem *in;      // round input
+    uint32_t in_count;
+    SearchItem *out;           // seed output / round spill output
+    unsigned int *out_count;
+    unsigned int *queue;       // next input item (device counter, zeroed by the host)
+    unsigned long long *inc;   // incumbent: f64 bits or integer cost (device, atomicMin)
+    SearchRecord *rec;         // record buffer (device)
+    unsigned int *rec_count;   // records claimed (may exceed rec_cap: overflow)
+    unsigned int rec_cap;
+    unsigned long long *nodes; // search nodes evaluated (device accumulator)
+    hipStream_t stream;
+};
+
+size_t search_lds_bytes(int n, bool f64);
+hipError_t launch_seed(const SearchArgs &a, bool f64, int grid);
+hipError_t launch_round(const SearchArgs &a, bool f64, int grid);
+
+}  // namespace tspgpu

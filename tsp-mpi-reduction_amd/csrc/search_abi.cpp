@@ -1,0 +1,624 @@
+// C-ABI of K2 (include/tspgpu.h, "K2"): one instance searched by the
+// prefix-parallel kernel (search.hip), optionally as one shard of several
+// GPUs, plus the host steps around it: the initial bound (a 2-opt tour), the
+// cheapest-incoming-edge bound table, and the selection of tsp()'s own tour
+// from the set O of optimal tours the search records.
+//
+// Why the selection reproduces the reference exactly:
+// tsp() returns the tour it reaches by backtracking from the closing min,
+// each step taking the SMALLEST predecessor m with G[S\k][m] + d[m][k] ==
+// G[S][k] (tsp.cpp:457-470, 483-499; K1 does the same on the device).  Let
+// F_j(tau) be the left fold of tau up to its j-th city.  Rounding is monotone,
+// so (i) a DP-optimal path to a state extended by the suffix of an optimal
+// tour is again an optimal tour, hence (ii) G[S_j][t_j] = min F_j over the
+// tours of O that share the suffix (t_j..t_N), and (iii) a predecessor m
+// satisfies the DP test iff some tour of O ends in (m, t_j..t_N) and
+// fl(min F_{j-1} over those + d[m][t_j]) == G[S_j][t_j].  So walking j = N..1
+// over O with that test picks the same cities as the DP, including when a
+// non-DP-optimal prefix is absorbed by rounding into the optimal cost.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cerrno>
+#include <climits>
+#include <cmath>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#include "ctx.h"
+#include "search.h"
+#include "tspgpu.h"
+
+using namespace tspgpu;
+
+static_assert(sizeof(SearchRecord) == sizeof(tspgpu_tour_record), "record layout");
+
+struct tspgpu_search {
+    tspgpu_ctx *ctx = nullptr;
+    int n = 0;
+    int dtype = TSPGPU_F64;
+    int depth = 0;
+    uint64_t items = 0;        // global prefixes
+    uint64_t local_items = 0;  // prefixes of this shard
+    uint32_t shard = 0, nshards = 1;
+    int grid = 0;
+    std::vector<double> hd;    // host copy (f64 view) for the selection
+    std::vector<int32_t> hi;
+    void *d_dist = nullptr, *d_amin = nullptr;
+    // [0] queue (u32), [1] incumbent, [2] nodes, [3] record count (u32), [4] items out (u32)
+    unsigned long long *d_words = nullptr;
+    SearchRecord *d_rec = nullptr;
+    unsigned int rec_cap = 0;
+    SearchItem *d_items[2] = {nullptr, nullptr};  // round input / output (ping-pong)
+    size_t item_cap[2] = {0, 0};
+    int cur = 0;                 // d_items[cur] holds the pending items
+    uint64_t pending = 0;        // items waiting for the next round
+    uint32_t budget = 256;       // DFS iterations per item per round
+    int rounds = 0;
+    double ms = 0.0;             // device time of all seed/round launches
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+};
+
+namespace {
+
+int herr(hipError_t e)
+{
+    if (e == hipSuccess) return 0;
+    if (e == hipErrorOutOfMemory) return -ENOMEM;
+    return -EIO;
+}
+
+// Left fold of the closed tour 0 -> t1 -> ... -> tN -> 0 (tsp.cpp's cost).
+template <typename V>
+V fold_tour(const V *d, int n, const int32_t *t)
+{
+    V c = 0;
+    int prev = 0;
+    for (int i = 0; i < n - 1; ++i) {
+        c = c + d[prev * n + t[i]];
+        prev = t[i];
+    }
+    return c + d[prev * n];
+}
+
+// Nearest neighbour + 2-opt (on the real-valued sum), then the exact fold in
+// the better of the two directions: a valid upper bound >= OPT.
+template <typename V>
+void heuristic(const V *d, int n, std::vector<int32_t> &best, V &cost)
+{
+    std::vector<int> t(n);
+    std::vector<char> used(n, 0);
+    t[0] = 0;
+    used[0] = 1;
+    for (int i = 1; i < n; ++i) {
+        int b = -1;
+        for (int j = 1; j < n; ++j)
+            if (!used[j] && (b < 0 || d[t[i - 1] * n + j] < d[t[i - 1] * n + b])) b = j;
+        t[i] = b;
+        used[b] = 1;
+    }
+    for (bool improved = true; improved;) {
+        improved = false;
+        for (int i = 1; i < n - 1; ++i)
+            for (int j = i + 1; j < n; ++j) {
+                const int a = t[i - 1], b = t[i], c = t[j], e = t[(j + 1) % n];
+                const double delta = ((double)d[a * n + c] + (double)d[b * n + e]) -
+                                     ((double)d[a * n + b] + (double)d[c * n + e]);
+                if (delta < -1e-9 * (1.0 + std::fabs((double)d[a * n + b]))) {
+                    std::reverse(t.begin() + i, t.begin() + j + 1);
+                    improved = true;
+                }
+            }
+    }
+    std::vector<int32_t> fw(t.begin() + 1, t.end()), bw(fw.rbegin(), fw.rend());
+    const V cf = fold_tour(d, n, fw.data()), cb = fold_tour(d, n, bw.data());
+    best = cb < cf ? bw : fw;
+    cost = cb < cf ? cb : cf;
+}
+
+template <typename V>
+int select_tour(const V *d, int n, const tspgpu_tour_record *rec, int count, V opt, int32_t *tour_out)
+{
+    const int N = n - 1;
+    // keep the optimal records; fold[c * N + j-1] = left fold up to the j-th inner city
+    std::vector<const uint8_t *> city;
+    std::vector<V> fold;
+    city.reserve(count);
+    fold.reserve((size_t)count * N);
+    for (int r = 0; r < count; ++r) {
+        const uint8_t *t = rec[r].city;
+        V acc = 0;
+        int prev = 0;
+        const size_t base = fold.size();
+        for (int j = 1; j <= N; ++j) {
+            acc = acc + d[prev * n + t[j - 1]];
+            fold.push_back(acc);
+            prev = t[j - 1];
+        }
+        if (!(acc + d[prev * n] == opt)) {  // recorded against an older incumbent
+            fold.resize(base);
+            continue;
+        }
+        city.push_back(t);
+    }
+    if (city.empty()) return -EIO;
+    std::vector<int> alive(city.size());
+    for (size_t i = 0; i < city.size(); ++i) alive[i] = (int)i;
+    std::vector<int32_t> tour(N + 2, 0);
+    std::vector<char> seen(n);
+    std::vector<V> best(n);
+    V target = opt;
+    int next = 0;
+    for (int j = N; j >= 1; --j) {
+        // t_j candidates among the tours sharing the chosen suffix: best prefix fold per city
+        std::fill(seen.begin(), seen.end(), 0);
+        for (int idx : alive) {
+            const int m = city[idx][j - 1];
+            const V f = fold[(size_t)idx * N + (j - 1)];
+            if (!seen[m] || f < best[m]) best[m] = f;
+            seen[m] = 1;
+        }
+        int pick = -1;
+        for (int m = 1; m <= N; ++m)
+            if (seen[m] && best[m] + d[m * n + next] == target) {
+                pick = m;
+                break;
+            }
+        if (pick < 0) return -EIO;
+        std::vector<int> keep;
+        for (int idx : alive)
+            if (city[idx][j - 1] == pick) keep.push_back(idx);
+        alive.swap(keep);
+        tour[j] = pick;
+        target = best[pick];
+        next = pick;
+    }
+    std::memcpy(tour_out, tour.data(), sizeof(int32_t) * (N + 2));
+    return 0;
+}
+
+int validate_search(const void *dist, int dtype, int n)
+{
+    if (!dist || n < 3 || n > TSPGPU_SEARCH_MAX_CITIES) return -EINVAL;
+    if (dtype == TSPGPU_F64) {
+        const double *d = static_cast<const double *>(dist);
+        double mx = 0.0;
+        for (int i = 0; i < n * n; ++i) {
+            if (!(d[i] >= 0.0) || !std::isfinite(d[i])) return -EINVAL;
+            mx = std::max(mx, d[i]);
+        }
+        if ((double)n * mx >= (double)INT_MAX) return -ERANGE;  // tsp.cpp:411,453 sentinel
+        return 0;
+    }
+    if (dtype == TSPGPU_I32) {
+        const int32_t *d = static_cast<const int32_t *>(dist);
+        long long mx = 0;
+        for (int i = 0; i < n * n; ++i) {
+            if (d[i] < 0) return -EINVAL;
+            mx = std::max<long long>(mx, d[i]);
+        }
+        if ((long long)n * mx >= (1ll << 30)) return -ERANGE;
+        return 0;
+    }
+    return -EINVAL;
+}
+
+uint64_t falling(int N, int D)
+{
+    uint64_t p = 1;
+    for (int l = 0; l < D; ++l) p *= (uint64_t)(N - l);
+    return p;
+}
+
+}  // namespace
+
+extern "C" {
+
+int tspgpu_search_create(tspgpu_ctx *c, const void *dist, int dtype, int n, int shard, int nshards, int depth,
+                         tspgpu_search **out)
+{
+    if (!c || !out) return -EINVAL;
+    *out = nullptr;
+    int rc = validate_search(dist, dtype, n);
+    if (rc) return rc;
+    if (nshards < 1 || shard < 0 || shard >= nshards) return -EINVAL;
+    const int N = n - 1;
+    const bool f64 = dtype == TSPGPU_F64;
+    if (hipSetDevice(c->device) != hipSuccess) return -ENODEV;
+    auto *s = new (std::nothrow) tspgpu_search();
+    if (!s) return -ENOMEM;
+    s->ctx = c;
+    s->n = n;
+    s->dtype = dtype;
+    s->shard = (uint32_t)shard;
+    s->nshards = (uint32_t)nshards;
+    const size_t lds = search_lds_bytes(n, f64);
+    const int per_cu = std::max(1, std::min(8, (int)((160 * 1024) / lds)));
+    s->grid = c->cu_count * per_cu;
+    // seed depth: the smallest D with at least one prefix per lane of the
+    // whole grid (the rounds split whatever is still too coarse), at most
+    // N-1, at least 1, and < 2^31 prefixes
+    const uint64_t lanes = (uint64_t)s->grid * kSearchThreads * (uint64_t)nshards;
+    if (depth <= 0) {
+        depth = 1;
+        while (depth < N - 1 && falling(N, depth + 1) < (1ull << 31) && falling(N, depth) < lanes) ++depth;
+    }
+    if (depth > N - 1) depth = N - 1;
+    while (depth > 1 && falling(N, depth) >= (1ull << 31)) --depth;
+    if (const char *e = std::getenv("TSPGPU_SEARCH_BUDGET")) {
+        const long v = std::atol(e);
+        if (v > 0) s->budget = (uint32_t)v;
+    }
+    s->depth = depth;
+    s->items = falling(N, depth);
+    s->local_items = s->items / nshards + (s->items % nshards > (uint64_t)shard ? 1 : 0);
+    const size_t vb = f64 ? sizeof(double) : sizeof(int32_t);
+    // cheapest incoming edge per city; f64 rounded DOWN to a 2^-20 grid
+    std::vector<double> ad(n);
+    std::vector<int32_t> ai(n);
+    if (f64) {
+        const double *d = static_cast<const double *>(dist);
+        s->hd.assign(d, d + n * n);
+        for (int x = 0; x < n; ++x) {
+            double m = INFINITY;
+            for (int i = 0; i < n; ++i)
+                if (i != x) m = std::min(m, d[i * n + x]);
+            ad[x] = std::ldexp(std::floor(std::ldexp(m, 20)), -20);
+        }
+    } else {
+        const int32_t *d = static_cast<const int32_t *>(dist);
+        s->hi.assign(d, d + n * n);
+        for (int x = 0; x < n; ++x) {
+            int32_t m = INT32_MAX;
+            for (int i = 0; i < n; ++i)
+                if (i != x) m = std::min(m, d[i * n + x]);
+            ai[x] = m;
+        }
+    }
+    s->rec_cap = 1u << 16;
+    hipError_t e = hipMalloc(&s->d_dist, vb * n * n);
+    if (e == hipSuccess) e = hipMalloc(&s->d_amin, vb * n);
+    if (e == hipSuccess) e = hipMalloc((void **)&s->d_words, 5 * sizeof(unsigned long long));
+    if (e == hipSuccess) e = hipMalloc((void **)&s->d_rec, sizeof(SearchRecord) * s->rec_cap);
+    if (e == hipSuccess) e = hipMemcpy(s->d_dist, dist, vb * n * n, hipMemcpyHostToDevice);
+    if (e == hipSuccess)
+        e = hipMemcpy(s->d_amin, f64 ? (const void *)ad.data() : (const void *)ai.data(), vb * n,
+                      hipMemcpyHostToDevice);
+    unsigned long long w[5] = {0, 0, 0, 0, 0};
+    if (f64) {
+        const double inf = INFINITY;
+        std::memcpy(&w[1], &inf, 8);
+    } else {
+        w[1] = (unsigned long long)INT32_MAX;
+    }
+    if (e == hipSuccess) e = hipMemcpy(s->d_words, w, sizeof w, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipEventCreate(&s->e0);
+    if (e == hipSuccess) e = hipEventCreate(&s->e1);
+    if (e != hipSuccess) {
+        tspgpu_search_destroy(s);
+        return herr(e);
+    }
+    *out = s;
+    return 0;
+}
+
+int tspgpu_search_destroy(tspgpu_search *s)
+{
+    if (!s) return 0;
+    (void)hipSetDevice(s->ctx->device);
+    (void)hipStreamSynchronize(s->ctx->stream);
+    if (s->d_dist) (void)hipFree(s->d_dist);
+    if (s->d_amin) (void)hipFree(s->d_amin);
+    if (s->d_words) (void)hipFree(s->d_words);
+    if (s->d_rec) (void)hipFree(s->d_rec);
+    for (auto *p : s->d_items)
+        if (p) (void)hipFree(p);
+    if (s->e0) (void)hipEventDestroy(s->e0);
+    if (s->e1) (void)hipEventDestroy(s->e1);
+    delete s;
+    return 0;
+}
+
+int tspgpu_search_info(const tspgpu_search *s, int *depth, uint64_t *items, uint64_t *local_items)
+{
+    if (!s) return -EINVAL;
+    if (depth) *depth = s->depth;
+    if (items) *items = s->items;
+    if (local_items) *local_items = s->local_items;
+    return 0;
+}
+
+int tspgpu_search_set_bound(tspgpu_search *s, double bound)
+{
+    if (!s) return -EINVAL;
+    unsigned long long w;
+    if (s->dtype == TSPGPU_F64) {
+        if (!(bound >= 0.0)) return -EINVAL;
+        std::memcpy(&w, &bound, 8);
+    } else {
+        if (!(bound >= 0.0)) return -EINVAL;
+        w = (unsigned long long)std::min<double>(bound, (double)INT32_MAX);
+    }
+    (void)hipSetDevice(s->ctx->device);
+    return herr(hipMemcpy(s->d_words + 1, &w, 8, hipMemcpyHostToDevice));
+}
+
+static SearchArgs args_of(tspgpu_search *s)
+{
+    SearchArgs a{};
+    a.dist = s->d_dist;
+    a.amin = s->d_amin;
+    a.n = s->n;
+    a.depth = s->depth;
+    a.items = (uint32_t)s->items;
+    a.shard = s->shard;
+    a.nshards = s->nshards;
+    a.budget = s->budget;
+    a.queue = reinterpret_cast<unsigned int *>(s->d_words);
+    a.inc = s->d_words + 1;
+    a.nodes = s->d_words + 2;
+    a.rec_count = reinterpret_cast<unsigned int *>(s->d_words + 3);
+    a.out_count = reinterpret_cast<unsigned int *>(s->d_words + 4);
+    a.rec = s->d_rec;
+    a.rec_cap = s->rec_cap;
+    a.stream = s->ctx->stream;
+    return a;
+}
+
+static int ensure_items(tspgpu_search *s, int which, size_t count)
+{
+    if (s->item_cap[which] >= count && s->d_items[which]) return 0;
+    if (s->d_items[which]) (void)hipFree(s->d_items[which]);
+    s->d_items[which] = nullptr;
+    s->item_cap[which] = 0;
+    const size_t cap = std::max<size_t>(count, 1024);
+    hipError_t e = hipMalloc((void **)&s->d_items[which], cap * sizeof(SearchItem));
+    if (e != hipSuccess) return herr(e);
+    s->item_cap[which] = cap;
+    return 0;
+}
+
+// launch + wait + read the item count the launch produced
+static int launch_and_count(tspgpu_search *s, bool seed, int grid, SearchArgs &a)
+{
+    hipStream_t st = s->ctx->stream;
+    hipError_t e = hipMemsetAsync(s->d_words, 0, 8, st);  // queue
+    if (e == hipSuccess) e = hipMemsetAsync(s->d_words + 4, 0, 8, st);  // items out
+    if (e != hipSuccess) return herr(e);
+    (void)hipEventRecord(s->e0, st);
+    e = seed ? launch_seed(a, s->dtype == TSPGPU_F64, grid) : launch_round(a, s->dtype == TSPGPU_F64, grid);
+    (void)hipEventRecord(s->e1, st);
+    if (e != hipSuccess) return herr(e);
+    unsigned long long out = 0;
+    e = hipMemcpyAsync(&out, s->d_words + 4, 8, hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (e != hipSuccess) return herr(e);
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, s->e0, s->e1) == hipSuccess) s->ms += ms;
+    s->pending = (uint32_t)out;
+    return 0;
+}
+
+int tspgpu_search_start(tspgpu_search *s)
+{
+    if (!s) return -EINVAL;
+    (void)hipSetDevice(s->ctx->device);
+    int rc = ensure_items(s, 0, s->local_items + 1);
+    if (rc) return rc;
+    SearchArgs a = args_of(s);
+    a.out = s->d_items[0];
+    s->cur = 0;
+    s->rounds = 0;
+    const uint64_t blocks = (s->local_items + kSearchThreads - 1) / kSearchThreads;
+    const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>(blocks, (uint64_t)s->ctx->cu_count * 8));
+    return launch_and_count(s, true, grid, a);
+}
+
+int tspgpu_search_step(tspgpu_search *s, uint64_t *pending)
+{
+    if (!s) return -EINVAL;
+    if (s->pending == 0) {
+        if (pending) *pending = 0;
+        return 0;
+    }
+    (void)hipSetDevice(s->ctx->device);
+    const int in = s->cur, out = 1 - s->cur;
+    // every item hands back at most one item per level of its stack
+    int rc = ensure_items(s, out, (size_t)s->pending * (size_t)(s->n - 1) + 64);
+    if (rc) return rc;
+    SearchArgs a = args_of(s);
+    a.in = s->d_items[in];
+    a.in_count = (uint32_t)s->pending;
+    a.out = s->d_items[out];
+    const uint64_t blocks = (s->pending + kSearchThreads - 1) / kSearchThreads;
+    const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>(blocks, (uint64_t)s->grid));
+    rc = launch_and_count(s, false, grid, a);
+    if (rc) return rc;
+    s->cur = out;
+    ++s->rounds;
+    if (pending) *pending = s->pending;
+    return 0;
+}
+
+int tspgpu_search_run_all(tspgpu_search *s)
+{
+    int rc = tspgpu_search_start(s);
+    uint64_t pending = 1;
+    while (!rc && pending) rc = tspgpu_search_step(s, &pending);
+    return rc;
+}
+
+int tspgpu_search_timing(const tspgpu_search *s, double *kernel_ms, int *rounds)
+{
+    if (!s) return -EINVAL;
+    if (kernel_ms) *kernel_ms = s->ms;
+    if (rounds) *rounds = s->rounds;
+    return 0;
+}
+
+void *tspgpu_search_incumbent_device(tspgpu_search *s) { return s ? (void *)(s->d_words + 1) : nullptr; }
+
+int tspgpu_search_counters(tspgpu_search *s, uint64_t *incumbent_bits, uint64_t *nodes, uint64_t *records)
+{
+    if (!s) return -EINVAL;
+    (void)hipSetDevice(s->ctx->device);
+    unsigned long long w[5];
+    hipError_t e = hipMemcpyAsync(w, s->d_words, sizeof w, hipMemcpyDeviceToHost, s->ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(s->ctx->stream);
+    if (e != hipSuccess) return herr(e);
+    if (incumbent_bits) *incumbent_bits = w[1];
+    if (nodes) *nodes = w[2];
+    if (records) *records = (uint32_t)w[3];
+    return 0;
+}
+
+int tspgpu_search_reset_records(tspgpu_search *s, unsigned int capacity)
+{
+    if (!s) return -EINVAL;
+    (void)hipSetDevice(s->ctx->device);
+    hipError_t e = hipStreamSynchronize(s->ctx->stream);
+    if (e == hipSuccess && capacity > s->rec_cap) {
+        (void)hipFree(s->d_rec);
+        s->d_rec = nullptr;
+        e = hipMalloc((void **)&s->d_rec, sizeof(SearchRecord) * (size_t)capacity);
+        if (e == hipSuccess) s->rec_cap = capacity;
+    }
+    if (e == hipSuccess) e = hipMemset(s->d_words + 3, 0, 8);
+    return herr(e);
+}
+
+int tspgpu_search_records(tspgpu_search *s, uint64_t cost_bits, tspgpu_tour_record *out, int cap, int *count)
+{
+    if (!s || !count || (cap > 0 && !out)) return -EINVAL;
+    uint64_t claimed = 0;
+    int rc = tspgpu_search_counters(s, nullptr, nullptr, &claimed);
+    if (rc) return rc;
+    if (claimed > s->rec_cap) return -EOVERFLOW;
+    std::vector<SearchRecord> h(claimed);
+    if (claimed) {
+        hipError_t e = hipMemcpy(h.data(), s->d_rec, sizeof(SearchRecord) * claimed, hipMemcpyDeviceToHost);
+        if (e != hipSuccess) return herr(e);
+    }
+    int k = 0;
+    for (const auto &r : h) {
+        if (r.cost != cost_bits) continue;
+        if (k < cap) std::memcpy(&out[k], &r, sizeof r);
+        ++k;
+    }
+    *count = k;
+    return k > cap ? -ENOSPC : 0;
+}
+
+int tspgpu_heuristic_tour(const void *dist, int dtype, int n, double *cost_out, int32_t *tour_out)
+{
+    int rc = validate_search(dist, dtype, n);
+    if (rc) return rc;
+    std::vector<int32_t> t;
+    if (dtype == TSPGPU_F64) {
+        double c;
+        heuristic(static_cast<const double *>(dist), n, t, c);
+        if (cost_out) *cost_out = c;
+    } else {
+        int32_t c;
+        heuristic(static_cast<const int32_t *>(dist), n, t, c);
+        if (cost_out) *cost_out = c;
+    }
+    if (tour_out) {
+        tour_out[0] = 0;
+        for (int i = 0; i < n - 1; ++i) tour_out[i + 1] = t[i];
+        tour_out[n] = 0;
+    }
+    return 0;
+}
+
+int tspgpu_select_tour(const void *dist, int dtype, int n, const tspgpu_tour_record *records, int count,
+                       uint64_t cost_bits, int32_t *tour_out)
+{
+    int rc = validate_search(dist, dtype, n);
+    if (rc) return rc;
+    if (count <= 0 || !records || !tour_out) return -EINVAL;
+    if (dtype == TSPGPU_F64) {
+        double opt;
+        std::memcpy(&opt, &cost_bits, 8);
+        return select_tour(static_cast<const double *>(dist), n, records, count, opt, tour_out);
+    }
+    return select_tour(static_cast<const int32_t *>(dist), n, records, count, (int32_t)(uint32_t)cost_bits,
+                       tour_out);
+}
+
+int tspgpu_search_solve(tspgpu_ctx *c, const void *dist, int dtype, int n, double *cost_out, int32_t *tour_out,
+                        tspgpu_search_stats *stats)
+{
+    if (!c || !cost_out || !tour_out) return -EINVAL;
+    tspgpu_search *s = nullptr;
+    int rc = tspgpu_search_create(c, dist, dtype, n, 0, 1, 0, &s);
+    if (rc) return rc;
+    if (const char *e = std::getenv("TSPGPU_SEARCH_RECORD_CAP")) {  // tests: force the second phase
+        const long v = std::atol(e);
+        if (v > 0) s->rec_cap = (unsigned int)std::min<long>(v, s->rec_cap);
+    }
+    double ub = 0.0;
+    rc = tspgpu_heuristic_tour(dist, dtype, n, &ub, nullptr);
+    if (!rc) rc = tspgpu_search_set_bound(s, ub);
+    int phases = 1, fallback = 0;
+    uint64_t inc = 0, nodes = 0, nodes_total = 0, recs = 0;
+    if (!rc) rc = tspgpu_search_run_all(s);
+    if (!rc) rc = tspgpu_search_counters(s, &inc, &nodes, &recs);
+    nodes_total = nodes;
+    // the record buffer overflowed: search again with the optimum as the bound,
+    // so only optimal tours are recorded, into a buffer of the size now known
+    constexpr uint64_t kPhase2Cap = 1u << 22;
+    if (!rc && recs > s->rec_cap && recs <= kPhase2Cap) {
+        phases = 2;
+        unsigned long long w = inc;
+        rc = tspgpu_search_reset_records(s, (unsigned int)recs);
+        if (!rc) rc = herr(hipMemcpy(s->d_words + 1, &w, 8, hipMemcpyHostToDevice));
+        if (!rc) rc = herr(hipMemset(s->d_words + 2, 0, 8));
+        if (!rc) rc = tspgpu_search_run_all(s);
+        if (!rc) rc = tspgpu_search_counters(s, &inc, &nodes, &recs);
+        nodes_total += nodes;
+    }
+    std::vector<tspgpu_tour_record> opt;
+    int count = 0;
+    if (!rc && recs > s->rec_cap) {
+        // |O| too large to enumerate (e.g. coincident cities): the DP itself
+        // (K1, also on the GPU) gives tsp()'s tour directly for n <= 20
+        if (dtype == TSPGPU_F64 && n <= TSPGPU_MAX_CITIES) {
+            fallback = 1;
+            rc = tspgpu_solve_blocks(c, static_cast<const double *>(dist), n, 1, cost_out, tour_out);
+        } else if (dtype == TSPGPU_I32 && n <= TSPGPU_MAX_CITIES) {
+            fallback = 1;
+            std::vector<double> dd(static_cast<const int32_t *>(dist), static_cast<const int32_t *>(dist) + n * n);
+            rc = tspgpu_solve_blocks(c, dd.data(), n, 1, cost_out, tour_out);
+        } else {
+            rc = -EOVERFLOW;
+        }
+    } else if (!rc) {
+        opt.resize(recs);
+        rc = tspgpu_search_records(s, inc, opt.data(), (int)recs, &count);
+        if (!rc) rc = tspgpu_select_tour(dist, dtype, n, opt.data(), count, inc, tour_out);
+        if (!rc) {
+            if (dtype == TSPGPU_F64)
+                std::memcpy(cost_out, &inc, 8);
+            else
+                *cost_out = (double)(int32_t)(uint32_t)inc;
+        }
+    }
+    if (stats) {
+        std::memset(stats, 0, sizeof *stats);
+        stats->nodes = nodes_total;
+        stats->records = recs;
+        stats->optimal_tours = fallback ? 0 : (uint64_t)count;
+        stats->depth = s->depth;
+        stats->phases = phases;
+        stats->fallback = fallback;
+        stats->kernel_ms = s->ms;
+        stats->items = s->items;
+        stats->rounds = s->rounds;
+    }
+    tspgpu_search_destroy(s);
+    return rc;
+}
+
+}  // extern "C"

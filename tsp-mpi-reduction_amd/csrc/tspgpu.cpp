@@ -19,6 +19,7 @@
 #include <mutex>
 #include <vector>
 
+#include "ctx.h"
 #include "heldkarp.h"
 
 namespace tspgpu {
@@ -76,31 +77,6 @@ void host_layer_info(int N, LayerInfo *info)
 
 using namespace tspgpu;
 
-struct tspgpu_ctx {
-    int device = 0;
-    int strict = 0;
-    int slots_opt = 0;
-    int cu_count = 256;
-    hipStream_t stream = nullptr;
-    uint32_t *d_masks[kMaxN + 1] = {};
-    LayerInfo *d_info[kMaxN + 1] = {};
-    double *d_slots = nullptr;
-    size_t slots_bytes = 0;
-    double *d_dist = nullptr;
-    size_t dist_bytes = 0;
-    double *d_cost = nullptr;
-    size_t cost_bytes = 0;
-    int32_t *d_tour = nullptr;
-    size_t tour_bytes = 0;
-    int last_grid = 0;
-    int threads = 0;     // workgroup size of the global-table kernels; 0 = per-N default
-    int wg_per_cu = 0;   // resident slots per CU (auto grid); 0 = per-N default
-    int lds_table_max_n = kLdsTableDefaultMaxN;  // largest N whose whole table stays in LDS
-    int variant = 1;     // K1 layer pass: 1 = compact (non-member destinations only), 0 = member sweep
-    hipEvent_t ev_start = nullptr, ev_stop = nullptr;
-    char name[256] = {0};
-    std::mutex mu;
-};
 
 namespace {
 

@@ -1,0 +1,145 @@
+"""Multi-GPU driver of K2 (one process per GPU, torch.distributed).
+
+One instance is split over the ranks of a process group: rank r searches the
+seed prefixes p with p mod W == r (libtspgpu's static shard); inside its GPU
+the work runs in rounds (a device queue hands items to lanes, items that
+exceed their budget are split and re-queued).  Between rounds the ranks
+all-reduce(MIN) the 64-bit incumbent word (IEEE bits of the
+f64 cost or the integer cost; both order like signed int64 for the
+non-negative costs the ABI accepts), so every GPU prunes with the best tour
+found anywhere.  At the end: all-reduce(MIN) of the incumbent = the optimum,
+all-gather of each rank's records at that cost (the optimal set O), and every
+rank applies the DP's tie rule (tspgpu_select_tour) to O — the same answer as
+tsp() / K1 on one GPU.
+
+With the "nccl" backend (RCCL on ROCm) the exchange is a device all-reduce
+over xGMI; "gloo" runs the same logic over host tensors (CPU tests, or several
+ranks sharing one GPU).  This replaces the reference's hand-rolled binary
+MPI_Send/MPI_Recv tree (tsp.cpp:52-134) for the one step of the search that
+needs a reduction: picking the global best tour.
+"""
+from __future__ import annotations
+
+import errno
+import time
+
+import numpy as np
+
+import tspgpu
+
+
+def _word_tensor(value: int, device):
+    import torch
+
+    return torch.tensor([value], dtype=torch.int64, device=device)
+
+
+def solve_sharded(ctx, dist, group=None, depth: int = 0, device=None):
+    """Search one instance over the ranks of `group` (None: the default group,
+    or a single process when torch.distributed is not initialised).
+
+    Returns (cost, tour (n+1,), stats dict); identical on every rank."""
+    import torch
+    import torch.distributed as tdist
+
+    dist_on = tdist.is_available() and tdist.is_initialized()
+    rank = tdist.get_rank(group) if dist_on else 0
+    world = tdist.get_world_size(group) if dist_on else 1
+    backend = tdist.get_backend(group) if dist_on else "none"
+    if device is None:
+        device = torch.device("cuda", torch.cuda.current_device()) if backend == "nccl" else torch.device("cpu")
+
+    def allmin(word: int) -> int:
+        if world == 1:
+            return word
+        t = _word_tensor(word, device)
+        tdist.all_reduce(t, op=tdist.ReduceOp.MIN, group=group)
+        return int(t.item())
+
+    S = tspgpu.Search(ctx, dist, shard=rank, nshards=world, depth=depth)
+    try:
+        ub, _ = tspgpu.heuristic_tour(dist)  # deterministic: the same bound on every rank
+        S.set_bound(ub)
+        t0 = time.perf_counter()
+        exchanges = 0
+        S.start()
+        busy = 1
+        while True:
+            # one round on this rank (if it still has work), then the exchange:
+            # incumbent MIN and "anyone still busy" as MIN of the negated flag
+            pending = S.step() if busy else 0
+            inc, _, _ = S.counters()
+            best = allmin(inc)
+            exchanges += 1
+            if best < inc:
+                S.set_bound(tspgpu.bits_cost(best, S.dtype))
+            busy = 1 if pending else 0
+            if allmin(-busy) == 0:
+                break
+        inc, nodes, recs = S.counters()
+        opt = allmin(inc)
+        phases = 1
+
+        def local_records():
+            try:
+                return S.records(opt), 0
+            except tspgpu.TspGpuError as e:
+                if e.code != -errno.EOVERFLOW:
+                    raise
+                return [], 1
+
+        mine, lost = local_records()
+        if allmin(-lost) < 0:
+            # some rank lost records: search again with the optimum as the bound,
+            # so only optimal tours are recorded, in a buffer of the needed size
+            phases = 2
+            S.reset_records(int(min(max(recs, 1 << 16), 1 << 22)))
+            S.set_bound(tspgpu.bits_cost(opt, S.dtype))
+            S.run_all()
+            _, nodes2, recs = S.counters()
+            nodes += nodes2
+            mine, lost = local_records()
+            if allmin(-lost) < 0:
+                # too many optimal tours to enumerate (coincident cities): the DP
+                # (K1 on this rank's GPU) gives tsp()'s tour directly for n <= 20
+                if S.n > 20:
+                    raise tspgpu.TspGpuError(-errno.EOVERFLOW, "solve_sharded")
+                d64 = np.asarray(dist, dtype=np.float64)[None]
+                c, t = ctx.solve_blocks(d64)
+                cost = float(c[0]) if S.dtype == tspgpu.F64 else int(c[0])
+                stats = {"nodes": int(nodes), "rank_nodes": int(nodes), "optimal_tours": 0, "depth": S.depth,
+                         "items": S.items, "phases": phases, "fallback": 1, "kernel_ms": S.timing()[0],
+                         "wall_s": time.perf_counter() - t0, "exchanges": exchanges, "world": world,
+                         "backend": backend}
+                return cost, t[0], stats
+        blob = np.frombuffer(b"".join(bytes(r) for r in mine), dtype=np.uint8) if mine else np.zeros(0, np.uint8)
+        if world > 1:
+            parts = [None] * world
+            tdist.all_gather_object(parts, blob, group=group)
+            node_t = _word_tensor(int(nodes), device)
+            tdist.all_reduce(node_t, op=tdist.ReduceOp.SUM, group=group)
+            total_nodes = int(node_t.item())
+        else:
+            parts, total_nodes = [blob], nodes
+        rsz = ctypes_sizeof_record()
+        allrec = []
+        for p in parts:
+            for i in range(0, len(p), rsz):
+                allrec.append(tspgpu.TourRecord.from_buffer_copy(bytes(p[i:i + rsz])))
+        cost = tspgpu.bits_cost(opt, S.dtype)
+        tour = tspgpu.select_tour(dist, allrec, cost)
+        wall = time.perf_counter() - t0
+        kernel_ms, rounds = S.timing()
+        stats = {"nodes": total_nodes, "rank_nodes": int(nodes), "optimal_tours": len(allrec), "depth": S.depth,
+                 "items": S.items, "phases": phases, "fallback": 0, "kernel_ms": kernel_ms, "rounds": rounds,
+                 "wall_s": wall,
+                 "exchanges": exchanges, "world": world, "backend": backend}
+        return cost, tour, stats
+    finally:
+        S.close()
+
+
+def ctypes_sizeof_record() -> int:
+    import ctypes
+
+    return ctypes.sizeof(tspgpu.TourRecord)

@@ -24,7 +24,30 @@ EXPORTED_SYMBOLS = (
     "tspgpu_table_bytes_per_block", "tspgpu_device_alloc", "tspgpu_device_free", "tspgpu_memcpy_htod",
     "tspgpu_memcpy_dtoh", "tspgpu_stream", "tspgpu_synchronize", "tspgpu_timer_start", "tspgpu_timer_stop",
     "tspgpu_device_info",
+    # K2
+    "tspgpu_search_solve", "tspgpu_search_create", "tspgpu_search_destroy", "tspgpu_search_info",
+    "tspgpu_search_set_bound", "tspgpu_search_start", "tspgpu_search_step", "tspgpu_search_run_all",
+    "tspgpu_search_timing", "tspgpu_search_incumbent_device",
+    "tspgpu_search_counters", "tspgpu_search_reset_records", "tspgpu_search_records", "tspgpu_heuristic_tour",
+    "tspgpu_select_tour",
 )
+
+F64, I32 = 0, 1
+SEARCH_MAX_CITIES = 32
+
+
+class TourRecord(ctypes.Structure):
+    """tspgpu_tour_record: cost bits + inner cities t1..tN."""
+    _fields_ = [("cost", ctypes.c_uint64), ("city", ctypes.c_uint8 * 32)]
+
+
+class SearchStats(ctypes.Structure):
+    _fields_ = [("nodes", ctypes.c_uint64), ("records", ctypes.c_uint64), ("optimal_tours", ctypes.c_uint64),
+                ("items", ctypes.c_uint64), ("depth", ctypes.c_int), ("phases", ctypes.c_int),
+                ("fallback", ctypes.c_int), ("rounds", ctypes.c_int), ("kernel_ms", ctypes.c_double)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
 
 
 class City(ctypes.Structure):
@@ -82,6 +105,26 @@ def lib():
         L.tspgpu_timer_start.argtypes = [vp]
         L.tspgpu_timer_stop.argtypes = [vp, ctypes.POINTER(ctypes.c_float)]
         L.tspgpu_device_info.argtypes = [vp, ctypes.POINTER(ctypes.c_int), ctypes.c_char_p, ctypes.c_int]
+        u64p = ctypes.POINTER(ctypes.c_uint64)
+        L.tspgpu_search_solve.argtypes = [vp, vp, ctypes.c_int, ctypes.c_int, dp, ip, ctypes.POINTER(SearchStats)]
+        L.tspgpu_search_create.argtypes = [vp, vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                           ctypes.c_int, ctypes.POINTER(vp)]
+        L.tspgpu_search_destroy.argtypes = [vp]
+        L.tspgpu_search_info.argtypes = [vp, ctypes.POINTER(ctypes.c_int), u64p, u64p]
+        L.tspgpu_search_set_bound.argtypes = [vp, ctypes.c_double]
+        L.tspgpu_search_start.argtypes = [vp]
+        L.tspgpu_search_step.argtypes = [vp, u64p]
+        L.tspgpu_search_run_all.argtypes = [vp]
+        L.tspgpu_search_timing.argtypes = [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int)]
+        L.tspgpu_search_incumbent_device.argtypes = [vp]
+        L.tspgpu_search_incumbent_device.restype = vp
+        L.tspgpu_search_counters.argtypes = [vp, u64p, u64p, u64p]
+        L.tspgpu_search_reset_records.argtypes = [vp, ctypes.c_uint]
+        L.tspgpu_search_records.argtypes = [vp, ctypes.c_uint64, ctypes.POINTER(TourRecord), ctypes.c_int,
+                                            ctypes.POINTER(ctypes.c_int)]
+        L.tspgpu_heuristic_tour.argtypes = [vp, ctypes.c_int, ctypes.c_int, dp, ip]
+        L.tspgpu_select_tour.argtypes = [vp, ctypes.c_int, ctypes.c_int, ctypes.POINTER(TourRecord), ctypes.c_int,
+                                         ctypes.c_uint64, ip]
         _lib = L
     return _lib
 
@@ -245,6 +288,142 @@ class Context:
         name = ctypes.create_string_buffer(256)
         self._check(lib().tspgpu_device_info(self.handle, ctypes.byref(cu), name, 256), "tspgpu_device_info")
         return cu.value, name.value.decode()
+
+
+def _search_dist(dist):
+    """(n, n) matrix -> (contiguous array, dtype code): float -> F64, integer -> I32."""
+    dist = np.asarray(dist)
+    if np.issubdtype(dist.dtype, np.integer):
+        return np.ascontiguousarray(dist, dtype=np.int32), I32
+    return np.ascontiguousarray(dist, dtype=np.float64), F64
+
+
+def cost_bits(cost, dtype: int) -> int:
+    """The 64-bit incumbent word of a cost (f64 IEEE bits or the integer)."""
+    if dtype == F64:
+        return int(np.array([cost], dtype=np.float64).view(np.uint64)[0])
+    return int(cost)
+
+
+def bits_cost(bits: int, dtype: int):
+    if dtype == F64:
+        return float(np.array([bits], dtype=np.uint64).view(np.float64)[0])
+    return int(np.uint32(bits).view(np.int32))
+
+
+def heuristic_tour(dist):
+    d, dt = _search_dist(dist)
+    n = d.shape[0]
+    cost = ctypes.c_double()
+    tour = np.zeros(n + 1, dtype=np.int32)
+    rc = lib().tspgpu_heuristic_tour(d.ctypes.data, dt, n, ctypes.byref(cost), _ip(tour))
+    if rc:
+        raise TspGpuError(rc, "tspgpu_heuristic_tour")
+    return cost.value, tour
+
+
+def select_tour(dist, records, cost):
+    """The DP's tie rule over the optimal set (tspgpu_select_tour)."""
+    d, dt = _search_dist(dist)
+    n = d.shape[0]
+    arr = (TourRecord * max(1, len(records)))(*records)
+    tour = np.zeros(n + 1, dtype=np.int32)
+    rc = lib().tspgpu_select_tour(d.ctypes.data, dt, n, arr, len(records), cost_bits(cost, dt), _ip(tour))
+    if rc:
+        raise TspGpuError(rc, "tspgpu_select_tour")
+    return tour
+
+
+class Search:
+    """One instance (or shard `shard` of `nshards`) of the K2 search on a Context."""
+
+    def __init__(self, ctx: "Context", dist, shard: int = 0, nshards: int = 1, depth: int = 0):
+        self.dist, self.dtype = _search_dist(dist)
+        self.n = self.dist.shape[0]
+        h = ctypes.c_void_p()
+        rc = lib().tspgpu_search_create(ctx.handle, self.dist.ctypes.data, self.dtype, self.n, shard, nshards,
+                                        depth, ctypes.byref(h))
+        if rc:
+            raise TspGpuError(rc, "tspgpu_search_create")
+        self.handle = h
+        dep, items, local = ctypes.c_int(), ctypes.c_uint64(), ctypes.c_uint64()
+        lib().tspgpu_search_info(h, ctypes.byref(dep), ctypes.byref(items), ctypes.byref(local))
+        self.depth, self.items, self.local_items = dep.value, items.value, local.value
+
+    def close(self):
+        if self.handle:
+            lib().tspgpu_search_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc, what):
+        if rc:
+            raise TspGpuError(rc, what)
+
+    def set_bound(self, bound: float):
+        self._check(lib().tspgpu_search_set_bound(self.handle, float(bound)), "tspgpu_search_set_bound")
+
+    def start(self):
+        """Seed this shard's live prefixes."""
+        self._check(lib().tspgpu_search_start(self.handle), "tspgpu_search_start")
+
+    def step(self) -> int:
+        """One round; returns the items pending for the next round."""
+        p = ctypes.c_uint64()
+        self._check(lib().tspgpu_search_step(self.handle, ctypes.byref(p)), "tspgpu_search_step")
+        return p.value
+
+    def run_all(self):
+        self._check(lib().tspgpu_search_run_all(self.handle), "tspgpu_search_run_all")
+
+    def timing(self):
+        ms, rounds = ctypes.c_double(), ctypes.c_int()
+        self._check(lib().tspgpu_search_timing(self.handle, ctypes.byref(ms), ctypes.byref(rounds)),
+                    "tspgpu_search_timing")
+        return ms.value, rounds.value
+
+    @property
+    def incumbent_ptr(self) -> int:
+        return lib().tspgpu_search_incumbent_device(self.handle)
+
+    def counters(self):
+        inc, nodes, recs = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
+        self._check(lib().tspgpu_search_counters(self.handle, ctypes.byref(inc), ctypes.byref(nodes),
+                                                 ctypes.byref(recs)), "tspgpu_search_counters")
+        return inc.value, nodes.value, recs.value
+
+    def reset_records(self, capacity: int = 0):
+        self._check(lib().tspgpu_search_reset_records(self.handle, capacity), "tspgpu_search_reset_records")
+
+    def records(self, bits: int):
+        """Recorded tours whose cost word equals `bits` (list of TourRecord)."""
+        cnt = ctypes.c_int()
+        rc = lib().tspgpu_search_records(self.handle, bits, None, 0, ctypes.byref(cnt))
+        if rc and rc != -errno.ENOSPC:
+            raise TspGpuError(rc, "tspgpu_search_records")
+        arr = (TourRecord * max(1, cnt.value))()
+        self._check(lib().tspgpu_search_records(self.handle, bits, arr, cnt.value, ctypes.byref(cnt)),
+                    "tspgpu_search_records")
+        return list(arr[:cnt.value])
+
+
+def search_solve(ctx: "Context", dist):
+    """One instance on one GPU: (cost, tour (n+1,), stats dict)."""
+    d, dt = _search_dist(dist)
+    n = d.shape[0]
+    cost = ctypes.c_double()
+    tour = np.zeros(n + 1, dtype=np.int32)
+    st = SearchStats()
+    rc = lib().tspgpu_search_solve(ctx.handle, d.ctypes.data, dt, n, ctypes.byref(cost), _ip(tour), ctypes.byref(st))
+    if rc:
+        raise TspGpuError(rc, "tspgpu_search_solve")
+    c = cost.value if dt == F64 else int(cost.value)
+    return c, tour, st.as_dict()
 
 
 def errno_name(code: int) -> str:
