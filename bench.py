@@ -174,6 +174,40 @@ def cpu_baseline(n, seconds_budget=20.0):
             "blocks_per_s": k / wall}
 
 
+def k2_single_instance(ctx, n, world, rank, local_rank, reps=3):
+    """K2 (prefix-parallel branch and bound, one instance over the whole GPU or,
+    with N ranks, sharded over N GPUs with an all-reduce MIN of the incumbent
+    between rounds over RCCL) on the reference's own instance `./tsp n 1 1000
+    1000`: time to the optimal tour and search nodes per second."""
+    import search_dist
+
+    blk = Shard(n, 1, 0, 1)
+    d = blk.distances()[0]
+    group, backend = None, "none"
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+
+        if torch.cuda.is_available():
+            torch.cuda.set_device(local_rank)
+            group, backend = dist.new_group(backend="nccl"), "nccl"
+        else:
+            group, backend = dist.new_group(backend="gloo"), "gloo"
+    best = None
+    for _ in range(reps):
+        t = time.perf_counter()
+        cost, tour, st = search_dist.solve_sharded(ctx, d, group=group)
+        wall = (time.perf_counter() - t) * 1e3
+        if best is None or wall < best[0]:
+            best = (wall, cost, tour, st)
+    wall, cost, tour, st = best
+    return {"instance": f"./tsp {n} 1 1000 1000 (block 0)", "cost": cost, "time_to_optimal_ms": wall,
+            "kernel_ms": st["kernel_ms"], "nodes": st["nodes"],
+            "nodes_per_s": st["nodes"] / max(st["kernel_ms"] * 1e-3, 1e-12), "rounds": st["rounds"],
+            "exchanges": st["exchanges"], "ranks": world, "exchange_backend": backend,
+            "optimal_tours": st["optimal_tours"], "tour": [int(x) for x in tour]}
+
+
 def pmc_traffic(n, blocks, timeout=90):
     """HBM bytes per launch of the dominant kernel from rocprofv3 PMC counters,
     one counter group per pass (MI355X_MICROARCH.md §HBM / rocprofv3 PMC slots):
@@ -229,6 +263,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pmc", action="store_true")
     ap.add_argument("--no-tto", action="store_true", help="skip the one-block time-to-optimal probe")
+    ap.add_argument("--no-k2", action="store_true", help="skip the K2 single-instance search probe")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
     if args.pmc_child:
@@ -288,6 +323,10 @@ def main():
             ctx.solve_device(d1, n, 1, c1, t1, stream)
         one_kernel_ms = ctx.timer_stop() / 10
 
+    k2 = None
+    if not args.no_k2:
+        k2 = k2_single_instance(ctx, n, world, rank, local_rank)
+
     if rank != 0:
         return
     alg_bytes = tspgpu.table_bytes_per_block(n) * Bp
@@ -327,6 +366,7 @@ def main():
                              f"(each DP entry written once, read once) x {Bp} blocks per launch / HIP-event "
                              f"launch time; traffic = PMC HBM bytes per launch ({traffic_note})"},
         "cpu_baseline": cpu,
+        "k2_single_instance": k2,
         "device": devname,
         "cus": cu,
     }
