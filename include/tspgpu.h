@@ -18,6 +18,9 @@
  *   -ENODEV  no HIP device / device ordinal out of range
  *   -ENOMEM  device allocation failed
  *   -EIO     a HIP runtime call or kernel launch failed
+ *   -EDEADLK (K3) the reference's mergeBlocks would never terminate for these paths
+ *            (its rotation loop, tsp.cpp:236-239, looks for a city that is not there)
+ *   -EOVERFLOW (K2) more optimal tours than can be enumerated, n > 20
  */
 #ifndef TSPGPU_H
 #define TSPGPU_H
@@ -202,6 +205,26 @@ int tspgpu_search_records(tspgpu_search *s, uint64_t cost_bits, tspgpu_tour_reco
 int tspgpu_heuristic_tour(const void *dist, int dtype, int n, double *cost_out, int32_t *tour_out);
 int tspgpu_select_tour(const void *dist, int dtype, int n, const tspgpu_tour_record *records, int count,
                        uint64_t cost_bits, int32_t *tour_out);
+
+/* ---------------------------------------------------------------------------
+ * K3: the reference's mergeBlocks (tsp.cpp:197-269) and its reduction tree
+ * (MPI_ManualReduce tsp.cpp:52-134 + the local fold tsp.cpp:348-352) with the
+ * paths on the GPU.  Same result as the reference bit for bit: the L1 x L2
+ * swap search runs on the device, near-minimal candidates are re-evaluated
+ * on the host with glibc pow (assignment2.h:141-144), the splice is a device
+ * gather.  Cities are the reference's City structs, paths include the
+ * closing city like BlockSolution.path.
+ * ------------------------------------------------------------------------- */
+/* mergeBlocks(p1, p2): out (L1+L2-1 cities), *cost_out = c1 + c2 + best swap.
+ * Returns the merged length, or a negative code. */
+int tspgpu_merge(tspgpu_ctx *ctx, const tspgpu_city *p1, int L1, double c1, const tspgpu_city *p2, int L2, double c2,
+                 tspgpu_city *out, double *cost_out);
+/* The distribution counts, every logical rank's left fold and the reduction
+ * tree for logical rank count nprocs, given each block's solution (paths of
+ * L cities, block-major).  Writes the final cost and the "process %i is about
+ * to receive %i cities from process %i" lines (tsp.cpp:88) into log. */
+int tspgpu_reduce(tspgpu_ctx *ctx, const tspgpu_city *paths, int L, const double *costs, int nblocks, int nprocs,
+                  double *final_cost, char *log, int logcap);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,441 @@
+// K3 — the reference's mergeBlocks (tsp.cpp:197-269) and its reduction tree
+// (tsp.cpp:52-134, 348-352) with the paths resident on the GPU.
+//
+// mergeBlocks looks for the pair of edges (A,B) of path 1 and (C,D) of path 2
+// (cyclic successors, the closing duplicate city included) with the smallest
+//     swapPairCost = ((d(A,D) + d(B,C)) - d(A,B)) - d(C,D)        (tsp.cpp:197-200)
+// first strict minimum in row-major (i, j) order from INT_MAX (tsp.cpp:204-227),
+// then splices path 2 (closing city dropped, rotated to start after C,
+// reversed) behind the first city of path 1 that is A or B (tsp.cpp:229-259).
+// The reference is O(L1 * L2^2) (it rotates a vector per step); the search is
+// an L1 x L2 argmin, i.e. GPU work once the running path grows (a rank folds
+// all its blocks into one path, so at ./tsp 16 16384 the fold alone is ~4e10
+// pair evaluations).
+//
+// Exactness.  d() is sqrt(pow(dx,2) + pow(dy,2)) with glibc pow, which differs
+// from dx*dx in ~0.08% of inputs, so the device cannot reproduce d() bit for
+// bit.  It computes every swap cost with dx*dx (a few ulp from the glibc
+// value) and keeps as candidates all pairs within 2*eps of its minimum, eps =
+// 2^-36 * 4 * Dmax (Dmax: the diagonal of the cities' bounding box) — about
+// 10^4 times the largest possible discrepancy.  The host re-evaluates the
+// candidates with glibc pow, in row-major order, with the reference's strict
+// <: the exact minimum and every pair tied with it are always among them.
+// If there are more candidates than the buffer holds, the host scans all
+// pairs itself.  The splice is a gather kernel; the first-occurrence searches
+// it needs are atomicMin reductions.  One host round trip per merge.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cerrno>
+#include <climits>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "ctx.h"
+#include "tspgpu.h"
+
+namespace {
+
+constexpr int kMergeThreads = 256;
+constexpr unsigned kCandCap = 1u << 16;
+
+struct Cand {
+    int i, j;
+    tspgpu_city a, b, c, d;
+};
+
+__device__ __forceinline__ double ddist(const tspgpu_city &p, const tspgpu_city &q)
+{
+    const double dx = p.x - q.x;
+    const double dy = p.y - q.y;
+    return sqrt(dx * dx + dy * dy);
+}
+
+__device__ __forceinline__ unsigned long long order_key(double v)
+{
+    const unsigned long long b = (unsigned long long)__double_as_longlong(v);
+    return (b >> 63) ? ~b : (b | 0x8000000000000000ull);
+}
+
+__host__ __device__ __forceinline__ double key_value(unsigned long long k)
+{
+    const unsigned long long b = (k >> 63) ? (k & 0x7fffffffffffffffull) : ~k;
+    return __builtin_bit_cast(double, b);
+}
+
+__device__ __forceinline__ double swap_cost(const tspgpu_city *c1, int L1, const tspgpu_city *c2, int L2,
+                                            unsigned long long q)
+{
+    const int i = (int)(q / (unsigned)L2), j = (int)(q % (unsigned)L2);
+    const tspgpu_city A = c1[i], B = c1[i + 1 == L1 ? 0 : i + 1];
+    const tspgpu_city C = c2[j], D = c2[j + 1 == L2 ? 0 : j + 1];
+    return ((ddist(A, D) + ddist(B, C)) - ddist(A, B)) - ddist(C, D);
+}
+
+// words[0]: min key; [1]: candidate count; [2]: first A/B in c1; [3]: first C in c2
+__global__ __launch_bounds__(kMergeThreads) void argmin_kernel(const tspgpu_city *c1, int L1, const tspgpu_city *c2,
+                                                               int L2, unsigned long long *words)
+{
+    const unsigned long long total = (unsigned long long)L1 * (unsigned)L2;
+    unsigned long long best = ~0ull;
+    for (unsigned long long q = blockIdx.x * (unsigned long long)kMergeThreads + threadIdx.x; q < total;
+         q += (unsigned long long)gridDim.x * kMergeThreads) {
+        const unsigned long long k = order_key(swap_cost(c1, L1, c2, L2, q));
+        best = k < best ? k : best;
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        const unsigned long long o = __shfl_xor(best, off);
+        best = o < best ? o : best;
+    }
+    if (__lane_id() == 0 && best != ~0ull) atomicMin(words, best);
+}
+
+__global__ __launch_bounds__(kMergeThreads) void cand_kernel(const tspgpu_city *c1, int L1, const tspgpu_city *c2,
+                                                             int L2, double eps2, unsigned long long *words,
+                                                             Cand *cand)
+{
+    const unsigned long long total = (unsigned long long)L1 * (unsigned)L2;
+    const double thr = key_value(words[0]) + eps2;
+    for (unsigned long long q = blockIdx.x * (unsigned long long)kMergeThreads + threadIdx.x; q < total;
+         q += (unsigned long long)gridDim.x * kMergeThreads) {
+        if (swap_cost(c1, L1, c2, L2, q) <= thr) {
+            const unsigned s = atomicAdd(reinterpret_cast<unsigned *>(words + 1), 1u);
+            if (s < kCandCap) {
+                const int i = (int)(q / (unsigned)L2), j = (int)(q % (unsigned)L2);
+                Cand c;
+                c.i = i;
+                c.j = j;
+                c.a = c1[i];
+                c.b = c1[i + 1 == L1 ? 0 : i + 1];
+                c.c = c2[j];
+                c.d = c2[j + 1 == L2 ? 0 : j + 1];
+                cand[s] = c;
+            }
+        }
+    }
+}
+
+// first index of c1 whose id is idA or idB, first index of c2[0..M) whose id is idC
+__global__ __launch_bounds__(kMergeThreads) void find_kernel(const tspgpu_city *c1, int L1, const tspgpu_city *c2,
+                                                             int M, int idA, int idB, int idC,
+                                                             unsigned long long *words)
+{
+    const int t = blockIdx.x * kMergeThreads + threadIdx.x;
+    const int stride = gridDim.x * kMergeThreads;
+    for (int i = t; i < L1; i += stride)
+        if (c1[i].id == idA || c1[i].id == idB) atomicMin(words + 2, (unsigned long long)i);
+    for (int j = t; j < M; j += stride)
+        if (c2[j].id == idC) atomicMin(words + 3, (unsigned long long)j);
+}
+
+// out = c1[0..p] ++ reverse(c2 rotated to start after C, closing city dropped) ++ c1[p+1..]
+__global__ __launch_bounds__(kMergeThreads) void splice_kernel(const tspgpu_city *c1, int L1, const tspgpu_city *c2,
+                                                               int M, const unsigned long long *words,
+                                                               tspgpu_city *out)
+{
+    const unsigned long long pw = words[2], sw = words[3];
+    if (pw >= (unsigned long long)L1 || sw >= (unsigned long long)M) return;  // host reports it
+    const int p = (int)pw, start = (int)((sw + 1) % (unsigned)M);
+    const int total = L1 + M;
+    for (int k = blockIdx.x * kMergeThreads + threadIdx.x; k < total; k += gridDim.x * kMergeThreads) {
+        tspgpu_city v;
+        if (k <= p)
+            v = c1[k];
+        else if (k <= p + M)
+            v = c2[(start + (M - 1 - (k - p - 1))) % M];
+        else
+            v = c1[k - M];
+        out[k] = v;
+    }
+}
+
+// ---- host side ---------------------------------------------------------------
+
+double (*volatile g_pow)(double, double) = ::pow;
+double (*volatile g_sqrt)(double) = ::sqrt;
+
+double hdist(const tspgpu_city &a, const tspgpu_city &b)
+{
+    return g_sqrt(g_pow(a.x - b.x, 2) + g_pow(a.y - b.y, 2));  // assignment2.h:141-144
+}
+
+double hswap(const tspgpu_city &A, const tspgpu_city &B, const tspgpu_city &C, const tspgpu_city &D)
+{
+    return ((hdist(A, D) + hdist(B, C)) - hdist(A, B)) - hdist(C, D);  // tsp.cpp:197-200
+}
+
+int herr(hipError_t e)
+{
+    if (e == hipSuccess) return 0;
+    if (e == hipErrorOutOfMemory) return -ENOMEM;
+    return -EIO;
+}
+
+struct DVec {
+    tspgpu_city *p = nullptr;
+    size_t len = 0, cap = 0;
+    int reserve(size_t n, hipStream_t st)
+    {
+        if (n <= cap) return 0;
+        size_t c = std::max<size_t>(n, cap * 2 + 64);
+        tspgpu_city *q = nullptr;
+        hipError_t e = hipMalloc((void **)&q, c * sizeof(tspgpu_city));
+        if (e != hipSuccess) return herr(e);
+        if (len) e = hipMemcpyAsync(q, p, len * sizeof(tspgpu_city), hipMemcpyDeviceToDevice, st);
+        if (e == hipSuccess) e = hipStreamSynchronize(st);
+        if (p) (void)hipFree(p);
+        p = q;
+        cap = c;
+        return herr(e);
+    }
+    void release()
+    {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        len = cap = 0;
+    }
+};
+
+struct Merger {
+    hipStream_t st = nullptr;
+    int cus = 256;
+    double eps2 = 0.0;
+    unsigned long long *words = nullptr;  // device
+    unsigned long long *hwords = nullptr; // pinned host
+    Cand *cand = nullptr;
+    std::vector<Cand> hc;
+    DVec tmp;
+    int init(tspgpu_ctx *c, double dmax)
+    {
+        st = c->stream;
+        cus = c->cu_count;
+        eps2 = 2.0 * std::ldexp(4.0 * dmax, -36);
+        hipError_t e = hipMalloc((void **)&words, 4 * sizeof(unsigned long long));
+        if (e == hipSuccess) e = hipHostMalloc((void **)&hwords, 4 * sizeof(unsigned long long), 0);
+        if (e == hipSuccess) e = hipMalloc((void **)&cand, kCandCap * sizeof(Cand));
+        return herr(e);
+    }
+    ~Merger()
+    {
+        if (words) (void)hipFree(words);
+        if (hwords) (void)hipHostFree(hwords);
+        if (cand) (void)hipFree(cand);
+        tmp.release();
+    }
+    int grid_for(unsigned long long work) const
+    {
+        const unsigned long long b = (work + kMergeThreads - 1) / kMergeThreads;
+        return (int)std::max<unsigned long long>(1, std::min<unsigned long long>(b, (unsigned long long)cus * 8));
+    }
+    // s1 <- mergeBlocks(s1, c2); returns 0, -EDEADLK if the reference would not terminate, or -errno
+    int merge(DVec &s1, double &cost1, const tspgpu_city *c2, int L2, double cost2)
+    {
+        const int L1 = (int)s1.len;
+        if (L1 < 1 || L2 < 2) return -EINVAL;
+        const unsigned long long init[4] = {~0ull, 0ull, ~0ull, ~0ull};
+        hipError_t e = hipMemcpyAsync(words, init, sizeof init, hipMemcpyHostToDevice, st);
+        if (e != hipSuccess) return herr(e);
+        const unsigned long long pairs = (unsigned long long)L1 * (unsigned)L2;
+        const int g = grid_for(pairs);
+        hipLaunchKernelGGL(argmin_kernel, dim3(g), dim3(kMergeThreads), 0, st, s1.p, L1, c2, L2, words);
+        hipLaunchKernelGGL(cand_kernel, dim3(g), dim3(kMergeThreads), 0, st, s1.p, L1, c2, L2, eps2, words, cand);
+        e = hipMemcpyAsync(hwords, words, 2 * sizeof(unsigned long long), hipMemcpyDeviceToHost, st);
+        if (e == hipSuccess) e = hipStreamSynchronize(st);
+        if (e != hipSuccess) return herr(e);
+        const unsigned nc = (unsigned)hwords[1];
+        double best = (double)INT_MAX;  // tsp.cpp:204
+        int bi = -1, bj = -1;
+        tspgpu_city A{}, B{}, C{};
+        if (nc > 0 && nc <= kCandCap) {
+            hc.resize(nc);
+            e = hipMemcpy(hc.data(), cand, nc * sizeof(Cand), hipMemcpyDeviceToHost);
+            if (e != hipSuccess) return herr(e);
+            std::sort(hc.begin(), hc.end(), [](const Cand &x, const Cand &y) {
+                return x.i != y.i ? x.i < y.i : x.j < y.j;
+            });
+            for (const Cand &k : hc) {
+                const double sc = hswap(k.a, k.b, k.c, k.d);
+                if (sc < best) {
+                    best = sc;
+                    bi = k.i;
+                    bj = k.j;
+                    A = k.a;
+                    B = k.b;
+                    C = k.c;
+                }
+            }
+        } else {
+            // too many near-ties for the buffer: exact scan on the host
+            std::vector<tspgpu_city> h1(L1), h2(L2);
+            e = hipMemcpy(h1.data(), s1.p, L1 * sizeof(tspgpu_city), hipMemcpyDeviceToHost);
+            if (e == hipSuccess) e = hipMemcpy(h2.data(), c2, L2 * sizeof(tspgpu_city), hipMemcpyDeviceToHost);
+            if (e != hipSuccess) return herr(e);
+            for (int i = 0; i < L1; ++i)
+                for (int j = 0; j < L2; ++j) {
+                    const tspgpu_city &a = h1[i], &b = h1[(i + 1) % L1], &c = h2[j], &d = h2[(j + 1) % L2];
+                    const double sc = hswap(a, b, c, d);
+                    if (sc < best) {
+                        best = sc;
+                        bi = i;
+                        bj = j;
+                        A = a;
+                        B = b;
+                        C = c;
+                    }
+                }
+        }
+        if (bi < 0) return -EIO;  // no swap below INT_MAX (distances are validated far below)
+        const int M = L2 - 1;
+        int rc = tmp.reserve((size_t)L1 + M, st);
+        if (rc) return rc;
+        const int gf = grid_for((unsigned long long)std::max(L1, M));
+        hipLaunchKernelGGL(find_kernel, dim3(gf), dim3(kMergeThreads), 0, st, s1.p, L1, c2, M, A.id, B.id, C.id,
+                           words);
+        hipLaunchKernelGGL(splice_kernel, dim3(grid_for((unsigned long long)L1 + M)), dim3(kMergeThreads), 0, st,
+                           s1.p, L1, c2, M, words, tmp.p);
+        e = hipMemcpyAsync(hwords + 2, words + 2, 2 * sizeof(unsigned long long), hipMemcpyDeviceToHost, st);
+        if (e == hipSuccess) e = hipStreamSynchronize(st);
+        if (e != hipSuccess) return herr(e);
+        if (hwords[3] >= (unsigned long long)M) return -EDEADLK;  // C not in path 2: tsp.cpp:236-239 never ends
+        if (hwords[2] >= (unsigned long long)L1) return -EIO;
+        std::swap(s1, tmp);
+        s1.len = (size_t)L1 + M;
+        tmp.len = 0;
+        cost1 = cost1 + cost2 + best;  // tsp.cpp:263
+        (void)bj;
+        return 0;
+    }
+};
+
+double bbox_diagonal(const tspgpu_city *c, size_t n)
+{
+    double x0 = INFINITY, x1 = -INFINITY, y0 = INFINITY, y1 = -INFINITY;
+    for (size_t i = 0; i < n; ++i) {
+        x0 = std::min(x0, c[i].x);
+        x1 = std::max(x1, c[i].x);
+        y0 = std::min(y0, c[i].y);
+        y1 = std::max(y1, c[i].y);
+    }
+    if (!(x1 >= x0) || !(y1 >= y0)) return 0.0;
+    return std::sqrt((x1 - x0) * (x1 - x0) + (y1 - y0) * (y1 - y0)) * (1.0 + 1e-9) + 1e-300;
+}
+
+bool finite_cities(const tspgpu_city *c, size_t n)
+{
+    for (size_t i = 0; i < n; ++i)
+        if (!std::isfinite(c[i].x) || !std::isfinite(c[i].y)) return false;
+    return true;
+}
+
+}  // namespace
+
+extern "C" {
+
+int tspgpu_merge(tspgpu_ctx *ctx, const tspgpu_city *p1, int L1, double c1, const tspgpu_city *p2, int L2, double c2,
+                 tspgpu_city *out, double *cost_out)
+{
+    if (!ctx || !p1 || !p2 || !out || !cost_out || L1 < 1 || L2 < 2) return -EINVAL;
+    if (!finite_cities(p1, L1) || !finite_cities(p2, L2)) return -EINVAL;
+    std::lock_guard<std::mutex> g(ctx->mu);
+    if (hipSetDevice(ctx->device) != hipSuccess) return -ENODEV;
+    std::vector<tspgpu_city> all(p1, p1 + L1);
+    all.insert(all.end(), p2, p2 + L2);
+    Merger m;
+    int rc = m.init(ctx, bbox_diagonal(all.data(), all.size()));
+    DVec s, b;
+    if (!rc) rc = s.reserve(L1, m.st);
+    if (!rc) rc = b.reserve(L2, m.st);
+    hipError_t e = hipSuccess;
+    if (!rc) e = hipMemcpyAsync(s.p, p1, L1 * sizeof(tspgpu_city), hipMemcpyHostToDevice, m.st);
+    if (!rc && e == hipSuccess) e = hipMemcpyAsync(b.p, p2, L2 * sizeof(tspgpu_city), hipMemcpyHostToDevice, m.st);
+    if (!rc) rc = herr(e);
+    s.len = L1;
+    double cost = c1;
+    if (!rc) rc = m.merge(s, cost, b.p, L2, c2);
+    if (!rc) rc = herr(hipMemcpy(out, s.p, s.len * sizeof(tspgpu_city), hipMemcpyDeviceToHost));
+    const int len = (int)s.len;
+    s.release();
+    b.release();
+    if (rc) return rc;
+    *cost_out = cost;
+    return len;
+}
+
+int tspgpu_reduce(tspgpu_ctx *ctx, const tspgpu_city *paths, int L, const double *costs, int nblocks, int nprocs,
+                  double *final_cost, char *log, int logcap)
+{
+    if (log && logcap > 0) log[0] = 0;
+    if (!ctx || !paths || !costs || !final_cost) return -EINVAL;
+    if (nblocks < 1 || nprocs < 1 || nblocks < nprocs || L < 2) return -EINVAL;
+    const size_t ncity = (size_t)nblocks * L;
+    if (!finite_cities(paths, ncity)) return -EINVAL;
+    std::lock_guard<std::mutex> g(ctx->mu);
+    if (hipSetDevice(ctx->device) != hipSuccess) return -ENODEV;
+    Merger m;
+    int rc = m.init(ctx, bbox_diagonal(paths, ncity));
+    if (rc) return rc;
+    DVec blocks;
+    rc = blocks.reserve(ncity, m.st);
+    if (!rc) rc = herr(hipMemcpy(blocks.p, paths, ncity * sizeof(tspgpu_city), hipMemcpyHostToDevice));
+    blocks.len = ncity;
+    // distributeBlocks' counts (tsp.cpp:167-192): rank r gets #{b in [1,B] : b mod P == r}
+    std::vector<int> cnt(nprocs, 0);
+    for (int b = nblocks; b > 0; --b) cnt[b % nprocs]++;
+    // each logical rank folds its contiguous block range left (tsp.cpp:348-352)
+    std::vector<DVec> rank(nprocs), received(nprocs);
+    std::vector<double> rcost(nprocs, 0.0);
+    int next = 0;
+    for (int r = 0; r < nprocs && !rc; ++r) {
+        rc = rank[r].reserve((size_t)L * cnt[r], m.st);
+        if (rc) break;
+        rc = herr(hipMemcpyAsync(rank[r].p, blocks.p + (size_t)next * L, L * sizeof(tspgpu_city),
+                                 hipMemcpyDeviceToDevice, m.st));
+        rank[r].len = L;
+        rcost[r] = costs[next];
+        ++next;
+        for (int j = 1; j < cnt[r] && !rc; ++j, ++next)
+            rc = m.merge(rank[r], rcost[r], blocks.p + (size_t)next * L, L, costs[next]);
+    }
+    // MPI_ManualReduce (tsp.cpp:52-134): the receiver appends every received
+    // path to one function-local list and merges with the WHOLE list
+    // (tsp.cpp:67,93-98,115-120)
+    std::string text;
+    auto receive = [&](int to, int from) -> int {
+        DVec &acc = received[to];
+        const size_t add = rank[from].len;
+        int r2 = acc.reserve(acc.len + add, m.st);
+        if (r2) return r2;
+        r2 = herr(hipMemcpyAsync(acc.p + acc.len, rank[from].p, add * sizeof(tspgpu_city), hipMemcpyDeviceToDevice,
+                                 m.st));
+        if (r2) return r2;
+        acc.len += add;
+        return m.merge(rank[to], rcost[to], acc.p, (int)acc.len, rcost[from]);
+    };
+    const int lastpower = 1 << (int)std::log2((double)nprocs);
+    for (int i = 0; i < nprocs - lastpower && !rc; ++i) {
+        char line[128];
+        std::snprintf(line, sizeof line, "process %i is about to receive %i cities from process %i\n", i,
+                      (int)rank[i + lastpower].len, i + lastpower);  // tsp.cpp:88
+        text += line;
+        rc = receive(i, i + lastpower);
+    }
+    for (int d = 0; d < (int)std::log2((double)lastpower) && !rc; ++d)
+        for (int k = 0; k < lastpower && !rc; k += 1 << (d + 1)) rc = receive(k, k + (1 << d));
+    for (auto &v : rank) v.release();
+    for (auto &v : received) v.release();
+    blocks.release();
+    if (rc) return rc;
+    *final_cost = rcost[0];
+    if (log && logcap > 0) {
+        const size_t k = std::min(text.size(), (size_t)logcap - 1);
+        std::memcpy(log, text.data(), k);
+        log[k] = 0;
+    }
+    return 0;
+}
+
+}  // extern "C"

@@ -209,6 +209,9 @@ const char *tspgpu_strerror(int code)
     case -ENODEV: return "no usable HIP device";
     case -ENOMEM: return "device allocation failed";
     case -EIO: return "HIP runtime or kernel launch failure";
+    case -EDEADLK: return "the reference's mergeBlocks would never terminate for these paths";
+    case -EOVERFLOW: return "too many optimal tours to enumerate (n > 20)";
+    case -ENOSPC: return "output buffer too small";
     default: return "unknown error";
     }
 }

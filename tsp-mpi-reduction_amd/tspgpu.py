@@ -30,6 +30,8 @@ EXPORTED_SYMBOLS = (
     "tspgpu_search_timing", "tspgpu_search_incumbent_device",
     "tspgpu_search_counters", "tspgpu_search_reset_records", "tspgpu_search_records", "tspgpu_heuristic_tour",
     "tspgpu_select_tour",
+    # K3
+    "tspgpu_merge", "tspgpu_reduce",
 )
 
 F64, I32 = 0, 1
@@ -125,6 +127,10 @@ def lib():
         L.tspgpu_heuristic_tour.argtypes = [vp, ctypes.c_int, ctypes.c_int, dp, ip]
         L.tspgpu_select_tour.argtypes = [vp, ctypes.c_int, ctypes.c_int, ctypes.POINTER(TourRecord), ctypes.c_int,
                                          ctypes.c_uint64, ip]
+        cp = ctypes.POINTER(City)
+        L.tspgpu_merge.argtypes = [vp, cp, ctypes.c_int, ctypes.c_double, cp, ctypes.c_int, ctypes.c_double, cp, dp]
+        L.tspgpu_reduce.argtypes = [vp, cp, ctypes.c_int, dp, ctypes.c_int, ctypes.c_int, dp, ctypes.c_char_p,
+                                    ctypes.c_int]
         _lib = L
     return _lib
 
@@ -282,6 +288,29 @@ class Context:
         ms = ctypes.c_float()
         self._check(lib().tspgpu_timer_stop(self.handle, ctypes.byref(ms)), "tspgpu_timer_stop")
         return ms.value
+
+    def merge(self, p1, c1, p2, c2):
+        """K3 mergeBlocks: paths are lists of (id, x, y) -> (merged path, cost)."""
+        a1, _, _ = cities_array([p1])
+        a2, _, _ = cities_array([p2])
+        out = (City * (len(p1) + len(p2)))()
+        cost = ctypes.c_double()
+        rc = lib().tspgpu_merge(self.handle, a1, len(p1), c1, a2, len(p2), c2, out, ctypes.byref(cost))
+        if rc < 0:
+            raise TspGpuError(rc, "tspgpu_merge")
+        return [(out[i].id, out[i].x, out[i].y) for i in range(rc)], cost.value
+
+    def reduce(self, paths, costs, nprocs: int):
+        """K3 reduction: paths (B lists of L cities), costs (B,) -> (final cost, log text)."""
+        B, L = len(paths), len(paths[0])
+        flat, _, _ = cities_array(paths)
+        c = np.ascontiguousarray(costs, dtype=np.float64)
+        final = ctypes.c_double()
+        log = ctypes.create_string_buffer(1 << 20)
+        rc = lib().tspgpu_reduce(self.handle, flat, L, _dp(c), B, nprocs, ctypes.byref(final), log, len(log))
+        if rc:
+            raise TspGpuError(rc, "tspgpu_reduce")
+        return final.value, log.value.decode()
 
     def device_info(self):
         cu = ctypes.c_int()
