@@ -272,6 +272,7 @@ __global__ __launch_bounds__(kSearchThreads) void round_kernel(SearchArgs a)
                     fl = (uint32_t)c1 + 1u;
                 }
             }
+            // the host sizes the output for (N-1) items per input item: always room
             unsigned int slot = cnt ? atomicAdd(a.out_count, cnt) : 0u;
             rl = rem;
             fl = from;

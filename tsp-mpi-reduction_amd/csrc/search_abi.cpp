@@ -369,10 +369,12 @@ static SearchArgs args_of(tspgpu_search *s)
 static int ensure_items(tspgpu_search *s, int which, size_t count)
 {
     if (s->item_cap[which] >= count && s->d_items[which]) return 0;
+    // grow geometrically (up to 2^27 items) so that rounds rarely reallocate
+    const size_t cap = std::max<size_t>(std::max<size_t>(count, 1024),
+                                        std::min<size_t>(2 * s->item_cap[which], (size_t)1 << 27));
     if (s->d_items[which]) (void)hipFree(s->d_items[which]);
     s->d_items[which] = nullptr;
     s->item_cap[which] = 0;
-    const size_t cap = std::max<size_t>(count, 1024);
     hipError_t e = hipMalloc((void **)&s->d_items[which], cap * sizeof(SearchItem));
     if (e != hipSuccess) return herr(e);
     s->item_cap[which] = cap;
@@ -424,17 +426,29 @@ int tspgpu_search_step(tspgpu_search *s, uint64_t *pending)
     }
     (void)hipSetDevice(s->ctx->device);
     const int in = s->cur, out = 1 - s->cur;
-    // every item hands back at most one item per level of its stack
-    int rc = ensure_items(s, out, (size_t)s->pending * (size_t)(s->n - 1) + 64);
+    // A round takes at most kMaxRound input items; every item hands back at
+    // most one item per level of its stack (N-1), so the output always has
+    // room for them plus the inputs carried over to the next round.
+    constexpr uint64_t kMaxRound = (uint64_t)1 << 22;
+    const uint64_t take = std::min<uint64_t>(s->pending, kMaxRound);
+    const uint64_t carry = s->pending - take;
+    int rc = ensure_items(s, out, (size_t)(take * (uint64_t)(s->n - 1) + carry + 64));
     if (rc) return rc;
     SearchArgs a = args_of(s);
     a.in = s->d_items[in];
-    a.in_count = (uint32_t)s->pending;
+    a.in_count = (uint32_t)take;
     a.out = s->d_items[out];
-    const uint64_t blocks = (s->pending + kSearchThreads - 1) / kSearchThreads;
+    const uint64_t blocks = (take + kSearchThreads - 1) / kSearchThreads;
     const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>(blocks, (uint64_t)s->grid));
     rc = launch_and_count(s, false, grid, a);
     if (rc) return rc;
+    if (carry) {  // inputs this round did not take: behind the spilled items
+        hipError_t e = hipMemcpyAsync(s->d_items[out] + s->pending, s->d_items[in] + take, carry * sizeof(SearchItem),
+                                      hipMemcpyDeviceToDevice, s->ctx->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(s->ctx->stream);
+        if (e != hipSuccess) return herr(e);
+        s->pending += carry;
+    }
     s->cur = out;
     ++s->rounds;
     if (pending) *pending = s->pending;

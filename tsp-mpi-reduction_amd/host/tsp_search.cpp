@@ -1,0 +1,354 @@
+// `tsp_search` — exact search of ONE instance on 1..G MI355X GPUs (K2), with
+// the extension inputs the reference's CLI cannot express (BASELINE.json
+// configs 1, 4 and 5):
+//
+//   tsp_search --random N [--seed S] [--clustered K]     uniform (or K Gaussian
+//                                                         clusters) cities in [0,1000)^2
+//   tsp_search --cities FILE [--tsplib-round]            "id x y" lines, or a TSPLIB
+//                                                         file with NODE_COORD_SECTION
+//   tsp_search --matrix FILE                              n, then n*n distances (all
+//                                                         integers -> integer mode)
+//   options: --gpus G (devices 0..G-1)  --solver auto|k1|k2  --verify (K2 with n <= 20: K1 too)
+//
+// City distances are the reference's computeDistanceMatrix (assignment2.h:
+// 184-200, glibc pow/sqrt, f64); --tsplib-round uses TSPLIB's EUC_2D nint()
+// instead (integer mode).  The answer is the reference's: the optimal
+// left-fold cost and the DP's tie-broken tour.
+//
+// Multi-GPU: one host thread and one context per device; shard g of G seeds
+// the prefixes p = g mod G; after every round the incumbent word is combined
+// in place with an RCCL all-reduce MIN (uint64, over xGMI), and the final
+// optimum is that all-reduce's result; the optimal records of all shards then
+// go through tspgpu_select_tour.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <atomic>
+#include <barrier>
+#include <cerrno>
+#include <chrono>
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <sstream>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "tspgpu.h"
+
+namespace {
+
+[[noreturn]] void die(const char *msg)
+{
+    std::fprintf(stderr, "tsp_search: %s\n", msg);
+    std::exit(2);
+}
+
+uint64_t splitmix(uint64_t &s)
+{
+    uint64_t z = (s += 0x9e3779b97f4a7c15ull);
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+    z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+    return z ^ (z >> 31);
+}
+double uniform(uint64_t &s) { return (double)(splitmix(s) >> 11) * 0x1p-53; }
+
+struct Instance {
+    int n = 0;
+    int dtype = TSPGPU_F64;
+    std::vector<double> d;
+    std::vector<int32_t> di;
+    std::string what;
+};
+
+std::vector<tspgpu_city> random_cities(int n, uint64_t seed, int clusters)
+{
+    std::vector<tspgpu_city> c(n);
+    uint64_t s = seed;
+    std::vector<double> cx(clusters > 0 ? clusters : 0), cy(cx.size());
+    for (size_t k = 0; k < cx.size(); ++k) {
+        cx[k] = 100.0 + 800.0 * uniform(s);
+        cy[k] = 100.0 + 800.0 * uniform(s);
+    }
+    for (int i = 0; i < n; ++i) {
+        c[i].id = i;
+        if (clusters > 0) {
+            // Box-Muller, sigma = 0.05 * grid
+            const int k = i % clusters;
+            const double u1 = 1.0 - uniform(s), u2 = uniform(s);
+            const double r = std::sqrt(-2.0 * std::log(u1)) * 50.0;
+            c[i].x = cx[k] + r * std::cos(2.0 * M_PI * u2);
+            c[i].y = cy[k] + r * std::sin(2.0 * M_PI * u2);
+        } else {
+            c[i].x = 1000.0 * uniform(s);
+            c[i].y = 1000.0 * uniform(s);
+        }
+    }
+    return c;
+}
+
+std::vector<tspgpu_city> read_cities(const char *path)
+{
+    std::ifstream f(path);
+    if (!f) die("cannot open the cities file");
+    std::vector<tspgpu_city> c;
+    std::string line;
+    bool tsplib = false, in_coords = false;
+    while (std::getline(f, line)) {
+        if (line.find("NODE_COORD_SECTION") != std::string::npos) {
+            tsplib = in_coords = true;
+            continue;
+        }
+        if (line.find("EOF") == 0) break;
+        if (tsplib && !in_coords) continue;
+        if (!tsplib && (line.find(':') != std::string::npos)) {  // a TSPLIB header line
+            tsplib = true;
+            continue;
+        }
+        std::istringstream ss(line);
+        tspgpu_city t{};
+        double id;
+        if (ss >> id >> t.x >> t.y) {
+            t.id = (int)c.size();
+            c.push_back(t);
+        }
+    }
+    if (c.size() < 3) die("need at least 3 cities");
+    return c;
+}
+
+Instance from_cities(const std::vector<tspgpu_city> &c, bool tsplib_round)
+{
+    Instance in;
+    in.n = (int)c.size();
+    in.d.resize((size_t)in.n * in.n);
+    if (int rc = tspgpu_distance_matrix(c.data(), in.n, 1, in.d.data())) die(tspgpu_strerror(rc));
+    if (tsplib_round) {
+        in.dtype = TSPGPU_I32;
+        in.di.resize(in.d.size());
+        for (size_t i = 0; i < in.d.size(); ++i) in.di[i] = (int32_t)std::lround(in.d[i]);  // TSPLIB nint
+    }
+    return in;
+}
+
+Instance read_matrix(const char *path)
+{
+    std::ifstream f(path);
+    if (!f) die("cannot open the matrix file");
+    Instance in;
+    if (!(f >> in.n) || in.n < 3) die("matrix file: first token must be n >= 3");
+    std::vector<std::string> tok((size_t)in.n * in.n);
+    bool integral = true;
+    for (auto &t : tok) {
+        if (!(f >> t)) die("matrix file: fewer than n*n entries");
+        if (t.find_first_of(".eE") != std::string::npos) integral = false;
+    }
+    if (integral) {
+        in.dtype = TSPGPU_I32;
+        in.di.resize(tok.size());
+        for (size_t i = 0; i < tok.size(); ++i) in.di[i] = (int32_t)std::strtol(tok[i].c_str(), nullptr, 10);
+    } else {
+        in.d.resize(tok.size());
+        for (size_t i = 0; i < tok.size(); ++i) in.d[i] = std::strtod(tok[i].c_str(), nullptr);
+    }
+    return in;
+}
+
+const void *dist_ptr(const Instance &in) { return in.dtype == TSPGPU_F64 ? (const void *)in.d.data() : in.di.data(); }
+
+struct Result {
+    double cost = 0.0;
+    std::vector<int32_t> tour;
+    uint64_t nodes = 0;
+    double kernel_ms = 0.0;
+    int rounds = 0;
+};
+
+// K2 over G GPUs of this process, RCCL all-reduce MIN of the incumbent between rounds.
+int search_multi(const Instance &in, int G, Result &res)
+{
+    // one RCCL communicator per GPU (a single GPU needs none)
+    std::vector<ncclComm_t> comms(G > 1 ? G : 0);
+    std::vector<int> devs(G);
+    for (int g = 0; g < G; ++g) devs[g] = g;
+    if (G > 1 && ncclCommInitAll(comms.data(), G, devs.data()) != ncclSuccess) die("RCCL initialisation failed");
+    double ub = 0.0;
+    if (int rc = tspgpu_heuristic_tour(dist_ptr(in), in.dtype, in.n, &ub, nullptr)) return rc;
+    std::vector<int> rcs(G, 0);
+    std::vector<std::vector<tspgpu_tour_record>> recs(G);
+    std::vector<uint64_t> nodes(G, 0), opt(G, 0);
+    std::vector<double> ms(G, 0.0);
+    std::vector<int> rounds(G, 0);
+    std::atomic<int> busy{0}, failed{0};
+    std::barrier sync(G);
+    std::vector<std::thread> th;
+    for (int g = 0; g < G; ++g) {
+        th.emplace_back([&, g] {
+            tspgpu_opts o;
+            std::memset(&o, 0, sizeof o);
+            o.device = g;
+            tspgpu_ctx *ctx = nullptr;
+            tspgpu_search *s = nullptr;
+            int rc = tspgpu_ctx_create(&o, &ctx);
+            if (!rc) rc = tspgpu_search_create(ctx, dist_ptr(in), in.dtype, in.n, g, G, 0, &s);
+            if (!rc) rc = tspgpu_search_set_bound(s, ub);
+            if (!rc) rc = tspgpu_search_start(s);
+            hipStream_t st = ctx ? (hipStream_t)tspgpu_stream(ctx) : nullptr;
+            // every shard must join every all-reduce: if one could not start, none enters the loop
+            if (rc) failed.store(1);
+            sync.arrive_and_wait();
+            uint64_t pending = 1;
+            for (; !failed.load();) {
+                if (!rc && pending) rc = tspgpu_search_step(s, &pending);
+                busy.fetch_add(!rc && pending ? 1 : 0);
+                // incumbent exchange: in-place RCCL all-reduce MIN on the device word
+                void *w = s ? tspgpu_search_incumbent_device(s) : nullptr;
+                if (G > 1 && w && ncclAllReduce(w, w, 1, ncclUint64, ncclMin, comms[g], st) != ncclSuccess) rc = -EIO;
+                if (st) (void)hipStreamSynchronize(st);
+                sync.arrive_and_wait();
+                const bool more = busy.load() > 0;
+                sync.arrive_and_wait();
+                if (g == 0) busy.store(0);
+                sync.arrive_and_wait();
+                if (!more) break;
+            }
+            uint64_t inc = 0, rec = 0;
+            if (!rc && failed.load()) rc = -EIO;
+            if (!rc) rc = tspgpu_search_counters(s, &inc, &nodes[g], &rec);
+            opt[g] = inc;  // identical on every shard after the last all-reduce
+            if (!rc) {
+                int cnt = 0;
+                recs[g].resize(rec);
+                rc = tspgpu_search_records(s, inc, recs[g].data(), (int)rec, &cnt);
+                recs[g].resize(cnt);
+            }
+            if (s) tspgpu_search_timing(s, &ms[g], &rounds[g]);
+            if (s) tspgpu_search_destroy(s);
+            if (ctx) tspgpu_ctx_destroy(ctx);
+            rcs[g] = rc;
+        });
+    }
+    for (auto &t : th) t.join();
+    for (auto &c : comms) ncclCommDestroy(c);
+    for (int rc : rcs)
+        if (rc) return rc;  // incl. -EOVERFLOW (too many tied optima: use --solver k1)
+    std::vector<tspgpu_tour_record> all;
+    for (auto &r : recs) all.insert(all.end(), r.begin(), r.end());
+    res.tour.assign(in.n + 1, 0);
+    if (int rc = tspgpu_select_tour(dist_ptr(in), in.dtype, in.n, all.data(), (int)all.size(), opt[0],
+                                    res.tour.data()))
+        return rc;
+    if (in.dtype == TSPGPU_F64)
+        std::memcpy(&res.cost, &opt[0], 8);
+    else
+        res.cost = (double)(int32_t)(uint32_t)opt[0];
+    for (int g = 0; g < G; ++g) {
+        res.nodes += nodes[g];
+        res.kernel_ms = std::max(res.kernel_ms, ms[g]);
+        res.rounds = std::max(res.rounds, rounds[g]);
+    }
+    return 0;
+}
+
+int solve_k1(const Instance &in, Result &res)
+{
+    if (in.n > TSPGPU_MAX_CITIES) return -EINVAL;
+    std::vector<double> d = in.d;
+    if (in.dtype == TSPGPU_I32) d.assign(in.di.begin(), in.di.end());
+    res.tour.assign(in.n + 1, -1);
+    tspgpu_opts o;
+    std::memset(&o, 0, sizeof o);
+    return tspgpu_solve(d.data(), in.n, 1, &res.cost, res.tour.data(), &o);
+}
+
+}  // namespace
+
+int main(int argc, char **argv)
+{
+    Instance in;
+    bool have = false, verify = false, tsplib_round = false;
+    int gpus = 1, random_n = 0, clusters = 0;
+    uint64_t seed = 1;
+    std::string solver = "auto", cities_file, matrix_file;
+    for (int i = 1; i < argc; ++i) {
+        const std::string a = argv[i];
+        auto next = [&]() -> const char * {
+            if (i + 1 >= argc) die("missing value");
+            return argv[++i];
+        };
+        if (a == "--random") random_n = std::atoi(next());
+        else if (a == "--seed") seed = std::strtoull(next(), nullptr, 10);
+        else if (a == "--clustered") clusters = std::atoi(next());
+        else if (a == "--cities") cities_file = next();
+        else if (a == "--matrix") matrix_file = next();
+        else if (a == "--tsplib-round") tsplib_round = true;
+        else if (a == "--gpus") gpus = std::atoi(next());
+        else if (a == "--solver") solver = next();
+        else if (a == "--verify") verify = true;
+        else {
+            std::fprintf(stderr, "usage: tsp_search (--random N [--seed S] [--clustered K] | --cities FILE "
+                                 "[--tsplib-round] | --matrix FILE) [--gpus G] [--solver auto|k1|k2] [--verify]\n");
+            return 1;
+        }
+    }
+    if (random_n) {
+        if (random_n < 3 || random_n > TSPGPU_SEARCH_MAX_CITIES) die("--random N needs 3 <= N <= 32");
+        in = from_cities(random_cities(random_n, seed, clusters), tsplib_round);
+        have = true;
+    } else if (!cities_file.empty()) {
+        in = from_cities(read_cities(cities_file.c_str()), tsplib_round);
+        have = true;
+    } else if (!matrix_file.empty()) {
+        in = read_matrix(matrix_file.c_str());
+        have = true;
+    }
+    if (!have) die("no instance (--random, --cities or --matrix)");
+    if (gpus < 1) gpus = 1;
+    // auto: the DP (K1) up to 20 cities on one GPU — far fewer operations than
+    // branch and bound there — else the search (K2) over all GPUs
+    if (solver == "auto") solver = (in.n <= TSPGPU_MAX_CITIES && gpus == 1) ? "k1" : "k2";
+    if (solver != "k1" && solver != "k2") die("--solver must be auto, k1 or k2");
+
+    Result res;
+    const auto t0 = std::chrono::steady_clock::now();
+    int rc = solver == "k1" ? solve_k1(in, res) : search_multi(in, gpus, res);
+    if (rc == -EOVERFLOW && in.n <= TSPGPU_MAX_CITIES) {
+        // more tied optima than the record buffers hold (e.g. coincident cities):
+        // the DP (K1) returns the same tour directly
+        std::fprintf(stderr, "tsp_search: too many tied optimal tours to enumerate; answering with K1\n");
+        solver = "k1";
+        rc = solve_k1(in, res);
+    }
+    const double wall = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    if (rc) {
+        std::fprintf(stderr, "tsp_search: %s (%d)\n", tspgpu_strerror(rc), rc);
+        return 3;
+    }
+    std::printf("cities %d  mode %s  solver %s  gpus %d\n", in.n, in.dtype == TSPGPU_F64 ? "f64" : "i32",
+                solver.c_str(), solver == "k1" ? 1 : gpus);
+    std::printf("optimal cost %.17g (%f)\n", res.cost, res.cost);
+    std::printf("tour");
+    for (int t : res.tour) std::printf(" %d", t);
+    std::printf("\n");
+    if (solver != "k1")
+        std::printf("search nodes %llu  rounds %d  kernel %.3f ms  %.3f Gnodes/s  wall %.3f ms\n",
+                    (unsigned long long)res.nodes, res.rounds, res.kernel_ms,
+                    res.kernel_ms > 0 ? res.nodes / res.kernel_ms / 1e6 : 0.0, wall);
+    else
+        std::printf("wall %.3f ms\n", wall);
+    if (verify && in.n <= TSPGPU_MAX_CITIES && solver != "k1") {
+        Result k1;
+        if ((rc = solve_k1(in, k1))) {
+            std::fprintf(stderr, "tsp_search: K1 check failed: %s\n", tspgpu_strerror(rc));
+            return 3;
+        }
+        const bool same = k1.cost == res.cost && k1.tour == res.tour;
+        std::printf("K1 check: %s\n", same ? "identical cost and tour" : "MISMATCH");
+        if (!same) return 4;
+    }
+    return 0;
+}
