@@ -98,8 +98,17 @@ def test_coincident_cities_fall_back_to_k1(tmp_path):
 
 @pytest.mark.gpu
 def test_rccl_path_with_one_gpu():
-    """--gpus 1 with K2 (the all-reduce is skipped for a single GPU) and auto (K1)."""
-    for solver in ("k2", "auto"):
-        rc, out, err = run("--random", 13, "--seed", 9, "--solver", solver)
+    """--gpus 1 with K2 (the all-reduce is skipped for a single GPU), auto
+    (K1-wide) and wide beyond K1's 20 cities, checked against K2."""
+    res = {}
+    for solver in ("k2", "auto", "k1"):
+        rc, out, err = run("--random", 13, "--seed", 9, "--solver", solver, "--verify")
         assert rc == 0, err
-        assert ("solver k1" in out) == (solver == "auto")
+        assert ("solver wide" in out) == (solver == "auto")
+        res[solver] = parse(out)
+    assert res["k2"] == res["auto"] == res["k1"]
+    rc, out, err = run("--random", 23, "--seed", 4, "--solver", "wide")
+    assert rc == 0, err
+    rc2, out2, err2 = run("--random", 23, "--seed", 4, "--solver", "k2")
+    assert rc2 == 0, err2
+    assert parse(out) == parse(out2)

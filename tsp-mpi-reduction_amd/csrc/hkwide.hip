@@ -1,0 +1,254 @@
+// K1-wide — ONE instance's Held-Karp over the whole GPU (all CUs cooperate
+// on every layer), for the single-instance time to the optimal tour and for
+// instances past K1's per-workgroup sizes (n <= 30: the table of
+// N*2^(N-1) doubles is 62 GB at n = 30 and fits one MI355X's 288 GB).
+//
+// Same recurrence and the same IEEE operations as K1 / tsp.cpp:405-509, so the
+// same bits: layer s is computed from layer s-1 by one launch with a thread
+// per DESTINATION state (S, k) in the position-major layout of K1
+// (heldkarp_impl.h): element e = p*C(N,s) + colexrank(S), p = position of k
+// in S, so the writes of a wave are one contiguous 512-B segment.  The thread
+// unranks S from colexrank(S) (binomials in LDS, no 2^N mask table), drops
+// k, and takes the first-strict-min-free min over the members m of T = S\k of
+// G[T][m] + d[m][k] (the min itself is order independent; the tie-break
+// happens in the backtracking, which picks the smallest m whose candidate
+// equals the state value, as K1 does).  A one-wave kernel closes the tour
+// (tsp.cpp:483-499) and backtracks.
+#include <hip/hip_runtime.h>
+
+#include <cerrno>
+#include <climits>
+#include <cstring>
+#include <vector>
+
+#include "ctx.h"
+#include "tspgpu.h"
+
+namespace {
+
+constexpr int kWideMaxN = 29;  // inner cities (n <= 30)
+constexpr int kWideThreads = 256;
+constexpr double kIntMaxD = 2147483647.0;
+
+struct WideInfo {
+    long long binom[kWideMaxN + 2][kWideMaxN + 2];  // C(a, b)
+    unsigned long long off[kWideMaxN + 2];          // doubles before layer t
+    unsigned long long cnt[kWideMaxN + 2];          // C(N, t)
+};
+
+__device__ __forceinline__ long long bn(const long long (*b)[kWideMaxN + 2], int a, int k)
+{
+    return (k < 0 || k > a) ? 0 : b[a][k];
+}
+
+// layer 1: G[{i}][i] = d[0][i+1]
+__global__ void wide_layer1(const double *__restrict__ d, int n, double *__restrict__ tab)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n - 1) tab[i] = d[i + 1];
+}
+
+__global__ __launch_bounds__(kWideThreads) void wide_layer(const double *__restrict__ dist, int N,
+                                                           const WideInfo *__restrict__ info, int s,
+                                                           double *__restrict__ tab)
+{
+    __shared__ long long B[kWideMaxN + 2][kWideMaxN + 2];
+    __shared__ double dl[(kWideMaxN + 1) * (kWideMaxN + 1)];
+    const int n = N + 1;
+    for (int i = threadIdx.x; i < (kWideMaxN + 2) * (kWideMaxN + 2); i += kWideThreads)
+        (&B[0][0])[i] = (&info->binom[0][0])[i];
+    for (int i = threadIdx.x; i < n * n; i += kWideThreads) dl[i] = dist[i];
+    __syncthreads();
+    const int t = s - 1;
+    const unsigned long long cs = info->cnt[s], ct = info->cnt[t];
+    const unsigned long long os = info->off[s], ot = info->off[t];
+    const unsigned long long total = cs * (unsigned long long)s;
+    for (unsigned long long e = blockIdx.x * (unsigned long long)kWideThreads + threadIdx.x; e < total;
+         e += (unsigned long long)gridDim.x * kWideThreads) {
+        const int p = (int)(e / cs);
+        long long r = (long long)(e - (unsigned long long)p * cs);
+        // colex unrank: members e_1 < ... < e_s with r = sum C(e_i, i)
+        uint32_t S = 0;
+        int c = N - 1;
+        for (int i = s; i >= 1; --i) {
+            while (bn(B, c, i) > r) --c;
+            r -= bn(B, c, i);
+            S |= 1u << c;
+            --c;
+        }
+        // k = p-th member (ascending); T = S \ k and its colex rank
+        uint32_t x = S;
+        for (int q = 0; q < p; ++q) x &= x - 1u;
+        const int k = __builtin_ctz(x);
+        const uint32_t T = S & ~(1u << k);
+        long long rT = 0;
+        {
+            uint32_t y = T;
+            int i = 1;
+            while (y) {
+                const int b = __builtin_ctz(y);
+                rT += bn(B, b, i++);
+                y &= y - 1u;
+            }
+        }
+        double acc = kIntMaxD;  // tsp.cpp:453 (candidates are < INT_MAX by validation)
+        uint32_t y = T;
+        int j = 0;
+        while (y) {
+            const int m = __builtin_ctz(y);
+            y &= y - 1u;
+            const double g = tab[ot + (unsigned long long)j * ct + (unsigned long long)rT];
+            acc = fmin(acc, g + dl[(m + 1) * n + (k + 1)]);
+            ++j;
+        }
+        tab[os + e] = acc;
+    }
+}
+
+// closing min + backtracking (one wave): lane m-1 holds candidate m
+__global__ void wide_close(const double *__restrict__ dist, int N, const WideInfo *__restrict__ info,
+                           const double *__restrict__ tab, double *__restrict__ cost_out, int32_t *__restrict__ tour)
+{
+    const int n = N + 1;
+    const int lane = threadIdx.x;
+    const int m = lane + 1;
+    const bool valid = m <= N;
+    auto rank_of = [&](uint32_t M) {
+        long long r = 0;
+        int i = 1;
+        while (M) {
+            r += info->binom[__builtin_ctz(M)][i++];
+            M &= M - 1u;
+        }
+        return r;
+    };
+    const double glast = valid ? tab[info->off[N] + (unsigned long long)(m - 1) * info->cnt[N]] : 0.0;
+    const double cand = valid ? glast + dist[m * n] : 1.0e300;
+    double best = cand;
+    for (int off = 32; off > 0; off >>= 1) best = fmin(best, __shfl_xor(best, off));
+    best = fmin(best, kIntMaxD);
+    const unsigned long long hit = __ballot(valid && cand == best && cand < kIntMaxD);
+    const int bestM = hit ? __ffsll(hit) : 0;
+    bool ok = bestM != 0;
+    uint32_t S = (uint32_t)((1ull << N) - 1ull);
+    int k = bestM;
+    int pos = n - 2;
+    double target = __shfl(glast, ok ? bestM - 1 : 0);
+    while (ok && __builtin_popcount(S) >= 2) {
+        const uint32_t T = S & ~(1u << (k - 1));
+        const int tt = __builtin_popcount(T);
+        const long long rT = rank_of(T);
+        const bool inT = valid && ((T >> (m - 1)) & 1u);
+        double gv = 0.0, c = 0.0;
+        if (inT) {
+            const int j = __builtin_popcount(T & ((1u << (m - 1)) - 1u));
+            gv = tab[info->off[tt] + (unsigned long long)j * info->cnt[tt] + (unsigned long long)rT];
+            c = gv + dist[m * n + k];
+        }
+        const unsigned long long bb = __ballot(inT && c == target);
+        const int pick = bb ? __ffsll(bb) : 0;
+        ok = pick != 0;
+        if (lane == 0) tour[pos] = pick;
+        target = __shfl(gv, ok ? pick - 1 : 0);
+        --pos;
+        S = T;
+        k = pick;
+    }
+    if (lane == 0) {
+        tour[0] = 0;
+        tour[n - 1] = bestM;
+        tour[n] = 0;
+        *cost_out = ok ? best : -1.0;
+    }
+}
+
+int herr(hipError_t e)
+{
+    if (e == hipSuccess) return 0;
+    if (e == hipErrorOutOfMemory) return -ENOMEM;
+    return -EIO;
+}
+
+}  // namespace
+
+extern "C" {
+
+int tspgpu_solve_instance(tspgpu_ctx *c, const double *dist, int n, double *cost_out, int32_t *tour_out,
+                          double *kernel_ms)
+{
+    if (!c || !dist || !cost_out || !tour_out) return -EINVAL;
+    if (n < 3 || n > kWideMaxN + 1) return -EINVAL;
+    int rc = tspgpu_validate(dist, n, 1, 0 /* n <= 20 checked below */);
+    if (rc == -EINVAL && n > TSPGPU_MAX_CITIES) {
+        // tspgpu_validate caps n at 20: check the values here
+        double mx = 0.0;
+        for (int i = 0; i < n * n; ++i) {
+            if (!(dist[i] >= 0.0) || !(dist[i] < INFINITY)) return -EINVAL;
+            mx = dist[i] > mx ? dist[i] : mx;
+        }
+        rc = (double)n * mx >= (double)INT_MAX ? -ERANGE : 0;
+    }
+    if (rc) return rc;
+    const int N = n - 1;
+    WideInfo h;
+    std::memset(&h, 0, sizeof h);
+    for (int a = 0; a <= kWideMaxN + 1; ++a) {
+        h.binom[a][0] = 1;
+        for (int b = 1; b <= a; ++b) h.binom[a][b] = h.binom[a - 1][b - 1] + (b <= a - 1 ? h.binom[a - 1][b] : 0);
+    }
+    unsigned long long off = 0;
+    for (int t = 1; t <= N; ++t) {
+        h.cnt[t] = (unsigned long long)h.binom[N][t];
+        h.off[t] = off;
+        off += h.cnt[t] * (unsigned long long)t;
+    }
+    std::lock_guard<std::mutex> g(c->mu);
+    if (hipSetDevice(c->device) != hipSuccess) return -ENODEV;
+    size_t freeb = 0, totalb = 0;
+    if (hipMemGetInfo(&freeb, &totalb) == hipSuccess && off * 8 + (64u << 20) > freeb) return -ENOMEM;
+    double *d_tab = nullptr, *d_dist = nullptr, *d_cost = nullptr;
+    int32_t *d_tour = nullptr;
+    WideInfo *d_info = nullptr;
+    hipStream_t st = c->stream;
+    hipError_t e = hipMalloc((void **)&d_tab, off * 8);
+    if (e == hipSuccess) e = hipMalloc((void **)&d_dist, sizeof(double) * n * n);
+    if (e == hipSuccess) e = hipMalloc((void **)&d_info, sizeof(WideInfo));
+    if (e == hipSuccess) e = hipMalloc((void **)&d_cost, sizeof(double));
+    if (e == hipSuccess) e = hipMalloc((void **)&d_tour, sizeof(int32_t) * (n + 1));
+    if (e == hipSuccess) e = hipMemcpyAsync(d_dist, dist, sizeof(double) * n * n, hipMemcpyHostToDevice, st);
+    if (e == hipSuccess) e = hipMemcpyAsync(d_info, &h, sizeof h, hipMemcpyHostToDevice, st);
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (e == hipSuccess) e = hipEventCreate(&e0);
+    if (e == hipSuccess) e = hipEventCreate(&e1);
+    if (e == hipSuccess) {
+        (void)hipEventRecord(e0, st);
+        hipLaunchKernelGGL(wide_layer1, dim3(1), dim3(64), 0, st, d_dist, n, d_tab);
+        for (int s = 2; s <= N; ++s) {
+            const unsigned long long total = h.cnt[s] * (unsigned long long)s;
+            const unsigned long long blocks = (total + kWideThreads - 1) / kWideThreads;
+            const int grid = (int)(blocks < (unsigned long long)c->cu_count * 16 ? blocks : (unsigned long long)c->cu_count * 16);
+            hipLaunchKernelGGL(wide_layer, dim3(grid), dim3(kWideThreads), 0, st, d_dist, N, d_info, s, d_tab);
+        }
+        hipLaunchKernelGGL(wide_close, dim3(1), dim3(64), 0, st, d_dist, N, d_info, d_tab, d_cost, d_tour);
+        (void)hipEventRecord(e1, st);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipMemcpyAsync(cost_out, d_cost, sizeof(double), hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipMemcpyAsync(tour_out, d_tour, sizeof(int32_t) * (n + 1), hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (e == hipSuccess && kernel_ms) {
+        float ms = 0.f;
+        if (hipEventElapsedTime(&ms, e0, e1) == hipSuccess) *kernel_ms = ms;
+    }
+    if (e0) (void)hipEventDestroy(e0);
+    if (e1) (void)hipEventDestroy(e1);
+    if (d_tab) (void)hipFree(d_tab);
+    if (d_dist) (void)hipFree(d_dist);
+    if (d_info) (void)hipFree(d_info);
+    if (d_cost) (void)hipFree(d_cost);
+    if (d_tour) (void)hipFree(d_tour);
+    if (e != hipSuccess) return herr(e);
+    return *cost_out < 0 ? -EIO : 0;
+}
+
+}  // extern "C"

@@ -597,14 +597,15 @@ int tspgpu_search_solve(tspgpu_ctx *c, const void *dist, int dtype, int n, doubl
     int count = 0;
     if (!rc && recs > s->rec_cap) {
         // |O| too large to enumerate (e.g. coincident cities): the DP itself
-        // (K1, also on the GPU) gives tsp()'s tour directly for n <= 20
-        if (dtype == TSPGPU_F64 && n <= TSPGPU_MAX_CITIES) {
+        // (K1-wide, also on the GPU) gives tsp()'s tour directly for n <= 30
+        if (n <= TSPGPU_WIDE_MAX_CITIES) {
             fallback = 1;
-            rc = tspgpu_solve_blocks(c, static_cast<const double *>(dist), n, 1, cost_out, tour_out);
-        } else if (dtype == TSPGPU_I32 && n <= TSPGPU_MAX_CITIES) {
-            fallback = 1;
-            std::vector<double> dd(static_cast<const int32_t *>(dist), static_cast<const int32_t *>(dist) + n * n);
-            rc = tspgpu_solve_blocks(c, dd.data(), n, 1, cost_out, tour_out);
+            std::vector<double> dd(n * n);
+            if (dtype == TSPGPU_F64)
+                std::memcpy(dd.data(), dist, sizeof(double) * n * n);
+            else
+                for (int i = 0; i < n * n; ++i) dd[i] = static_cast<const int32_t *>(dist)[i];
+            rc = tspgpu_solve_instance(c, dd.data(), n, cost_out, tour_out, nullptr);
         } else {
             rc = -EOVERFLOW;
         }

@@ -8,7 +8,9 @@
 //                                                         file with NODE_COORD_SECTION
 //   tsp_search --matrix FILE                              n, then n*n distances (all
 //                                                         integers -> integer mode)
-//   options: --gpus G (devices 0..G-1)  --solver auto|k1|k2  --verify (K2 with n <= 20: K1 too)
+//   options: --gpus G (devices 0..G-1)  --solver auto|wide|k1|k2  --verify (n <= 20: K1 too)
+//   auto = K1-wide (the DP with every CU on each layer) up to 30 cities on one
+//   GPU, else K2 over the GPUs.
 //
 // City distances are the reference's computeDistanceMatrix (assignment2.h:
 // 184-200, glibc pow/sqrt, f64); --tsplib-round uses TSPLIB's EUC_2D nint()
@@ -265,6 +267,23 @@ int solve_k1(const Instance &in, Result &res)
     return tspgpu_solve(d.data(), in.n, 1, &res.cost, res.tour.data(), &o);
 }
 
+// K1-wide: the DP with every CU on each layer (n <= 30); integers are exact as f64
+int solve_wide(const Instance &in, Result &res)
+{
+    if (in.n > TSPGPU_WIDE_MAX_CITIES) return -EINVAL;
+    std::vector<double> d = in.d;
+    if (in.dtype == TSPGPU_I32) d.assign(in.di.begin(), in.di.end());
+    res.tour.assign(in.n + 1, -1);
+    tspgpu_opts o;
+    std::memset(&o, 0, sizeof o);
+    o.device = 0;
+    tspgpu_ctx *ctx = nullptr;
+    int rc = tspgpu_ctx_create(&o, &ctx);
+    if (!rc) rc = tspgpu_solve_instance(ctx, d.data(), in.n, &res.cost, res.tour.data(), &res.kernel_ms);
+    if (ctx) tspgpu_ctx_destroy(ctx);
+    return rc;
+}
+
 }  // namespace
 
 int main(int argc, char **argv)
@@ -291,7 +310,7 @@ int main(int argc, char **argv)
         else if (a == "--verify") verify = true;
         else {
             std::fprintf(stderr, "usage: tsp_search (--random N [--seed S] [--clustered K] | --cities FILE "
-                                 "[--tsplib-round] | --matrix FILE) [--gpus G] [--solver auto|k1|k2] [--verify]\n");
+                                 "[--tsplib-round] | --matrix FILE) [--gpus G] [--solver auto|wide|k1|k2] [--verify]\n");
             return 1;
         }
     }
@@ -308,20 +327,21 @@ int main(int argc, char **argv)
     }
     if (!have) die("no instance (--random, --cities or --matrix)");
     if (gpus < 1) gpus = 1;
-    // auto: the DP (K1) up to 20 cities on one GPU — far fewer operations than
-    // branch and bound there — else the search (K2) over all GPUs
-    if (solver == "auto") solver = (in.n <= TSPGPU_MAX_CITIES && gpus == 1) ? "k1" : "k2";
-    if (solver != "k1" && solver != "k2") die("--solver must be auto, k1 or k2");
+    // auto: the DP over the whole GPU (K1-wide) up to 30 cities on one GPU —
+    // far fewer operations than branch and bound there — else the search (K2)
+    // over all GPUs
+    if (solver == "auto") solver = (in.n <= TSPGPU_WIDE_MAX_CITIES && gpus == 1) ? "wide" : "k2";
+    if (solver != "k1" && solver != "k2" && solver != "wide") die("--solver must be auto, wide, k1 or k2");
 
     Result res;
     const auto t0 = std::chrono::steady_clock::now();
-    int rc = solver == "k1" ? solve_k1(in, res) : search_multi(in, gpus, res);
-    if (rc == -EOVERFLOW && in.n <= TSPGPU_MAX_CITIES) {
+    int rc = solver == "k1" ? solve_k1(in, res) : solver == "wide" ? solve_wide(in, res) : search_multi(in, gpus, res);
+    if (rc == -EOVERFLOW && in.n <= TSPGPU_WIDE_MAX_CITIES) {
         // more tied optima than the record buffers hold (e.g. coincident cities):
-        // the DP (K1) returns the same tour directly
-        std::fprintf(stderr, "tsp_search: too many tied optimal tours to enumerate; answering with K1\n");
-        solver = "k1";
-        rc = solve_k1(in, res);
+        // the DP returns the same tour directly
+        std::fprintf(stderr, "tsp_search: too many tied optimal tours to enumerate; answering with the DP\n");
+        solver = "wide";
+        rc = solve_wide(in, res);
     }
     const double wall = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     if (rc) {
@@ -329,15 +349,17 @@ int main(int argc, char **argv)
         return 3;
     }
     std::printf("cities %d  mode %s  solver %s  gpus %d\n", in.n, in.dtype == TSPGPU_F64 ? "f64" : "i32",
-                solver.c_str(), solver == "k1" ? 1 : gpus);
+                solver.c_str(), solver == "k2" ? gpus : 1);
     std::printf("optimal cost %.17g (%f)\n", res.cost, res.cost);
     std::printf("tour");
     for (int t : res.tour) std::printf(" %d", t);
     std::printf("\n");
-    if (solver != "k1")
+    if (solver == "k2")
         std::printf("search nodes %llu  rounds %d  kernel %.3f ms  %.3f Gnodes/s  wall %.3f ms\n",
                     (unsigned long long)res.nodes, res.rounds, res.kernel_ms,
                     res.kernel_ms > 0 ? res.nodes / res.kernel_ms / 1e6 : 0.0, wall);
+    else if (solver == "wide")
+        std::printf("kernel %.3f ms  wall %.3f ms\n", res.kernel_ms, wall);
     else
         std::printf("wall %.3f ms\n", wall);
     if (verify && in.n <= TSPGPU_MAX_CITIES && solver != "k1") {

@@ -101,17 +101,16 @@ def solve_sharded(ctx, dist, group=None, depth: int = 0, device=None):
             mine, lost = local_records()
             if allmin(-lost) < 0:
                 # too many optimal tours to enumerate (coincident cities): the DP
-                # (K1 on this rank's GPU) gives tsp()'s tour directly for n <= 20
-                if S.n > 20:
+                # (K1-wide on this rank's GPU) gives tsp()'s tour directly for n <= 30
+                if S.n > 30:
                     raise tspgpu.TspGpuError(-errno.EOVERFLOW, "solve_sharded")
-                d64 = np.asarray(dist, dtype=np.float64)[None]
-                c, t = ctx.solve_blocks(d64)
-                cost = float(c[0]) if S.dtype == tspgpu.F64 else int(c[0])
+                c, t, _ = ctx.solve_instance(np.asarray(dist, dtype=np.float64))
+                cost = float(c) if S.dtype == tspgpu.F64 else int(c)
                 stats = {"nodes": int(nodes), "rank_nodes": int(nodes), "optimal_tours": 0, "depth": S.depth,
                          "items": S.items, "phases": phases, "fallback": 1, "kernel_ms": S.timing()[0],
                          "wall_s": time.perf_counter() - t0, "exchanges": exchanges, "world": world,
                          "backend": backend}
-                return cost, t[0], stats
+                return cost, t, stats
         blob = np.frombuffer(b"".join(bytes(r) for r in mine), dtype=np.uint8) if mine else np.zeros(0, np.uint8)
         if world > 1:
             parts = [None] * world

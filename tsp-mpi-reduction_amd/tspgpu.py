@@ -32,6 +32,8 @@ EXPORTED_SYMBOLS = (
     "tspgpu_select_tour",
     # K3
     "tspgpu_merge", "tspgpu_reduce",
+    # K1-wide
+    "tspgpu_solve_instance",
 )
 
 F64, I32 = 0, 1
@@ -128,6 +130,7 @@ def lib():
         L.tspgpu_select_tour.argtypes = [vp, ctypes.c_int, ctypes.c_int, ctypes.POINTER(TourRecord), ctypes.c_int,
                                          ctypes.c_uint64, ip]
         cp = ctypes.POINTER(City)
+        L.tspgpu_solve_instance.argtypes = [vp, dp, ctypes.c_int, dp, ip, dp]
         L.tspgpu_merge.argtypes = [vp, cp, ctypes.c_int, ctypes.c_double, cp, ctypes.c_int, ctypes.c_double, cp, dp]
         L.tspgpu_reduce.argtypes = [vp, cp, ctypes.c_int, dp, ctypes.c_int, ctypes.c_int, dp, ctypes.c_char_p,
                                     ctypes.c_int]
@@ -288,6 +291,17 @@ class Context:
         ms = ctypes.c_float()
         self._check(lib().tspgpu_timer_stop(self.handle, ctypes.byref(ms)), "tspgpu_timer_stop")
         return ms.value
+
+    def solve_instance(self, dist):
+        """K1-wide: one instance over the whole GPU -> (cost, tour (n+1,), kernel ms)."""
+        d = np.ascontiguousarray(dist, dtype=np.float64)
+        n = d.shape[0]
+        cost, ms = ctypes.c_double(), ctypes.c_double()
+        tour = np.zeros(n + 1, dtype=np.int32)
+        rc = lib().tspgpu_solve_instance(self.handle, _dp(d), n, ctypes.byref(cost), _ip(tour), ctypes.byref(ms))
+        if rc:
+            raise TspGpuError(rc, "tspgpu_solve_instance")
+        return cost.value, tour, ms.value
 
     def merge(self, p1, c1, p2, c2):
         """K3 mergeBlocks: paths are lists of (id, x, y) -> (merged path, cost)."""
