@@ -37,7 +37,8 @@ struct LaunchArgs {
     int32_t *tour;
     bool use_lds;
     int threads;            // 256 / 512 / 1024 threads per workgroup (global-table kernels)
-    int variant;            // layer pass: 0 = member sweep over all N cities, 1 = compact (non-members only)
+    int variant;            // layer pass: 0 = member sweep over all N cities, 1 = compact (non-members only),
+                            // 2 = compact with the next row prefetched
     hipStream_t stream;
 };
 

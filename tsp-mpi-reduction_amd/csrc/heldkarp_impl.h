@@ -273,7 +273,9 @@ __device__ __forceinline__ void layer_pass_lds(const LdsTable &tab, const double
 // t*(N-t) relaxations per row instead of t*N for the member sweep: no lane
 // computes a value that is thrown away.  Registers: t + 2(N-t) + O(1) per
 // thread, so the kernel runs at 8 waves/SIMD without spilling.
-template <int N, int T, int THREADS, typename Tab>
+// PREFETCH: the next row's mask and t values are loaded before the current
+// row is relaxed (software pipelining into 2t more VGPRs).
+template <int N, int T, int THREADS, bool PREFETCH, typename Tab>
 __device__ __forceinline__ void layer_pass_compact(const Tab &tab, const double *__restrict__ dl,
                                                    const int *__restrict__ rl, const uint32_t *__restrict__ masks,
                                                    uint32_t tid)
@@ -287,11 +289,33 @@ __device__ __forceinline__ void layer_pass_compact(const Tab &tab, const double 
     constexpr uint32_t DST = layer_off(N, S);
     constexpr uint32_t FULL = (1u << N) - 1u;
     const uint32_t *mt = masks + mask_off(N, T);
-    for (uint32_t r = tid; r < ROWS; r += THREADS) {
-        const uint32_t Tm = mt[r];
-        double g[T];
+    uint32_t nmask = 0;
+    double gn[T];
+    if constexpr (PREFETCH) {
+        if (tid < ROWS) {
+            nmask = mt[tid];
 #pragma unroll
-        for (int j = 0; j < T; ++j) g[j] = tab.load(SRC + j * ROWS + r);
+            for (int j = 0; j < T; ++j) gn[j] = tab.load(SRC + j * ROWS + tid);
+        }
+    }
+    for (uint32_t r = tid; r < ROWS; r += THREADS) {
+        uint32_t Tm;
+        double g[T];
+        if constexpr (PREFETCH) {
+            Tm = nmask;
+#pragma unroll
+            for (int j = 0; j < T; ++j) g[j] = gn[j];
+            const uint32_t rn = r + THREADS;
+            if (rn < ROWS) {
+                nmask = mt[rn];
+#pragma unroll
+                for (int j = 0; j < T; ++j) gn[j] = tab.load(SRC + j * ROWS + rn);
+            }
+        } else {
+            Tm = mt[r];
+#pragma unroll
+            for (int j = 0; j < T; ++j) g[j] = tab.load(SRC + j * ROWS + r);
+        }
         uint32_t kb[Q];
         uint32_t nb = ~Tm & FULL;
 #pragma unroll
@@ -320,14 +344,14 @@ __device__ __forceinline__ void layer_pass_compact(const Tab &tab, const double 
     }
 }
 
-template <int N, int T, int THREADS, typename Tab>
+template <int N, int T, int THREADS, bool PREFETCH, typename Tab>
 __device__ __forceinline__ void all_layers_compact(const Tab &tab, const double *dl, const int *rl,
                                                    const uint32_t *masks, uint32_t tid)
 {
     if constexpr (T < N) {
-        layer_pass_compact<N, T, THREADS>(tab, dl, rl, masks, tid);
+        layer_pass_compact<N, T, THREADS, PREFETCH>(tab, dl, rl, masks, tid);
         __syncthreads();
-        all_layers_compact<N, T + 1, THREADS>(tab, dl, rl, masks, tid);
+        all_layers_compact<N, T + 1, THREADS, PREFETCH>(tab, dl, rl, masks, tid);
     }
 }
 
@@ -351,12 +375,13 @@ __device__ __forceinline__ void all_layers(const Tab &tab, const double *dl, con
 // Occupancy target (waves per SIMD): the member sweep holds N running minima
 // plus a prefetched row (<= 128 VGPRs, 4 waves); the compact pass needs about
 // half of that (<= 64 VGPRs, 8 waves) at the reference's sizes.
-__host__ __device__ constexpr int min_waves(int N, bool compact)
+// VAR: 0 member sweep, 1 compact, 2 compact + next-row prefetch
+__host__ __device__ constexpr int min_waves(int N, int var)
 {
-    return compact ? (N <= 15 ? 8 : 4) : (N <= 15 ? 4 : 2);
+    return var == 1 ? (N <= 15 ? 8 : 4) : (N <= 15 ? 4 : 2);
 }
-template <int N, bool LDS_TABLE, int THREADS, bool COMPACT>
-__global__ __launch_bounds__(THREADS, min_waves(N, COMPACT)) void heldkarp_kernel(
+template <int N, bool LDS_TABLE, int THREADS, int VAR>
+__global__ __launch_bounds__(THREADS, min_waves(N, VAR)) void heldkarp_kernel(
     const double *__restrict__ dist, int nblocks, double *__restrict__ slots, size_t slot_doubles,
     const uint32_t *__restrict__ masks, const LayerInfo *__restrict__ info, double *__restrict__ cost_out,
     int32_t *__restrict__ tour_out)
@@ -410,8 +435,8 @@ __global__ __launch_bounds__(THREADS, min_waves(N, COMPACT)) void heldkarp_kerne
         // costs ~200 VGPRs of 64-bit pointers).
         int tid_b = tid;
         asm volatile("" : "+v"(tid_b));
-        if constexpr (COMPACT)
-            all_layers_compact<N, 1, THREADS>(th, dl, rl, masks, (uint32_t)tid_b);
+        if constexpr (VAR >= 1)
+            all_layers_compact<N, 1, THREADS, VAR == 2>(th, dl, rl, masks, (uint32_t)tid_b);
         else
             all_layers<N, 1, THREADS>(th, dl, binom, lds_rest + tid_b, masks, (uint32_t)tid_b);
 
@@ -465,21 +490,21 @@ __global__ __launch_bounds__(THREADS, min_waves(N, COMPACT)) void heldkarp_kerne
     }
 }
 
-template <int N, bool LDS, int THREADS, bool COMPACT>
+template <int N, bool LDS, int THREADS, int VAR>
 hipError_t launch_n(const LaunchArgs &a, int grid)
 {
-    const size_t lds = lds_bytes(N, LDS, THREADS, COMPACT);
+    const size_t lds = lds_bytes(N, LDS, THREADS, VAR >= 1);
     if (lds > 64 * 1024) {
         static bool raised = false;  // once per instantiation
         if (!raised) {
             hipError_t e = hipFuncSetAttribute(
-                reinterpret_cast<const void *>(&heldkarp_kernel<N, LDS, THREADS, COMPACT>),
+                reinterpret_cast<const void *>(&heldkarp_kernel<N, LDS, THREADS, VAR>),
                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
             if (e != hipSuccess) return e;
             raised = true;
         }
     }
-    hipLaunchKernelGGL((heldkarp_kernel<N, LDS, THREADS, COMPACT>), dim3(grid), dim3(THREADS), lds, a.stream, a.dist,
+    hipLaunchKernelGGL((heldkarp_kernel<N, LDS, THREADS, VAR>), dim3(grid), dim3(THREADS), lds, a.stream, a.dist,
                        a.nblocks, a.slots, a.slot_doubles, a.masks, a.info, a.cost, a.tour);
     return hipGetLastError();
 }
@@ -488,23 +513,24 @@ hipError_t launch_n(const LaunchArgs &a, int grid)
 // admits one workgroup per CU, so it gets 1024 threads (4 waves per SIMD).
 __host__ __device__ constexpr int lds_table_threads(int N) { return N >= 11 ? 1024 : 256; }
 
-template <int N, bool COMPACT>
+template <int N, int VAR>
 hipError_t launch_threads_v(const LaunchArgs &a, int grid)
 {
     if constexpr (N <= kLdsTableMaxN) {
-        if (a.use_lds) return launch_n<N, true, lds_table_threads(N), COMPACT>(a, grid);
+        if (a.use_lds) return launch_n<N, true, lds_table_threads(N), VAR == 2 ? 1 : VAR>(a, grid);
     }
     if constexpr (N >= 12 && N <= 15) {
-        if (a.threads == 512) return launch_n<N, false, 512, COMPACT>(a, grid);
-        if (a.threads == 1024) return launch_n<N, false, 1024, COMPACT>(a, grid);
+        if (a.threads == 512) return launch_n<N, false, 512, VAR>(a, grid);
+        if (a.threads == 1024) return launch_n<N, false, 1024, VAR>(a, grid);
     }
-    return launch_n<N, false, 256, COMPACT>(a, grid);
+    return launch_n<N, false, 256, VAR>(a, grid);
 }
 
 template <int N>
 hipError_t launch_threads(const LaunchArgs &a, int grid)
 {
-    return a.variant == 1 ? launch_threads_v<N, true>(a, grid) : launch_threads_v<N, false>(a, grid);
+    if (a.variant == 2) return launch_threads_v<N, 2>(a, grid);
+    return a.variant == 1 ? launch_threads_v<N, 1>(a, grid) : launch_threads_v<N, 0>(a, grid);
 }
 
 }  // namespace tspgpu

@@ -160,15 +160,17 @@ int solve_device_locked(tspgpu_ctx *c, const double *d_dist, int n, int nblocks,
         a.masks = c->d_masks[N];
         a.info = c->d_info[N];
         a.use_lds = N <= c->lds_table_max_n;
-        // per-N defaults measured on MI355X (profiles/r01/sweep_*.log): small
-        // tables want many blocks in flight, n = 13..16 two 512-thread slots per CU
-        const int def_threads = N <= 11 ? 256 : (N <= 15 ? 512 : 256);
-        const int def_wg = N <= 11 ? 8 : 2;
+        // per-N defaults measured on MI355X (profiles/r01/*sweep*.log): small
+        // tables want many blocks in flight; at n = 15, 16 one 1024-thread slot
+        // per CU keeps the live layers of the 256 resident blocks in the
+        // Infinity Cache (n = 15: 1.45x over two 512-thread slots)
+        const int def_threads = N <= 11 ? 256 : (N <= 13 ? 512 : (N <= 15 ? 1024 : 256));
+        const int def_wg = N <= 11 ? 8 : (N <= 13 ? 2 : (N <= 15 ? 1 : 2));
         a.threads = c->threads > 0 ? c->threads : def_threads;
         a.variant = c->variant;
         if (a.use_lds) {
             // as many resident workgroups as the LDS allows, then persistent
-            const int per_cu = (int)(160 * 1024 / lds_bytes_for(N, true, threads_for(N, true, 0), c->variant == 1));
+            const int per_cu = (int)(160 * 1024 / lds_bytes_for(N, true, threads_for(N, true, 0), c->variant >= 1));
             const int cap = c->cu_count * (per_cu > 0 ? per_cu : 1);
             grid = nblocks < cap ? nblocks : cap;
         } else {
@@ -307,7 +309,10 @@ int tspgpu_ctx_create(const tspgpu_opts *opts, tspgpu_ctx **out)
         const int v = std::atoi(e);
         c->lds_table_max_n = v < kLdsTableMaxN ? v : kLdsTableMaxN;
     }
-    if (const char *e = std::getenv("TSPGPU_K1")) c->variant = std::atoi(e) == 0 ? 0 : 1;
+    if (const char *e = std::getenv("TSPGPU_K1")) {
+        const int v = std::atoi(e);
+        c->variant = v < 0 ? 1 : (v > 2 ? 2 : v);
+    }
     if (const char *e = std::getenv("TSPGPU_WG_PER_CU")) c->wg_per_cu = std::atoi(e) > 0 ? std::atoi(e) : 0;
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
         delete c;
