@@ -76,12 +76,42 @@ __host__ __device__ constexpr int rank_lut_ints(int N)
     return N <= 7 ? kRankR1 : (N <= 14 ? kRankR1 + kRankR2 : kRankLutInts);
 }
 __host__ __device__ constexpr int rank_lut_bytes(int N) { return (rank_lut_ints(N) * 4 + 15) & ~15; }
-// LDS: binomials | distance rows | rank LUT | table (LDS_TABLE) or per-thread
-// row slots (member-sweep global kernels only)
+__host__ __device__ constexpr size_t layer_bytes(int N, int t) { return (size_t)cbinom(N, t) * t * 8; }
+__host__ __device__ constexpr size_t low_bytes(int N, int a)
+{
+    size_t b = 0;
+    for (int t = 1; t <= a; ++t) b += layer_bytes(N, t);
+    return b;
+}
+__host__ __device__ constexpr size_t high_bytes(int N, int a)
+{
+    size_t b = 0;
+    for (int t = N - a + 1; t <= N; ++t) b += layer_bytes(N, t);
+    return b;
+}
+__host__ __device__ constexpr size_t lds_base_bytes(int N) { return kBinomBytesPadded + dl_bytes(N) + rank_lut_bytes(N); }
+// Compact global-table kernels keep the a smallest-index and the a
+// largest-index layers (the smallest layers, e.g. 1-4 and 12-15 of N = 15) in
+// LDS: a workgroup of THREADS threads gets THREADS/1024 of a CU's 160 KiB
+// (the launch places 1024/THREADS workgroups per CU at most).  Those passes
+// then neither touch HBM nor wait on global round trips.
+__host__ __device__ constexpr int lds_end_layers(int N, int threads)
+{
+    const size_t budget = (size_t)160 * 1024 * (size_t)threads / 1024;
+    const size_t base = lds_base_bytes(N) + 1024;
+    if (budget <= base) return 0;
+    int a = 0;
+    while (2 * (a + 1) < N && low_bytes(N, a + 1) + high_bytes(N, a + 1) <= budget - base) ++a;
+    return a;
+}
+// LDS: binomials | distance rows | rank LUT | table (LDS_TABLE) | end layers
+// (compact global kernels) | per-thread row slots (member-sweep global kernels)
 __host__ __device__ constexpr size_t lds_bytes(int N, bool lds_table, int threads, bool compact)
 {
-    return kBinomBytesPadded + dl_bytes(N) + rank_lut_bytes(N) +
-           (lds_table ? ((size_t)N << (N - 1)) * 8 : (compact ? 0 : (size_t)(N - 1) * threads * 8));
+    return lds_base_bytes(N) +
+           (lds_table ? ((size_t)N << (N - 1)) * 8
+                      : (compact ? low_bytes(N, lds_end_layers(N, threads)) + high_bytes(N, lds_end_layers(N, threads))
+                                 : (size_t)(N - 1) * threads * 8));
 }
 
 // colex rank through the three-digit LUT (heldkarp.h)
@@ -147,12 +177,37 @@ struct GlobalTable {
 };
 struct LdsTable {
     double *p;
-    __device__ __forceinline__ double load(uint32_t idx) const { return p[idx]; }
+    uint32_t base = 0;  // table index of p[0]
+    __device__ __forceinline__ double load(uint32_t idx) const { return p[idx - base]; }
     __device__ __forceinline__ void store_if(bool pred, uint32_t idx, double v) const
     {
-        if (pred) p[idx] = v;
+        if (pred) p[idx - base] = v;
     }
-    __device__ __forceinline__ void store(uint32_t idx, double v) const { p[idx] = v; }
+    __device__ __forceinline__ void store(uint32_t idx, double v) const { p[idx - base] = v; }
+};
+
+// The table of a compact global kernel: layers 1..A and N-A+1..N in LDS, the
+// rest in the workgroup's HBM slot (same indices everywhere).
+template <int N, int A>
+struct SplitTable {
+    GlobalTable g;
+    double *lo, *hi;
+    template <int t>
+    __device__ __forceinline__ auto layer() const
+    {
+        if constexpr (A > 0 && t <= A)
+            return LdsTable{lo, 0u};
+        else if constexpr (A > 0 && t >= N - A + 1)
+            return LdsTable{hi, (uint32_t)layer_off(N, N - A + 1)};
+        else
+            return g;
+    }
+    __device__ __forceinline__ double get(int t, uint32_t idx) const
+    {
+        if (A > 0 && t <= A) return lo[idx];
+        if (A > 0 && t >= N - A + 1) return hi[idx - layer_off(N, N - A + 1)];
+        return g.load(idx);
+    }
 };
 
 // acc[k] = min(acc[k], g + d[m][k+1]) for all k: one member of the source row.
@@ -275,8 +330,8 @@ __device__ __forceinline__ void layer_pass_lds(const LdsTable &tab, const double
 // thread, so the kernel runs at 8 waves/SIMD without spilling.
 // PREFETCH: the next row's mask and t values are loaded before the current
 // row is relaxed (software pipelining into 2t more VGPRs).
-template <int N, int T, int THREADS, bool PREFETCH, typename Tab>
-__device__ __forceinline__ void layer_pass_compact(const Tab &tab, const double *__restrict__ dl,
+template <int N, int T, int THREADS, bool PREFETCH, typename SrcTab, typename DstTab>
+__device__ __forceinline__ void layer_pass_compact(const SrcTab &src, const DstTab &dst, const double *__restrict__ dl,
                                                    const int *__restrict__ rl, const uint32_t *__restrict__ masks,
                                                    uint32_t tid)
 {
@@ -295,7 +350,7 @@ __device__ __forceinline__ void layer_pass_compact(const Tab &tab, const double 
         if (tid < ROWS) {
             nmask = mt[tid];
 #pragma unroll
-            for (int j = 0; j < T; ++j) gn[j] = tab.load(SRC + j * ROWS + tid);
+            for (int j = 0; j < T; ++j) gn[j] = src.load(SRC + j * ROWS + tid);
         }
     }
     for (uint32_t r = tid; r < ROWS; r += THREADS) {
@@ -309,12 +364,12 @@ __device__ __forceinline__ void layer_pass_compact(const Tab &tab, const double 
             if (rn < ROWS) {
                 nmask = mt[rn];
 #pragma unroll
-                for (int j = 0; j < T; ++j) gn[j] = tab.load(SRC + j * ROWS + rn);
+                for (int j = 0; j < T; ++j) gn[j] = src.load(SRC + j * ROWS + rn);
             }
         } else {
             Tm = mt[r];
 #pragma unroll
-            for (int j = 0; j < T; ++j) g[j] = tab.load(SRC + j * ROWS + r);
+            for (int j = 0; j < T; ++j) g[j] = src.load(SRC + j * ROWS + r);
         }
         uint32_t kb[Q];
         uint32_t nb = ~Tm & FULL;
@@ -339,7 +394,7 @@ __device__ __forceinline__ void layer_pass_compact(const Tab &tab, const double 
         for (int q = 0; q < Q; ++q) {
             const uint32_t k = kb[q];
             const uint32_t rank = lut_rank<N>(Tm | (1u << k), rl);
-            tab.store(DST + (k - (uint32_t)q) * ROWS_S + rank, acc[q]);
+            dst.store(DST + (k - (uint32_t)q) * ROWS_S + rank, acc[q]);
         }
     }
 }
@@ -349,9 +404,20 @@ __device__ __forceinline__ void all_layers_compact(const Tab &tab, const double 
                                                    const uint32_t *masks, uint32_t tid)
 {
     if constexpr (T < N) {
-        layer_pass_compact<N, T, THREADS, PREFETCH>(tab, dl, rl, masks, tid);
+        layer_pass_compact<N, T, THREADS, PREFETCH>(tab, tab, dl, rl, masks, tid);
         __syncthreads();
         all_layers_compact<N, T + 1, THREADS, PREFETCH>(tab, dl, rl, masks, tid);
+    }
+}
+template <int N, int A, int T, int THREADS, bool PREFETCH>
+__device__ __forceinline__ void all_layers_split(const SplitTable<N, A> &tb, const double *dl, const int *rl,
+                                                 const uint32_t *masks, uint32_t tid)
+{
+    if constexpr (T < N) {
+        layer_pass_compact<N, T, THREADS, PREFETCH>(tb.template layer<T>(), tb.template layer<T + 1>(), dl, rl, masks,
+                                                    tid);
+        __syncthreads();
+        all_layers_split<N, A, T + 1, THREADS, PREFETCH>(tb, dl, rl, masks, tid);
     }
 }
 
@@ -404,6 +470,11 @@ __global__ __launch_bounds__(THREADS, min_waves(N, VAR)) void heldkarp_kernel(
     else
         tab = slots + (size_t)blockIdx.x * slot_doubles;
     using Tab = typename std::conditional<LDS_TABLE, LdsTable, GlobalTable>::type;
+    // compact global kernels: the end layers live in LDS behind the LUT
+    constexpr int A = (!LDS_TABLE && VAR >= 1) ? lds_end_layers(N, THREADS) : 0;
+    SplitTable<N, A> tb;
+    tb.lo = lds_rest;
+    tb.hi = lds_rest + low_bytes(N, A) / 8;
     Tab th;
     if constexpr (LDS_TABLE) {
         th.p = tab;
@@ -416,7 +487,17 @@ __global__ __launch_bounds__(THREADS, min_waves(N, VAR)) void heldkarp_kernel(
         const int bytes = __builtin_amdgcn_readfirstlane((int)(slot_doubles * 8));
         th.rs = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void *>(((uint64_t)hi << 32) | lo), 0, bytes,
                                                   0x00020000);
+        tb.g = th;
     }
+    // table entry (layer t, index idx) wherever it lives
+    auto tget = [&](int t, uint32_t idx) -> double {
+        if constexpr (LDS_TABLE)
+            return tab[idx];
+        else if constexpr (A > 0)
+            return tb.get(t, idx);
+        else
+            return tab[idx];
+    };
 
     for (int blk = blockIdx.x; blk < nblocks; blk += gridDim.x) {
         const double *dsrc = dist + (size_t)blk * n * n;
@@ -427,7 +508,12 @@ __global__ __launch_bounds__(THREADS, min_waves(N, VAR)) void heldkarp_kernel(
         __syncthreads();
 
         // layer 1: G[{i}][i] = d[0][i]; colex rank of {i} is i-1, position 0
-        if (tid < N) tab[tid] = dget<N>(dl, 0, tid + 1);
+        if (tid < N) {
+            if constexpr (A > 0)
+                tb.lo[tid] = dget<N>(dl, 0, tid + 1);
+            else
+                tab[tid] = dget<N>(dl, 0, tid + 1);
+        }
         __syncthreads();
 
         // Opaque per-block copies: keeps the compiler from hoisting every
@@ -435,7 +521,9 @@ __global__ __launch_bounds__(THREADS, min_waves(N, VAR)) void heldkarp_kernel(
         // costs ~200 VGPRs of 64-bit pointers).
         int tid_b = tid;
         asm volatile("" : "+v"(tid_b));
-        if constexpr (VAR >= 1)
+        if constexpr (!LDS_TABLE && VAR >= 1)
+            all_layers_split<N, A, 1, THREADS, VAR == 2>(tb, dl, rl, masks, (uint32_t)tid_b);
+        else if constexpr (VAR >= 1)
             all_layers_compact<N, 1, THREADS, VAR == 2>(th, dl, rl, masks, (uint32_t)tid_b);
         else
             all_layers<N, 1, THREADS>(th, dl, binom, lds_rest + tid_b, masks, (uint32_t)tid_b);
@@ -447,9 +535,9 @@ __global__ __launch_bounds__(THREADS, min_waves(N, VAR)) void heldkarp_kernel(
             const int lane = tid;
             const int m = lane + 1;
             const uint32_t full = (1u << N) - 1u;
-            const double *last = tab + layer_off(N, N);  // one row: position m-1 at m-1
             const bool valid = m <= N;
-            const double glast = valid ? last[m - 1] : 0.0;
+            // the last layer is one row: position m-1 at m-1
+            const double glast = valid ? tget(N, layer_off(N, N) + (uint32_t)(m - 1)) : 0.0;
             const double cand = valid ? glast + dget<N>(dl, m, 0) : 1.0e300;
             const double best = fmin(wave_min(cand), kIntMax);
             const unsigned long long hit = __ballot(valid && cand == best && cand < kIntMax);
@@ -467,7 +555,7 @@ __global__ __launch_bounds__(THREADS, min_waves(N, VAR)) void heldkarp_kernel(
                 const bool inT = valid && ((T >> (m - 1)) & 1u);
                 double gv = 0.0, c = 0.0;
                 if (inT) {
-                    gv = tab[info->off[tt] + __builtin_popcount(T & ((1u << (m - 1)) - 1u)) * info->count[tt] + rT];
+                    gv = tget(tt, info->off[tt] + __builtin_popcount(T & ((1u << (m - 1)) - 1u)) * info->count[tt] + rT);
                     c = gv + dget<N>(dl, m, k);
                 }
                 const unsigned long long bb = __ballot(inT && c == target);
