@@ -328,9 +328,9 @@ __device__ __forceinline__ void layer_pass_lds(const LdsTable &tab, const double
 // t*(N-t) relaxations per row instead of t*N for the member sweep: no lane
 // computes a value that is thrown away.  Registers: t + 2(N-t) + O(1) per
 // thread, so the kernel runs at 8 waves/SIMD without spilling.
-// PREFETCH: the next row's mask and t values are loaded before the current
-// row is relaxed (software pipelining into 2t more VGPRs).
-template <int N, int T, int THREADS, bool PREFETCH, typename SrcTab, typename DstTab>
+// PF (prefetch depth): the masks and t values of the next PF rows are in
+// flight while the current row is relaxed (software pipelining, 2t VGPRs per row).
+template <int N, int T, int THREADS, int PF, typename SrcTab, typename DstTab>
 __device__ __forceinline__ void layer_pass_compact(const SrcTab &src, const DstTab &dst, const double *__restrict__ dl,
                                                    const int *__restrict__ rl, const uint32_t *__restrict__ masks,
                                                    uint32_t tid)
@@ -344,32 +344,50 @@ __device__ __forceinline__ void layer_pass_compact(const SrcTab &src, const DstT
     constexpr uint32_t DST = layer_off(N, S);
     constexpr uint32_t FULL = (1u << N) - 1u;
     const uint32_t *mt = masks + mask_off(N, T);
-    uint32_t nmask = 0;
-    double gn[T];
-    if constexpr (PREFETCH) {
+    uint32_t m1 = 0, m2 = 0;
+    double g1[T], g2[T];
+    if constexpr (PF >= 1) {
         if (tid < ROWS) {
-            nmask = mt[tid];
+            m1 = mt[tid];
 #pragma unroll
-            for (int j = 0; j < T; ++j) gn[j] = src.load(SRC + j * ROWS + tid);
+            for (int j = 0; j < T; ++j) g1[j] = src.load(SRC + j * ROWS + tid);
+        }
+    }
+    if constexpr (PF >= 2) {
+        if (tid + THREADS < ROWS) {
+            m2 = mt[tid + THREADS];
+#pragma unroll
+            for (int j = 0; j < T; ++j) g2[j] = src.load(SRC + j * ROWS + tid + THREADS);
         }
     }
     for (uint32_t r = tid; r < ROWS; r += THREADS) {
         uint32_t Tm;
         double g[T];
-        if constexpr (PREFETCH) {
-            Tm = nmask;
-#pragma unroll
-            for (int j = 0; j < T; ++j) g[j] = gn[j];
-            const uint32_t rn = r + THREADS;
-            if (rn < ROWS) {
-                nmask = mt[rn];
-#pragma unroll
-                for (int j = 0; j < T; ++j) gn[j] = src.load(SRC + j * ROWS + rn);
-            }
-        } else {
+        if constexpr (PF == 0) {
             Tm = mt[r];
 #pragma unroll
             for (int j = 0; j < T; ++j) g[j] = src.load(SRC + j * ROWS + r);
+        } else {
+            Tm = m1;
+#pragma unroll
+            for (int j = 0; j < T; ++j) g[j] = g1[j];
+            if constexpr (PF >= 2) {
+                m1 = m2;
+#pragma unroll
+                for (int j = 0; j < T; ++j) g1[j] = g2[j];
+            }
+            const uint32_t rn = r + PF * THREADS;
+            if (rn < ROWS) {
+                if constexpr (PF >= 2) {
+                    m2 = mt[rn];
+#pragma unroll
+                    for (int j = 0; j < T; ++j) g2[j] = src.load(SRC + j * ROWS + rn);
+                } else {
+                    m1 = mt[rn];
+#pragma unroll
+                    for (int j = 0; j < T; ++j) g1[j] = src.load(SRC + j * ROWS + rn);
+                }
+            }
         }
         uint32_t kb[Q];
         uint32_t nb = ~Tm & FULL;
@@ -399,25 +417,24 @@ __device__ __forceinline__ void layer_pass_compact(const SrcTab &src, const DstT
     }
 }
 
-template <int N, int T, int THREADS, bool PREFETCH, typename Tab>
+template <int N, int T, int THREADS, int PF, typename Tab>
 __device__ __forceinline__ void all_layers_compact(const Tab &tab, const double *dl, const int *rl,
                                                    const uint32_t *masks, uint32_t tid)
 {
     if constexpr (T < N) {
-        layer_pass_compact<N, T, THREADS, PREFETCH>(tab, tab, dl, rl, masks, tid);
+        layer_pass_compact<N, T, THREADS, PF>(tab, tab, dl, rl, masks, tid);
         __syncthreads();
-        all_layers_compact<N, T + 1, THREADS, PREFETCH>(tab, dl, rl, masks, tid);
+        all_layers_compact<N, T + 1, THREADS, PF>(tab, dl, rl, masks, tid);
     }
 }
-template <int N, int A, int T, int THREADS, bool PREFETCH>
+template <int N, int A, int T, int THREADS, int PF>
 __device__ __forceinline__ void all_layers_split(const SplitTable<N, A> &tb, const double *dl, const int *rl,
                                                  const uint32_t *masks, uint32_t tid)
 {
     if constexpr (T < N) {
-        layer_pass_compact<N, T, THREADS, PREFETCH>(tb.template layer<T>(), tb.template layer<T + 1>(), dl, rl, masks,
-                                                    tid);
+        layer_pass_compact<N, T, THREADS, PF>(tb.template layer<T>(), tb.template layer<T + 1>(), dl, rl, masks, tid);
         __syncthreads();
-        all_layers_split<N, A, T + 1, THREADS, PREFETCH>(tb, dl, rl, masks, tid);
+        all_layers_split<N, A, T + 1, THREADS, PF>(tb, dl, rl, masks, tid);
     }
 }
 
@@ -441,7 +458,7 @@ __device__ __forceinline__ void all_layers(const Tab &tab, const double *dl, con
 // Occupancy target (waves per SIMD): the member sweep holds N running minima
 // plus a prefetched row (<= 128 VGPRs, 4 waves); the compact pass needs about
 // half of that (<= 64 VGPRs, 8 waves) at the reference's sizes.
-// VAR: 0 member sweep, 1 compact, 2 compact + next-row prefetch
+// VAR: 0 member sweep, 1 compact, 2 compact + next-row prefetch, 3 compact + two rows prefetched
 __host__ __device__ constexpr int min_waves(int N, int var)
 {
     return var == 1 ? (N <= 15 ? 8 : 4) : (N <= 15 ? 4 : 2);
@@ -522,9 +539,9 @@ __global__ __launch_bounds__(THREADS, min_waves(N, VAR)) void heldkarp_kernel(
         int tid_b = tid;
         asm volatile("" : "+v"(tid_b));
         if constexpr (!LDS_TABLE && VAR >= 1)
-            all_layers_split<N, A, 1, THREADS, VAR == 2>(tb, dl, rl, masks, (uint32_t)tid_b);
+            all_layers_split<N, A, 1, THREADS, VAR - 1>(tb, dl, rl, masks, (uint32_t)tid_b);
         else if constexpr (VAR >= 1)
-            all_layers_compact<N, 1, THREADS, VAR == 2>(th, dl, rl, masks, (uint32_t)tid_b);
+            all_layers_compact<N, 1, THREADS, VAR - 1>(th, dl, rl, masks, (uint32_t)tid_b);
         else
             all_layers<N, 1, THREADS>(th, dl, binom, lds_rest + tid_b, masks, (uint32_t)tid_b);
 
@@ -605,7 +622,7 @@ template <int N, int VAR>
 hipError_t launch_threads_v(const LaunchArgs &a, int grid)
 {
     if constexpr (N <= kLdsTableMaxN) {
-        if (a.use_lds) return launch_n<N, true, lds_table_threads(N), VAR == 2 ? 1 : VAR>(a, grid);
+        if (a.use_lds) return launch_n<N, true, lds_table_threads(N), VAR >= 2 ? 1 : VAR>(a, grid);
     }
     if constexpr (N >= 12 && N <= 15) {
         if (a.threads == 512) return launch_n<N, false, 512, VAR>(a, grid);
@@ -617,7 +634,8 @@ hipError_t launch_threads_v(const LaunchArgs &a, int grid)
 template <int N>
 hipError_t launch_threads(const LaunchArgs &a, int grid)
 {
-    if (a.variant == 2) return launch_threads_v<N, 2>(a, grid);
+    // (VAR 3, two rows in flight, measured no faster than one: not instantiated)
+    if (a.variant >= 2) return launch_threads_v<N, 2>(a, grid);
     return a.variant == 1 ? launch_threads_v<N, 1>(a, grid) : launch_threads_v<N, 0>(a, grid);
 }
 
