@@ -33,4 +33,7 @@ struct tspgpu_ctx {
     hipEvent_t ev_start = nullptr, ev_stop = nullptr;
     char name[256] = {0};
     std::mutex mu;
+    // K1-wide per-context cache (buffers + captured launch graph of the last n), hkwide.hip
+    void *wide_cache = nullptr;
+    void (*wide_free)(void *) = nullptr;
 };

@@ -18,7 +18,9 @@
 
 #include <cerrno>
 #include <climits>
+#include <cstdlib>
 #include <cstring>
+#include <new>
 #include <vector>
 
 #include "ctx.h"
@@ -169,6 +171,43 @@ int herr(hipError_t e)
     return -EIO;
 }
 
+// Device buffers of one table size, kept in the context between calls.
+// (A hipGraph capture of the N launches was measured: same device time,
+// the ~8 us per layer at small n is the kernel boundary itself.)
+struct WideState {
+    int N = 0;
+    double *tab = nullptr, *dist = nullptr, *cost = nullptr;
+    int32_t *tour = nullptr;
+    WideInfo *info = nullptr;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+};
+
+void wide_state_free(void *p)
+{
+    WideState *w = static_cast<WideState *>(p);
+    if (!w) return;
+    if (w->e0) (void)hipEventDestroy(w->e0);
+    if (w->e1) (void)hipEventDestroy(w->e1);
+    for (void *q : {(void *)w->tab, (void *)w->dist, (void *)w->cost, (void *)w->tour, (void *)w->info})
+        if (q) (void)hipFree(q);
+    delete w;
+}
+
+// layer 1, layers 2..N, closing + backtracking
+void enqueue_wide(const WideState *w, const WideInfo &h, int n, int cus, hipStream_t st)
+{
+    const int N = n - 1;
+    hipLaunchKernelGGL(wide_layer1, dim3(1), dim3(64), 0, st, w->dist, n, w->tab);
+    for (int s = 2; s <= N; ++s) {
+        const unsigned long long total = h.cnt[s] * (unsigned long long)s;
+        const unsigned long long blocks = (total + kWideThreads - 1) / kWideThreads;
+        const unsigned long long cap = (unsigned long long)cus * 16;
+        const int grid = (int)(blocks < cap ? blocks : cap);
+        hipLaunchKernelGGL(wide_layer, dim3(grid), dim3(kWideThreads), 0, st, w->dist, N, w->info, s, w->tab);
+    }
+    hipLaunchKernelGGL(wide_close, dim3(1), dim3(64), 0, st, w->dist, N, w->info, w->tab, w->cost, w->tour);
+}
+
 }  // namespace
 
 extern "C" {
@@ -204,49 +243,51 @@ int tspgpu_solve_instance(tspgpu_ctx *c, const double *dist, int n, double *cost
     }
     std::lock_guard<std::mutex> g(c->mu);
     if (hipSetDevice(c->device) != hipSuccess) return -ENODEV;
-    size_t freeb = 0, totalb = 0;
-    if (hipMemGetInfo(&freeb, &totalb) == hipSuccess && off * 8 + (64u << 20) > freeb) return -ENOMEM;
-    double *d_tab = nullptr, *d_dist = nullptr, *d_cost = nullptr;
-    int32_t *d_tour = nullptr;
-    WideInfo *d_info = nullptr;
     hipStream_t st = c->stream;
-    hipError_t e = hipMalloc((void **)&d_tab, off * 8);
-    if (e == hipSuccess) e = hipMalloc((void **)&d_dist, sizeof(double) * n * n);
-    if (e == hipSuccess) e = hipMalloc((void **)&d_info, sizeof(WideInfo));
-    if (e == hipSuccess) e = hipMalloc((void **)&d_cost, sizeof(double));
-    if (e == hipSuccess) e = hipMalloc((void **)&d_tour, sizeof(int32_t) * (n + 1));
-    if (e == hipSuccess) e = hipMemcpyAsync(d_dist, dist, sizeof(double) * n * n, hipMemcpyHostToDevice, st);
-    if (e == hipSuccess) e = hipMemcpyAsync(d_info, &h, sizeof h, hipMemcpyHostToDevice, st);
-    hipEvent_t e0 = nullptr, e1 = nullptr;
-    if (e == hipSuccess) e = hipEventCreate(&e0);
-    if (e == hipSuccess) e = hipEventCreate(&e1);
-    if (e == hipSuccess) {
-        (void)hipEventRecord(e0, st);
-        hipLaunchKernelGGL(wide_layer1, dim3(1), dim3(64), 0, st, d_dist, n, d_tab);
-        for (int s = 2; s <= N; ++s) {
-            const unsigned long long total = h.cnt[s] * (unsigned long long)s;
-            const unsigned long long blocks = (total + kWideThreads - 1) / kWideThreads;
-            const int grid = (int)(blocks < (unsigned long long)c->cu_count * 16 ? blocks : (unsigned long long)c->cu_count * 16);
-            hipLaunchKernelGGL(wide_layer, dim3(grid), dim3(kWideThreads), 0, st, d_dist, N, d_info, s, d_tab);
+    WideState *w = static_cast<WideState *>(c->wide_cache);
+    if (!w || w->N != N) {
+        if (w) wide_state_free(w);
+        c->wide_cache = nullptr;
+        c->wide_free = nullptr;
+        size_t freeb = 0, totalb = 0;
+        if (hipMemGetInfo(&freeb, &totalb) == hipSuccess && off * 8 + (64u << 20) > freeb) return -ENOMEM;
+        w = new (std::nothrow) WideState();
+        if (!w) return -ENOMEM;
+        w->N = N;
+        hipError_t e = hipMalloc((void **)&w->tab, off * 8);
+        if (e == hipSuccess) e = hipMalloc((void **)&w->dist, sizeof(double) * n * n);
+        if (e == hipSuccess) e = hipMalloc((void **)&w->info, sizeof(WideInfo));
+        if (e == hipSuccess) e = hipMalloc((void **)&w->cost, sizeof(double));
+        if (e == hipSuccess) e = hipMalloc((void **)&w->tour, sizeof(int32_t) * (n + 1));
+        if (e == hipSuccess) e = hipMemcpyAsync(w->info, &h, sizeof h, hipMemcpyHostToDevice, st);
+        if (e == hipSuccess) e = hipEventCreate(&w->e0);
+        if (e == hipSuccess) e = hipEventCreate(&w->e1);
+        if (e == hipSuccess) e = hipStreamSynchronize(st);
+        if (e != hipSuccess) {
+            wide_state_free(w);
+            return herr(e);
         }
-        hipLaunchKernelGGL(wide_close, dim3(1), dim3(64), 0, st, d_dist, N, d_info, d_tab, d_cost, d_tour);
-        (void)hipEventRecord(e1, st);
-        e = hipGetLastError();
+        // keep small tables for the next call; free >1 GB ones after use
+        if (off * 8 <= ((size_t)1 << 30)) {
+            c->wide_cache = w;
+            c->wide_free = wide_state_free;
+        }
     }
-    if (e == hipSuccess) e = hipMemcpyAsync(cost_out, d_cost, sizeof(double), hipMemcpyDeviceToHost, st);
-    if (e == hipSuccess) e = hipMemcpyAsync(tour_out, d_tour, sizeof(int32_t) * (n + 1), hipMemcpyDeviceToHost, st);
+    hipError_t e = hipMemcpyAsync(w->dist, dist, sizeof(double) * n * n, hipMemcpyHostToDevice, st);
+    if (e == hipSuccess) {
+        (void)hipEventRecord(w->e0, st);
+        enqueue_wide(w, h, n, c->cu_count, st);
+        (void)hipEventRecord(w->e1, st);
+        if (e == hipSuccess) e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipMemcpyAsync(cost_out, w->cost, sizeof(double), hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipMemcpyAsync(tour_out, w->tour, sizeof(int32_t) * (n + 1), hipMemcpyDeviceToHost, st);
     if (e == hipSuccess) e = hipStreamSynchronize(st);
     if (e == hipSuccess && kernel_ms) {
         float ms = 0.f;
-        if (hipEventElapsedTime(&ms, e0, e1) == hipSuccess) *kernel_ms = ms;
+        if (hipEventElapsedTime(&ms, w->e0, w->e1) == hipSuccess) *kernel_ms = ms;
     }
-    if (e0) (void)hipEventDestroy(e0);
-    if (e1) (void)hipEventDestroy(e1);
-    if (d_tab) (void)hipFree(d_tab);
-    if (d_dist) (void)hipFree(d_dist);
-    if (d_info) (void)hipFree(d_info);
-    if (d_cost) (void)hipFree(d_cost);
-    if (d_tour) (void)hipFree(d_tour);
+    if (c->wide_cache != w) wide_state_free(w);
     if (e != hipSuccess) return herr(e);
     return *cost_out < 0 ? -EIO : 0;
 }
