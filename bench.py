@@ -242,6 +242,53 @@ def pmc_traffic(n, blocks, timeout=90):
                                        "fetch_corrected_x2": fetch}
 
 
+SQ_PASS = ("SQ_WAVES", "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES", "SQ_ACTIVE_INST_VALU", "SQ_INSTS_VALU",
+           "SQ_ACTIVE_INST_LDS", "SQ_LDS_BANK_CONFLICT", "GRBM_GUI_ACTIVE")
+
+
+def pmc_counters(n, blocks, cus, timeout=90):
+    """One more rocprofv3 pass (7 SQ + 1 GRBM counters, within one pass's
+    limits) over the dominant kernel: VALU activity, LDS bank conflicts and
+    wave occupancy.  SQ_*_CYCLES / SQ_ACTIVE_INST_* count quad-cycles
+    (MI355X_MICROARCH.md); GRBM_GUI_ACTIVE is summed over the 8 XCDs."""
+    rocprof = shutil.which("rocprofv3")
+    if not rocprof:
+        return None
+    d = os.path.join(ROOT, "gpurun_out", "pmc_sq")
+    shutil.rmtree(d, ignore_errors=True)
+    cmd = ["timeout", "-s", "KILL", str(timeout), rocprof, "--pmc", *SQ_PASS, "--output-format", "csv",
+           "-d", d, "-o", "pmc", "--", sys.executable, os.path.abspath(__file__), "--pmc-child",
+           "--n", str(n), "--blocks-per-gpu", str(blocks)]
+    p = subprocess.run(cmd, capture_output=True, text=True, cwd="/tmp")
+    if p.returncode != 0:
+        return {"error": f"rc={p.returncode} {p.stderr[-300:]}"}
+    import csv
+    import collections
+
+    vals = collections.defaultdict(list)
+    for root, _, files in os.walk(d):
+        for f in files:
+            if f.endswith("counter_collection.csv"):
+                with open(os.path.join(root, f)) as fh:
+                    for row in csv.DictReader(fh):
+                        if DOMINANT_KERNEL in row.get("Kernel_Name", ""):
+                            vals[row["Counter_Name"]].append(float(row["Counter_Value"]))
+    c = {k: statistics.median(v) for k, v in vals.items()}
+    if not all(k in c for k in SQ_PASS):
+        return {"error": "missing counters", "got": sorted(c)}
+    cycles = c["GRBM_GUI_ACTIVE"] / 8.0  # per XCD = kernel cycles
+    simds = 4 * cus
+    return {
+        "valu_active_per_simd_cycle": 4.0 * c["SQ_ACTIVE_INST_VALU"] / (simds * cycles),
+        "valu_instructions_per_block": c["SQ_INSTS_VALU"] / blocks,
+        "lds_bank_conflict_cycles_over_lds_active": c["SQ_LDS_BANK_CONFLICT"] / max(c["SQ_ACTIVE_INST_LDS"], 1.0),
+        "mean_resident_waves_per_cu": 4.0 * c["SQ_WAVE_CYCLES"] / (cus * cycles),
+        "waves": c["SQ_WAVES"],
+        "raw": c,
+        "blocks_per_launch": blocks,
+    }
+
+
 def pmc_child(args):
     ctx = tspgpu.Context(device=0)
     shard = Shard(args.n, args.blocks_per_gpu, 0, args.blocks_per_gpu)
@@ -343,6 +390,9 @@ def main():
         traffic, traffic_note = pmc_traffic(n, min(Bp, 4096))
         if traffic is not None:
             traffic = traffic * (Bp / min(Bp, 4096))  # per launch of this run's size (same per-block bytes)
+    counters = None
+    if world == 1 and not args.no_pmc:
+        counters = pmc_counters(n, min(Bp, 4096), cu)
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(n)
@@ -370,9 +420,10 @@ def main():
         "kernel_ms_per_launch": kernel_ms,
         "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK, "traffic": traffic,
-                     "note": f"{DOMINANT_KERNEL}<15,false>: algorithmic bytes = 2*8*N*2^(N-1) per block "
+                     "note": f"{DOMINANT_KERNEL} (n={n}): algorithmic bytes = 2*8*N*2^(N-1) per block "
                              f"(each DP entry written once, read once) x {Bp} blocks per launch / HIP-event "
                              f"launch time; traffic = PMC HBM bytes per launch ({traffic_note})"},
+        "counters": counters,
         "cpu_baseline": cpu,
         "k2_single_instance": k2,
         "device": devname,
