@@ -80,3 +80,11 @@ def test_no_device_fails_loudly():
         return
     ctx.close()
     pytest.skip("a GPU is present")
+
+
+def test_distance_matrix_threaded_batch_bit_exact():
+    """A whole rank's batch (threaded on the host) equals the per-block oracle."""
+    blocks = O.generate(16, 1200, 1000, 1000)
+    d = tspgpu.distance_matrix(blocks)
+    for b in range(0, 1200, 37):
+        assert np.array_equal(d[b], O.distance_matrix(blocks[b]))

@@ -75,9 +75,9 @@ __device__ __forceinline__ double swap_cost(const tspgpu_city *c1, int L1, const
     return ((ddist(A, D) + ddist(B, C)) - ddist(A, B)) - ddist(C, D);
 }
 
-// words[0]: min key; [1]: candidate count; [2]: first A/B in c1; [3]: first C in c2
+// *key: min order key of all swap costs
 __global__ __launch_bounds__(kMergeThreads) void argmin_kernel(const tspgpu_city *c1, int L1, const tspgpu_city *c2,
-                                                               int L2, unsigned long long *words)
+                                                               int L2, unsigned long long *key)
 {
     const unsigned long long total = (unsigned long long)L1 * (unsigned)L2;
     unsigned long long best = ~0ull;
@@ -91,7 +91,7 @@ __global__ __launch_bounds__(kMergeThreads) void argmin_kernel(const tspgpu_city
         const unsigned long long o = __shfl_xor(best, off);
         best = o < best ? o : best;
     }
-    if (__lane_id() == 0 && best != ~0ull) atomicMin(words, best);
+    if (__lane_id() == 0 && best != ~0ull) atomicMin(key, best);
 }
 
 __global__ __launch_bounds__(kMergeThreads) void cand_kernel(const tspgpu_city *c1, int L1, const tspgpu_city *c2,
@@ -99,11 +99,11 @@ __global__ __launch_bounds__(kMergeThreads) void cand_kernel(const tspgpu_city *
                                                              Cand *cand)
 {
     const unsigned long long total = (unsigned long long)L1 * (unsigned)L2;
-    const double thr = key_value(words[0]) + eps2;
+    const double thr = key_value(words[1]) + eps2;  // words[1]: min key, words[0]: count
     for (unsigned long long q = blockIdx.x * (unsigned long long)kMergeThreads + threadIdx.x; q < total;
          q += (unsigned long long)gridDim.x * kMergeThreads) {
         if (swap_cost(c1, L1, c2, L2, q) <= thr) {
-            const unsigned s = atomicAdd(reinterpret_cast<unsigned *>(words + 1), 1u);
+            const unsigned s = atomicAdd(reinterpret_cast<unsigned *>(words), 1u);
             if (s < kCandCap) {
                 const int i = (int)(q / (unsigned)L2), j = (int)(q % (unsigned)L2);
                 Cand c;
@@ -119,17 +119,16 @@ __global__ __launch_bounds__(kMergeThreads) void cand_kernel(const tspgpu_city *
     }
 }
 
-// first index of c1 whose id is idA or idB, first index of c2[0..M) whose id is idC
+// first index of c1 whose id is idA or idB -> fw[0], first index of c2[0..M) whose id is idC -> fw[1]
 __global__ __launch_bounds__(kMergeThreads) void find_kernel(const tspgpu_city *c1, int L1, const tspgpu_city *c2,
-                                                             int M, int idA, int idB, int idC,
-                                                             unsigned long long *words)
+                                                             int M, int idA, int idB, int idC, unsigned long long *fw)
 {
     const int t = blockIdx.x * kMergeThreads + threadIdx.x;
     const int stride = gridDim.x * kMergeThreads;
     for (int i = t; i < L1; i += stride)
-        if (c1[i].id == idA || c1[i].id == idB) atomicMin(words + 2, (unsigned long long)i);
+        if (c1[i].id == idA || c1[i].id == idB) atomicMin(fw, (unsigned long long)i);
     for (int j = t; j < M; j += stride)
-        if (c2[j].id == idC) atomicMin(words + 3, (unsigned long long)j);
+        if (c2[j].id == idC) atomicMin(fw + 1, (unsigned long long)j);
 }
 
 // out = c1[0..p] ++ reverse(c2 rotated to start after C, closing city dropped) ++ c1[p+1..]
@@ -137,7 +136,7 @@ __global__ __launch_bounds__(kMergeThreads) void splice_kernel(const tspgpu_city
                                                                int M, const unsigned long long *words,
                                                                tspgpu_city *out)
 {
-    const unsigned long long pw = words[2], sw = words[3];
+    const unsigned long long pw = words[0], sw = words[1];
     if (pw >= (unsigned long long)L1 || sw >= (unsigned long long)M) return;  // host reports it
     const int p = (int)pw, start = (int)((sw + 1) % (unsigned)M);
     const int total = L1 + M;
@@ -204,26 +203,32 @@ struct Merger {
     hipStream_t st = nullptr;
     int cus = 256;
     double eps2 = 0.0;
-    unsigned long long *words = nullptr;  // device
-    unsigned long long *hwords = nullptr; // pinned host
+    // device words: [0] candidate count, [1] min key, [2,3] / [4,5] first A|B and
+    // first C of the two most recent splices (alternating), then the candidates
+    unsigned long long *words = nullptr;
     Cand *cand = nullptr;
+    unsigned long long *hx = nullptr;  // pinned host mirror: 6 words + kFirstCands candidates
     std::vector<Cand> hc;
     DVec tmp;
+    int parity = 0;
+    bool pending = false;     // a splice whose find words are not checked yet
+    int pend_L1 = 0, pend_M = 0, pend_slot = 0;
+    static constexpr unsigned kFirstCands = 64;
+    static constexpr size_t kWordBytes = 6 * sizeof(unsigned long long);
     int init(tspgpu_ctx *c, double dmax)
     {
         st = c->stream;
         cus = c->cu_count;
         eps2 = 2.0 * std::ldexp(4.0 * dmax, -36);
-        hipError_t e = hipMalloc((void **)&words, 4 * sizeof(unsigned long long));
-        if (e == hipSuccess) e = hipHostMalloc((void **)&hwords, 4 * sizeof(unsigned long long), 0);
-        if (e == hipSuccess) e = hipMalloc((void **)&cand, kCandCap * sizeof(Cand));
+        hipError_t e = hipMalloc((void **)&words, kWordBytes + kCandCap * sizeof(Cand));
+        if (e == hipSuccess) e = hipHostMalloc((void **)&hx, kWordBytes + kFirstCands * sizeof(Cand), 0);
+        cand = reinterpret_cast<Cand *>(reinterpret_cast<char *>(words) + kWordBytes);
         return herr(e);
     }
     ~Merger()
     {
         if (words) (void)hipFree(words);
-        if (hwords) (void)hipHostFree(hwords);
-        if (cand) (void)hipFree(cand);
+        if (hx) (void)hipHostFree(hx);
         tmp.release();
     }
     int grid_for(unsigned long long work) const
@@ -231,29 +236,58 @@ struct Merger {
         const unsigned long long b = (work + kMergeThreads - 1) / kMergeThreads;
         return (int)std::max<unsigned long long>(1, std::min<unsigned long long>(b, (unsigned long long)cus * 8));
     }
-    // s1 <- mergeBlocks(s1, c2); returns 0, -EDEADLK if the reference would not terminate, or -errno
+    // the previous splice's first-occurrence searches (copied with the last transfer)
+    int check_pending()
+    {
+        if (!pending) return 0;
+        pending = false;
+        const unsigned long long pa = hx[2 + 2 * pend_slot], pc = hx[3 + 2 * pend_slot];
+        if (pc >= (unsigned long long)pend_M) return -EDEADLK;  // C not in path 2: tsp.cpp:236-239 never ends
+        if (pa >= (unsigned long long)pend_L1) return -EIO;
+        return 0;
+    }
+    // wait for the last splice and check it
+    int flush()
+    {
+        if (!pending) return 0;
+        hipError_t e = hipMemcpyAsync(hx, words, kWordBytes, hipMemcpyDeviceToHost, st);
+        if (e == hipSuccess) e = hipStreamSynchronize(st);
+        if (e != hipSuccess) return herr(e);
+        return check_pending();
+    }
+    // s1 <- mergeBlocks(s1, c2); returns 0, -EDEADLK if the reference would not terminate, or -errno.
+    // One host round trip: the argmin + candidates come back with the previous
+    // splice's checks; the splice of this merge is checked by the next one (or flush()).
     int merge(DVec &s1, double &cost1, const tspgpu_city *c2, int L2, double cost2)
     {
         const int L1 = (int)s1.len;
         if (L1 < 1 || L2 < 2) return -EINVAL;
-        const unsigned long long init[4] = {~0ull, 0ull, ~0ull, ~0ull};
-        hipError_t e = hipMemcpyAsync(words, init, sizeof init, hipMemcpyHostToDevice, st);
+        hipError_t e = hipMemsetAsync(words, 0, 8, st);               // candidate count
+        if (e == hipSuccess) e = hipMemsetAsync(words + 1, 0xFF, 8, st);  // min key
         if (e != hipSuccess) return herr(e);
         const unsigned long long pairs = (unsigned long long)L1 * (unsigned)L2;
         const int g = grid_for(pairs);
-        hipLaunchKernelGGL(argmin_kernel, dim3(g), dim3(kMergeThreads), 0, st, s1.p, L1, c2, L2, words);
+        hipLaunchKernelGGL(argmin_kernel, dim3(g), dim3(kMergeThreads), 0, st, s1.p, L1, c2, L2, words + 1);
         hipLaunchKernelGGL(cand_kernel, dim3(g), dim3(kMergeThreads), 0, st, s1.p, L1, c2, L2, eps2, words, cand);
-        e = hipMemcpyAsync(hwords, words, 2 * sizeof(unsigned long long), hipMemcpyDeviceToHost, st);
+        e = hipMemcpyAsync(hx, words, kWordBytes + kFirstCands * sizeof(Cand), hipMemcpyDeviceToHost, st);
         if (e == hipSuccess) e = hipStreamSynchronize(st);
         if (e != hipSuccess) return herr(e);
-        const unsigned nc = (unsigned)hwords[1];
+        int rc = check_pending();
+        if (rc) return rc;
+        const unsigned nc = (unsigned)hx[0];
         double best = (double)INT_MAX;  // tsp.cpp:204
-        int bi = -1, bj = -1;
+        int bi = -1;
         tspgpu_city A{}, B{}, C{};
         if (nc > 0 && nc <= kCandCap) {
             hc.resize(nc);
-            e = hipMemcpy(hc.data(), cand, nc * sizeof(Cand), hipMemcpyDeviceToHost);
-            if (e != hipSuccess) return herr(e);
+            std::memcpy(hc.data(), reinterpret_cast<const char *>(hx) + kWordBytes,
+                        std::min(nc, kFirstCands) * sizeof(Cand));
+            if (nc > kFirstCands) {
+                e = hipMemcpyAsync(hc.data() + kFirstCands, cand + kFirstCands, (nc - kFirstCands) * sizeof(Cand),
+                                   hipMemcpyDeviceToHost, st);
+                if (e == hipSuccess) e = hipStreamSynchronize(st);
+                if (e != hipSuccess) return herr(e);
+            }
             std::sort(hc.begin(), hc.end(), [](const Cand &x, const Cand &y) {
                 return x.i != y.i ? x.i < y.i : x.j < y.j;
             });
@@ -262,7 +296,6 @@ struct Merger {
                 if (sc < best) {
                     best = sc;
                     bi = k.i;
-                    bj = k.j;
                     A = k.a;
                     B = k.b;
                     C = k.c;
@@ -271,8 +304,9 @@ struct Merger {
         } else {
             // too many near-ties for the buffer: exact scan on the host
             std::vector<tspgpu_city> h1(L1), h2(L2);
-            e = hipMemcpy(h1.data(), s1.p, L1 * sizeof(tspgpu_city), hipMemcpyDeviceToHost);
-            if (e == hipSuccess) e = hipMemcpy(h2.data(), c2, L2 * sizeof(tspgpu_city), hipMemcpyDeviceToHost);
+            e = hipMemcpyAsync(h1.data(), s1.p, L1 * sizeof(tspgpu_city), hipMemcpyDeviceToHost, st);
+            if (e == hipSuccess) e = hipMemcpyAsync(h2.data(), c2, L2 * sizeof(tspgpu_city), hipMemcpyDeviceToHost, st);
+            if (e == hipSuccess) e = hipStreamSynchronize(st);
             if (e != hipSuccess) return herr(e);
             for (int i = 0; i < L1; ++i)
                 for (int j = 0; j < L2; ++j) {
@@ -281,7 +315,6 @@ struct Merger {
                     if (sc < best) {
                         best = sc;
                         bi = i;
-                        bj = j;
                         A = a;
                         B = b;
                         C = c;
@@ -290,23 +323,24 @@ struct Merger {
         }
         if (bi < 0) return -EIO;  // no swap below INT_MAX (distances are validated far below)
         const int M = L2 - 1;
-        int rc = tmp.reserve((size_t)L1 + M, st);
+        rc = tmp.reserve((size_t)L1 + M, st);
         if (rc) return rc;
-        const int gf = grid_for((unsigned long long)std::max(L1, M));
-        hipLaunchKernelGGL(find_kernel, dim3(gf), dim3(kMergeThreads), 0, st, s1.p, L1, c2, M, A.id, B.id, C.id,
-                           words);
-        hipLaunchKernelGGL(splice_kernel, dim3(grid_for((unsigned long long)L1 + M)), dim3(kMergeThreads), 0, st,
-                           s1.p, L1, c2, M, words, tmp.p);
-        e = hipMemcpyAsync(hwords + 2, words + 2, 2 * sizeof(unsigned long long), hipMemcpyDeviceToHost, st);
-        if (e == hipSuccess) e = hipStreamSynchronize(st);
+        unsigned long long *fw = words + 2 + 2 * parity;
+        e = hipMemsetAsync(fw, 0xFF, 2 * sizeof(unsigned long long), st);
         if (e != hipSuccess) return herr(e);
-        if (hwords[3] >= (unsigned long long)M) return -EDEADLK;  // C not in path 2: tsp.cpp:236-239 never ends
-        if (hwords[2] >= (unsigned long long)L1) return -EIO;
+        const int gf = grid_for((unsigned long long)std::max(L1, M));
+        hipLaunchKernelGGL(find_kernel, dim3(gf), dim3(kMergeThreads), 0, st, s1.p, L1, c2, M, A.id, B.id, C.id, fw);
+        hipLaunchKernelGGL(splice_kernel, dim3(grid_for((unsigned long long)L1 + M)), dim3(kMergeThreads), 0, st,
+                           s1.p, L1, c2, M, fw, tmp.p);
+        pending = true;
+        pend_L1 = L1;
+        pend_M = M;
+        pend_slot = parity;
+        parity ^= 1;
         std::swap(s1, tmp);
         s1.len = (size_t)L1 + M;
         tmp.len = 0;
         cost1 = cost1 + cost2 + best;  // tsp.cpp:263
-        (void)bj;
         return 0;
     }
 };
@@ -356,7 +390,9 @@ int tspgpu_merge(tspgpu_ctx *ctx, const tspgpu_city *p1, int L1, double c1, cons
     s.len = L1;
     double cost = c1;
     if (!rc) rc = m.merge(s, cost, b.p, L2, c2);
-    if (!rc) rc = herr(hipMemcpy(out, s.p, s.len * sizeof(tspgpu_city), hipMemcpyDeviceToHost));
+    if (!rc) rc = m.flush();
+    if (!rc) rc = herr(hipMemcpyAsync(out, s.p, s.len * sizeof(tspgpu_city), hipMemcpyDeviceToHost, m.st));
+    if (!rc) rc = herr(hipStreamSynchronize(m.st));
     const int len = (int)s.len;
     s.release();
     b.release();
@@ -425,6 +461,7 @@ int tspgpu_reduce(tspgpu_ctx *ctx, const tspgpu_city *paths, int L, const double
     }
     for (int d = 0; d < (int)std::log2((double)lastpower) && !rc; ++d)
         for (int k = 0; k < lastpower && !rc; k += 1 << (d + 1)) rc = receive(k, k + (1 << d));
+    if (!rc) rc = m.flush();
     for (auto &v : rank) v.release();
     for (auto &v : received) v.release();
     blocks.release();

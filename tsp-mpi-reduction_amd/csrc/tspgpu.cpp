@@ -9,6 +9,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cerrno>
 #include <climits>
 #include <cmath>
@@ -17,6 +18,7 @@
 #include <cstring>
 #include <memory>
 #include <mutex>
+#include <thread>
 #include <vector>
 
 #include "ctx.h"
@@ -239,16 +241,31 @@ int tspgpu_distance_matrix(const tspgpu_city *cities, int n, int nblocks, double
     static double (*volatile pow_fn)(double, double) = ::pow;
     static double (*volatile sqrt_fn)(double) = ::sqrt;
     if (n < 1 || nblocks < 0 || (nblocks > 0 && (!cities || !dist))) return -EINVAL;
-    for (int b = 0; b < nblocks; ++b) {
-        const tspgpu_city *c = cities + (size_t)b * n;
-        double *d = dist + (size_t)b * n * n;
-        for (int i = 0; i < n; ++i)
-            for (int j = 0; j < n; ++j) {
-                const double dx = pow_fn(c[i].x - c[j].x, 2);
-                const double dy = pow_fn(c[i].y - c[j].y, 2);
-                d[i * n + j] = sqrt_fn(dx + dy);
-            }
+    auto run = [&](int b0, int b1) {
+        for (int b = b0; b < b1; ++b) {
+            const tspgpu_city *c = cities + (size_t)b * n;
+            double *d = dist + (size_t)b * n * n;
+            for (int i = 0; i < n; ++i)
+                for (int j = 0; j < n; ++j) {
+                    const double dx = pow_fn(c[i].x - c[j].x, 2);
+                    const double dy = pow_fn(c[i].y - c[j].y, 2);
+                    d[i * n + j] = sqrt_fn(dx + dy);
+                }
+        }
+    };
+    // large batches (a whole rank's blocks) on up to 16 host threads
+    const long long work = (long long)nblocks * n * n;
+    int nt = (int)std::min<unsigned>(16u, std::max(1u, std::thread::hardware_concurrency()));
+    if (work < (1 << 18)) nt = 1;
+    if (nt > nblocks) nt = nblocks > 0 ? nblocks : 1;
+    if (nt <= 1) {
+        run(0, nblocks);
+        return 0;
     }
+    std::vector<std::thread> th;
+    for (int t = 0; t < nt; ++t)
+        th.emplace_back(run, (int)((long long)nblocks * t / nt), (int)((long long)nblocks * (t + 1) / nt));
+    for (auto &x : th) x.join();
     return 0;
 }
 
