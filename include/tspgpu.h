@@ -20,7 +20,7 @@
  *   -EIO     a HIP runtime call or kernel launch failed
  *   -EDEADLK (K3) the reference's mergeBlocks would never terminate for these paths
  *            (its rotation loop, tsp.cpp:236-239, looks for a city that is not there)
- *   -EOVERFLOW (K2) more optimal tours than can be enumerated, n > 30
+ *   -EOVERFLOW (K2) more optimal tours than can be enumerated, n > 31
  */
 #ifndef TSPGPU_H
 #define TSPGPU_H
@@ -123,11 +123,11 @@ double tspgpu_table_bytes_per_block(int n);
 /* ---------------------------------------------------------------------------
  * K1-wide: ONE instance's Held-Karp with every CU of the GPU on each layer
  * (K1 gives each block one workgroup).  The single-instance time to the
- * optimal tour, and exact instances up to n = 30 (table N*2^(N-1) doubles:
- * 62 GB at n = 30).  Same cost and tour bits as K1 / tsp().  dist: n*n f64
+ * optimal tour, and exact instances up to n = 31 (table N*2^(N-1) doubles:
+ * 129 GB at n = 31).  Same cost and tour bits as K1 / tsp().  dist: n*n f64
  * (host); tour_out: n+1 entries; kernel_ms (optional): device time.
  * ------------------------------------------------------------------------- */
-#define TSPGPU_WIDE_MAX_CITIES 30
+#define TSPGPU_WIDE_MAX_CITIES 31
 int tspgpu_solve_instance(tspgpu_ctx *ctx, const double *dist, int n, double *cost_out, int32_t *tour_out,
                           double *kernel_ms);
 
@@ -160,7 +160,7 @@ typedef struct
     uint64_t items;         /* prefixes (work items) N!/(N-D)! */
     int depth;              /* prefix depth D */
     int phases;             /* 1, or 2 when the record buffer overflowed (second search, bound = optimum) */
-    int fallback;           /* 1: |O| too large to enumerate, the answer came from K1-wide (n <= 30) */
+    int fallback;           /* 1: |O| too large to enumerate, the answer came from K1-wide (n <= 31) */
     int rounds;             /* search rounds of the last phase (items split and re-queued between rounds) */
     double kernel_ms;       /* device time of the search launches */
 } tspgpu_search_stats;
@@ -170,7 +170,7 @@ typedef struct tspgpu_search tspgpu_search; /* one instance (or one shard of it)
 /* One-shot: whole instance on the context's GPU.  cost_out: the optimal cost
  * (an integer value for TSPGPU_I32); tour_out: n+1 entries 0,t1..tN,0.
  * When more tours tie for the optimum than can be enumerated (coincident
- * cities), n <= 30 is answered by K1-wide (stats->fallback = 1), larger n
+ * cities), n <= 31 is answered by K1-wide (stats->fallback = 1), larger n
  * return -EOVERFLOW. */
 int tspgpu_search_solve(tspgpu_ctx *ctx, const void *dist, int dtype, int n, double *cost_out,
                         int32_t *tour_out, tspgpu_search_stats *stats);

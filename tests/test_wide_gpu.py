@@ -58,7 +58,7 @@ def test_beyond_k1_agrees_with_k2(gpu_ctx, n):
 
 def test_rejects_bad_input(gpu_ctx):
     with pytest.raises(tspgpu.TspGpuError):
-        gpu_ctx.solve_instance(np.zeros((31, 31)))
+        gpu_ctx.solve_instance(np.zeros((32, 32)))
     bad = np.ones((5, 5))
     bad[0, 1] = np.nan
     with pytest.raises(tspgpu.TspGpuError):

@@ -1,7 +1,7 @@
 // K1-wide — ONE instance's Held-Karp over the whole GPU (all CUs cooperate
 // on every layer), for the single-instance time to the optimal tour and for
-// instances past K1's per-workgroup sizes (n <= 30: the table of
-// N*2^(N-1) doubles is 62 GB at n = 30 and fits one MI355X's 288 GB).
+// instances past K1's per-workgroup sizes (n <= 31: the table of
+// N*2^(N-1) doubles is 129 GB at n = 31 and fits one MI355X's 288 GB).
 //
 // Same recurrence and the same IEEE operations as K1 / tsp.cpp:405-509, so the
 // same bits: layer s is computed from layer s-1 by one launch with a thread
@@ -28,7 +28,7 @@
 
 namespace {
 
-constexpr int kWideMaxN = 29;  // inner cities (n <= 30)
+constexpr int kWideMaxN = 30;  // inner cities (n <= 31: a 129 GB table)
 constexpr int kWideThreads = 256;
 constexpr double kIntMaxD = 2147483647.0;
 

@@ -597,7 +597,7 @@ int tspgpu_search_solve(tspgpu_ctx *c, const void *dist, int dtype, int n, doubl
     int count = 0;
     if (!rc && recs > s->rec_cap) {
         // |O| too large to enumerate (e.g. coincident cities): the DP itself
-        // (K1-wide, also on the GPU) gives tsp()'s tour directly for n <= 30
+        // (K1-wide, also on the GPU) gives tsp()'s tour directly for n <= 31
         if (n <= TSPGPU_WIDE_MAX_CITIES) {
             fallback = 1;
             std::vector<double> dd(n * n);

@@ -9,7 +9,7 @@
 //   tsp_search --matrix FILE                              n, then n*n distances (all
 //                                                         integers -> integer mode)
 //   options: --gpus G (devices 0..G-1)  --solver auto|wide|k1|k2  --verify (n <= 20: K1 too)
-//   auto = K1-wide (the DP with every CU on each layer) up to 30 cities on one
+//   auto = K1-wide (the DP with every CU on each layer) up to 31 cities on one
 //   GPU, else K2 over the GPUs.
 //
 // City distances are the reference's computeDistanceMatrix (assignment2.h:
@@ -267,7 +267,7 @@ int solve_k1(const Instance &in, Result &res)
     return tspgpu_solve(d.data(), in.n, 1, &res.cost, res.tour.data(), &o);
 }
 
-// K1-wide: the DP with every CU on each layer (n <= 30); integers are exact as f64
+// K1-wide: the DP with every CU on each layer (n <= 31); integers are exact as f64
 int solve_wide(const Instance &in, Result &res)
 {
     if (in.n > TSPGPU_WIDE_MAX_CITIES) return -EINVAL;
@@ -327,7 +327,7 @@ int main(int argc, char **argv)
     }
     if (!have) die("no instance (--random, --cities or --matrix)");
     if (gpus < 1) gpus = 1;
-    // auto: the DP over the whole GPU (K1-wide) up to 30 cities on one GPU —
+    // auto: the DP over the whole GPU (K1-wide) up to 31 cities on one GPU —
     // far fewer operations than branch and bound there — else the search (K2)
     // over all GPUs
     if (solver == "auto") solver = (in.n <= TSPGPU_WIDE_MAX_CITIES && gpus == 1) ? "wide" : "k2";

@@ -101,8 +101,8 @@ def solve_sharded(ctx, dist, group=None, depth: int = 0, device=None):
             mine, lost = local_records()
             if allmin(-lost) < 0:
                 # too many optimal tours to enumerate (coincident cities): the DP
-                # (K1-wide on this rank's GPU) gives tsp()'s tour directly for n <= 30
-                if S.n > 30:
+                # (K1-wide on this rank's GPU) gives tsp()'s tour directly for n <= 31
+                if S.n > 31:
                     raise tspgpu.TspGpuError(-errno.EOVERFLOW, "solve_sharded")
                 c, t, _ = ctx.solve_instance(np.asarray(dist, dtype=np.float64))
                 cost = float(c) if S.dtype == tspgpu.F64 else int(c)
