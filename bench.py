@@ -374,6 +374,30 @@ def main():
         assert all(w[0] == cost[0] for w in wide), "K1-wide disagrees with K1"
         wide_ms = min(w[2] for w in wide)
 
+    # extension probe: the same launch on the rounded integer matrices (K1 i32)
+    i32 = None
+    if os.environ.get("BENCH_I32", "1") != "0":
+        try:
+            di = np.rint(d).astype(np.int32)
+            pi, ci, ti = ctx.upload(di), ctx.alloc(Bp * 4), ctx.alloc(Bp * (n + 1) * 4)
+            ctx.solve_device_i32(pi, n, Bp, ci, ti, stream)
+            ctx.timer_start()
+            for _ in range(5):
+                ctx.solve_device_i32(pi, n, Bp, ci, ti, stream)
+            i32_ms = ctx.timer_stop() / 5
+            ci_h = ctx.download(ci, (Bp,), np.int32)
+            ti_h = ctx.download(ti, (Bp, n + 1), np.int32)
+            for b in range(0, Bp, max(1, Bp // 64)):
+                assert sum(int(di[b, ti_h[b, i], ti_h[b, i + 1]]) for i in range(n)) == int(ci_h[b])
+            for p_ in (pi, ci, ti):
+                ctx.free(p_)
+            i32 = {"kernel_ms_per_launch": i32_ms, "blocks_per_s": Bp / (i32_ms * 1e-3),
+                   "relaxations_per_s": Bp * tspgpu.relaxations_per_block(n) / (i32_ms * 1e-3),
+                   "hbm_alg_GBps": tspgpu.table_bytes_per_block(n) / 2 * Bp / (i32_ms * 1e-3) / 1e9,
+                   "note": "extension (no reference counterpart): rint(distances) as int32, same DP and tie rule"}
+        except Exception as e:  # the probe must never cost the headline line
+            i32 = {"error": f"{type(e).__name__}: {e}"}
+
     k2 = None
     if not args.no_k2 and os.environ.get("BENCH_K2", "1") != "0":
         try:
@@ -426,6 +450,7 @@ def main():
         "counters": counters,
         "cpu_baseline": cpu,
         "k2_single_instance": k2,
+        "k1_i32_extension": i32,
         "device": devname,
         "cus": cu,
     }

@@ -90,6 +90,18 @@ int tspgpu_solve_cities(tspgpu_ctx *ctx, const tspgpu_city *cities, int n, int n
 int tspgpu_solve_blocks_device(tspgpu_ctx *ctx, const double *d_dist, int n, int nblocks, double *d_cost,
                                int32_t *d_tour, void *hip_stream);
 
+/* Integer-weight extension (TSPLIB-style rounded distances; no reference
+ * counterpart — the reference computes f64 Euclidean distances only): the same
+ * DP, tie rule and tour layout on int32 distances.  Results equal
+ * tspgpu_solve_blocks on the same matrix converted to double (every partial
+ * sum is an exact integer below 2^31); the table and its HBM traffic are half
+ * the size.  Validation: d >= 0 and n * max(d) < INT_MAX (else -ERANGE). */
+int tspgpu_validate_i32(const int32_t *dist, int n, int nblocks, int strict);
+int tspgpu_solve_blocks_i32(tspgpu_ctx *ctx, const int32_t *dist, int n, int nblocks, int32_t *cost_out,
+                            int32_t *tour_out);
+int tspgpu_solve_blocks_i32_device(tspgpu_ctx *ctx, const int32_t *d_dist, int n, int nblocks, int32_t *d_cost,
+                                   int32_t *d_tour, void *hip_stream);
+
 /* Context-free convenience form (uses a per-thread default context on the
  * current device, created on first use). */
 int tspgpu_solve(const double *dist, int n, int nblocks, double *cost_out, int32_t *tour_out,

@@ -71,6 +71,17 @@ def test_validation_host_side():
     assert tspgpu.validate(np.zeros((1, 21, 21)), strict=False) == -errno.EINVAL
 
 
+def test_validation_i32_host_side():
+    ok = np.zeros((2, 5, 5), dtype=np.int32)
+    assert tspgpu.validate_i32(ok) == 0
+    bad = ok.copy()
+    bad[1, 2, 3] = -1
+    assert tspgpu.validate_i32(bad) == -errno.EINVAL
+    assert tspgpu.validate_i32(np.full((1, 5, 5), 2147483647 // 5 + 1, dtype=np.int32)) == -errno.ERANGE
+    assert tspgpu.validate_i32(np.full((1, 5, 5), 2147483647 // 5, dtype=np.int32)) == 0
+    assert tspgpu.validate_i32(np.zeros((1, 21, 21), dtype=np.int32)) == -errno.EINVAL
+
+
 def test_no_device_fails_loudly():
     """Without a GPU the product refuses (no CPU fallback)."""
     try:

@@ -3,6 +3,7 @@
     python tools/sweep.py [n ...]
 Each configuration is a fresh context created under TSPGPU_THREADS /
 TSPGPU_WG_PER_CU; all configurations run interleaved in one process.
+SWEEP_I32=1 runs the integer-distance K1 on the rounded matrices.
 """
 import os
 import sys
@@ -24,6 +25,10 @@ for n in ns:
     B = {16: 8192, 15: 16384, 14: 16384, 13: 32768, 12: 65536}.get(n, 65536)
     shard = Shard(n, B, 0, B)
     d = shard.distances()
+    i32 = os.environ.get("SWEEP_I32") == "1"
+    vb = 4 if i32 else 8
+    if i32:
+        d = np.rint(d).astype(np.int32)
     rows = []
     ctxs = []
     for v, th, wg in configs:
@@ -31,24 +36,25 @@ for n in ns:
         os.environ["TSPGPU_THREADS"] = str(th)
         os.environ["TSPGPU_WG_PER_CU"] = str(wg)
         ctx = tspgpu.Context(device=0)
-        ctxs.append((v, th, wg, ctx, ctx.upload(d), ctx.alloc(B * 8), ctx.alloc(B * (n + 1) * 4)))
+        ctxs.append((v, th, wg, ctx, ctx.upload(d), ctx.alloc(B * vb), ctx.alloc(B * (n + 1) * 4)))
     ref = None
     for rep in range(2):
         for v, th, wg, ctx, dd, dc, dt in ctxs:
-            ctx.solve_device(dd, n, B, dc, dt, ctx.stream)
+            solve = ctx.solve_device_i32 if i32 else ctx.solve_device
+            solve(dd, n, B, dc, dt, ctx.stream)
             ctx.timer_start()
             for _ in range(3):
-                ctx.solve_device(dd, n, B, dc, dt, ctx.stream)
+                solve(dd, n, B, dc, dt, ctx.stream)
             ms = ctx.timer_stop() / 3
-            c = ctx.download(dc, (B,), np.float64)
+            c = ctx.download(dc, (B,), np.int32 if i32 else np.float64)
             if ref is None:
                 ref = c
             ok = np.array_equal(c, ref)
             if rep == 1:
                 relax = tspgpu.relaxations_per_block(n) * B
-                tb = tspgpu.table_bytes_per_block(n) * B
-                print(f"n={n} B={B} k1={v} threads={th} wg/cu={wg} grid={ctx.last_grid()} {ms:.3f} ms "
-                      f"{B / ms * 1e3:.3e} blocks/s {relax / ms / 1e9:.3f} Trelax/s {tb / ms / 1e9:.0f} GB/s alg "
+                tb = tspgpu.table_bytes_per_block(n) * B * vb / 8
+                print(f"n={n} B={B} {'i32' if i32 else 'f64'} k1={v} threads={th} wg/cu={wg} grid={ctx.last_grid()} {ms:.3f} ms "
+                      f"{B / ms * 1e3:.3e} blocks/s {relax / ms / 1e9:.3f} Trelax/s {tb / ms / 1e6:.0f} GB/s alg "
                       f"{'ok' if ok else 'MISMATCH'}", flush=True)
     for *_, ctx, dd, dc, dt in ctxs:
         for p in (dd, dc, dt):

@@ -26,15 +26,16 @@ struct LayerInfo {
 };
 
 struct LaunchArgs {
-    const double *dist;     // nblocks * n * n (device)
+    const void *dist;       // nblocks * n * n (device), f64 or i32 (vbytes)
     int n;
     int nblocks;
-    double *slots;          // grid * slot_doubles (device), unused when use_lds
-    size_t slot_doubles;
+    void *slots;            // grid * slot_doubles values (device), unused when use_lds
+    size_t slot_doubles;    // table values per slot
     const uint32_t *masks;  // all N-bit masks sorted by (popcount, value)
     const LayerInfo *info;  // device copy
-    double *cost;
+    void *cost;             // nblocks values (f64 or i32)
     int32_t *tour;
+    int vbytes;             // 8: f64 distances, 4: i32 distances
     bool use_lds;
     int threads;            // 256 / 512 / 1024 threads per workgroup (global-table kernels)
     int variant;            // layer pass: 0 = member sweep over all N cities, 1 = compact (non-members only),
@@ -45,7 +46,7 @@ struct LaunchArgs {
 void host_layer_info(int N, LayerInfo *info);
 size_t table_doubles(int N);
 hipError_t launch_heldkarp(const LaunchArgs &a, int grid);
-size_t lds_bytes_for(int N, bool lds_table, int threads, bool compact);
+size_t lds_bytes_for(int N, bool lds_table, int threads, bool compact, int vbytes = 8);
 int threads_for(int N, bool lds_table, int requested);
 
 }  // namespace tspgpu

@@ -12,12 +12,13 @@ TSPGPU_EXTERN(14) TSPGPU_EXTERN(15) TSPGPU_EXTERN(16) TSPGPU_EXTERN(17) TSPGPU_E
 
 // n == 2: tsp.cpp:483-502 with cityNums = {1}: key(empty,1) is default-inserted
 // with cost 0, so cost = 0 + d[1][0] and the path is [1, 0].
-__global__ void two_city_kernel(const double *__restrict__ dist, int nblocks, double *__restrict__ cost_out,
+template <typename V>
+__global__ void two_city_kernel(const V *__restrict__ dist, int nblocks, V *__restrict__ cost_out,
                                 int32_t *__restrict__ tour_out)
 {
     const int b = blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= nblocks) return;
-    cost_out[b] = 0.0 + dist[(size_t)b * 4 + 2];
+    cost_out[b] = V(0) + dist[(size_t)b * 4 + 2];
     tour_out[(size_t)b * 3 + 0] = 1;
     tour_out[(size_t)b * 3 + 1] = 0;
     tour_out[(size_t)b * 3 + 2] = -1;
@@ -30,9 +31,9 @@ int threads_for(int N, bool lds_table, int requested)
     return 256;
 }
 
-size_t lds_bytes_for(int N, bool lds_table, int threads, bool compact)
+size_t lds_bytes_for(int N, bool lds_table, int threads, bool compact, int vbytes)
 {
-    return N >= 2 && N <= kMaxN ? lds_bytes(N, lds_table, threads, compact) : 0;
+    return N >= 2 && N <= kMaxN ? lds_bytes(N, lds_table, threads, compact, vbytes) : 0;
 }
 
 hipError_t launch_heldkarp(const LaunchArgs &a, int grid)
@@ -40,8 +41,13 @@ hipError_t launch_heldkarp(const LaunchArgs &a, int grid)
     if (a.nblocks <= 0) return hipSuccess;
     const int N = a.n - 1;
     if (N == 1) {
-        hipLaunchKernelGGL(two_city_kernel, dim3((a.nblocks + 255) / 256), dim3(256), 0, a.stream, a.dist, a.nblocks,
-                           a.cost, a.tour);
+        if (a.vbytes == 4)
+            hipLaunchKernelGGL(two_city_kernel<int32_t>, dim3((a.nblocks + 255) / 256), dim3(256), 0, a.stream,
+                               static_cast<const int32_t *>(a.dist), a.nblocks, static_cast<int32_t *>(a.cost),
+                               a.tour);
+        else
+            hipLaunchKernelGGL(two_city_kernel<double>, dim3((a.nblocks + 255) / 256), dim3(256), 0, a.stream,
+                               static_cast<const double *>(a.dist), a.nblocks, static_cast<double *>(a.cost), a.tour);
         return hipGetLastError();
     }
     switch (N) {

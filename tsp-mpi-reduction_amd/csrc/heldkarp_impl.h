@@ -46,6 +46,25 @@ constexpr int kBinomStride = kBinomCols;   // ints per binomial row, C(a,b) a<=2
 constexpr int kBinomBytesPadded = 2048;    // 21*24*4 = 2016 rounded to 16
 constexpr double kIntMax = 2147483647.0;   // the reference's sentinel (tsp.cpp:411,453)
 
+// Value type of the DP: f64 (the reference's distances) or i32 (the integer
+// matrix extension; exact, half the table bytes, integer VALU ops).
+template <typename V>
+struct ValT;
+template <>
+struct ValT<double> {
+    static constexpr double inf = 2147483647.0;  // INT_MAX, tsp.cpp:411,453
+    static constexpr double invalid = 1.0e300;
+    static constexpr int bytes = 8;
+    __device__ static double vmin(double a, double b) { return fmin(a, b); }
+};
+template <>
+struct ValT<int32_t> {
+    static constexpr int32_t inf = 2147483647;
+    static constexpr int32_t invalid = 2147483647;
+    static constexpr int bytes = 4;
+    __device__ static int32_t vmin(int32_t a, int32_t b) { return a < b ? a : b; }
+};
+
 __host__ __device__ constexpr int cbinom(int a, int b)
 {
     if (b < 0 || b > a) return 0;
@@ -69,48 +88,52 @@ __host__ __device__ constexpr int mask_off(int N, int t)
 // so distinct rows start on distinct 16-B bank groups (ds_read_b128).
 __host__ __device__ constexpr int dist_stride(int N) { return ((N + 2) & ~1) + 2; }
 __host__ __device__ constexpr size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
-__host__ __device__ constexpr size_t dl_bytes(int N) { return align16((size_t)(N + 1) * dist_stride(N) * 8); }
+__host__ __device__ constexpr size_t dl_bytes(int N, int vb = 8) { return align16((size_t)(N + 1) * dist_stride(N) * vb); }
 // only the digit groups N needs are staged in LDS
 __host__ __device__ constexpr int rank_lut_ints(int N)
 {
     return N <= 7 ? kRankR1 : (N <= 14 ? kRankR1 + kRankR2 : kRankLutInts);
 }
 __host__ __device__ constexpr int rank_lut_bytes(int N) { return (rank_lut_ints(N) * 4 + 15) & ~15; }
-__host__ __device__ constexpr size_t layer_bytes(int N, int t) { return (size_t)cbinom(N, t) * t * 8; }
-__host__ __device__ constexpr size_t low_bytes(int N, int a)
+__host__ __device__ constexpr size_t layer_bytes(int N, int t, int vb = 8) { return (size_t)cbinom(N, t) * t * vb; }
+__host__ __device__ constexpr size_t low_bytes(int N, int a, int vb = 8)
 {
     size_t b = 0;
-    for (int t = 1; t <= a; ++t) b += layer_bytes(N, t);
+    for (int t = 1; t <= a; ++t) b += layer_bytes(N, t, vb);
     return b;
 }
-__host__ __device__ constexpr size_t high_bytes(int N, int a)
+__host__ __device__ constexpr size_t high_bytes(int N, int a, int vb = 8)
 {
     size_t b = 0;
-    for (int t = N - a + 1; t <= N; ++t) b += layer_bytes(N, t);
+    for (int t = N - a + 1; t <= N; ++t) b += layer_bytes(N, t, vb);
     return b;
 }
-__host__ __device__ constexpr size_t lds_base_bytes(int N) { return kBinomBytesPadded + dl_bytes(N) + rank_lut_bytes(N); }
+__host__ __device__ constexpr size_t lds_base_bytes(int N, int vb = 8)
+{
+    return kBinomBytesPadded + dl_bytes(N, vb) + rank_lut_bytes(N);
+}
 // Compact global-table kernels keep the a smallest-index and the a
 // largest-index layers (the smallest layers, e.g. 1-4 and 12-15 of N = 15) in
 // LDS: a workgroup of THREADS threads gets THREADS/1024 of a CU's 160 KiB
 // (the launch places 1024/THREADS workgroups per CU at most).  Those passes
 // then neither touch HBM nor wait on global round trips.
-__host__ __device__ constexpr int lds_end_layers(int N, int threads)
+__host__ __device__ constexpr int lds_end_layers(int N, int threads, int vb = 8)
 {
     const size_t budget = (size_t)160 * 1024 * (size_t)threads / 1024;
-    const size_t base = lds_base_bytes(N) + 1024;
+    const size_t base = lds_base_bytes(N, vb) + 1024;
     if (budget <= base) return 0;
     int a = 0;
-    while (2 * (a + 1) < N && low_bytes(N, a + 1) + high_bytes(N, a + 1) <= budget - base) ++a;
+    while (2 * (a + 1) < N && low_bytes(N, a + 1, vb) + high_bytes(N, a + 1, vb) <= budget - base) ++a;
     return a;
 }
 // LDS: binomials | distance rows | rank LUT | table (LDS_TABLE) | end layers
 // (compact global kernels) | per-thread row slots (member-sweep global kernels)
-__host__ __device__ constexpr size_t lds_bytes(int N, bool lds_table, int threads, bool compact)
+__host__ __device__ constexpr size_t lds_bytes(int N, bool lds_table, int threads, bool compact, int vb = 8)
 {
-    return lds_base_bytes(N) +
-           (lds_table ? ((size_t)N << (N - 1)) * 8
-                      : (compact ? low_bytes(N, lds_end_layers(N, threads)) + high_bytes(N, lds_end_layers(N, threads))
+    return lds_base_bytes(N, vb) +
+           (lds_table ? ((size_t)N << (N - 1)) * vb
+                      : (compact ? low_bytes(N, lds_end_layers(N, threads, vb), vb) +
+                                       high_bytes(N, lds_end_layers(N, threads, vb), vb)
                                  : (size_t)(N - 1) * threads * 8));
 }
 
@@ -137,17 +160,18 @@ __device__ __forceinline__ int colex_rank(uint32_t mask, const int *binom)
     return rank;
 }
 
-__device__ __forceinline__ double wave_min(double v)
+template <typename V>
+__device__ __forceinline__ V wave_min(V v)
 {
 #pragma unroll
-    for (int off = 32; off > 0; off >>= 1) v = fmin(v, __shfl_xor(v, off));
+    for (int off = 32; off > 0; off >>= 1) v = ValT<V>::vmin(v, __shfl_xor(v, off));
     return v;
 }
 
 // dl row m holds d[m][1..N] at [0, N) and d[m][0] at N: the N values a row
 // sweep needs start 16-B aligned.
-template <int N>
-__device__ __forceinline__ double dget(const double *dl, int m, int k)
+template <int N, typename V>
+__device__ __forceinline__ V dget(const V *dl, int m, int k)
 {
     return dl[m * dist_stride(N) + (k == 0 ? N : k - 1)];
 }
@@ -155,7 +179,22 @@ __device__ __forceinline__ double dget(const double *dl, int m, int k)
 // Global table access through a buffer resource (SRSRC): 32-bit offsets in
 // one VGPR instead of 64-bit pointers, and the hardware range check turns
 // any out-of-slot index into a dropped access instead of a fault.
-struct GlobalTable {
+template <typename V>
+struct GlobalTableT;
+template <>
+struct GlobalTableT<int32_t> {
+    __amdgpu_buffer_rsrc_t rs;
+    __device__ __forceinline__ int32_t load(uint32_t idx) const
+    {
+        return (int32_t)__builtin_amdgcn_raw_buffer_load_b32(rs, (int)(idx * 4u), 0, 0);
+    }
+    __device__ __forceinline__ void store(uint32_t idx, int32_t v) const
+    {
+        __builtin_amdgcn_raw_buffer_store_b32((uint32_t)v, rs, (int)(idx * 4u), 0, 0);
+    }
+};
+template <>
+struct GlobalTableT<double> {
     __amdgpu_buffer_rsrc_t rs;
     __device__ __forceinline__ double load(uint32_t idx) const
     {
@@ -175,34 +214,37 @@ struct GlobalTable {
         __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2, v), rs, (int)(idx * 8u), 0, 0);
     }
 };
-struct LdsTable {
-    double *p;
+using GlobalTable = GlobalTableT<double>;
+template <typename V>
+struct LdsTableT {
+    V *p;
     uint32_t base = 0;  // table index of p[0]
-    __device__ __forceinline__ double load(uint32_t idx) const { return p[idx - base]; }
-    __device__ __forceinline__ void store_if(bool pred, uint32_t idx, double v) const
+    __device__ __forceinline__ V load(uint32_t idx) const { return p[idx - base]; }
+    __device__ __forceinline__ void store_if(bool pred, uint32_t idx, V v) const
     {
         if (pred) p[idx - base] = v;
     }
-    __device__ __forceinline__ void store(uint32_t idx, double v) const { p[idx - base] = v; }
+    __device__ __forceinline__ void store(uint32_t idx, V v) const { p[idx - base] = v; }
 };
+using LdsTable = LdsTableT<double>;
 
 // The table of a compact global kernel: layers 1..A and N-A+1..N in LDS, the
 // rest in the workgroup's HBM slot (same indices everywhere).
-template <int N, int A>
+template <typename V, int N, int A>
 struct SplitTable {
-    GlobalTable g;
-    double *lo, *hi;
+    GlobalTableT<V> g;
+    V *lo, *hi;
     template <int t>
     __device__ __forceinline__ auto layer() const
     {
         if constexpr (A > 0 && t <= A)
-            return LdsTable{lo, 0u};
+            return LdsTableT<V>{lo, 0u};
         else if constexpr (A > 0 && t >= N - A + 1)
-            return LdsTable{hi, (uint32_t)layer_off(N, N - A + 1)};
+            return LdsTableT<V>{hi, (uint32_t)layer_off(N, N - A + 1)};
         else
             return g;
     }
-    __device__ __forceinline__ double get(int t, uint32_t idx) const
+    __device__ __forceinline__ V get(int t, uint32_t idx) const
     {
         if (A > 0 && t <= A) return lo[idx];
         if (A > 0 && t >= N - A + 1) return hi[idx - layer_off(N, N - A + 1)];
@@ -330,8 +372,8 @@ __device__ __forceinline__ void layer_pass_lds(const LdsTable &tab, const double
 // thread, so the kernel runs at 8 waves/SIMD without spilling.
 // PF (prefetch depth): the masks and t values of the next PF rows are in
 // flight while the current row is relaxed (software pipelining, 2t VGPRs per row).
-template <int N, int T, int THREADS, int PF, typename SrcTab, typename DstTab>
-__device__ __forceinline__ void layer_pass_compact(const SrcTab &src, const DstTab &dst, const double *__restrict__ dl,
+template <typename V, int N, int T, int THREADS, int PF, typename SrcTab, typename DstTab>
+__device__ __forceinline__ void layer_pass_compact(const SrcTab &src, const DstTab &dst, const V *__restrict__ dl,
                                                    const int *__restrict__ rl, const uint32_t *__restrict__ masks,
                                                    uint32_t tid)
 {
@@ -345,7 +387,7 @@ __device__ __forceinline__ void layer_pass_compact(const SrcTab &src, const DstT
     constexpr uint32_t FULL = (1u << N) - 1u;
     const uint32_t *mt = masks + mask_off(N, T);
     uint32_t m1 = 0, m2 = 0;
-    double g1[T], g2[T];
+    V g1[T], g2[T];
     if constexpr (PF >= 1) {
         if (tid < ROWS) {
             m1 = mt[tid];
@@ -362,7 +404,7 @@ __device__ __forceinline__ void layer_pass_compact(const SrcTab &src, const DstT
     }
     for (uint32_t r = tid; r < ROWS; r += THREADS) {
         uint32_t Tm;
-        double g[T];
+        V g[T];
         if constexpr (PF == 0) {
             Tm = mt[r];
 #pragma unroll
@@ -396,17 +438,17 @@ __device__ __forceinline__ void layer_pass_compact(const SrcTab &src, const DstT
             kb[q] = __builtin_ctz(nb);
             nb &= nb - 1u;
         }
-        double acc[Q];
+        V acc[Q];
 #pragma unroll
-        for (int q = 0; q < Q; ++q) acc[q] = kIntMax;
+        for (int q = 0; q < Q; ++q) acc[q] = ValT<V>::inf;
         uint32_t bits = Tm;
 #pragma unroll
         for (int j = 0; j < T; ++j) {
             const int m = __builtin_ctz(bits) + 1;
             bits &= bits - 1u;
-            const double *drow = dl + m * DS;
+            const V *drow = dl + m * DS;
 #pragma unroll
-            for (int q = 0; q < Q; ++q) acc[q] = fmin(acc[q], g[j] + drow[kb[q]]);
+            for (int q = 0; q < Q; ++q) acc[q] = ValT<V>::vmin(acc[q], g[j] + drow[kb[q]]);
         }
 #pragma unroll
         for (int q = 0; q < Q; ++q) {
@@ -417,24 +459,25 @@ __device__ __forceinline__ void layer_pass_compact(const SrcTab &src, const DstT
     }
 }
 
-template <int N, int T, int THREADS, int PF, typename Tab>
-__device__ __forceinline__ void all_layers_compact(const Tab &tab, const double *dl, const int *rl,
+template <typename V, int N, int T, int THREADS, int PF, typename Tab>
+__device__ __forceinline__ void all_layers_compact(const Tab &tab, const V *dl, const int *rl,
                                                    const uint32_t *masks, uint32_t tid)
 {
     if constexpr (T < N) {
-        layer_pass_compact<N, T, THREADS, PF>(tab, tab, dl, rl, masks, tid);
+        layer_pass_compact<V, N, T, THREADS, PF>(tab, tab, dl, rl, masks, tid);
         __syncthreads();
-        all_layers_compact<N, T + 1, THREADS, PF>(tab, dl, rl, masks, tid);
+        all_layers_compact<V, N, T + 1, THREADS, PF>(tab, dl, rl, masks, tid);
     }
 }
-template <int N, int A, int T, int THREADS, int PF>
-__device__ __forceinline__ void all_layers_split(const SplitTable<N, A> &tb, const double *dl, const int *rl,
+template <typename V, int N, int A, int T, int THREADS, int PF>
+__device__ __forceinline__ void all_layers_split(const SplitTable<V, N, A> &tb, const V *dl, const int *rl,
                                                  const uint32_t *masks, uint32_t tid)
 {
     if constexpr (T < N) {
-        layer_pass_compact<N, T, THREADS, PF>(tb.template layer<T>(), tb.template layer<T + 1>(), dl, rl, masks, tid);
+        layer_pass_compact<V, N, T, THREADS, PF>(tb.template layer<T>(), tb.template layer<T + 1>(), dl, rl, masks,
+                                                 tid);
         __syncthreads();
-        all_layers_split<N, A, T + 1, THREADS, PF>(tb, dl, rl, masks, tid);
+        all_layers_split<V, N, A, T + 1, THREADS, PF>(tb, dl, rl, masks, tid);
     }
 }
 
@@ -463,35 +506,36 @@ __host__ __device__ constexpr int min_waves(int N, int var)
 {
     return var == 1 ? (N <= 15 ? 8 : 4) : (N <= 15 ? 4 : 2);
 }
-template <int N, bool LDS_TABLE, int THREADS, int VAR>
+template <typename V, int N, bool LDS_TABLE, int THREADS, int VAR>
 __global__ __launch_bounds__(THREADS, min_waves(N, VAR)) void heldkarp_kernel(
-    const double *__restrict__ dist, int nblocks, double *__restrict__ slots, size_t slot_doubles,
-    const uint32_t *__restrict__ masks, const LayerInfo *__restrict__ info, double *__restrict__ cost_out,
+    const V *__restrict__ dist, int nblocks, V *__restrict__ slots, size_t slot_doubles,
+    const uint32_t *__restrict__ masks, const LayerInfo *__restrict__ info, V *__restrict__ cost_out,
     int32_t *__restrict__ tour_out)
 {
     constexpr int n = N + 1;
     constexpr int DS = dist_stride(N);
+    constexpr int VB = ValT<V>::bytes;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     int *binom = reinterpret_cast<int *>(smem);
-    double *dl = reinterpret_cast<double *>(smem + kBinomBytesPadded);
-    int *rl = reinterpret_cast<int *>(smem + kBinomBytesPadded + dl_bytes(N));
-    double *lds_rest = reinterpret_cast<double *>(smem + kBinomBytesPadded + dl_bytes(N) + rank_lut_bytes(N));
+    V *dl = reinterpret_cast<V *>(smem + kBinomBytesPadded);
+    int *rl = reinterpret_cast<int *>(smem + kBinomBytesPadded + dl_bytes(N, VB));
+    V *lds_rest = reinterpret_cast<V *>(smem + kBinomBytesPadded + dl_bytes(N, VB) + rank_lut_bytes(N));
     const int tid = threadIdx.x;
 
     for (int i = tid; i < kBinomRows * kBinomStride; i += THREADS) binom[i] = info->binom[i];
     for (int i = tid; i < rank_lut_ints(N); i += THREADS) rl[i] = info->rlut[i];
 
-    double *tab;
+    V *tab;
     if constexpr (LDS_TABLE)
         tab = lds_rest;
     else
         tab = slots + (size_t)blockIdx.x * slot_doubles;
-    using Tab = typename std::conditional<LDS_TABLE, LdsTable, GlobalTable>::type;
+    using Tab = typename std::conditional<LDS_TABLE, LdsTableT<V>, GlobalTableT<V>>::type;
     // compact global kernels: the end layers live in LDS behind the LUT
-    constexpr int A = (!LDS_TABLE && VAR >= 1) ? lds_end_layers(N, THREADS) : 0;
-    SplitTable<N, A> tb;
+    constexpr int A = (!LDS_TABLE && VAR >= 1) ? lds_end_layers(N, THREADS, VB) : 0;
+    SplitTable<V, N, A> tb;
     tb.lo = lds_rest;
-    tb.hi = lds_rest + low_bytes(N, A) / 8;
+    tb.hi = lds_rest + low_bytes(N, A, VB) / VB;
     Tab th;
     if constexpr (LDS_TABLE) {
         th.p = tab;
@@ -501,13 +545,13 @@ __global__ __launch_bounds__(THREADS, min_waves(N, VAR)) void heldkarp_kernel(
         const uint64_t base = reinterpret_cast<uint64_t>(tab);
         const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)base);
         const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(base >> 32));
-        const int bytes = __builtin_amdgcn_readfirstlane((int)(slot_doubles * 8));
+        const int bytes = __builtin_amdgcn_readfirstlane((int)(slot_doubles * VB));
         th.rs = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void *>(((uint64_t)hi << 32) | lo), 0, bytes,
                                                   0x00020000);
         tb.g = th;
     }
     // table entry (layer t, index idx) wherever it lives
-    auto tget = [&](int t, uint32_t idx) -> double {
+    auto tget = [&](int t, uint32_t idx) -> V {
         if constexpr (LDS_TABLE)
             return tab[idx];
         else if constexpr (A > 0)
@@ -517,7 +561,7 @@ __global__ __launch_bounds__(THREADS, min_waves(N, VAR)) void heldkarp_kernel(
     };
 
     for (int blk = blockIdx.x; blk < nblocks; blk += gridDim.x) {
-        const double *dsrc = dist + (size_t)blk * n * n;
+        const V *dsrc = dist + (size_t)blk * n * n;
         for (int i = tid; i < n * n; i += THREADS) {
             const int row = i / n, col = i % n;
             dl[row * DS + (col == 0 ? N : col - 1)] = dsrc[i];
@@ -539,10 +583,10 @@ __global__ __launch_bounds__(THREADS, min_waves(N, VAR)) void heldkarp_kernel(
         int tid_b = tid;
         asm volatile("" : "+v"(tid_b));
         if constexpr (!LDS_TABLE && VAR >= 1)
-            all_layers_split<N, A, 1, THREADS, VAR - 1>(tb, dl, rl, masks, (uint32_t)tid_b);
+            all_layers_split<V, N, A, 1, THREADS, VAR - 1>(tb, dl, rl, masks, (uint32_t)tid_b);
         else if constexpr (VAR >= 1)
-            all_layers_compact<N, 1, THREADS, VAR - 1>(th, dl, rl, masks, (uint32_t)tid_b);
-        else
+            all_layers_compact<V, N, 1, THREADS, VAR - 1>(th, dl, rl, masks, (uint32_t)tid_b);
+        else if constexpr (std::is_same<V, double>::value)
             all_layers<N, 1, THREADS>(th, dl, binom, lds_rest + tid_b, masks, (uint32_t)tid_b);
 
         // closing min (tsp.cpp:483-499) and backtracking, one wave: lane m-1
@@ -554,23 +598,23 @@ __global__ __launch_bounds__(THREADS, min_waves(N, VAR)) void heldkarp_kernel(
             const uint32_t full = (1u << N) - 1u;
             const bool valid = m <= N;
             // the last layer is one row: position m-1 at m-1
-            const double glast = valid ? tget(N, layer_off(N, N) + (uint32_t)(m - 1)) : 0.0;
-            const double cand = valid ? glast + dget<N>(dl, m, 0) : 1.0e300;
-            const double best = fmin(wave_min(cand), kIntMax);
-            const unsigned long long hit = __ballot(valid && cand == best && cand < kIntMax);
+            const V glast = valid ? tget(N, layer_off(N, N) + (uint32_t)(m - 1)) : V(0);
+            const V cand = valid ? glast + dget<N>(dl, m, 0) : ValT<V>::invalid;
+            const V best = ValT<V>::vmin(wave_min(cand), ValT<V>::inf);
+            const unsigned long long hit = __ballot(valid && cand == best && cand < ValT<V>::inf);
             const int bestM = hit ? __ffsll(hit) : 0;
             int32_t *tour = tour_out + (size_t)blk * (n + 1);
             uint32_t S = full;
             int k = bestM;
             int pos = n - 2;
             bool ok = bestM != 0;
-            double target = __shfl(glast, ok ? bestM - 1 : 0);
+            V target = __shfl(glast, ok ? bestM - 1 : 0);
             while (ok && __builtin_popcount(S) >= 2) {
                 const uint32_t T = S & ~(1u << (k - 1));
                 const int tt = __builtin_popcount(T);
                 const uint32_t rT = lut_rank<N>(T, rl);
                 const bool inT = valid && ((T >> (m - 1)) & 1u);
-                double gv = 0.0, c = 0.0;
+                V gv = V(0), c = V(0);
                 if (inT) {
                     gv = tget(tt, info->off[tt] + __builtin_popcount(T & ((1u << (m - 1)) - 1u)) * info->count[tt] + rT);
                     c = gv + dget<N>(dl, m, k);
@@ -588,29 +632,30 @@ __global__ __launch_bounds__(THREADS, min_waves(N, VAR)) void heldkarp_kernel(
                 tour[0] = 0;
                 tour[n - 1] = bestM;
                 tour[n] = 0;
-                cost_out[blk] = ok ? best : -1.0;  // -1: no predecessor matched (never expected)
+                cost_out[blk] = ok ? best : V(-1);  // -1: no predecessor matched (never expected)
             }
         }
         __syncthreads();
     }
 }
 
-template <int N, bool LDS, int THREADS, int VAR>
+template <typename V, int N, bool LDS, int THREADS, int VAR>
 hipError_t launch_n(const LaunchArgs &a, int grid)
 {
-    const size_t lds = lds_bytes(N, LDS, THREADS, VAR >= 1);
+    const size_t lds = lds_bytes(N, LDS, THREADS, VAR >= 1, ValT<V>::bytes);
     if (lds > 64 * 1024) {
         static bool raised = false;  // once per instantiation
         if (!raised) {
             hipError_t e = hipFuncSetAttribute(
-                reinterpret_cast<const void *>(&heldkarp_kernel<N, LDS, THREADS, VAR>),
+                reinterpret_cast<const void *>(&heldkarp_kernel<V, N, LDS, THREADS, VAR>),
                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
             if (e != hipSuccess) return e;
             raised = true;
         }
     }
-    hipLaunchKernelGGL((heldkarp_kernel<N, LDS, THREADS, VAR>), dim3(grid), dim3(THREADS), lds, a.stream, a.dist,
-                       a.nblocks, a.slots, a.slot_doubles, a.masks, a.info, a.cost, a.tour);
+    hipLaunchKernelGGL((heldkarp_kernel<V, N, LDS, THREADS, VAR>), dim3(grid), dim3(THREADS), lds, a.stream,
+                       static_cast<const V *>(a.dist), a.nblocks, static_cast<V *>(a.slots), a.slot_doubles, a.masks,
+                       a.info, static_cast<V *>(a.cost), a.tour);
     return hipGetLastError();
 }
 
@@ -618,25 +663,27 @@ hipError_t launch_n(const LaunchArgs &a, int grid)
 // admits one workgroup per CU, so it gets 1024 threads (4 waves per SIMD).
 __host__ __device__ constexpr int lds_table_threads(int N) { return N >= 11 ? 1024 : 256; }
 
-template <int N, int VAR>
+template <typename V, int N, int VAR>
 hipError_t launch_threads_v(const LaunchArgs &a, int grid)
 {
     if constexpr (N <= kLdsTableMaxN) {
-        if (a.use_lds) return launch_n<N, true, lds_table_threads(N), VAR >= 2 ? 1 : VAR>(a, grid);
+        if (a.use_lds) return launch_n<V, N, true, lds_table_threads(N), VAR >= 2 ? 1 : VAR>(a, grid);
     }
     if constexpr (N >= 12 && N <= 15) {
-        if (a.threads == 512) return launch_n<N, false, 512, VAR>(a, grid);
-        if (a.threads == 1024) return launch_n<N, false, 1024, VAR>(a, grid);
+        if (a.threads == 512) return launch_n<V, N, false, 512, VAR>(a, grid);
+        if (a.threads == 1024) return launch_n<V, N, false, 1024, VAR>(a, grid);
     }
-    return launch_n<N, false, 256, VAR>(a, grid);
+    return launch_n<V, N, false, 256, VAR>(a, grid);
 }
 
 template <int N>
 hipError_t launch_threads(const LaunchArgs &a, int grid)
 {
+    // integer matrices: the default (compact + prefetch) pass only
+    if (a.vbytes == 4) return launch_threads_v<int32_t, N, 2>(a, grid);
     // (VAR 3, two rows in flight, measured no faster than one: not instantiated)
-    if (a.variant >= 2) return launch_threads_v<N, 2>(a, grid);
-    return a.variant == 1 ? launch_threads_v<N, 1>(a, grid) : launch_threads_v<N, 0>(a, grid);
+    if (a.variant >= 2) return launch_threads_v<double, N, 2>(a, grid);
+    return a.variant == 1 ? launch_threads_v<double, N, 1>(a, grid) : launch_threads_v<double, N, 0>(a, grid);
 }
 
 }  // namespace tspgpu

@@ -139,8 +139,8 @@ int check_n(int n, int strict)
     return 0;
 }
 
-int solve_device_locked(tspgpu_ctx *c, const double *d_dist, int n, int nblocks, double *d_cost,
-                        int32_t *d_tour, hipStream_t stream)
+int solve_device_locked(tspgpu_ctx *c, const void *d_dist, int n, int nblocks, void *d_cost, int32_t *d_tour,
+                        hipStream_t stream, int vbytes)
 {
     int rc = check_n(n, c->strict);
     if (rc) return rc;
@@ -155,6 +155,7 @@ int solve_device_locked(tspgpu_ctx *c, const double *d_dist, int n, int nblocks,
     a.cost = d_cost;
     a.tour = d_tour;
     a.stream = stream;
+    a.vbytes = vbytes;
     int grid = nblocks;
     if (N >= 2) {
         rc = ensure_tables(c, N);
@@ -166,13 +167,19 @@ int solve_device_locked(tspgpu_ctx *c, const double *d_dist, int n, int nblocks,
         // tables want many blocks in flight; at n = 15, 16 one 1024-thread slot
         // per CU keeps the live layers of the 256 resident blocks in the
         // Infinity Cache (n = 15: 1.45x over two 512-thread slots)
-        const int def_threads = N <= 11 ? 256 : (N <= 13 ? 512 : (N <= 15 ? 1024 : 256));
-        const int def_wg = N <= 11 ? 8 : (N <= 13 ? 2 : (N <= 15 ? 1 : 2));
+        // (i32 tables are half the bytes: 512-thread pairs at n = 15, 16 and
+        // 8 workgroups per CU up to n = 13; profiles/r01/i32_sweep*.log)
+        int def_threads = N <= 11 ? 256 : (N <= 13 ? 512 : (N <= 15 ? 1024 : 256));
+        int def_wg = N <= 11 ? 8 : (N <= 13 ? 2 : (N <= 15 ? 1 : 2));
+        if (vbytes == 4) {
+            def_threads = N <= 13 ? 256 : (N <= 15 ? 512 : 256);
+            def_wg = N <= 12 ? 8 : (N <= 13 ? 4 : 2);
+        }
         a.threads = c->threads > 0 ? c->threads : def_threads;
         a.variant = c->variant;
         if (a.use_lds) {
             // as many resident workgroups as the LDS allows, then persistent
-            const int per_cu = (int)(160 * 1024 / lds_bytes_for(N, true, threads_for(N, true, 0), c->variant >= 1));
+            const int per_cu = (int)(160 * 1024 / lds_bytes_for(N, true, threads_for(N, true, 0), vbytes == 4 || c->variant >= 1, vbytes));
             const int cap = c->cu_count * (per_cu > 0 ? per_cu : 1);
             grid = nblocks < cap ? nblocks : cap;
         } else {
@@ -181,7 +188,7 @@ int solve_device_locked(tspgpu_ctx *c, const double *d_dist, int n, int nblocks,
             const int per_cu = N >= 16 ? (wg < 2 ? wg : 2) : wg;
             int slots = c->slots_opt > 0 ? c->slots_opt : c->cu_count * per_cu;
             // keep the workspace under ~8 GiB for the largest extension sizes
-            const size_t per = table_doubles(N) * sizeof(double);
+            const size_t per = table_doubles(N) * (size_t)vbytes;
             const size_t budget = (size_t)8 << 30;
             if ((size_t)slots * per > budget) slots = (int)(budget / per);
             if (slots < 1) slots = 1;
@@ -197,6 +204,9 @@ int solve_device_locked(tspgpu_ctx *c, const double *d_dist, int n, int nblocks,
 }
 
 thread_local std::unique_ptr<tspgpu_ctx, int (*)(tspgpu_ctx *)> t_default(nullptr, tspgpu_ctx_destroy);
+
+template <typename V>
+int solve_host_copy(tspgpu_ctx *c, const V *dist, int n, int nblocks, V *cost_out, int32_t *tour_out);
 
 }  // namespace
 
@@ -365,7 +375,15 @@ int tspgpu_solve_blocks_device(tspgpu_ctx *c, const double *d_dist, int n, int n
 {
     if (!c) return -EINVAL;
     std::lock_guard<std::mutex> g(c->mu);
-    return solve_device_locked(c, d_dist, n, nblocks, d_cost, d_tour, (hipStream_t)hip_stream);
+    return solve_device_locked(c, d_dist, n, nblocks, d_cost, d_tour, (hipStream_t)hip_stream, 8);
+}
+
+int tspgpu_solve_blocks_i32_device(tspgpu_ctx *c, const int32_t *d_dist, int n, int nblocks, int32_t *d_cost,
+                                   int32_t *d_tour, void *hip_stream)
+{
+    if (!c) return -EINVAL;
+    std::lock_guard<std::mutex> g(c->mu);
+    return solve_device_locked(c, d_dist, n, nblocks, d_cost, d_tour, (hipStream_t)hip_stream, 4);
 }
 
 int tspgpu_solve_blocks(tspgpu_ctx *c, const double *dist, int n, int nblocks, double *cost_out,
@@ -374,12 +392,51 @@ int tspgpu_solve_blocks(tspgpu_ctx *c, const double *dist, int n, int nblocks, d
     if (!c) return -EINVAL;
     int rc = tspgpu_validate(dist, n, nblocks, c->strict);
     if (rc) return rc;
+    return solve_host_copy(c, dist, n, nblocks, cost_out, tour_out);
+}
+
+int tspgpu_solve_blocks_i32(tspgpu_ctx *c, const int32_t *dist, int n, int nblocks, int32_t *cost_out,
+                            int32_t *tour_out)
+{
+    if (!c) return -EINVAL;
+    int rc = tspgpu_validate_i32(dist, n, nblocks, c->strict);
+    if (rc) return rc;
+    return solve_host_copy(c, dist, n, nblocks, cost_out, tour_out);
+}
+
+int tspgpu_validate_i32(const int32_t *dist, int n, int nblocks, int strict)
+{
+    int rc = check_n(n, strict);
+    if (rc) return rc;
+    if (nblocks < 0 || (nblocks > 0 && !dist)) return -EINVAL;
+    for (int b = 0; b < nblocks; ++b) {
+        const int32_t *d = dist + (size_t)b * n * n;
+        int64_t mx = 0;
+        for (int i = 0; i < n * n; ++i) {
+            if (d[i] < 0) return -EINVAL;
+            if (d[i] > mx) mx = d[i];
+        }
+        // n edges per tour stay below INT_MAX: no i32 overflow, and the same
+        // sentinel argument as tspgpu_validate
+        if ((int64_t)n * mx >= (int64_t)INT_MAX) return -ERANGE;
+    }
+    return 0;
+}
+
+}  // extern "C"
+
+namespace {
+
+template <typename V>
+int solve_host_copy(tspgpu_ctx *c, const V *dist, int n, int nblocks, V *cost_out, int32_t *tour_out)
+{
+    int rc = 0;
     if (nblocks > 0 && (!cost_out || !tour_out)) return -EINVAL;
     if (nblocks == 0) return 0;
     std::lock_guard<std::mutex> g(c->mu);
     if (hipSetDevice(c->device) != hipSuccess) return -ENODEV;
-    const size_t db = (size_t)nblocks * n * n * sizeof(double);
-    const size_t cb = (size_t)nblocks * sizeof(double);
+    const size_t db = (size_t)nblocks * n * n * sizeof(V);
+    const size_t cb = (size_t)nblocks * sizeof(V);
     const size_t tb = (size_t)nblocks * (n + 1) * sizeof(int32_t);
     if ((rc = ensure(&c->d_dist, &c->dist_bytes, db))) return rc;
     if ((rc = ensure(&c->d_cost, &c->cost_bytes, cb))) return rc;
@@ -387,16 +444,20 @@ int tspgpu_solve_blocks(tspgpu_ctx *c, const double *dist, int n, int nblocks, d
     hipError_t e = hipMemcpyAsync(c->d_dist, dist, db, hipMemcpyHostToDevice, c->stream);
     if (e == hipSuccess) e = hipMemsetAsync(c->d_tour, 0xff, tb, c->stream);
     if (e != hipSuccess) return hip_err(e);
-    rc = solve_device_locked(c, c->d_dist, n, nblocks, c->d_cost, c->d_tour, c->stream);
+    rc = solve_device_locked(c, c->d_dist, n, nblocks, c->d_cost, c->d_tour, c->stream, (int)sizeof(V));
     if (rc) return rc;
     e = hipMemcpyAsync(cost_out, c->d_cost, cb, hipMemcpyDeviceToHost, c->stream);
     if (e == hipSuccess) e = hipMemcpyAsync(tour_out, c->d_tour, tb, hipMemcpyDeviceToHost, c->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
     if (e != hipSuccess) return hip_err(e);
     for (int b = 0; b < nblocks; ++b)
-        if (cost_out[b] < 0.0) return -EIO;  // backtracking found no predecessor
+        if (cost_out[b] < V(0)) return -EIO;  // backtracking found no predecessor
     return 0;
 }
+
+}  // namespace
+
+extern "C" {
 
 int tspgpu_solve_cities(tspgpu_ctx *c, const tspgpu_city *cities, int n, int nblocks, double *cost_out,
                         int32_t *tour_out)

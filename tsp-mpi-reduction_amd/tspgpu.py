@@ -34,6 +34,8 @@ EXPORTED_SYMBOLS = (
     "tspgpu_merge", "tspgpu_reduce",
     # K1-wide
     "tspgpu_solve_instance",
+    # K1 on integer distances
+    "tspgpu_validate_i32", "tspgpu_solve_blocks_i32", "tspgpu_solve_blocks_i32_device",
 )
 
 F64, I32 = 0, 1
@@ -93,6 +95,9 @@ def lib():
         L.tspgpu_solve_blocks.argtypes = [vp, dp, ctypes.c_int, ctypes.c_int, dp, ip]
         L.tspgpu_solve_cities.argtypes = [vp, ctypes.POINTER(City), ctypes.c_int, ctypes.c_int, dp, ip]
         L.tspgpu_solve_blocks_device.argtypes = [vp, vp, ctypes.c_int, ctypes.c_int, vp, vp, vp]
+        L.tspgpu_validate_i32.argtypes = [ip, ctypes.c_int, ctypes.c_int, ctypes.c_int]
+        L.tspgpu_solve_blocks_i32.argtypes = [vp, ip, ctypes.c_int, ctypes.c_int, ip, ip]
+        L.tspgpu_solve_blocks_i32_device.argtypes = [vp, vp, ctypes.c_int, ctypes.c_int, vp, vp, vp]
         L.tspgpu_solve.argtypes = [dp, ctypes.c_int, ctypes.c_int, dp, ip, ctypes.POINTER(Opts)]
         L.tspgpu_last_grid.argtypes = [vp]
         L.tspgpu_relaxations_per_block.argtypes = [ctypes.c_int]
@@ -196,6 +201,12 @@ def validate(dist: np.ndarray, strict: bool = False) -> int:
     return lib().tspgpu_validate(_dp(dist), n, B, int(strict))
 
 
+def validate_i32(dist: np.ndarray, strict: bool = False) -> int:
+    dist = np.ascontiguousarray(dist, dtype=np.int32)
+    B, n, _ = dist.shape
+    return lib().tspgpu_validate_i32(_ip(dist), n, B, int(strict))
+
+
 class Context:
     """Owns a tspgpu_ctx (device memory, stream) on one HIP device."""
 
@@ -234,6 +245,24 @@ class Context:
         if rc:
             raise TspGpuError(rc, "tspgpu_solve_blocks")
         return cost, tour
+
+    def solve_blocks_i32(self, dist: np.ndarray):
+        """dist: (B, n, n) int32 -> (costs (B,) int32, tours (B, n+1) int32, -1 padded)."""
+        dist = np.ascontiguousarray(dist, dtype=np.int32)
+        B, n, _ = dist.shape
+        cost = np.zeros(B, dtype=np.int32)
+        tour = np.full((B, n + 1), -1, dtype=np.int32)
+        rc = lib().tspgpu_solve_blocks_i32(self.handle, _ip(dist), n, B, _ip(cost), _ip(tour))
+        if rc:
+            raise TspGpuError(rc, "tspgpu_solve_blocks_i32")
+        return cost, tour
+
+    def solve_device_i32(self, d_dist_ptr: int, n: int, nblocks: int, d_cost_ptr: int, d_tour_ptr: int,
+                         stream_ptr: int = 0):
+        rc = lib().tspgpu_solve_blocks_i32_device(self.handle, d_dist_ptr, n, nblocks, d_cost_ptr, d_tour_ptr,
+                                                  stream_ptr)
+        if rc:
+            raise TspGpuError(rc, "tspgpu_solve_blocks_i32_device")
 
     def solve_cities(self, blocks):
         arr, n, B = cities_array(blocks)
