@@ -175,6 +175,9 @@ typedef struct
     int fallback;           /* 1: |O| too large to enumerate, the answer came from K1-wide (n <= 31) */
     int rounds;             /* search rounds of the last phase (items split and re-queued between rounds) */
     double kernel_ms;       /* device time of the search launches */
+    uint64_t lane_steps;    /* lane slots of the search loop (64 per wave step) */
+    uint64_t active_steps;  /* ... of which a lane worked on an item (lane utilisation = active/lane) */
+    uint64_t item_loads;    /* items loaded by lanes (seeds and hand-backs) */
 } tspgpu_search_stats;
 
 typedef struct tspgpu_search tspgpu_search; /* one instance (or one shard of it) on one context */

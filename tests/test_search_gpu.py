@@ -103,8 +103,9 @@ def test_k2_matches_k1(gpu_ctx):
 
 @pytest.mark.parametrize("budget", ["1", "64"])
 def test_tiny_budget_splits_everything(gpu_ctx, monkeypatch, budget):
-    """Budgets of 1 and 64 iterations: nearly every item is cut and re-queued
-    many times; the answer must not change."""
+    """Round kernel (2), budgets of 1 and 64 iterations: nearly every item is
+    cut and re-queued many times; the answer must not change."""
+    monkeypatch.setenv("TSPGPU_SEARCH_KERNEL", "2")
     monkeypatch.setenv("TSPGPU_SEARCH_BUDGET", budget)
     rng = np.random.default_rng(int(budget))
     for n in (9, 12):
@@ -115,6 +116,32 @@ def test_tiny_budget_splits_everything(gpu_ctx, monkeypatch, budget):
         assert (cost, tour.tolist()) == (oc, ot), st
         if n == 12 and budget == "1":
             assert st["rounds"] > 2, st
+
+
+@pytest.mark.parametrize("mode", ["donate_always", "small_ring", "kernel1", "kernel2"])
+def test_search_kernels_and_hand_off_stress(gpu_ctx, monkeypatch, mode):
+    """Persistent search with a donation at every chance (every busy lane
+    splits its root level whenever it may), with a 64-item ring (donations
+    mostly refused by the capacity check), and the two round kernels: same
+    cost and tour as the oracle, tie-heavy and random instances."""
+    env = {"donate_always": {"TSPGPU_SEARCH_HUNGRY": "-1000000000", "TSPGPU_SEARCH_MIN_SPLIT": "0"},
+           "small_ring": {"TSPGPU_SEARCH_RING_LOG2": "6", "TSPGPU_SEARCH_HUNGRY": "-1000000000",
+                          "TSPGPU_SEARCH_MIN_SPLIT": "0"},
+           "kernel1": {"TSPGPU_SEARCH_KERNEL": "1"}, "kernel2": {"TSPGPU_SEARCH_KERNEL": "2"}}[mode]
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    monkeypatch.setenv("TSPGPU_SEARCH_WALL_S", "30")
+    rng = np.random.default_rng(len(mode))
+    for n in (5, 9, 12, 14):
+        for kind in ("ties", "random"):
+            if kind == "ties":
+                xy = rng.integers(0, 4, size=(n, 2)).astype(np.float64)
+            else:
+                xy = rng.uniform(0, 1000, size=(n, 2))
+            d = O.distance_matrix([(i, xy[i, 0], xy[i, 1]) for i in range(n)])
+            cost, tour, st = tspgpu.search_solve(gpu_ctx, d)
+            oc, ot = O.solve_block(d)
+            assert (cost, tour.tolist()) == (oc, ot), (mode, n, kind, st)
 
 
 @pytest.mark.parametrize("nshards", [2, 3, 5])

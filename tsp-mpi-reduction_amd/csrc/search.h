@@ -29,6 +29,24 @@ struct SearchItem {
     uint8_t pad[2];
 };
 
+// Device words of the persistent search (search_persist_kernel), zeroed by
+// the host before every launch except work = this shard's seed count.  Each
+// word has a 256-byte line of its own: the counters take atomics from every
+// wave and idle waves poll `work`, so sharing a line would serialise them.
+struct alignas(256) PersistWord {
+    unsigned long long v;
+    unsigned long long pad[31];
+};
+struct PersistState {
+    PersistWord seed_cursor;  // next seed (index into this shard's prefixes)
+    PersistWord head;         // ring tickets claimed by lanes
+    PersistWord tail;         // ring tickets reserved by donors
+    PersistWord consumed;     // ring items read
+    PersistWord work;         // items created (seeds + donations) and not finished
+    PersistWord abort;        // 1: watchdog, 2: ring lapped (never expected)
+};
+constexpr int kRingWords = 5;  // ring item: 4 words of city bytes + (ticket+1) << 32 | from << 8 | len
+
 struct SearchArgs {
     const void *dist;          // n*n row-major, f64 or i32 (device)
     const void *amin;          // n: cheapest edge entering each city (device), f64 on a 2^-20 grid or i32
@@ -47,11 +65,23 @@ struct SearchArgs {
     unsigned int *rec_count;   // records claimed (may exceed rec_cap: overflow)
     unsigned int rec_cap;
     unsigned long long *nodes; // search nodes evaluated (device accumulator)
+    unsigned long long *util;  // v2: [0] lane slots, [1] active lane steps, [2] item loads
+    uint32_t refill;           // v2: a wave refills once this many lanes wait for an item
+    // persistent search (kernel 3)
+    PersistState *ps;
+    unsigned long long *ring;  // kRingWords u64 per item
+    uint32_t ring_mask;        // capacity - 1 (power of two)
+    uint32_t ring_margin;      // reservations stop this far below capacity
+    int32_t hungry;            // donate while more than this many lanes wait for unreserved tickets
+    uint32_t min_split;        // steps on an item before it may donate
+    unsigned long long wall_limit;  // watchdog, wall_clock64 ticks
+    int kernel;                // round kernel: 2 (lock-step DFS, default) or 1 (branching DFS); 3 = persistent
     hipStream_t stream;
 };
 
-size_t search_lds_bytes(int n, bool f64);
+size_t search_lds_bytes(int n, bool f64, int kernel = 2);
 hipError_t launch_seed(const SearchArgs &a, bool f64, int grid);
 hipError_t launch_round(const SearchArgs &a, bool f64, int grid);
+hipError_t launch_persist(const SearchArgs &a, bool f64, int grid);
 
 }  // namespace tspgpu

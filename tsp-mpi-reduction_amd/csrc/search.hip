@@ -145,9 +145,10 @@ __global__ __launch_bounds__(kSearchThreads) void seed_kernel(SearchArgs a)
     }
 }
 
-// One round over the items a.in[0 .. in_count).
+// One round over the items a.in[0 .. in_count) (v1: one DFS iteration per
+// loop trip with a branch per case; kept for A/B measurements).
 template <typename V>
-__global__ __launch_bounds__(kSearchThreads) void round_kernel(SearchArgs a)
+__global__ __launch_bounds__(kSearchThreads) void round_kernel_v1(SearchArgs a)
 {
     using W = typename Num<V>::Wide;
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -352,9 +353,690 @@ __global__ __launch_bounds__(kSearchThreads) void round_kernel(SearchArgs a)
     atomicAdd(a.nodes, nodes);
 }
 
+
+// ---------------------------------------------------------------------------
+// v2 round kernel: the same search, but every lane of a wave advances its DFS
+// by exactly one step per trip of a branch-free inner loop.  A step evaluates
+// the next untried child j of the path's last city k — one search node: the
+// fold cost c = ck + d[k][j] and the bound c + (remA - a[j]) — and then
+// descends (push j), moves to the next sibling, or backs up one level (pop),
+// all as selects.  At the third-to-last level the child's completion is
+// forced (one city r left), so the step closes the tour directly,
+// ((c + d[j][r]) + d[r][0]), instead of descending twice and popping twice.
+// Only the rare record (a complete tour within the incumbent), the refill of
+// lanes whose item is finished and the budget hand-back leave the loop.  v1
+// ran each case as its own branch, so a wave executed all of them every
+// iteration (5.1 wave instructions per node, 9% of the lane slots useful).
+//
+// Per-lane state in VGPRs: level L, path end k, unvisited set rem, the
+// untried-children mask fm of level L, fold cost ck, sum remA of the cheapest
+// incoming edges still to be paid.  Stack in LDS, [level][lane] (conflict
+// free): the fold cost and the city of every level, written one level above
+// the current one on every step (dead unless the step descends) and read one
+// level below (used only by a pop).  remA is restored exactly on a pop
+// (remA + a[k]: a[] lies on a grid), so it needs no stack.
+//
+// LDS: d (n rows of stride 32) | {a[x], d[x][0]} pairs | cost stack [n][T] |
+//      city stack [n][T] | wave item buffers.
+template <typename V>
+struct Thr;  // prune threshold from the incumbent: prune iff bound > thr
+template <>
+struct Thr<double> {
+    // bound > inc*(1+2^-39) implies bound*(1-2^-40) > inc: v1's margin
+    __device__ static double of(double inc) { return inc * (1.0 + 0x1p-39); }
+};
+template <>
+struct Thr<int32_t> {
+    __device__ static int32_t of(int32_t inc) { return inc; }
+};
+
+template <typename V>
+struct alignas(2 * sizeof(V)) APair {
+    V a;   // cheapest edge into x (bound)
+    V d0;  // d[x][0] (closing edge)
+};
+
+constexpr int kRow = 32;  // LDS row stride of d (row offset k << 5)
+template <typename V>
+__host__ __device__ constexpr size_t v2_ad(int n) { return align16((size_t)n * kRow * sizeof(V)); }
+template <typename V>
+__host__ __device__ constexpr size_t v2_cost(int n) { return v2_ad<V>(n) + align16((size_t)n * sizeof(APair<V>)); }
+template <typename V>
+__host__ __device__ constexpr size_t v2_city(int n) { return v2_cost<V>(n) + (size_t)n * kSearchThreads * sizeof(V); }
+template <typename V>
+__host__ __device__ constexpr size_t v2_wbuf(int n) { return align16(v2_city<V>(n) + (size_t)n * kSearchThreads); }
+template <typename V>
+__host__ __device__ constexpr size_t v2_lds(int n)
+{
+    return v2_wbuf<V>(n) + (size_t)(kSearchThreads / 64) * kChunk * sizeof(SearchItem);
+}
+
+template <typename V>
+__global__ __launch_bounds__(kSearchThreads) void round_kernel(SearchArgs a)
+{
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    constexpr int T = kSearchThreads;
+    const int n = a.n;
+    const int tid = threadIdx.x;
+    V *dl = reinterpret_cast<V *>(smem);
+    APair<V> *ad = reinterpret_cast<APair<V> *>(smem + v2_ad<V>(n));
+    V *myc = reinterpret_cast<V *>(smem + v2_cost<V>(n)) + tid;              // cost of level l: myc[l*T]
+    uint8_t *myk = reinterpret_cast<uint8_t *>(smem + v2_city<V>(n)) + tid;  // city of level l: myk[l*T]
+    const V *gd = static_cast<const V *>(a.dist);
+    const V *ga = static_cast<const V *>(a.amin);
+    for (int i = tid; i < n * n; i += T) dl[(i / n) * kRow + i % n] = gd[i];
+    for (int i = tid; i < n; i += T) {
+        ad[i].a = ga[i];
+        ad[i].d0 = gd[i * n];
+    }
+    __syncthreads();
+
+    const uint32_t full = (uint32_t)((1ull << n) - 1ull) & ~1u;  // cities 1..N
+    V aall = 0;
+    for (int x = 0; x < n; ++x) aall += ad[x].a;                 // exact: grid values
+    V inc = Num<V>::val(__hip_atomic_load(a.inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    V thr = Thr<V>::of(inc);
+    unsigned long long nodes = 0;  // wave-uniform counts
+    unsigned long long wsteps = 0, wactive = 0, wloads = 0;
+    int L = -1, root = 1;          // L < root: the lane needs an item
+    int k = 0, krow = 0;           // path end and its row offset in d
+    uint32_t rem = 0, fm = 0, t0 = 0;
+    V ck = 0, remA = 0;
+    bool done = false;
+    uint32_t tick = 0;
+    const int lane = __lane_id();
+    SearchItem *wbuf = reinterpret_cast<SearchItem *>(smem + v2_wbuf<V>(n)) + (tid / 64) * kChunk;
+    uint32_t pbase = 0, pnext = 0, pend = 0;
+
+    // rebuild an item's stack: the same left fold as when it was cut
+    auto load_item = [&](const SearchItem &it) {
+        const int len = it.len;
+        uint32_t rr = full;
+        V ra = aall, c = 0;
+        int prev = 0;
+        myk[0] = 0;
+        myc[0] = 0;
+        for (int l = 1; l < len; ++l) {
+            const int t = it.city[l];
+            c = c + dl[prev * kRow + t];
+            rr &= ~(1u << t);
+            ra -= ad[t].a;
+            myk[l * T] = (uint8_t)t;
+            myc[l * T] = c;
+            prev = t;
+        }
+        if (!(c + ra > thr)) {
+            root = len - 1;
+            L = root;
+            k = prev;
+            krow = prev * kRow;
+            ck = c;
+            rem = rr;
+            remA = ra;
+            fm = 0xFFFFFFFEu << (it.from - 1);
+            t0 = tick;
+        }
+    };
+
+    auto step = [&]() {
+        const bool act = L >= root;
+        wsteps += 64;
+        wactive += (unsigned long long)__popcll(__ballot(act));
+        const uint32_t cand = act ? (rem & fm) : 0u;
+        const bool has = cand != 0u;
+        const int j = has ? __builtin_ctz(cand) : 0;
+        const uint32_t others = rem & ~(1u << j);
+        const int r = others ? __builtin_ctz(others) : 0;  // the forced last city when L == n-3
+        const bool sc = L == n - 3;
+        const bool lf = L == n - 2;  // only for items seeded at depth n-2 (tiny n)
+        const int lm1 = L > 0 ? L - 1 : 0;
+        const V dkj = dl[krow + j];
+        const APair<V> pr = ad[sc ? r : j];
+        const V djr = dl[j * kRow + r];
+        const V ak = ad[k].a;
+        const V cprev = myc[lm1 * T];
+        const int kprev = myk[lm1 * T];
+        const V c = ck + dkj;
+        const V total = (sc ? c + djr : c) + pr.d0;
+        const V rest = remA - pr.a;
+        const bool close = has && (sc || lf);
+        nodes += (unsigned long long)__popcll(__ballot(has)) + (unsigned long long)__popcll(__ballot(has && sc));
+        if (close && total <= inc) {
+            // a complete tour within the incumbent (tsp.cpp:483-499): record it
+            const uint64_t tb = Num<V>::bits(total);
+            const unsigned long long old = atomicMin(a.inc, (unsigned long long)tb);
+            if (tb <= old) {
+                const unsigned int s = atomicAdd(a.rec_count, 1u);
+                if (s < a.rec_cap) {
+                    SearchRecord *R = a.rec + s;
+                    R->cost = tb;
+                    for (int l = 1; l <= L; ++l) R->city[l - 1] = myk[l * T];
+                    R->city[L] = (uint8_t)j;
+                    if (sc) R->city[L + 1] = (uint8_t)r;
+                }
+            }
+            const V o = Num<V>::val(old);
+            inc = o < total ? o : total;
+            thr = Thr<V>::of(inc);
+        }
+        const bool desc = has && !close && !(c + rest > thr);
+        const bool pop = act && !has;
+        myc[(L + 1) * T] = c;  // dead unless desc (L + 1 <= n - 2)
+        myk[(L + 1) * T] = (uint8_t)j;
+        rem = (rem & ~(desc ? (1u << j) : 0u)) | (pop ? (1u << k) : 0u);
+        fm = desc ? 0xFFFFFFFEu : (0xFFFFFFFEu << (has ? j : k));
+        remA = desc ? rest : (pop ? remA + ak : remA);
+        ck = desc ? c : (pop ? cprev : ck);
+        k = desc ? j : (pop ? kprev : k);
+        krow = k * kRow;
+        L = (pop && L == root) ? -1 : L + (desc ? 1 : 0) - (pop ? 1 : 0);
+    };
+
+    for (;;) {
+        // ---- refill: lanes without an item take consecutive queue entries
+        const bool need = !done && L < root;
+        const unsigned long long nm = __ballot(need);
+        if (nm) {
+            const uint32_t cnt = (uint32_t)__popcll(nm);
+            const uint32_t r = (uint32_t)__popcll(nm & ((1ull << lane) - 1ull));
+            const uint32_t left = pend - pnext;
+            if (need && r < left) {
+                if (pnext + r >= a.in_count)
+                    done = true;
+                else
+                    load_item(wbuf[pnext - pbase + r]);
+            }
+            if (cnt > left) {
+                const int leader = __ffsll((long long)nm) - 1;
+                uint32_t base = 0;
+                if (lane == leader) base = atomicAdd(a.queue, kChunk);
+                base = __shfl(base, leader);
+                __builtin_amdgcn_wave_barrier();
+                if (base + lane < a.in_count) wbuf[lane] = a.in[base + lane];
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                if (need && r >= left) {
+                    if (base + (r - left) >= a.in_count)
+                        done = true;
+                    else
+                        load_item(wbuf[r - left]);
+                }
+                pbase = base;
+                pnext = base + (cnt - left);
+                pend = base + kChunk;
+            } else {
+                pnext += cnt;
+            }
+        }
+        wloads += (unsigned long long)__popcll(nm) - (unsigned long long)__popcll(__ballot(done) & nm);
+        const unsigned long long live = __ballot(!done);
+        if (live == 0) break;
+        if (__ballot(L >= root) == 0) continue;  // every loaded item was pruned: refill again
+
+        // ---- lock-step DFS, two steps per exit test
+        for (;;) {
+            tick += 2;
+            if ((tick & 255u) == 0) {
+                const V g = Num<V>::val(__hip_atomic_load(a.inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+                if (g < inc) {
+                    inc = g;
+                    thr = Thr<V>::of(g);
+                }
+            }
+            step();
+            step();
+            const unsigned long long needm = __ballot(L < root) & live;
+            const unsigned long long over = __ballot(L >= root && tick - t0 > a.budget);
+            if (needm == live || (uint32_t)__popcll(needm) >= a.refill || over) break;
+        }
+
+        // ---- budget spent: hand back, level by level, the children not tried yet
+        if (L >= root && tick - t0 > a.budget) {
+            uint32_t rl = rem, fl = fm ? (uint32_t)__builtin_ctz(fm) : 32u;
+            unsigned int cnt = 0;
+            for (int l = L; l >= root; --l) {
+                if (rl & (uint32_t)(0xFFFFFFFFull << fl)) ++cnt;
+                if (l > root) {
+                    const int c1 = myk[l * T];
+                    rl |= 1u << c1;
+                    fl = (uint32_t)c1 + 1u;
+                }
+            }
+            // the host sizes the output for (N-1) items per input item: always room
+            unsigned int slot = cnt ? atomicAdd(a.out_count, cnt) : 0u;
+            rl = rem;
+            fl = fm ? (uint32_t)__builtin_ctz(fm) : 32u;
+            for (int l = L; l >= root; --l) {
+                if (rl & (uint32_t)(0xFFFFFFFFull << fl)) {
+                    uint32_t *dst = reinterpret_cast<uint32_t *>(a.out + slot);
+                    for (int b = 0; b < 8; ++b) {
+                        uint32_t word = 0;
+                        for (int q = 0; q < 4; ++q) {
+                            const int lv = 4 * b + q;
+                            if (lv <= l) word |= (uint32_t)myk[lv * T] << (8 * q);
+                        }
+                        dst[b] = word;
+                    }
+                    dst[8] = (uint32_t)(l + 1) | (fl << 8);
+                    ++slot;
+                }
+                if (l > root) {
+                    const int c1 = myk[l * T];
+                    rl |= 1u << c1;
+                    fl = (uint32_t)c1 + 1u;
+                }
+            }
+            L = -1;
+        }
+    }
+    if (lane == 0) {
+        atomicAdd(a.nodes, nodes);
+        atomicAdd(a.util, wsteps);
+        atomicAdd(a.util + 1, wactive);
+        atomicAdd(a.util + 2, wloads);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Persistent search (kernel 3): ONE launch runs the whole search.  Lanes take
+// this shard's seed prefixes from a cursor (decoded on the fly, no seed
+// array), then items from a device ring; a busy lane donates work only when
+// the ring runs low ("hungry"): its root level's untried children become one
+// ring item and its own root moves one level down (the largest untried piece
+// goes, the lane keeps its current path).  No rounds, no host round trips, no
+// budget splitting while every lane is busy.  Termination: `work` counts
+// items created and not finished (a donor adds before publishing, a lane
+// subtracts when its item is done); a wave whose lanes all wait for ring
+// items exits when work == 0.  A watchdog (wall clock) and a ring-lap check
+// end every wave with an abort code instead of hanging.
+//
+// Hand-off (cross-XCD, MI355X L2s are per XCD): the donor writes the item's
+// four payload words with agent-scope atomic stores (write-through), drains
+// them (s_waitcnt vmcnt(0)), then stores the tag word (ticket+1 in the high
+// half); the claimer polls the tag relaxed, then one agent-scope acquire, then
+// agent-scope loads of the payload.
+using gu64 = unsigned long long;
+
+__device__ __forceinline__ gu64 ld_agent(const gu64 *p)
+{
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_agent(gu64 *p, gu64 v)
+{
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <typename V>
+__global__ __launch_bounds__(kSearchThreads) void persist_kernel(SearchArgs a)
+{
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    __shared__ uint32_t pv[33];
+    constexpr int T = kSearchThreads;
+    const int n = a.n, N = n - 1, D = a.depth;
+    const int tid = threadIdx.x;
+    V *dl = reinterpret_cast<V *>(smem);
+    APair<V> *ad = reinterpret_cast<APair<V> *>(smem + v2_ad<V>(n));
+    V *myc = reinterpret_cast<V *>(smem + v2_cost<V>(n)) + tid;
+    uint8_t *myk = reinterpret_cast<uint8_t *>(smem + v2_city<V>(n)) + tid;
+    const V *gd = static_cast<const V *>(a.dist);
+    const V *ga = static_cast<const V *>(a.amin);
+    for (int i = tid; i < n * n; i += T) dl[(i / n) * kRow + i % n] = gd[i];
+    for (int i = tid; i < n; i += T) {
+        ad[i].a = ga[i];
+        ad[i].d0 = gd[i * n];
+    }
+    if (tid == 0) {
+        uint32_t p = 1;
+        pv[D] = 1;
+        for (int l = D; l >= 2; --l) {
+            p *= (uint32_t)(N - l + 1);
+            pv[l - 1] = p;
+        }
+    }
+    __syncthreads();
+    const long long t_start = wall_clock64();
+    PersistState *ps = a.ps;
+    const uint32_t full = (uint32_t)((1ull << n) - 1ull) & ~1u;
+    V aall = 0;
+    for (int x = 0; x < n; ++x) aall += ad[x].a;
+    V inc = Num<V>::val(__hip_atomic_load(a.inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    V thr = Thr<V>::of(inc);
+    const unsigned long long local = a.items / a.nshards + (a.items % a.nshards > a.shard ? 1u : 0u);
+    const int lane = __lane_id();
+
+    // lane state (as the v2 round kernel) + ring claim
+    int L = -1, root = 1, k = 0, krow = 0;
+    uint32_t rem = 0, fm = 0, t0 = 0;
+    V ck = 0, remA = 0;
+    bool owned = false, done = false;
+    long long slot = -1;
+    // wave-uniform state
+    uint32_t tick = 0, idle = 0;
+    bool seeds_left = true, hungry = false;
+    unsigned long long nodes = 0, wsteps = 0, wactive = 0, wloads = 0, wfin = 0;
+
+    auto start = [&](int len, int prev, V c, uint32_t rr, V ra, uint32_t from) {
+        root = len - 1;
+        L = root;
+        k = prev;
+        krow = prev * kRow;
+        ck = c;
+        rem = rr;
+        remA = ra;
+        fm = 0xFFFFFFFEu << (from - 1);
+        t0 = tick;
+    };
+    // seed prefix `idx` of this shard: decode (as seed_kernel), fold, bound
+    auto load_seed = [&](unsigned long long idx) -> bool {
+        uint32_t p = (uint32_t)(idx * a.nshards + a.shard);
+        uint32_t rr = full;
+        V ra = aall, c = 0;
+        int prev = 0;
+        myk[0] = 0;
+        myc[0] = 0;
+        for (int l = 1; l <= D; ++l) {
+            const uint32_t q = p / pv[l];
+            p -= q * pv[l];
+            uint32_t x = rr;
+            for (uint32_t s2 = 0; s2 < q; ++s2) x &= x - 1u;
+            const int t = __builtin_ctz(x);
+            c = c + dl[prev * kRow + t];
+            rr &= ~(1u << t);
+            ra -= ad[t].a;
+            myk[l * T] = (uint8_t)t;
+            myc[l * T] = c;
+            prev = t;
+            if (c + ra > thr) return false;
+        }
+        start(D + 1, prev, c, rr, ra, 1u);
+        return true;
+    };
+    // ring item: refold the prefix (the same left fold as when it was cut)
+    auto load_ring = [&](const gu64 *w, uint32_t meta) -> bool {
+        const int len = (int)(meta & 0xFFu);
+        const uint32_t from = (meta >> 8) & 0xFFu;
+        uint32_t rr = full;
+        V ra = aall, c = 0;
+        int prev = 0;
+        myk[0] = 0;
+        myc[0] = 0;
+        gu64 word = 0;
+        for (int l = 1; l < len; ++l) {
+            if ((l & 7) == 0 || l == 1) word = ld_agent(w + (l >> 3));
+            const int t = (int)((word >> (8 * (l & 7))) & 0xFFu);
+            c = c + dl[prev * kRow + t];
+            rr &= ~(1u << t);
+            ra -= ad[t].a;
+            myk[l * T] = (uint8_t)t;
+            myc[l * T] = c;
+            prev = t;
+        }
+        if (c + ra > thr) return false;
+        start(len, prev, c, rr, ra, from);
+        return true;
+    };
+
+    auto step = [&]() {
+        const bool act = L >= root;
+        wsteps += 64;
+        wactive += (unsigned long long)__popcll(__ballot(act));
+        const uint32_t cand = act ? (rem & fm) : 0u;
+        const bool has = cand != 0u;
+        const int j = has ? __builtin_ctz(cand) : 0;
+        const uint32_t others = rem & ~(1u << j);
+        const int r = others ? __builtin_ctz(others) : 0;
+        const bool sc = L == n - 3;
+        const bool lf = L == n - 2;
+        const int lm1 = L > 0 ? L - 1 : 0;
+        const V dkj = dl[krow + j];
+        const APair<V> pr = ad[sc ? r : j];
+        const V djr = dl[j * kRow + r];
+        const V ak = ad[k].a;
+        const V cprev = myc[lm1 * T];
+        const int kprev = myk[lm1 * T];
+        const V c = ck + dkj;
+        const V total = (sc ? c + djr : c) + pr.d0;
+        const V rest = remA - pr.a;
+        const bool close = has && (sc || lf);
+        nodes += (unsigned long long)__popcll(__ballot(has)) + (unsigned long long)__popcll(__ballot(has && sc));
+        if (close && total <= inc) {
+            const uint64_t tb = Num<V>::bits(total);
+            const unsigned long long old = atomicMin(a.inc, (unsigned long long)tb);
+            if (tb <= old) {
+                const unsigned int s2 = atomicAdd(a.rec_count, 1u);
+                if (s2 < a.rec_cap) {
+                    SearchRecord *R = a.rec + s2;
+                    R->cost = tb;
+                    for (int l = 1; l <= L; ++l) R->city[l - 1] = myk[l * T];
+                    R->city[L] = (uint8_t)j;
+                    if (sc) R->city[L + 1] = (uint8_t)r;
+                }
+            }
+            const V o = Num<V>::val(old);
+            inc = o < total ? o : total;
+            thr = Thr<V>::of(inc);
+        }
+        const bool desc = has && !close && !(c + rest > thr);
+        const bool pop = act && !has;
+        myc[(L + 1) * T] = c;
+        myk[(L + 1) * T] = (uint8_t)j;
+        rem = (rem & ~(desc ? (1u << j) : 0u)) | (pop ? (1u << k) : 0u);
+        fm = desc ? 0xFFFFFFFEu : (0xFFFFFFFEu << (has ? j : k));
+        remA = desc ? rest : (pop ? remA + ak : remA);
+        ck = desc ? c : (pop ? cprev : ck);
+        k = desc ? j : (pop ? kprev : k);
+        krow = k * kRow;
+        L = (pop && L == root) ? -1 : L + (desc ? 1 : 0) - (pop ? 1 : 0);
+    };
+
+    for (;;) {
+        // ---- finished items leave `work` (before this wave can wait on it)
+        const bool fin = owned && L < root;
+        if (fin) owned = false;
+        wfin += (unsigned long long)__popcll(__ballot(fin));
+        if (wfin) {
+            if (lane == 0) atomicAdd(&ps->work.v, (unsigned long long)0 - wfin);
+            wfin = 0;
+        }
+        // ---- lanes without an item: seeds first, then ring tickets
+        bool need = !done && L < root && slot < 0;
+        unsigned long long nm = __ballot(need);
+        if (nm && seeds_left) {
+            const uint32_t cnt = (uint32_t)__popcll(nm);
+            const uint32_t r = (uint32_t)__popcll(nm & ((1ull << lane) - 1ull));
+            const int leader = __ffsll((long long)nm) - 1;
+            unsigned long long base = 0;
+            if (lane == leader) base = atomicAdd(&ps->seed_cursor.v, (unsigned long long)cnt);
+            base = __shfl(base, leader);
+            if (base + cnt >= local) seeds_left = false;
+            const bool got = need && base + r < local;
+            bool live = false;
+            if (got) {
+                live = load_seed(base + r);
+                owned = live;
+            }
+            wloads += (unsigned long long)__popcll(__ballot(got));
+            wfin += (unsigned long long)__popcll(__ballot(got && !live));
+            need = need && !got;
+            nm = __ballot(need);
+        }
+        if (nm && !seeds_left) {
+            const uint32_t cnt = (uint32_t)__popcll(nm);
+            const uint32_t r = (uint32_t)__popcll(nm & ((1ull << lane) - 1ull));
+            const int leader = __ffsll((long long)nm) - 1;
+            unsigned long long base = 0;
+            if (lane == leader) base = atomicAdd(&ps->head.v, (unsigned long long)cnt);
+            base = __shfl(base, leader);
+            if (need) slot = (long long)(base + r);
+        }
+        // ---- claimed tickets: take the item once its tag shows up
+        const bool wt = slot >= 0;
+        if (__ballot(wt)) {
+            bool ready = false, live = false;
+            if (wt) {
+                const gu64 *w = a.ring + (size_t)((uint64_t)slot & a.ring_mask) * kRingWords;
+                const gu64 meta = ld_agent(w + 4);
+                const uint32_t tag = (uint32_t)(meta >> 32), want = (uint32_t)(slot + 1);
+                if (tag == want) {
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                    ready = true;
+                    slot = -1;
+                    live = load_ring(w, (uint32_t)meta);
+                    owned = live;
+                } else if ((int32_t)(tag - want) > 0) {
+                    atomicOr((unsigned int *)&ps->abort.v, 2u);  // lapped: never expected (capacity check)
+                }
+            }
+            const unsigned long long rm = __ballot(ready);
+            if (rm) {
+                if (lane == __ffsll((long long)rm) - 1) atomicAdd(&ps->consumed.v, (unsigned long long)__popcll(rm));
+                wloads += (unsigned long long)__popcll(rm);
+                wfin += (unsigned long long)__popcll(__ballot(ready && !live));
+            }
+        }
+        // ---- nothing to step: flush, then wait for tickets or the end
+        if (__ballot(L >= root) == 0) {
+            if (wfin) {
+                if (lane == 0) atomicAdd(&ps->work.v, (unsigned long long)0 - wfin);
+                wfin = 0;
+            }
+            if (__ballot(!done) == 0) break;
+            if (seeds_left) continue;  // seeds were pruned at once: take more
+            // every wave polls its own ring tags each pass; the shared words only every 16th
+            if ((++idle & 15u) == 0) {
+                const gu64 w = ld_agent(&ps->work.v);
+                const unsigned ab = (unsigned)ld_agent(&ps->abort.v);
+                if (w == 0 || ab) break;
+                if (wall_clock64() - t_start > (long long)a.wall_limit) {
+                    if (lane == 0) atomicOr((unsigned int *)&ps->abort.v, 1u);
+                    break;
+                }
+            }
+            __builtin_amdgcn_s_sleep(8);
+            continue;
+        }
+        const unsigned long long live = __ballot(!done);
+
+        // ---- lock-step DFS, two steps per exit test
+        for (;;) {
+            tick += 2;
+            if ((tick & 255u) == 0) {
+                const V g = Num<V>::val(__hip_atomic_load(a.inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+                if (g < inc) {
+                    inc = g;
+                    thr = Thr<V>::of(g);
+                }
+                const gu64 sc = ld_agent(&ps->seed_cursor.v), h = ld_agent(&ps->head.v), t = ld_agent(&ps->tail.v);
+                // hungry: lanes hold tickets no donor has reserved yet
+                hungry = sc >= local && (long long)(h - t) > (long long)a.hungry;
+                if ((tick & 65535u) == 0) {
+                    const unsigned ab = (unsigned)ld_agent(&ps->abort.v);
+                    if (ab || wall_clock64() - t_start > (long long)a.wall_limit) {
+                        if (lane == 0) atomicOr((unsigned int *)&ps->abort.v, 1u);
+                        done = true;
+                        L = -1;
+                        owned = false;
+                        break;
+                    }
+                }
+            }
+            step();
+            step();
+            // lanes holding a ticket are already served: they count for the
+            // refill only as idle lanes, and their tags are polled every 128 ticks
+            const unsigned long long idlem = __ballot(L < root) & live;
+            const unsigned long long needm = idlem & ~__ballot(slot >= 0);
+            const bool don = hungry && L > root && tick - t0 > a.min_split;
+            if (idlem == live || (uint32_t)__popcll(needm) >= a.refill || __ballot(don) ||
+                ((tick & 255u) == 0 && idlem != needm))
+                break;
+        }
+        if (__ballot(done)) break;  // watchdog
+
+        // ---- donate: the root level's untried children become one ring item
+        if (hungry) {
+            bool don = L > root && tick - t0 > a.min_split;
+            int c1 = 0;
+            if (don) {
+                // unvisited set at the root level; a root level with nothing
+                // left untried moves the root down (the same remaining work)
+                uint32_t rr = rem;
+                for (int l = root + 1; l <= L; ++l) rr |= 1u << myk[l * T];
+                don = false;
+                while (root < L) {
+                    c1 = myk[(root + 1) * T];
+                    rr &= ~(1u << c1);
+                    if ((rr & (0xFFFFFFFEu << c1)) != 0u) {
+                        don = true;
+                        break;
+                    }
+                    root += 1;
+                }
+                if (!don) t0 = tick;
+            }
+            const unsigned long long dm = __ballot(don);
+            if (dm) {
+                const uint32_t cnt = (uint32_t)__popcll(dm);
+                const uint32_t r = (uint32_t)__popcll(dm & ((1ull << lane) - 1ull));
+                const int leader = __ffsll((long long)dm) - 1;
+                unsigned long long base = ~0ull;
+                if (lane == leader) {
+                    const gu64 t = ld_agent(&ps->tail.v), cns = ld_agent(&ps->consumed.v);
+                    if (t + cnt - cns <= (gu64)a.ring_mask + 1 - a.ring_margin) {
+                        atomicAdd(&ps->work.v, (unsigned long long)cnt);  // before anything is published
+                        base = atomicAdd(&ps->tail.v, (unsigned long long)cnt);
+                    }
+                }
+                base = __shfl(base, leader);
+                if (base != ~0ull && don) {
+                    const unsigned long long tk = base + r;
+                    gu64 *w = a.ring + (size_t)(tk & a.ring_mask) * kRingWords;
+                    for (int b = 0; b < 4; ++b) {
+                        gu64 word = 0;
+                        for (int q = 0; q < 8; ++q) {
+                            const int lv = 8 * b + q;
+                            if (lv <= root) word |= (gu64)myk[lv * T] << (8 * q);
+                        }
+                        st_agent(w + b, word);
+                    }
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    st_agent(w + 4, ((gu64)(uint32_t)(tk + 1) << 32) | ((gu64)(c1 + 1) << 8) | (gu64)(root + 1));
+                    root += 1;
+                    t0 = tick;
+                }
+            }
+        }
+    }
+    if (lane == 0) {
+        atomicAdd(a.nodes, nodes);
+        atomicAdd(a.util, wsteps);
+        atomicAdd(a.util + 1, wactive);
+        atomicAdd(a.util + 2, wloads);
+    }
+}
+
 }  // namespace
 
-size_t search_lds_bytes(int n, bool f64) { return f64 ? lds_bytes<double>(n) : lds_bytes<int32_t>(n); }
+size_t search_lds_bytes(int n, bool f64, int kernel)
+{
+    if (kernel == 1) return f64 ? lds_bytes<double>(n) : lds_bytes<int32_t>(n);
+    if (kernel == 3) return f64 ? v2_wbuf<double>(n) : v2_wbuf<int32_t>(n);  // no item buffers
+    return f64 ? v2_lds<double>(n) : v2_lds<int32_t>(n);
+}
+
+hipError_t launch_persist(const SearchArgs &a, bool f64, int grid)
+{
+    const size_t lds = search_lds_bytes(a.n, f64, 3);
+    void (*fn)(SearchArgs) = f64 ? persist_kernel<double> : persist_kernel<int32_t>;
+    if (lds > 64 * 1024) {
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(fn),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(fn, dim3(grid), dim3(kSearchThreads), lds, a.stream, a);
+    return hipGetLastError();
+}
 
 hipError_t launch_seed(const SearchArgs &a, bool f64, int grid)
 {
@@ -367,17 +1049,15 @@ hipError_t launch_seed(const SearchArgs &a, bool f64, int grid)
 
 hipError_t launch_round(const SearchArgs &a, bool f64, int grid)
 {
-    const size_t lds = search_lds_bytes(a.n, f64);
-    const void *fn = f64 ? reinterpret_cast<const void *>(&round_kernel<double>)
-                         : reinterpret_cast<const void *>(&round_kernel<int32_t>);
+    const size_t lds = search_lds_bytes(a.n, f64, a.kernel);
+    void (*fn)(SearchArgs) = a.kernel == 1 ? (f64 ? round_kernel_v1<double> : round_kernel_v1<int32_t>)
+                                           : (f64 ? round_kernel<double> : round_kernel<int32_t>);
     if (lds > 64 * 1024) {
-        hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(fn),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;
     }
-    if (f64)
-        hipLaunchKernelGGL(round_kernel<double>, dim3(grid), dim3(kSearchThreads), lds, a.stream, a);
-    else
-        hipLaunchKernelGGL(round_kernel<int32_t>, dim3(grid), dim3(kSearchThreads), lds, a.stream, a);
+    hipLaunchKernelGGL(fn, dim3(grid), dim3(kSearchThreads), lds, a.stream, a);
     return hipGetLastError();
 }
 

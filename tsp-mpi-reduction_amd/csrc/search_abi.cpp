@@ -27,6 +27,8 @@
 #include <vector>
 
 #include "ctx.h"
+#include <cstdio>
+
 #include "search.h"
 #include "tspgpu.h"
 
@@ -55,6 +57,18 @@ struct tspgpu_search {
     int cur = 0;                 // d_items[cur] holds the pending items
     uint64_t pending = 0;        // items waiting for the next round
     uint32_t budget = 256;       // DFS iterations per item per round
+    uint32_t refill = 16;        // v2/persistent: refill a wave once this many lanes wait
+    // round kernel (TSPGPU_SEARCH_KERNEL): 2 lock-step DFS (default), 1 branching DFS;
+    // 3 = run_all as ONE persistent launch with a device work ring (measured
+    // 1.3-2x slower than rounds at n = 18: profiles/r01/k2_persistent.log)
+    int kernel = 2;
+    // persistent search
+    PersistState *d_ps = nullptr;
+    unsigned long long *d_ring = nullptr;
+    uint32_t ring_cap = 1u << 20;
+    int32_t hungry = 0;
+    uint32_t min_split = 64;
+    double wall_s = 300.0;
     int rounds = 0;
     double ms = 0.0;             // device time of all seed/round launches
     hipEvent_t e0 = nullptr, e1 = nullptr;
@@ -233,7 +247,22 @@ int tspgpu_search_create(tspgpu_ctx *c, const void *dist, int dtype, int n, int 
     s->dtype = dtype;
     s->shard = (uint32_t)shard;
     s->nshards = (uint32_t)nshards;
-    const size_t lds = search_lds_bytes(n, f64);
+    if (const char *e = std::getenv("TSPGPU_SEARCH_KERNEL")) {
+        const int v = std::atoi(e);
+        s->kernel = v == 1 ? 1 : (v == 3 ? 3 : 2);
+    }
+    if (const char *e = std::getenv("TSPGPU_SEARCH_HUNGRY")) s->hungry = (int32_t)std::atol(e);
+    if (const char *e = std::getenv("TSPGPU_SEARCH_MIN_SPLIT")) s->min_split = (uint32_t)std::max(0L, std::atol(e));
+    if (const char *e = std::getenv("TSPGPU_SEARCH_WALL_S")) s->wall_s = std::max(0.1, std::atof(e));
+    if (const char *e = std::getenv("TSPGPU_SEARCH_RING_LOG2")) {  // tests: a small ring
+        const int v = std::atoi(e);
+        if (v >= 6 && v <= 24) s->ring_cap = 1u << v;
+    }
+    if (const char *e = std::getenv("TSPGPU_SEARCH_REFILL")) {
+        const long v = std::atol(e);
+        if (v > 0) s->refill = (uint32_t)std::min<long>(v, 64);
+    }
+    const size_t lds = search_lds_bytes(n, f64, s->kernel == 1 ? 1 : 2);
     const int per_cu = std::max(1, std::min(8, (int)((160 * 1024) / lds)));
     s->grid = c->cu_count * per_cu;
     // seed depth: the smallest D with at least one prefix per lane of the
@@ -279,13 +308,13 @@ int tspgpu_search_create(tspgpu_ctx *c, const void *dist, int dtype, int n, int 
     s->rec_cap = 1u << 16;
     hipError_t e = hipMalloc(&s->d_dist, vb * n * n);
     if (e == hipSuccess) e = hipMalloc(&s->d_amin, vb * n);
-    if (e == hipSuccess) e = hipMalloc((void **)&s->d_words, 5 * sizeof(unsigned long long));
+    if (e == hipSuccess) e = hipMalloc((void **)&s->d_words, 8 * sizeof(unsigned long long));
     if (e == hipSuccess) e = hipMalloc((void **)&s->d_rec, sizeof(SearchRecord) * s->rec_cap);
     if (e == hipSuccess) e = hipMemcpy(s->d_dist, dist, vb * n * n, hipMemcpyHostToDevice);
     if (e == hipSuccess)
         e = hipMemcpy(s->d_amin, f64 ? (const void *)ad.data() : (const void *)ai.data(), vb * n,
                       hipMemcpyHostToDevice);
-    unsigned long long w[5] = {0, 0, 0, 0, 0};
+    unsigned long long w[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     if (f64) {
         const double inf = INFINITY;
         std::memcpy(&w[1], &inf, 8);
@@ -312,6 +341,8 @@ int tspgpu_search_destroy(tspgpu_search *s)
     if (s->d_amin) (void)hipFree(s->d_amin);
     if (s->d_words) (void)hipFree(s->d_words);
     if (s->d_rec) (void)hipFree(s->d_rec);
+    if (s->d_ps) (void)hipFree(s->d_ps);
+    if (s->d_ring) (void)hipFree(s->d_ring);
     for (auto *p : s->d_items)
         if (p) (void)hipFree(p);
     if (s->e0) (void)hipEventDestroy(s->e0);
@@ -355,11 +386,14 @@ static SearchArgs args_of(tspgpu_search *s)
     a.shard = s->shard;
     a.nshards = s->nshards;
     a.budget = s->budget;
+    a.refill = s->refill;
+    a.kernel = s->kernel == 1 ? 1 : 2;  // the round kernels
     a.queue = reinterpret_cast<unsigned int *>(s->d_words);
     a.inc = s->d_words + 1;
     a.nodes = s->d_words + 2;
     a.rec_count = reinterpret_cast<unsigned int *>(s->d_words + 3);
     a.out_count = reinterpret_cast<unsigned int *>(s->d_words + 4);
+    a.util = s->d_words + 5;
     a.rec = s->d_rec;
     a.rec_cap = s->rec_cap;
     a.stream = s->ctx->stream;
@@ -455,8 +489,67 @@ int tspgpu_search_step(tspgpu_search *s, uint64_t *pending)
     return 0;
 }
 
+// The whole search in ONE persistent launch (kernel 3): seeds decoded on the
+// fly, work handed between lanes through a device ring, no rounds.
+static int run_persist(tspgpu_search *s)
+{
+    (void)hipSetDevice(s->ctx->device);
+    hipStream_t st = s->ctx->stream;
+    hipError_t e = hipSuccess;
+    if (!s->d_ps) e = hipMalloc((void **)&s->d_ps, sizeof(PersistState));
+    if (e == hipSuccess && !s->d_ring)
+        e = hipMalloc((void **)&s->d_ring, (size_t)s->ring_cap * kRingWords * sizeof(unsigned long long));
+    if (e != hipSuccess) return herr(e);
+    const bool f64 = s->dtype == TSPGPU_F64;
+    const size_t lds = search_lds_bytes(s->n, f64, 3);
+    const int per_cu = std::max(1, std::min(8, (int)((160 * 1024) / lds)));
+    const int grid = s->ctx->cu_count * per_cu;
+    PersistState h{};
+    h.work.v = s->local_items;
+    int wall_khz = 0;
+    if (hipDeviceGetAttribute(&wall_khz, hipDeviceAttributeWallClockRate, s->ctx->device) != hipSuccess || wall_khz <= 0)
+        wall_khz = 100000;
+    SearchArgs a = args_of(s);
+    a.kernel = 3;
+    a.ps = s->d_ps;
+    a.ring = s->d_ring;
+    a.ring_mask = s->ring_cap - 1;
+    // every resident wave may reserve up to 64 tickets between two capacity checks
+    a.ring_margin = (uint32_t)std::min<uint64_t>((uint64_t)grid * (kSearchThreads / 64) * 64, s->ring_cap / 2);
+    a.hungry = s->hungry;
+    a.min_split = s->min_split;
+    a.wall_limit = (unsigned long long)(s->wall_s * wall_khz * 1000.0);
+    // tags of a previous launch would match this launch's tickets: clear the ring
+    e = hipMemcpyAsync(s->d_ps, &h, sizeof h, hipMemcpyHostToDevice, st);
+    if (e == hipSuccess)
+        e = hipMemsetAsync(s->d_ring, 0, (size_t)s->ring_cap * kRingWords * sizeof(unsigned long long), st);
+    if (e == hipSuccess) e = hipMemsetAsync(s->d_words, 0, 8, st);
+    if (e != hipSuccess) return herr(e);
+    (void)hipEventRecord(s->e0, st);
+    e = launch_persist(a, f64, grid);
+    (void)hipEventRecord(s->e1, st);
+    if (e != hipSuccess) return herr(e);
+    e = hipMemcpyAsync(&h, s->d_ps, sizeof h, hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (e != hipSuccess) return herr(e);
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, s->e0, s->e1) == hipSuccess) s->ms += ms;
+    s->pending = 0;
+    s->rounds = 1;
+    if (std::getenv("TSPGPU_SEARCH_DEBUG"))
+        std::fprintf(stderr, "persist: grid %d seeds %llu/%llu head %llu tail %llu consumed %llu work %llu abort %llu ms %.3f\n",
+                     grid, h.seed_cursor.v, (unsigned long long)s->local_items, h.head.v, h.tail.v, h.consumed.v,
+                     h.work.v, h.abort.v, ms);
+    if (h.abort.v & 1u) return -ETIMEDOUT;
+    if (h.abort.v) return -EIO;
+    if (h.work.v != 0) return -EIO;  // every item must have finished
+    return 0;
+}
+
 int tspgpu_search_run_all(tspgpu_search *s)
 {
+    if (!s) return -EINVAL;
+    if (s->kernel == 3) return run_persist(s);
     int rc = tspgpu_search_start(s);
     uint64_t pending = 1;
     while (!rc && pending) rc = tspgpu_search_step(s, &pending);
@@ -631,6 +724,12 @@ int tspgpu_search_solve(tspgpu_ctx *c, const void *dist, int dtype, int n, doubl
         stats->kernel_ms = s->ms;
         stats->items = s->items;
         stats->rounds = s->rounds;
+        unsigned long long u[3] = {0, 0, 0};
+        if (hipMemcpy(u, s->d_words + 5, sizeof u, hipMemcpyDeviceToHost) == hipSuccess) {
+            stats->lane_steps = u[0];
+            stats->active_steps = u[1];
+            stats->item_loads = u[2];
+        }
     }
     tspgpu_search_destroy(s);
     return rc;

@@ -226,6 +226,7 @@ const char *tspgpu_strerror(int code)
     case -EDEADLK: return "the reference's mergeBlocks would never terminate for these paths";
     case -EOVERFLOW: return "too many optimal tours to enumerate (n > 20)";
     case -ENOSPC: return "output buffer too small";
+    case -ETIMEDOUT: return "search watchdog expired (TSPGPU_SEARCH_WALL_S)";
     default: return "unknown error";
     }
 }

@@ -50,7 +50,8 @@ class TourRecord(ctypes.Structure):
 class SearchStats(ctypes.Structure):
     _fields_ = [("nodes", ctypes.c_uint64), ("records", ctypes.c_uint64), ("optimal_tours", ctypes.c_uint64),
                 ("items", ctypes.c_uint64), ("depth", ctypes.c_int), ("phases", ctypes.c_int),
-                ("fallback", ctypes.c_int), ("rounds", ctypes.c_int), ("kernel_ms", ctypes.c_double)]
+                ("fallback", ctypes.c_int), ("rounds", ctypes.c_int), ("kernel_ms", ctypes.c_double),
+                ("lane_steps", ctypes.c_uint64), ("active_steps", ctypes.c_uint64), ("item_loads", ctypes.c_uint64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
