@@ -41,16 +41,36 @@ namespace {
 
 constexpr int kMergeThreads = 256;
 constexpr unsigned kCandCap = 1u << 16;
+constexpr int kChunk = 1024;       // path-2 cities staged in LDS per block column
+constexpr int kBatch = 2048;       // merges in flight between two host synchronisations
+constexpr int kMaxBlocks = 4096;   // argmin / candidate grid (per-block minima kept)
 
 struct Cand {
     int i, j;
     tspgpu_city a, b, c, d;
 };
 
-__device__ __forceinline__ double ddist(const tspgpu_city &p, const tspgpu_city &q)
+// Device control words of the merge stream.
+struct Ctl {
+    unsigned long long count;     // candidates of the current merge
+    unsigned long long minkey;    // min order key of its swap costs
+    unsigned long long done;      // candidate blocks finished (last block decides)
+    unsigned long long stall;     // 0 ok; 1 the host must pick (several candidates); 2 EDEADLK; 3 EIO
+    unsigned long long stall_at;  // batch index of the merge that stalled
+    unsigned long long fw[2];     // first index of A|B in path 1, of C in path 2
+    unsigned long long pad;
+};
+
+// What each merge leaves for the host: the chosen pair (the exact swap cost
+// is recomputed with glibc pow on the host, tsp.cpp:263).
+struct Pick {
+    Cand c;
+};
+
+__device__ __forceinline__ double ddist(double ax, double ay, double bx, double by)
 {
-    const double dx = p.x - q.x;
-    const double dy = p.y - q.y;
+    const double dx = ax - bx;
+    const double dy = ay - by;
     return sqrt(dx * dx + dy * dy);
 }
 
@@ -66,89 +86,288 @@ __host__ __device__ __forceinline__ double key_value(unsigned long long k)
     return __builtin_bit_cast(double, b);
 }
 
-__device__ __forceinline__ double swap_cost(const tspgpu_city *c1, int L1, const tspgpu_city *c2, int L2,
-                                            unsigned long long q)
+// Stage path-2 cities [j0, j0 + J] (successor included, cyclic) and the path-2
+// edge lengths d(C_j, D_j) in LDS.
+struct Stage {
+    double x[kChunk + 1], y[kChunk + 1], e[kChunk];
+};
+__device__ __forceinline__ int stage_chunk(Stage &sm, const tspgpu_city *c2, int L2, int j0)
 {
-    const int i = (int)(q / (unsigned)L2), j = (int)(q % (unsigned)L2);
-    const tspgpu_city A = c1[i], B = c1[i + 1 == L1 ? 0 : i + 1];
-    const tspgpu_city C = c2[j], D = c2[j + 1 == L2 ? 0 : j + 1];
-    return ((ddist(A, D) + ddist(B, C)) - ddist(A, B)) - ddist(C, D);
+    const int J = min(kChunk, L2 - j0);
+    for (int t = threadIdx.x; t <= J; t += kMergeThreads) {
+        const int j = j0 + t;
+        const tspgpu_city c = c2[j < L2 ? j : j - L2];
+        sm.x[t] = c.x;
+        sm.y[t] = c.y;
+    }
+    __syncthreads();
+    for (int t = threadIdx.x; t < J; t += kMergeThreads) sm.e[t] = ddist(sm.x[t], sm.y[t], sm.x[t + 1], sm.y[t + 1]);
+    __syncthreads();
+    return J;
 }
 
-// *key: min order key of all swap costs
-__global__ __launch_bounds__(kMergeThreads) void argmin_kernel(const tspgpu_city *c1, int L1, const tspgpu_city *c2,
-                                                               int L2, unsigned long long *key)
+// Approximate swap costs (dx*dx, IEEE sqrt; tsp.cpp:197-200 order of operations)
+// of path-1 edge i against the staged path-2 edges; calls f(j, cost).
+template <typename F>
+__device__ __forceinline__ void sweep_row(const Stage &sm, int J, const tspgpu_city *c1, int L1, int i, F &&f)
 {
-    const unsigned long long total = (unsigned long long)L1 * (unsigned)L2;
+    const tspgpu_city A = c1[i], B = c1[i + 1 == L1 ? 0 : i + 1];
+    const double eab = ddist(A.x, A.y, B.x, B.y);
+    for (int t = 0; t < J; ++t) {
+        const double sc = ((ddist(A.x, A.y, sm.x[t + 1], sm.y[t + 1]) + ddist(B.x, B.y, sm.x[t], sm.y[t])) - eab) -
+                          sm.e[t];
+        f(t, sc);
+    }
+}
+
+// Pass 1: min swap key over all L1 x L2 pairs; blockIdx.y = path-2 chunk.
+// Also resets this merge's first-occurrence words for find_kernel.
+__global__ __launch_bounds__(kMergeThreads) void argmin_kernel(const tspgpu_city *c1, int L1, const tspgpu_city *c2,
+                                                               int L2, Ctl *ctl, unsigned long long *blockmin)
+{
+    if (ctl->stall) return;
+    __shared__ Stage sm;
+    __shared__ unsigned long long wmin[kMergeThreads / 64];
+    if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {
+        ctl->fw[0] = ~0ull;
+        ctl->fw[1] = ~0ull;
+    }
     unsigned long long best = ~0ull;
-    for (unsigned long long q = blockIdx.x * (unsigned long long)kMergeThreads + threadIdx.x; q < total;
-         q += (unsigned long long)gridDim.x * kMergeThreads) {
-        const unsigned long long k = order_key(swap_cost(c1, L1, c2, L2, q));
-        best = k < best ? k : best;
+    for (int j0 = blockIdx.y * kChunk; j0 < L2; j0 += gridDim.y * kChunk) {
+        const int J = stage_chunk(sm, c2, L2, j0);
+        for (int i = blockIdx.x * kMergeThreads + threadIdx.x; i < L1; i += gridDim.x * kMergeThreads)
+            sweep_row(sm, J, c1, L1, i, [&](int, double sc) {
+                const unsigned long long k = order_key(sc);
+                best = k < best ? k : best;
+            });
+        __syncthreads();  // before the next chunk overwrites the stage
     }
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) {
         const unsigned long long o = __shfl_xor(best, off);
         best = o < best ? o : best;
     }
-    if (__lane_id() == 0 && best != ~0ull) atomicMin(key, best);
-}
-
-__global__ __launch_bounds__(kMergeThreads) void cand_kernel(const tspgpu_city *c1, int L1, const tspgpu_city *c2,
-                                                             int L2, double eps2, unsigned long long *words,
-                                                             Cand *cand)
-{
-    const unsigned long long total = (unsigned long long)L1 * (unsigned)L2;
-    const double thr = key_value(words[1]) + eps2;  // words[1]: min key, words[0]: count
-    for (unsigned long long q = blockIdx.x * (unsigned long long)kMergeThreads + threadIdx.x; q < total;
-         q += (unsigned long long)gridDim.x * kMergeThreads) {
-        if (swap_cost(c1, L1, c2, L2, q) <= thr) {
-            const unsigned s = atomicAdd(reinterpret_cast<unsigned *>(words), 1u);
-            if (s < kCandCap) {
-                const int i = (int)(q / (unsigned)L2), j = (int)(q % (unsigned)L2);
-                Cand c;
-                c.i = i;
-                c.j = j;
-                c.a = c1[i];
-                c.b = c1[i + 1 == L1 ? 0 : i + 1];
-                c.c = c2[j];
-                c.d = c2[j + 1 == L2 ? 0 : j + 1];
-                cand[s] = c;
-            }
-        }
+    if (__lane_id() == 0) wmin[threadIdx.x / 64] = best;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long b = wmin[0];
+        for (int w = 1; w < kMergeThreads / 64; ++w) b = wmin[w] < b ? wmin[w] : b;
+        blockmin[blockIdx.y * gridDim.x + blockIdx.x] = b;
+        if (b != ~0ull) atomicMin(&ctl->minkey, b);
     }
 }
 
-// first index of c1 whose id is idA or idB -> fw[0], first index of c2[0..M) whose id is idC -> fw[1]
-__global__ __launch_bounds__(kMergeThreads) void find_kernel(const tspgpu_city *c1, int L1, const tspgpu_city *c2,
-                                                             int M, int idA, int idB, int idC, unsigned long long *fw)
+// Fold merges (path 2 is one block tour, L2 <= kChunk; path 1 holds each
+// city once plus the closing copy of its first city): ONE kernel does both
+// passes and the decision.  Every block computes its minimum; the last block
+// to finish rescans the blocks within eps2 of the global minimum, and with
+// exactly one candidate it logs the pick and the splice positions directly:
+// the first city of path 1 that is A or B is index i (0 when A or B is the
+// start city), C's first index in path 2 is j (0 for the closing copy).
+// Otherwise the stream stalls for the host.
+__global__ __launch_bounds__(kMergeThreads) void fold_pick_kernel(const tspgpu_city *c1, int L1, const tspgpu_city *c2,
+                                                                  int L2, double eps2, Ctl *ctl,
+                                                                  unsigned long long *blockmin, Cand *cand,
+                                                                  Pick *picks, int idx)
 {
+    if (ctl->stall) return;
+    __shared__ Stage sm;
+    __shared__ unsigned long long wmin[kMergeThreads / 64];
+    __shared__ bool last;
+    __shared__ unsigned nc;
+    const int J = stage_chunk(sm, c2, L2, 0);
+    unsigned long long best = ~0ull;
+    for (int i = blockIdx.x * kMergeThreads + threadIdx.x; i < L1; i += gridDim.x * kMergeThreads)
+        sweep_row(sm, J, c1, L1, i, [&](int, double sc) {
+            const unsigned long long k = order_key(sc);
+            best = k < best ? k : best;
+        });
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        const unsigned long long o = __shfl_xor(best, off);
+        best = o < best ? o : best;
+    }
+    if (__lane_id() == 0) wmin[threadIdx.x / 64] = best;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long b = wmin[0];
+        for (int w = 1; w < kMergeThreads / 64; ++w) b = wmin[w] < b ? wmin[w] : b;
+        blockmin[blockIdx.x] = b;
+        if (b != ~0ull) atomicMin(&ctl->minkey, b);
+        __threadfence();
+        last = atomicAdd(&ctl->done, 1ull) == (unsigned long long)gridDim.x - 1;
+        nc = 0;
+    }
+    __syncthreads();
+    if (!last) return;
+    __threadfence();
+    const double thr = key_value(__hip_atomic_load(&ctl->minkey, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) + eps2;
+    // the blocks within eps2 of the minimum (usually one), gathered in parallel
+    __shared__ int close[64];
+    __shared__ unsigned nclose;
+    if (threadIdx.x == 0) nclose = 0;
+    __syncthreads();
+    for (int b = threadIdx.x; b < (int)gridDim.x; b += kMergeThreads) {
+        const unsigned long long bm = __hip_atomic_load(&blockmin[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (key_value(bm) <= thr) {
+            const unsigned q = atomicAdd(&nclose, 1u);
+            if (q < 64) close[q] = b;
+        }
+    }
+    __syncthreads();
+    const bool all = nclose > 64;  // (many near-ties: rescan every block)
+    const int nb = all ? (int)gridDim.x : (int)nclose;
+    for (int q = 0; q < nb; ++q) {
+        const int b = all ? q : close[q];
+        for (int i = b * kMergeThreads + threadIdx.x; i < L1; i += gridDim.x * kMergeThreads)
+            sweep_row(sm, J, c1, L1, i, [&](int t, double sc) {
+                if (sc <= thr) {
+                    const unsigned s2 = atomicAdd(&nc, 1u);
+                    if (s2 < kCandCap) {
+                        Cand c;
+                        c.i = i;
+                        c.j = t;
+                        c.a = c1[i];
+                        c.b = c1[i + 1 == L1 ? 0 : i + 1];
+                        c.c = c2[t];
+                        c.d = c2[t + 1 == L2 ? 0 : t + 1];
+                        cand[s2] = c;
+                    }
+                }
+            });
+    }
+    __syncthreads();
+    if (threadIdx.x != 0) return;
+    __threadfence();
+    ctl->count = nc;
+    if (nc != 1) {
+        ctl->stall_at = (unsigned long long)idx;
+        ctl->stall = 1;
+        return;
+    }
+    const Cand k = cand[0];
+    picks[idx].c = k;
+    const int first = c1[0].id;
+    ctl->fw[0] = (k.a.id == first || k.b.id == first) ? 0ull : (unsigned long long)k.i;
+    ctl->fw[1] = k.j == L2 - 1 ? 0ull : (unsigned long long)k.j;
+}
+
+// Pass 2: every pair within eps2 of the minimum is a candidate (only blocks
+// whose own minimum is that close rescan; the others return at once).
+__global__ __launch_bounds__(kMergeThreads) void cand_kernel(const tspgpu_city *c1, int L1, const tspgpu_city *c2,
+                                                             int L2, double eps2, Ctl *ctl,
+                                                             const unsigned long long *blockmin, Cand *cand)
+{
+    if (ctl->stall) return;
+    __shared__ Stage sm;
+    const double thr = key_value(ctl->minkey) + eps2;
+    if (!(key_value(blockmin[blockIdx.y * gridDim.x + blockIdx.x]) <= thr)) return;
+    for (int j0 = blockIdx.y * kChunk; j0 < L2; j0 += gridDim.y * kChunk) {
+        const int J = stage_chunk(sm, c2, L2, j0);
+        for (int i = blockIdx.x * kMergeThreads + threadIdx.x; i < L1; i += gridDim.x * kMergeThreads)
+            sweep_row(sm, J, c1, L1, i, [&](int t, double sc) {
+                if (sc <= thr) {
+                    const unsigned s2 = (unsigned)atomicAdd(&ctl->count, 1ull);
+                    if (s2 < kCandCap) {
+                        const int j = j0 + t;
+                        Cand c;
+                        c.i = i;
+                        c.j = j;
+                        c.a = c1[i];
+                        c.b = c1[i + 1 == L1 ? 0 : i + 1];
+                        c.c = c2[j];
+                        c.d = c2[j + 1 == L2 ? 0 : j + 1];
+                        cand[s2] = c;
+                    }
+                }
+            });
+        __syncthreads();
+    }
+}
+
+// first index of path 1 whose id is A or B -> fw[0], first index of path 2
+// [0, M) whose id is C -> fw[1] (tsp.cpp:229-239); ids from the pick unless given
+// Unforced: exactly one candidate -> it is the reference's pair (the exact
+// minimum and all its ties are always inside the window): log it as the
+// merge's pick; else stall the stream for the host's exact re-evaluation.
+__global__ __launch_bounds__(kMergeThreads) void find_kernel(const tspgpu_city *c1, int L1, const tspgpu_city *c2,
+                                                             int M, Ctl *ctl, const Cand *cand, Pick *picks, int idx,
+                                                             int idA, int idB, int idC, int forced)
+{
+    if (ctl->stall && !forced) return;
+    if (!forced) {
+        __shared__ int ids[4];
+        if (threadIdx.x == 0) {
+            const bool one = ctl->count == 1;
+            ids[3] = one;
+            if (one) {
+                const Cand k = cand[0];
+                ids[0] = k.a.id;
+                ids[1] = k.b.id;
+                ids[2] = k.c.id;
+                if (blockIdx.x == 0) picks[idx].c = k;
+            } else if (blockIdx.x == 0) {
+                ctl->stall_at = (unsigned long long)idx;
+                ctl->stall = 1;
+            }
+        }
+        __syncthreads();
+        if (!ids[3]) return;
+        idA = ids[0];
+        idB = ids[1];
+        idC = ids[2];
+    }
     const int t = blockIdx.x * kMergeThreads + threadIdx.x;
     const int stride = gridDim.x * kMergeThreads;
     for (int i = t; i < L1; i += stride)
-        if (c1[i].id == idA || c1[i].id == idB) atomicMin(fw, (unsigned long long)i);
+        if (c1[i].id == idA || c1[i].id == idB) atomicMin(&ctl->fw[0], (unsigned long long)i);
     for (int j = t; j < M; j += stride)
-        if (c2[j].id == idC) atomicMin(fw + 1, (unsigned long long)j);
+        if (c2[j].id == idC) atomicMin(&ctl->fw[1], (unsigned long long)j);
 }
 
 // out = c1[0..p] ++ reverse(c2 rotated to start after C, closing city dropped) ++ c1[p+1..]
+// (tsp.cpp:240-259), copied as 8-byte words (3 per city); then clears the
+// words of the next merge.
 __global__ __launch_bounds__(kMergeThreads) void splice_kernel(const tspgpu_city *c1, int L1, const tspgpu_city *c2,
-                                                               int M, const unsigned long long *words,
-                                                               tspgpu_city *out)
+                                                               int M, Ctl *ctl, tspgpu_city *out, int idx, int forced)
 {
-    const unsigned long long pw = words[0], sw = words[1];
-    if (pw >= (unsigned long long)L1 || sw >= (unsigned long long)M) return;  // host reports it
+    static_assert(sizeof(tspgpu_city) == 24, "City layout");
+    if (ctl->stall && !forced) return;
+    const unsigned long long pw = ctl->fw[0], sw = ctl->fw[1];
+    if (pw >= (unsigned long long)L1 || sw >= (unsigned long long)M) {
+        if (blockIdx.x == 0 && threadIdx.x == 0) {
+            ctl->stall_at = (unsigned long long)idx;
+            ctl->stall = sw >= (unsigned long long)M ? 2 : 3;  // C not in path 2: tsp.cpp:236-239 never ends
+        }
+        return;
+    }
     const int p = (int)pw, start = (int)((sw + 1) % (unsigned)M);
-    const int total = L1 + M;
-    for (int k = blockIdx.x * kMergeThreads + threadIdx.x; k < total; k += gridDim.x * kMergeThreads) {
-        tspgpu_city v;
-        if (k <= p)
-            v = c1[k];
-        else if (k <= p + M)
-            v = c2[(start + (M - 1 - (k - p - 1))) % M];
-        else
-            v = c1[k - M];
-        out[k] = v;
+    const unsigned long long *w1 = reinterpret_cast<const unsigned long long *>(c1);
+    const unsigned long long *w2 = reinterpret_cast<const unsigned long long *>(c2);
+    unsigned long long *wo = reinterpret_cast<unsigned long long *>(out);
+    const int total = 3 * (L1 + M);
+    for (int w = blockIdx.x * kMergeThreads + threadIdx.x; w < total; w += gridDim.x * kMergeThreads) {
+        const int k = w / 3, f = w - 3 * k;
+        int src;
+        const unsigned long long *base;
+        if (k <= p) {
+            base = w1;
+            src = k;
+        } else if (k <= p + M) {
+            const int q = start + (M - 1 - (k - p - 1));
+            base = w2;
+            src = q >= M ? q - M : q;
+        } else {
+            base = w1;
+            src = k - M;
+        }
+        wo[w] = base[3 * src + f];
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        ctl->count = 0;
+        ctl->minkey = ~0ull;
+        ctl->done = 0;
+        if (forced) ctl->stall = 0;
     }
 }
 
@@ -177,6 +396,7 @@ int herr(hipError_t e)
 struct DVec {
     tspgpu_city *p = nullptr;
     size_t len = 0, cap = 0;
+    // grows only when nothing in flight references it (callers reserve up front)
     int reserve(size_t n, hipStream_t st)
     {
         if (n <= cap) return 0;
@@ -199,148 +419,214 @@ struct DVec {
     }
 };
 
+// The merge stream.  merge() only enqueues: argmin, candidates, find, splice,
+// all on the context's stream, no host round trip.  When exactly one pair is
+// within eps2 of the device minimum it is the reference's pair (the exact
+// minimum and all its ties are always inside the window) and the device
+// splices at once; otherwise the stream stalls (later kernels return at once)
+// and sync() lets the host pick with glibc pow, re-runs the stalled merge with
+// the host's pair and re-enqueues the rest.  Costs, which need the exact swap
+// cost (glibc pow) of every chosen pair, are folded on the host in merge order
+// at sync(): cost_target = (cost_target + cost2) + best (tsp.cpp:263).
 struct Merger {
     hipStream_t st = nullptr;
     int cus = 256;
     double eps2 = 0.0;
-    // device words: [0] candidate count, [1] min key, [2,3] / [4,5] first A|B and
-    // first C of the two most recent splices (alternating), then the candidates
-    unsigned long long *words = nullptr;
+    Ctl *ctl = nullptr;
     Cand *cand = nullptr;
-    unsigned long long *hx = nullptr;  // pinned host mirror: 6 words + kFirstCands candidates
-    std::vector<Cand> hc;
-    DVec tmp;
-    int parity = 0;
-    bool pending = false;     // a splice whose find words are not checked yet
-    int pend_L1 = 0, pend_M = 0, pend_slot = 0;
-    static constexpr unsigned kFirstCands = 64;
-    static constexpr size_t kWordBytes = 6 * sizeof(unsigned long long);
+    Pick *picks = nullptr;
+    unsigned long long *blockmin = nullptr;
+    Ctl *hctl = nullptr;    // pinned mirror
+    Pick *hpicks = nullptr; // pinned mirror
+    struct Op {
+        const tspgpu_city *src;
+        tspgpu_city *dst;
+        int L1;
+        const tspgpu_city *c2;
+        int L2;
+        double *target;
+        const double *cost2;
+        bool fold;  // path 1 holds each city once + closing copy, path 2 is one block tour
+    };
+    std::vector<Op> ops;
     int init(tspgpu_ctx *c, double dmax)
     {
         st = c->stream;
         cus = c->cu_count;
         eps2 = 2.0 * std::ldexp(4.0 * dmax, -36);
-        hipError_t e = hipMalloc((void **)&words, kWordBytes + kCandCap * sizeof(Cand));
-        if (e == hipSuccess) e = hipHostMalloc((void **)&hx, kWordBytes + kFirstCands * sizeof(Cand), 0);
-        cand = reinterpret_cast<Cand *>(reinterpret_cast<char *>(words) + kWordBytes);
+        hipError_t e = hipMalloc((void **)&ctl, sizeof(Ctl));
+        if (e == hipSuccess) e = hipMalloc((void **)&cand, kCandCap * sizeof(Cand));
+        if (e == hipSuccess) e = hipMalloc((void **)&picks, kBatch * sizeof(Pick));
+        if (e == hipSuccess) e = hipMalloc((void **)&blockmin, kMaxBlocks * sizeof(unsigned long long));
+        if (e == hipSuccess) e = hipHostMalloc((void **)&hctl, sizeof(Ctl), 0);
+        if (e == hipSuccess) e = hipHostMalloc((void **)&hpicks, kBatch * sizeof(Pick), 0);
+        if (e == hipSuccess) {
+            Ctl z{};
+            z.minkey = ~0ull;
+            e = hipMemcpyAsync(ctl, &z, sizeof z, hipMemcpyHostToDevice, st);
+        }
+        ops.reserve(kBatch);
         return herr(e);
     }
     ~Merger()
     {
-        if (words) (void)hipFree(words);
-        if (hx) (void)hipHostFree(hx);
-        tmp.release();
+        if (ctl) (void)hipFree(ctl);
+        if (cand) (void)hipFree(cand);
+        if (picks) (void)hipFree(picks);
+        if (blockmin) (void)hipFree(blockmin);
+        if (hctl) (void)hipHostFree(hctl);
+        if (hpicks) (void)hipHostFree(hpicks);
     }
     int grid_for(unsigned long long work) const
     {
         const unsigned long long b = (work + kMergeThreads - 1) / kMergeThreads;
         return (int)std::max<unsigned long long>(1, std::min<unsigned long long>(b, (unsigned long long)cus * 8));
     }
-    // the previous splice's first-occurrence searches (copied with the last transfer)
-    int check_pending()
+    // blockIdx.x strides path-1 edges, blockIdx.y path-2 chunks; gx * gy <= kMaxBlocks
+    dim3 pair_grid(int L1, int L2) const
     {
-        if (!pending) return 0;
-        pending = false;
-        const unsigned long long pa = hx[2 + 2 * pend_slot], pc = hx[3 + 2 * pend_slot];
-        if (pc >= (unsigned long long)pend_M) return -EDEADLK;  // C not in path 2: tsp.cpp:236-239 never ends
-        if (pa >= (unsigned long long)pend_L1) return -EIO;
-        return 0;
+        const int cap = std::min(cus * 8, kMaxBlocks);
+        const int gy = std::min((L2 + kChunk - 1) / kChunk, cap);
+        const int gx = std::max(1, std::min((L1 + kMergeThreads - 1) / kMergeThreads, cap / gy));
+        return dim3(gx, gy);
     }
-    // wait for the last splice and check it
-    int flush()
+    void enqueue(const Op &o, int idx)
     {
-        if (!pending) return 0;
-        hipError_t e = hipMemcpyAsync(hx, words, kWordBytes, hipMemcpyDeviceToHost, st);
-        if (e == hipSuccess) e = hipStreamSynchronize(st);
-        if (e != hipSuccess) return herr(e);
-        return check_pending();
+        const int M = o.L2 - 1;
+        if (o.fold && o.L2 <= kChunk) {
+            const int gx = std::max(1, std::min((o.L1 + kMergeThreads - 1) / kMergeThreads, std::min(cus * 8, kMaxBlocks)));
+            hipLaunchKernelGGL(fold_pick_kernel, dim3(gx), dim3(kMergeThreads), 0, st, o.src, o.L1, o.c2, o.L2, eps2,
+                               ctl, blockmin, cand, picks, idx);
+            hipLaunchKernelGGL(splice_kernel, dim3(grid_for(3ull * ((unsigned long long)o.L1 + M))),
+                               dim3(kMergeThreads), 0, st, o.src, o.L1, o.c2, M, ctl, o.dst, idx, 0);
+            return;
+        }
+        const dim3 g = pair_grid(o.L1, o.L2);
+        hipLaunchKernelGGL(argmin_kernel, g, dim3(kMergeThreads), 0, st, o.src, o.L1, o.c2, o.L2, ctl, blockmin);
+        hipLaunchKernelGGL(cand_kernel, g, dim3(kMergeThreads), 0, st, o.src, o.L1, o.c2, o.L2, eps2, ctl, blockmin,
+                           cand);
+        hipLaunchKernelGGL(find_kernel, dim3(grid_for((unsigned long long)std::max(o.L1, M))), dim3(kMergeThreads), 0,
+                           st, o.src, o.L1, o.c2, M, ctl, cand, picks, idx, 0, 0, 0, 0);
+        hipLaunchKernelGGL(splice_kernel, dim3(grid_for(3ull * ((unsigned long long)o.L1 + M))), dim3(kMergeThreads),
+                           0, st, o.src, o.L1, o.c2, M, ctl, o.dst, idx, 0);
     }
-    // s1 <- mergeBlocks(s1, c2); returns 0, -EDEADLK if the reference would not terminate, or -errno.
-    // One host round trip: the argmin + candidates come back with the previous
-    // splice's checks; the splice of this merge is checked by the next one (or flush()).
-    int merge(DVec &s1, double &cost1, const tspgpu_city *c2, int L2, double cost2)
+    // s1 <- mergeBlocks(s1, c2); *cost1 = (*cost1 + *cost2) + best once sync() ran.
+    // tmp: a buffer of capacity >= s1.len + L2 - 1 (swapped with s1).
+    int merge(DVec &s1, DVec &tmp, double *cost1, const tspgpu_city *c2, int L2, const double *cost2,
+              bool fold = false)
     {
         const int L1 = (int)s1.len;
         if (L1 < 1 || L2 < 2) return -EINVAL;
-        hipError_t e = hipMemsetAsync(words, 0, 8, st);               // candidate count
-        if (e == hipSuccess) e = hipMemsetAsync(words + 1, 0xFF, 8, st);  // min key
-        if (e != hipSuccess) return herr(e);
-        const unsigned long long pairs = (unsigned long long)L1 * (unsigned)L2;
-        const int g = grid_for(pairs);
-        hipLaunchKernelGGL(argmin_kernel, dim3(g), dim3(kMergeThreads), 0, st, s1.p, L1, c2, L2, words + 1);
-        hipLaunchKernelGGL(cand_kernel, dim3(g), dim3(kMergeThreads), 0, st, s1.p, L1, c2, L2, eps2, words, cand);
-        e = hipMemcpyAsync(hx, words, kWordBytes + kFirstCands * sizeof(Cand), hipMemcpyDeviceToHost, st);
-        if (e == hipSuccess) e = hipStreamSynchronize(st);
-        if (e != hipSuccess) return herr(e);
-        int rc = check_pending();
-        if (rc) return rc;
-        const unsigned nc = (unsigned)hx[0];
-        double best = (double)INT_MAX;  // tsp.cpp:204
-        int bi = -1;
-        tspgpu_city A{}, B{}, C{};
+        const int M = L2 - 1;
+        if ((int)ops.size() == kBatch || tmp.cap < (size_t)L1 + M) {
+            // (the reference's stale received lists can grow a path past all
+            // cities: grow the spare buffer once nothing in flight uses it)
+            int rc = sync();
+            if (!rc) rc = tmp.reserve((size_t)L1 + M, st);
+            if (rc) return rc;
+        }
+        Op o{s1.p, tmp.p, L1, c2, L2, cost1, cost2, fold};
+        ops.push_back(o);
+        enqueue(o, (int)ops.size() - 1);
+        if (hipPeekAtLastError() != hipSuccess) return herr(hipGetLastError());
+        std::swap(s1, tmp);
+        s1.len = (size_t)L1 + M;
+        tmp.len = 0;
+        return 0;
+    }
+    // the host's pick for a stalled merge: exact (glibc) re-evaluation of the
+    // candidates in row-major order with the reference's strict < from INT_MAX
+    int host_pick(const Op &o, Cand &pick, double &best)
+    {
+        hipError_t e = hipSuccess;
+        const unsigned long long nc = hctl->count;
+        best = (double)INT_MAX;  // tsp.cpp:204
+        bool found = false;
         if (nc > 0 && nc <= kCandCap) {
-            hc.resize(nc);
-            std::memcpy(hc.data(), reinterpret_cast<const char *>(hx) + kWordBytes,
-                        std::min(nc, kFirstCands) * sizeof(Cand));
-            if (nc > kFirstCands) {
-                e = hipMemcpyAsync(hc.data() + kFirstCands, cand + kFirstCands, (nc - kFirstCands) * sizeof(Cand),
-                                   hipMemcpyDeviceToHost, st);
-                if (e == hipSuccess) e = hipStreamSynchronize(st);
-                if (e != hipSuccess) return herr(e);
-            }
-            std::sort(hc.begin(), hc.end(), [](const Cand &x, const Cand &y) {
-                return x.i != y.i ? x.i < y.i : x.j < y.j;
-            });
+            std::vector<Cand> hc(nc);
+            e = hipMemcpyAsync(hc.data(), cand, nc * sizeof(Cand), hipMemcpyDeviceToHost, st);
+            if (e == hipSuccess) e = hipStreamSynchronize(st);
+            if (e != hipSuccess) return herr(e);
+            std::sort(hc.begin(), hc.end(),
+                      [](const Cand &x, const Cand &y) { return x.i != y.i ? x.i < y.i : x.j < y.j; });
             for (const Cand &k : hc) {
                 const double sc = hswap(k.a, k.b, k.c, k.d);
                 if (sc < best) {
                     best = sc;
-                    bi = k.i;
-                    A = k.a;
-                    B = k.b;
-                    C = k.c;
+                    pick = k;
+                    found = true;
                 }
             }
         } else {
             // too many near-ties for the buffer: exact scan on the host
-            std::vector<tspgpu_city> h1(L1), h2(L2);
-            e = hipMemcpyAsync(h1.data(), s1.p, L1 * sizeof(tspgpu_city), hipMemcpyDeviceToHost, st);
-            if (e == hipSuccess) e = hipMemcpyAsync(h2.data(), c2, L2 * sizeof(tspgpu_city), hipMemcpyDeviceToHost, st);
+            std::vector<tspgpu_city> h1(o.L1), h2(o.L2);
+            e = hipMemcpyAsync(h1.data(), o.src, o.L1 * sizeof(tspgpu_city), hipMemcpyDeviceToHost, st);
+            if (e == hipSuccess)
+                e = hipMemcpyAsync(h2.data(), o.c2, o.L2 * sizeof(tspgpu_city), hipMemcpyDeviceToHost, st);
             if (e == hipSuccess) e = hipStreamSynchronize(st);
             if (e != hipSuccess) return herr(e);
-            for (int i = 0; i < L1; ++i)
-                for (int j = 0; j < L2; ++j) {
-                    const tspgpu_city &a = h1[i], &b = h1[(i + 1) % L1], &c = h2[j], &d = h2[(j + 1) % L2];
+            for (int i = 0; i < o.L1; ++i)
+                for (int j = 0; j < o.L2; ++j) {
+                    const tspgpu_city &a = h1[i], &b = h1[(i + 1) % o.L1], &c = h2[j], &d = h2[(j + 1) % o.L2];
                     const double sc = hswap(a, b, c, d);
                     if (sc < best) {
                         best = sc;
-                        bi = i;
-                        A = a;
-                        B = b;
-                        C = c;
+                        pick = Cand{i, j, a, b, c, d};
+                        found = true;
                     }
                 }
         }
-        if (bi < 0) return -EIO;  // no swap below INT_MAX (distances are validated far below)
-        const int M = L2 - 1;
-        rc = tmp.reserve((size_t)L1 + M, st);
-        if (rc) return rc;
-        unsigned long long *fw = words + 2 + 2 * parity;
-        e = hipMemsetAsync(fw, 0xFF, 2 * sizeof(unsigned long long), st);
-        if (e != hipSuccess) return herr(e);
-        const int gf = grid_for((unsigned long long)std::max(L1, M));
-        hipLaunchKernelGGL(find_kernel, dim3(gf), dim3(kMergeThreads), 0, st, s1.p, L1, c2, M, A.id, B.id, C.id, fw);
-        hipLaunchKernelGGL(splice_kernel, dim3(grid_for((unsigned long long)L1 + M)), dim3(kMergeThreads), 0, st,
-                           s1.p, L1, c2, M, fw, tmp.p);
-        pending = true;
-        pend_L1 = L1;
-        pend_M = M;
-        pend_slot = parity;
-        parity ^= 1;
-        std::swap(s1, tmp);
-        s1.len = (size_t)L1 + M;
-        tmp.len = 0;
-        cost1 = cost1 + cost2 + best;  // tsp.cpp:263
+        return found ? 0 : -EIO;  // no swap below INT_MAX (distances are validated far below)
+    }
+    // run every enqueued merge to completion, resolving stalls on the host,
+    // and fold their costs in order
+    int sync()
+    {
+        size_t first = 0;  // ops[first..] not yet folded
+        for (;;) {
+            hipError_t e = hipMemcpyAsync(hctl, ctl, sizeof(Ctl), hipMemcpyDeviceToHost, st);
+            if (e == hipSuccess) e = hipStreamSynchronize(st);
+            if (e != hipSuccess) return herr(e);
+            const size_t upto = hctl->stall ? (size_t)hctl->stall_at : ops.size();
+            if (upto > first) {
+                e = hipMemcpy(hpicks + first, picks + first, (upto - first) * sizeof(Pick), hipMemcpyDeviceToHost);
+                if (e != hipSuccess) return herr(e);
+                for (size_t m = first; m < upto; ++m) {
+                    const Cand &k = hpicks[m].c;
+                    *ops[m].target = (*ops[m].target + *ops[m].cost2) + hswap(k.a, k.b, k.c, k.d);
+                }
+                first = upto;
+            }
+            if (!hctl->stall) break;
+            if (hctl->stall == 2) return -EDEADLK;
+            if (hctl->stall != 1) return -EIO;
+            // the host picks merge `first`, then the device splices it and the rest resumes
+            const Op &o = ops[first];
+            Cand pk{};
+            double best = 0.0;
+            int rc = host_pick(o, pk, best);
+            if (rc) return rc;
+            const int M = o.L2 - 1;
+            Ctl reset = *hctl;
+            reset.fw[0] = reset.fw[1] = ~0ull;
+            e = hipMemcpyAsync(ctl, &reset, sizeof reset, hipMemcpyHostToDevice, st);
+            if (e != hipSuccess) return herr(e);
+            hipLaunchKernelGGL(find_kernel, dim3(grid_for((unsigned long long)std::max(o.L1, M))),
+                               dim3(kMergeThreads), 0, st, o.src, o.L1, o.c2, M, ctl, cand, picks, (int)first,
+                               pk.a.id, pk.b.id, pk.c.id, 1);
+            hipLaunchKernelGGL(splice_kernel, dim3(grid_for(3ull * ((unsigned long long)o.L1 + M))),
+                               dim3(kMergeThreads), 0, st, o.src, o.L1, o.c2, M, ctl, o.dst, (int)first, 1);
+            e = hipMemcpyAsync(hctl, ctl, sizeof(Ctl), hipMemcpyDeviceToHost, st);
+            if (e == hipSuccess) e = hipStreamSynchronize(st);
+            if (e != hipSuccess) return herr(e);
+            if (hctl->stall == 2) return -EDEADLK;
+            if (hctl->stall) return -EIO;
+            *o.target = (*o.target + *o.cost2) + best;
+            ++first;
+            for (size_t m = first; m < ops.size(); ++m) enqueue(ops[m], (int)m);
+            if (hipPeekAtLastError() != hipSuccess) return herr(hipGetLastError());
+        }
+        ops.clear();
         return 0;
     }
 };
@@ -380,8 +666,9 @@ int tspgpu_merge(tspgpu_ctx *ctx, const tspgpu_city *p1, int L1, double c1, cons
     all.insert(all.end(), p2, p2 + L2);
     Merger m;
     int rc = m.init(ctx, bbox_diagonal(all.data(), all.size()));
-    DVec s, b;
+    DVec s, t, b;
     if (!rc) rc = s.reserve(L1, m.st);
+    if (!rc) rc = t.reserve((size_t)L1 + L2, m.st);
     if (!rc) rc = b.reserve(L2, m.st);
     hipError_t e = hipSuccess;
     if (!rc) e = hipMemcpyAsync(s.p, p1, L1 * sizeof(tspgpu_city), hipMemcpyHostToDevice, m.st);
@@ -389,12 +676,13 @@ int tspgpu_merge(tspgpu_ctx *ctx, const tspgpu_city *p1, int L1, double c1, cons
     if (!rc) rc = herr(e);
     s.len = L1;
     double cost = c1;
-    if (!rc) rc = m.merge(s, cost, b.p, L2, c2);
-    if (!rc) rc = m.flush();
+    if (!rc) rc = m.merge(s, t, &cost, b.p, L2, &c2);
+    if (!rc) rc = m.sync();
     if (!rc) rc = herr(hipMemcpyAsync(out, s.p, s.len * sizeof(tspgpu_city), hipMemcpyDeviceToHost, m.st));
     if (!rc) rc = herr(hipStreamSynchronize(m.st));
     const int len = (int)s.len;
     s.release();
+    t.release();
     b.release();
     if (rc) return rc;
     *cost_out = cost;
@@ -421,35 +709,59 @@ int tspgpu_reduce(tspgpu_ctx *ctx, const tspgpu_city *paths, int L, const double
     // distributeBlocks' counts (tsp.cpp:167-192): rank r gets #{b in [1,B] : b mod P == r}
     std::vector<int> cnt(nprocs, 0);
     for (int b = nblocks; b > 0; --b) cnt[b % nprocs]++;
-    // each logical rank folds its contiguous block range left (tsp.cpp:348-352)
+    // one-kernel fold merges need block tours that close on their first city
+    // and ids unique across blocks (the reference's generator numbers cities
+    // globally); anything else takes the general path
+    bool fold_ok = L >= 3;
+    if (fold_ok) {
+        std::vector<int> ids;
+        ids.reserve((size_t)nblocks * (L - 1));
+        for (int b = 0; b < nblocks && fold_ok; ++b) {
+            const tspgpu_city *pb = paths + (size_t)b * L;
+            if (pb[0].id != pb[L - 1].id) fold_ok = false;
+            for (int k = 0; k < L - 1; ++k) ids.push_back(pb[k].id);
+        }
+        std::sort(ids.begin(), ids.end());
+        if (fold_ok && std::adjacent_find(ids.begin(), ids.end()) != ids.end()) fold_ok = false;
+    }
+    // Every buffer a queued merge may touch is sized up front (a merged path
+    // never exceeds all cities; a received list never exceeds all cities), so
+    // nothing is reallocated while merges are in flight.
     std::vector<DVec> rank(nprocs), received(nprocs);
+    DVec tmp;
     std::vector<double> rcost(nprocs, 0.0);
+    if (!rc) rc = tmp.reserve(ncity, m.st);
     int next = 0;
     for (int r = 0; r < nprocs && !rc; ++r) {
-        rc = rank[r].reserve((size_t)L * cnt[r], m.st);
+        rc = rank[r].reserve(ncity, m.st);
         if (rc) break;
         rc = herr(hipMemcpyAsync(rank[r].p, blocks.p + (size_t)next * L, L * sizeof(tspgpu_city),
                                  hipMemcpyDeviceToDevice, m.st));
         rank[r].len = L;
         rcost[r] = costs[next];
         ++next;
+        // each logical rank folds its contiguous block range left (tsp.cpp:348-352)
         for (int j = 1; j < cnt[r] && !rc; ++j, ++next)
-            rc = m.merge(rank[r], rcost[r], blocks.p + (size_t)next * L, L, costs[next]);
+            rc = m.merge(rank[r], tmp, &rcost[r], blocks.p + (size_t)next * L, L, &costs[next], fold_ok);
     }
     // MPI_ManualReduce (tsp.cpp:52-134): the receiver appends every received
     // path to one function-local list and merges with the WHOLE list
     // (tsp.cpp:67,93-98,115-120)
     std::string text;
     auto receive = [&](int to, int from) -> int {
+        // the copy below reads rank[from]'s final path: every queued merge
+        // (and any stall) must be resolved first
+        int r2 = m.sync();
+        if (r2) return r2;
         DVec &acc = received[to];
         const size_t add = rank[from].len;
-        int r2 = acc.reserve(acc.len + add, m.st);
+        r2 = acc.reserve(std::max(acc.len + add, ncity), m.st);
         if (r2) return r2;
         r2 = herr(hipMemcpyAsync(acc.p + acc.len, rank[from].p, add * sizeof(tspgpu_city), hipMemcpyDeviceToDevice,
                                  m.st));
         if (r2) return r2;
         acc.len += add;
-        return m.merge(rank[to], rcost[to], acc.p, (int)acc.len, rcost[from]);
+        return m.merge(rank[to], tmp, &rcost[to], acc.p, (int)acc.len, &rcost[from]);
     };
     const int lastpower = 1 << (int)std::log2((double)nprocs);
     for (int i = 0; i < nprocs - lastpower && !rc; ++i) {
@@ -461,9 +773,11 @@ int tspgpu_reduce(tspgpu_ctx *ctx, const tspgpu_city *paths, int L, const double
     }
     for (int d = 0; d < (int)std::log2((double)lastpower) && !rc; ++d)
         for (int k = 0; k < lastpower && !rc; k += 1 << (d + 1)) rc = receive(k, k + (1 << d));
-    if (!rc) rc = m.flush();
+    if (!rc) rc = m.sync();
+    (void)hipStreamSynchronize(m.st);
     for (auto &v : rank) v.release();
     for (auto &v : received) v.release();
+    tmp.release();
     blocks.release();
     if (rc) return rc;
     *final_cost = rcost[0];
