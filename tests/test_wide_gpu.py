@@ -63,3 +63,26 @@ def test_rejects_bad_input(gpu_ctx):
     bad[0, 1] = np.nan
     with pytest.raises(tspgpu.TspGpuError):
         gpu_ctx.solve_instance(bad)
+
+
+@pytest.mark.parametrize("form", ["0", "1"])
+def test_push_and_pull_forms(gpu_ctx, monkeypatch, form):
+    """Both layer forms (row-owner push, per-destination pull) on the goldens
+    (tie-heavy included) and on random / lattice instances vs the oracle."""
+    monkeypatch.setenv("TSPGPU_WIDE_PULL", form)
+    for inst in O.load_golden("tie_blocks.json"):
+        cities = [(c[0], O.hexf(c[1]), O.hexf(c[2])) for c in inst["cities"]]
+        if len(cities) < 3:
+            continue
+        d = tspgpu.distance_matrix([cities])[0]
+        cost, tour, _ = gpu_ctx.solve_instance(d)
+        assert cost == O.hexf(inst["solution"]["cost_hex"])
+        assert [cities[t][0] for t in tour] == inst["solution"]["ids"]
+    rng = np.random.default_rng(int(form) + 77)
+    for n in (3, 5, 9, 13, 16, 18, 20):
+        for lattice in (False, True):
+            xy = rng.integers(0, 4, size=(n, 2)).astype(np.float64) if lattice else rng.uniform(0, 1000, size=(n, 2))
+            d = O.distance_matrix([(i, xy[i, 0], xy[i, 1]) for i in range(n)])
+            cost, tour, _ = gpu_ctx.solve_instance(d)
+            oc, ot = O.solve_block(d)
+            assert cost == oc and tour.tolist() == ot, (form, n, lattice)

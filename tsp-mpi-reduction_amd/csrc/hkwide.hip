@@ -107,6 +107,73 @@ __global__ __launch_bounds__(kWideThreads) void wide_layer(const double *__restr
     }
 }
 
+// Row-owner ("push") form of a layer, t -> t+1 (default): a thread owns a
+// SOURCE row T of layer t (its t values are coalesced loads: consecutive
+// threads hold consecutive colex ranks) and writes every destination
+// G[T+k][k] = min_{m in T} G[T][m] + d[m][k] for the N - t cities k not in T —
+// the whole min of a destination comes from that one row, so every table
+// entry is read once and written once (the pull form above reads each entry
+// N - t times through scattered loads).  The destination rank follows from
+// prefix sums over T's members: colexrank(T+k) = sum_{m<k} C(m, i_m) +
+// C(k, c+1) + sum_{m>k} C(m, i_m + 1), c = #members below k = the position of
+// k in T+k.  Consecutive rows differ in their low members, so the writes of
+// one k are mostly contiguous runs.  Templated on t: the row lives in VGPRs.
+template <int T>
+__global__ __launch_bounds__(kWideThreads) void wide_push(const double *__restrict__ dist, int N,
+                                                          const WideInfo *__restrict__ info,
+                                                          double *__restrict__ tab)
+{
+    __shared__ int B[kWideMaxN + 2][kWideMaxN + 3];  // C(a, b), b <= 31 (ranks < 2^31 for N <= 30)
+    __shared__ double dl[(kWideMaxN + 1) * (kWideMaxN + 1)];
+    const int n = N + 1;
+    for (int i = threadIdx.x; i < (kWideMaxN + 2) * (kWideMaxN + 3); i += kWideThreads) {
+        const int a = i / (kWideMaxN + 3), b = i % (kWideMaxN + 3);
+        (&B[0][0])[i] = b <= kWideMaxN + 1 ? (int)info->binom[a][b] : 0;
+    }
+    for (int i = threadIdx.x; i < n * n; i += kWideThreads) dl[i] = dist[i];
+    __syncthreads();
+    const unsigned long long ct = info->cnt[T], cs = info->cnt[T + 1];
+    const unsigned long long ot = info->off[T], os = info->off[T + 1];
+    for (unsigned long long r0 = blockIdx.x * (unsigned long long)kWideThreads + threadIdx.x; r0 < ct;
+         r0 += (unsigned long long)gridDim.x * kWideThreads) {
+        // colex unrank of T: members m_1 < ... < m_T with r0 = sum C(m_i, i)
+        int m[T];
+        long long r = (long long)r0;
+        int c = N - 1;
+#pragma unroll
+        for (int i = T; i >= 1; --i) {
+            while (B[c][i] > r) --c;
+            r -= B[c][i];
+            m[i - 1] = c;
+            --c;
+        }
+        double g[T];
+#pragma unroll
+        for (int j = 0; j < T; ++j) g[j] = tab[ot + (unsigned long long)j * ct + r0];
+        uint32_t mask = 0;
+        long long hi = 0;  // sum_j C(m_j, j+2): every member above k
+#pragma unroll
+        for (int j = 0; j < T; ++j) {
+            mask |= 1u << m[j];
+            hi += B[m[j]][j + 2];
+        }
+        long long lo = 0;  // sum over members below k of C(m_j, j+1) - C(m_j, j+2)
+        int cb = 0;        // members below k
+        for (int k = 0; k < N; ++k) {
+            if ((mask >> k) & 1u) {
+                lo += (long long)B[k][cb + 1] - (long long)B[k][cb + 2];
+                ++cb;
+                continue;
+            }
+            double acc = kIntMaxD;  // tsp.cpp:453 (candidates are < INT_MAX by validation)
+#pragma unroll
+            for (int j = 0; j < T; ++j) acc = fmin(acc, g[j] + dl[(m[j] + 1) * n + (k + 1)]);
+            const long long rs = hi + lo + B[k][cb + 1];
+            tab[os + (unsigned long long)cb * cs + (unsigned long long)rs] = acc;
+        }
+    }
+}
+
 // closing min + backtracking (one wave): lane m-1 holds candidate m
 __global__ void wide_close(const double *__restrict__ dist, int N, const WideInfo *__restrict__ info,
                            const double *__restrict__ tab, double *__restrict__ cost_out, int32_t *__restrict__ tour)
@@ -193,11 +260,41 @@ void wide_state_free(void *p)
     delete w;
 }
 
+void launch_push(int t, int grid, hipStream_t st, const double *dist, int N, const WideInfo *info, double *tab)
+{
+    switch (t) {
+#define TSPGPU_PUSH(TT) \
+    case TT: hipLaunchKernelGGL(wide_push<TT>, dim3(grid), dim3(kWideThreads), 0, st, dist, N, info, tab); break;
+    TSPGPU_PUSH(1) TSPGPU_PUSH(2) TSPGPU_PUSH(3) TSPGPU_PUSH(4) TSPGPU_PUSH(5) TSPGPU_PUSH(6) TSPGPU_PUSH(7)
+    TSPGPU_PUSH(8) TSPGPU_PUSH(9) TSPGPU_PUSH(10) TSPGPU_PUSH(11) TSPGPU_PUSH(12) TSPGPU_PUSH(13) TSPGPU_PUSH(14)
+    TSPGPU_PUSH(15) TSPGPU_PUSH(16) TSPGPU_PUSH(17) TSPGPU_PUSH(18) TSPGPU_PUSH(19) TSPGPU_PUSH(20) TSPGPU_PUSH(21)
+    TSPGPU_PUSH(22) TSPGPU_PUSH(23) TSPGPU_PUSH(24) TSPGPU_PUSH(25) TSPGPU_PUSH(26) TSPGPU_PUSH(27) TSPGPU_PUSH(28)
+    TSPGPU_PUSH(29)
+#undef TSPGPU_PUSH
+    default: break;
+    }
+}
+
 // layer 1, layers 2..N, closing + backtracking
 void enqueue_wide(const WideState *w, const WideInfo &h, int n, int cus, hipStream_t st)
 {
     const int N = n - 1;
     hipLaunchKernelGGL(wide_layer1, dim3(1), dim3(64), 0, st, w->dist, n, w->tab);
+    // per-destination (pull) form up to 17 cities, where both are bound by the
+    // ~8 us kernel boundary per layer and pull is a little faster; TSPGPU_WIDE_PULL
+    // = 0 / 1 forces either (measured: profiles/r01/k1wide_push_vs_pull.log)
+    const char *force = std::getenv("TSPGPU_WIDE_PULL");
+    const bool pull = force ? std::atoi(force) != 0 : n <= 17;
+    if (!pull) {
+        for (int t = 1; t < N; ++t) {
+            const unsigned long long blocks = (h.cnt[t] + kWideThreads - 1) / kWideThreads;
+            const unsigned long long cap = (unsigned long long)cus * 16;
+            const int grid = (int)(blocks < cap ? blocks : cap);
+            launch_push(t, grid, st, w->dist, N, w->info, w->tab);
+        }
+        hipLaunchKernelGGL(wide_close, dim3(1), dim3(64), 0, st, w->dist, N, w->info, w->tab, w->cost, w->tour);
+        return;
+    }
     for (int s = 2; s <= N; ++s) {
         const unsigned long long total = h.cnt[s] * (unsigned long long)s;
         const unsigned long long blocks = (total + kWideThreads - 1) / kWideThreads;
