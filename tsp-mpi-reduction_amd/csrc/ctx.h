@@ -29,7 +29,8 @@ struct tspgpu_ctx {
     int threads = 0;     // workgroup size of the global-table kernels; 0 = per-N default
     int wg_per_cu = 0;   // resident slots per CU (auto grid); 0 = per-N default
     int lds_table_max_n = tspgpu::kLdsTableDefaultMaxN;  // largest N whose whole table stays in LDS
-    int variant = 2;     // K1 layer pass: 2 = compact + next-row prefetch, 1 = compact, 0 = member sweep
+    int variant = -1;    // K1 layer pass (-1: per-n default): 4 = 2 + ping-pong values + parent words,
+                         // 2 = compact + next-row prefetch, 1 = compact, 0 = member sweep
     hipEvent_t ev_start = nullptr, ev_stop = nullptr;
     char name[256] = {0};
     std::mutex mu;

@@ -228,9 +228,58 @@ struct LdsTableT {
 };
 using LdsTable = LdsTableT<double>;
 
+// Ping-pong value layout (VAR 4): a middle layer t lives in buffer t & 1 at
+// the start of the slot instead of its own span, so the two live layers of
+// all resident workgroups stay in the Infinity Cache and are rewritten there
+// (1.4x at n = 16, profiles/r01/k1_pingpong_experiment.log); the backtracking
+// then follows the parent bytes stored by the forward pass instead of the
+// values.  Logical indices stay those of the compact layout.
+template <typename V, long SHIFT>
+struct ShiftTable {
+    GlobalTableT<V> g;
+    __device__ __forceinline__ V load(uint32_t idx) const { return g.load((uint32_t)((long)idx - SHIFT)); }
+    __device__ __forceinline__ void store(uint32_t idx, V v) const { g.store((uint32_t)((long)idx - SHIFT), v); }
+};
+__host__ __device__ constexpr uint32_t max_layer_elems(int N)
+{
+    uint32_t m = 0;
+    for (int t = 1; t <= N; ++t) m = m > cbinom(N, t) * t ? m : cbinom(N, t) * t;
+    return m;
+}
+// byte offset of the parent bytes in a VAR-4 slot (behind the two buffers)
+template <typename V>
+__host__ __device__ constexpr uint32_t parent_base(int N)
+{
+    return 2u * max_layer_elems(N) * (uint32_t)sizeof(V);
+}
+// Parents (N <= 15): for every SOURCE row T of layer t, one 64-bit word
+// holding, per non-member k of T (q-th non-member, 4 bits at 4q), m - 1 for
+// the city m of the first strict minimum over m ascending (tsp.cpp:457-471)
+// of destination (T+k, k).  One coalesced 8-byte store per row (consecutive
+// threads own consecutive rows) instead of N - t scattered bytes; word index
+// = the row's place in the colex mask list (mask_off(N, t) + rank).
+struct ParentTable {
+    static constexpr bool on = true;
+    __amdgpu_buffer_rsrc_t rs;
+    uint32_t base;
+    __device__ __forceinline__ void store(uint32_t widx, uint64_t w) const
+    {
+        using u2 = decltype(__builtin_amdgcn_raw_buffer_load_b64(rs, 0, 0, 0));
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2, w), rs, (int)(base + widx * 8u), 0, 0);
+    }
+    __device__ __forceinline__ uint64_t load(uint32_t widx) const
+    {
+        return __builtin_bit_cast(uint64_t, __builtin_amdgcn_raw_buffer_load_b64(rs, (int)(base + widx * 8u), 0, 0));
+    }
+};
+struct NoParents {
+    static constexpr bool on = false;
+    __device__ __forceinline__ void store(uint32_t, uint64_t) const {}
+};
+
 // The table of a compact global kernel: layers 1..A and N-A+1..N in LDS, the
 // rest in the workgroup's HBM slot (same indices everywhere).
-template <typename V, int N, int A>
+template <typename V, int N, int A, bool PP = false>
 struct SplitTable {
     GlobalTableT<V> g;
     V *lo, *hi;
@@ -241,6 +290,8 @@ struct SplitTable {
             return LdsTableT<V>{lo, 0u};
         else if constexpr (A > 0 && t >= N - A + 1)
             return LdsTableT<V>{hi, (uint32_t)layer_off(N, N - A + 1)};
+        else if constexpr (PP)
+            return ShiftTable<V, (long)layer_off(N, t) - ((t & 1) ? 0L : (long)max_layer_elems(N))>{g};
         else
             return g;
     }
@@ -372,10 +423,10 @@ __device__ __forceinline__ void layer_pass_lds(const LdsTable &tab, const double
 // thread, so the kernel runs at 8 waves/SIMD without spilling.
 // PF (prefetch depth): the masks and t values of the next PF rows are in
 // flight while the current row is relaxed (software pipelining, 2t VGPRs per row).
-template <typename V, int N, int T, int THREADS, int PF, typename SrcTab, typename DstTab>
+template <typename V, int N, int T, int THREADS, int PF, typename SrcTab, typename DstTab, typename PTab = NoParents>
 __device__ __forceinline__ void layer_pass_compact(const SrcTab &src, const DstTab &dst, const V *__restrict__ dl,
                                                    const int *__restrict__ rl, const uint32_t *__restrict__ masks,
-                                                   uint32_t tid)
+                                                   uint32_t tid, const PTab &par = PTab{})
 {
     constexpr int S = T + 1;
     constexpr int Q = N - T;
@@ -439,8 +490,12 @@ __device__ __forceinline__ void layer_pass_compact(const SrcTab &src, const DstT
             nb &= nb - 1u;
         }
         V acc[Q];
+        uint32_t arg[Q];
 #pragma unroll
-        for (int q = 0; q < Q; ++q) acc[q] = ValT<V>::inf;
+        for (int q = 0; q < Q; ++q) {
+            acc[q] = ValT<V>::inf;
+            arg[q] = 0;
+        }
         uint32_t bits = Tm;
 #pragma unroll
         for (int j = 0; j < T; ++j) {
@@ -448,13 +503,28 @@ __device__ __forceinline__ void layer_pass_compact(const SrcTab &src, const DstT
             bits &= bits - 1u;
             const V *drow = dl + m * DS;
 #pragma unroll
-            for (int q = 0; q < Q; ++q) acc[q] = ValT<V>::vmin(acc[q], g[j] + drow[kb[q]]);
+            for (int q = 0; q < Q; ++q) {
+                const V cnd = g[j] + drow[kb[q]];
+                if constexpr (PTab::on) {
+                    // first strict minimum over m ascending (tsp.cpp:465): the parent
+                    arg[q] = cnd < acc[q] ? (uint32_t)m : arg[q];
+                    acc[q] = ValT<V>::vmin(acc[q], cnd);
+                } else {
+                    acc[q] = ValT<V>::vmin(acc[q], cnd);
+                }
+            }
         }
 #pragma unroll
         for (int q = 0; q < Q; ++q) {
             const uint32_t k = kb[q];
             const uint32_t rank = lut_rank<N>(Tm | (1u << k), rl);
             dst.store(DST + (k - (uint32_t)q) * ROWS_S + rank, acc[q]);
+        }
+        if constexpr (PTab::on) {
+            uint64_t w = 0;
+#pragma unroll
+            for (int q = 0; q < Q; ++q) w |= (uint64_t)(arg[q] - 1u) << (4 * q);
+            par.store(mask_off(N, T) + r, w);
         }
     }
 }
@@ -469,15 +539,15 @@ __device__ __forceinline__ void all_layers_compact(const Tab &tab, const V *dl, 
         all_layers_compact<V, N, T + 1, THREADS, PF>(tab, dl, rl, masks, tid);
     }
 }
-template <typename V, int N, int A, int T, int THREADS, int PF>
-__device__ __forceinline__ void all_layers_split(const SplitTable<V, N, A> &tb, const V *dl, const int *rl,
-                                                 const uint32_t *masks, uint32_t tid)
+template <typename V, int N, int A, int T, int THREADS, int PF, bool PP, typename PTab>
+__device__ __forceinline__ void all_layers_split(const SplitTable<V, N, A, PP> &tb, const V *dl, const int *rl,
+                                                 const uint32_t *masks, uint32_t tid, const PTab &par)
 {
     if constexpr (T < N) {
         layer_pass_compact<V, N, T, THREADS, PF>(tb.template layer<T>(), tb.template layer<T + 1>(), dl, rl, masks,
-                                                 tid);
+                                                 tid, par);
         __syncthreads();
-        all_layers_split<V, N, A, T + 1, THREADS, PF>(tb, dl, rl, masks, tid);
+        all_layers_split<V, N, A, T + 1, THREADS, PF>(tb, dl, rl, masks, tid, par);
     }
 }
 
@@ -501,7 +571,9 @@ __device__ __forceinline__ void all_layers(const Tab &tab, const double *dl, con
 // Occupancy target (waves per SIMD): the member sweep holds N running minima
 // plus a prefetched row (<= 128 VGPRs, 4 waves); the compact pass needs about
 // half of that (<= 64 VGPRs, 8 waves) at the reference's sizes.
-// VAR: 0 member sweep, 1 compact, 2 compact + next-row prefetch, 3 compact + two rows prefetched
+// VAR: 0 member sweep, 1 compact, 2 compact + next-row prefetch, 3 compact + two rows prefetched,
+// 4 = 2 + ping-pong values + parent bytes
+__host__ __device__ constexpr int var_pf(int var) { return var == 4 ? 1 : var - 1; }
 __host__ __device__ constexpr int min_waves(int N, int var)
 {
     return var == 1 ? (N <= 15 ? 8 : 4) : (N <= 15 ? 4 : 2);
@@ -533,7 +605,8 @@ __global__ __launch_bounds__(THREADS, min_waves(N, VAR)) void heldkarp_kernel(
     using Tab = typename std::conditional<LDS_TABLE, LdsTableT<V>, GlobalTableT<V>>::type;
     // compact global kernels: the end layers live in LDS behind the LUT
     constexpr int A = (!LDS_TABLE && VAR >= 1) ? lds_end_layers(N, THREADS, VB) : 0;
-    SplitTable<V, N, A> tb;
+    constexpr bool PP = VAR == 4 && !LDS_TABLE;
+    SplitTable<V, N, A, PP> tb;
     tb.lo = lds_rest;
     tb.hi = lds_rest + low_bytes(N, A, VB) / VB;
     Tab th;
@@ -549,6 +622,11 @@ __global__ __launch_bounds__(THREADS, min_waves(N, VAR)) void heldkarp_kernel(
         th.rs = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void *>(((uint64_t)hi << 32) | lo), 0, bytes,
                                                   0x00020000);
         tb.g = th;
+    }
+    ParentTable par{};
+    if constexpr (PP) {
+        par.rs = th.rs;
+        par.base = parent_base<V>(N);
     }
     // table entry (layer t, index idx) wherever it lives
     auto tget = [&](int t, uint32_t idx) -> V {
@@ -582,17 +660,49 @@ __global__ __launch_bounds__(THREADS, min_waves(N, VAR)) void heldkarp_kernel(
         // costs ~200 VGPRs of 64-bit pointers).
         int tid_b = tid;
         asm volatile("" : "+v"(tid_b));
-        if constexpr (!LDS_TABLE && VAR >= 1)
-            all_layers_split<V, N, A, 1, THREADS, VAR - 1>(tb, dl, rl, masks, (uint32_t)tid_b);
+        if constexpr (PP)
+            all_layers_split<V, N, A, 1, THREADS, var_pf(VAR)>(tb, dl, rl, masks, (uint32_t)tid_b, par);
+        else if constexpr (!LDS_TABLE && VAR >= 1)
+            all_layers_split<V, N, A, 1, THREADS, var_pf(VAR)>(tb, dl, rl, masks, (uint32_t)tid_b, NoParents{});
         else if constexpr (VAR >= 1)
-            all_layers_compact<V, N, 1, THREADS, VAR - 1>(th, dl, rl, masks, (uint32_t)tid_b);
+            all_layers_compact<V, N, 1, THREADS, var_pf(VAR)>(th, dl, rl, masks, (uint32_t)tid_b);
         else if constexpr (std::is_same<V, double>::value)
             all_layers<N, 1, THREADS>(th, dl, binom, lds_rest + tid_b, masks, (uint32_t)tid_b);
 
         // closing min (tsp.cpp:483-499) and backtracking, one wave: lane m-1
         // holds candidate m.  The state value of the next step is the g value
         // the picked lane loaded, so each step costs one dependent load.
-        if (tid < 64) {
+        if (PP && tid < 64) {
+            // closing min as below; the tour follows the parent bytes
+            const int lane = tid;
+            const int m = lane + 1;
+            const bool valid = m <= N;
+            const V glast = valid ? tb.template layer<N>().load(layer_off(N, N) + (uint32_t)(m - 1)) : V(0);
+            const V cand = valid ? glast + dget<N>(dl, m, 0) : ValT<V>::invalid;
+            const V best = ValT<V>::vmin(wave_min(cand), ValT<V>::inf);
+            const unsigned long long hit = __ballot(valid && cand == best && cand < ValT<V>::inf);
+            const int bestM = hit ? __ffsll(hit) : 0;
+            if (lane == 0) {
+                int32_t *tour = tour_out + (size_t)blk * (n + 1);
+                uint32_t S = (1u << N) - 1u;
+                int k = bestM;
+                for (int pos = n - 2; bestM && pos >= 1; --pos) {
+                    // parent word of the source row T = S \ k (layer |S| - 1), nibble of k
+                    const uint32_t T = S & ~(1u << (k - 1));
+                    const int tt = __builtin_popcount(T);
+                    const int q = (k - 1) - __builtin_popcount(T & ((1u << (k - 1)) - 1u));
+                    const uint64_t w = par.load((uint32_t)info->moff[tt] + lut_rank<N>(T, rl));
+                    const int pm = (int)((w >> (4 * q)) & 15u) + 1;
+                    tour[pos] = pm;
+                    S &= ~(1u << (k - 1));
+                    k = pm;
+                }
+                tour[0] = 0;
+                tour[n - 1] = bestM;
+                tour[n] = 0;
+                cost_out[blk] = bestM ? best : V(-1);
+            }
+        } else if (tid < 64) {
             const int lane = tid;
             const int m = lane + 1;
             const uint32_t full = (1u << N) - 1u;
@@ -669,6 +779,10 @@ hipError_t launch_threads_v(const LaunchArgs &a, int grid)
     if constexpr (N <= kLdsTableMaxN) {
         if (a.use_lds) return launch_n<V, N, true, lds_table_threads(N), VAR >= 2 ? 1 : VAR>(a, grid);
     }
+    if constexpr (VAR == 4 && (N < 11 || N > 15)) {
+        // ping-pong + parent words: 12..16 cities (4-bit parents, <= 14 per row)
+        return launch_n<V, N, false, 256, 2>(a, grid);
+    }
     if constexpr (N >= 12 && N <= 15) {
         if (a.threads == 512) return launch_n<V, N, false, 512, VAR>(a, grid);
         if (a.threads == 1024) return launch_n<V, N, false, 1024, VAR>(a, grid);
@@ -682,6 +796,7 @@ hipError_t launch_threads(const LaunchArgs &a, int grid)
     // integer matrices: the default (compact + prefetch) pass only
     if (a.vbytes == 4) return launch_threads_v<int32_t, N, 2>(a, grid);
     // (VAR 3, two rows in flight, measured no faster than one: not instantiated)
+    if (a.variant >= 4) return launch_threads_v<double, N, 4>(a, grid);
     if (a.variant >= 2) return launch_threads_v<double, N, 2>(a, grid);
     return a.variant == 1 ? launch_threads_v<double, N, 1>(a, grid) : launch_threads_v<double, N, 0>(a, grid);
 }

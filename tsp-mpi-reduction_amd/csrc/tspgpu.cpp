@@ -176,10 +176,14 @@ int solve_device_locked(tspgpu_ctx *c, const void *d_dist, int n, int nblocks, v
             def_wg = N <= 12 ? 8 : (N <= 13 ? 4 : 2);
         }
         a.threads = c->threads > 0 ? c->threads : def_threads;
-        a.variant = c->variant;
+        // ping-pong + parents pays at 16 cities (the two live middle layers of
+        // all 256 resident blocks then stay in the Infinity Cache), not below
+        // (with a full wave of blocks: one block alone is latency-bound and the
+        // argmin's extra VALU only costs there)
+        a.variant = c->variant >= 0 ? c->variant : (N == 15 && vbytes == 8 && nblocks >= c->cu_count ? 4 : 2);
         if (a.use_lds) {
             // as many resident workgroups as the LDS allows, then persistent
-            const int per_cu = (int)(160 * 1024 / lds_bytes_for(N, true, threads_for(N, true, 0), vbytes == 4 || c->variant >= 1, vbytes));
+            const int per_cu = (int)(160 * 1024 / lds_bytes_for(N, true, threads_for(N, true, 0), vbytes == 4 || a.variant >= 1, vbytes));
             const int cap = c->cu_count * (per_cu > 0 ? per_cu : 1);
             grid = nblocks < cap ? nblocks : cap;
         } else {
@@ -339,7 +343,7 @@ int tspgpu_ctx_create(const tspgpu_opts *opts, tspgpu_ctx **out)
     }
     if (const char *e = std::getenv("TSPGPU_K1")) {
         const int v = std::atoi(e);
-        c->variant = v < 0 ? 1 : (v > 2 ? 2 : v);
+        c->variant = v < 0 ? 1 : (v >= 4 ? 4 : (v > 2 ? 2 : v));
     }
     if (const char *e = std::getenv("TSPGPU_WG_PER_CU")) c->wg_per_cu = std::atoi(e) > 0 ? std::atoi(e) : 0;
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {

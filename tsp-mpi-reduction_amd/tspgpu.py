@@ -13,7 +13,8 @@ import os
 import numpy as np
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(PKG_DIR, "lib", "libtspgpu.so")
+# TSPGPU_LIB: another build of the same ABI (development A/B experiments)
+LIB_PATH = os.environ.get("TSPGPU_LIB") or os.path.join(PKG_DIR, "lib", "libtspgpu.so")
 HOST_LIB_PATH = os.path.join(PKG_DIR, "lib", "libtsphost.so")
 TSP_BIN = os.path.join(PKG_DIR, "bin", "tsp")
 
