@@ -794,7 +794,8 @@ template <int N>
 hipError_t launch_threads(const LaunchArgs &a, int grid)
 {
     // integer matrices: the default (compact + prefetch) pass only
-    if (a.vbytes == 4) return launch_threads_v<int32_t, N, 2>(a, grid);
+    if (a.vbytes == 4)
+        return a.variant >= 4 ? launch_threads_v<int32_t, N, 4>(a, grid) : launch_threads_v<int32_t, N, 2>(a, grid);
     // (VAR 3, two rows in flight, measured no faster than one: not instantiated)
     if (a.variant >= 4) return launch_threads_v<double, N, 4>(a, grid);
     if (a.variant >= 2) return launch_threads_v<double, N, 2>(a, grid);
