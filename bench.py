@@ -22,6 +22,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
 import shutil
 import statistics
@@ -207,6 +208,29 @@ def cpu_optimized(n, seconds_budget=5.0):
     return {"value": k * tspgpu.relaxations_per_block(n) / wall, "unit": "search nodes/s", "cores": cores,
             "kind": "port", "sample": f"{k} blocks x {n} cities, oracle array Held-Karp (C -O2) on {cores} threads, "
                                       f"{wall:.1f} s", "blocks_per_s": k / wall}
+
+
+def k2_exhaustive(ctx, n=14, reps=3):
+    """BASELINE config 2: `./tsp 14 1 1000 1000` by exhaustive enumeration on
+    one GPU (K2 with the bound off; every one of the 13! tours folded, the
+    last four cities of every path in registers).  Node roofline (SURVEY
+    §8(d)): 9.8 T nodes/s (LDS-bound; 19.7 T on VALU alone)."""
+    d = Shard(n, 1, 0, 1).distances()[0]
+    best = None
+    for _ in range(reps):
+        t = time.perf_counter()
+        cost, tour, st = tspgpu.search_solve(ctx, d, exhaustive=True)
+        wall = (time.perf_counter() - t) * 1e3
+        if best is None or wall < best[0]:
+            best = (wall, cost, tour, st)
+    wall, cost, tour, st = best
+    nps = st["nodes"] / max(st["kernel_ms"] * 1e-3, 1e-12)
+    tours = math.factorial(n - 1)
+    return {"instance": f"./tsp {n} 1 1000 1000 (block 0)", "cost": cost, "tour": [int(x) for x in tour],
+            "time_to_optimal_ms": wall, "kernel_ms": st["kernel_ms"], "tours": tours,
+            "tours_per_s": tours / max(st["kernel_ms"] * 1e-3, 1e-12), "nodes": st["nodes"], "nodes_per_s": nps,
+            "node_roofline_frac": nps / 9.8e12, "lane_utilisation": st["active_steps"] / max(st["lane_steps"], 1),
+            "rounds": st["rounds"]}
 
 
 def k2_single_instance(ctx, n, world, rank, local_rank, reps=3):
@@ -433,6 +457,13 @@ def main():
         except Exception as e:  # the probe must never cost the headline line
             i32 = {"error": f"{type(e).__name__}: {e}"}
 
+    exh = None
+    if not args.no_k2 and os.environ.get("BENCH_K2", "1") != "0" and rank == 0:
+        try:
+            exh = k2_exhaustive(ctx)
+        except Exception as e:  # the probe must never cost the headline line
+            exh = {"error": f"{type(e).__name__}: {e}"}
+
     k2 = None
     if not args.no_k2 and os.environ.get("BENCH_K2", "1") != "0":
         try:
@@ -491,6 +522,7 @@ def main():
         "cpu_optimized": cpu_opt,
         "k2_single_instance": k2,
         "k1_i32_extension": i32,
+        "k2_exhaustive_14": exh,
         "device": devname,
         "cus": cu,
     }

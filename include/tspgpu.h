@@ -190,6 +190,15 @@ typedef struct tspgpu_search tspgpu_search; /* one instance (or one shard of it)
 int tspgpu_search_solve(tspgpu_ctx *ctx, const void *dist, int dtype, int n, double *cost_out,
                         int32_t *tour_out, tspgpu_search_stats *stats);
 
+/* Exhaustive enumeration (BASELINE config 2: "14-city exhaustive enumeration
+ * on 1 MI355X"): the same search with the bound switched off — every one of
+ * the (n-1)! tours is folded (the left fold of tsp.cpp), the tours within the
+ * incumbent are recorded and the DP's tie rule picks among the optimal ones,
+ * so the result equals tspgpu_search_solve / tsp().  stats->nodes counts every
+ * partial path (about e*(n-1)!).  Practical up to ~15 cities. */
+int tspgpu_search_enumerate(tspgpu_ctx *ctx, const void *dist, int dtype, int n, double *cost_out,
+                            int32_t *tour_out, tspgpu_search_stats *stats);
+
 /* Sharded form for multi-GPU drivers (one process or thread per GPU): shard s
  * of S seeds the depth-D prefixes p with p mod S == s (static interleave).
  * Inside the GPU the work runs in rounds: lanes take items from a device

@@ -209,3 +209,30 @@ def test_forced_second_phase_and_k1_fallback(gpu_ctx, monkeypatch):
     cost, tour, st = tspgpu.search_solve(gpu_ctx, d)
     oc, ot = O.solve_block(d)
     assert (cost, tour.tolist()) == (oc, ot) and st["fallback"] == 1, st
+
+
+@pytest.mark.parametrize("n", [3, 4, 6, 8, 10, 11])
+def test_exhaustive_enumeration_against_oracle(gpu_ctx, n):
+    """No bound at all: every tour folded; same cost bits and tour as tsp()."""
+    rng = np.random.default_rng(9000 + n)
+    for lattice in (False, True):
+        xy = rng.integers(0, 4, size=(n, 2)).astype(np.float64) if lattice else rng.uniform(0, 1000, size=(n, 2))
+        d = O.distance_matrix([(i, xy[i, 0], xy[i, 1]) for i in range(n)])
+        cost, tour, st = tspgpu.search_solve(gpu_ctx, d, exhaustive=True)
+        oc, ot = O.solve_block(d)
+        assert (cost, tour.tolist()) == (oc, ot), (n, lattice, st)
+        # every complete tour is a node below the seed depth: at least (n-1)! of them
+        import math
+        assert st["nodes"] >= math.factorial(n - 1), (st["nodes"], n)
+
+
+def test_exhaustive_14_golden(gpu_ctx):
+    """BASELINE config 2: `./tsp 14 1 1000 1000` by exhaustive enumeration
+    (13! = 6.2e9 tours) — the reference's golden cost and tour."""
+    case = next(c for c in O.load_golden("seed0_blocks.json") if c["n"] == 14 and c["B"] == 1 and c["X"] == 1000)
+    cities = _cities(case["cities"][0])
+    d = tspgpu.distance_matrix([cities])[0]
+    cost, tour, st = tspgpu.search_solve(gpu_ctx, d, exhaustive=True)
+    assert cost == O.hexf(case["solutions"][0]["cost_hex"]), st
+    assert [cities[t][0] for t in tour] == case["solutions"][0]["ids"], st
+    assert st["nodes"] > 6.0e9, st

@@ -3,7 +3,9 @@
 #   gpurun -- 'bash tools/k2_pmc.sh TAG [n]'
 set -u
 cd "$(dirname "$0")/.."
-TAG=${1:-k2pmc}; N=${2:-16}
+TAG=${1:-k2pmc}; N=${2:-16}; MODE=${3:-bnb}   # bnb: tools/k2_time.py, exh: tools/k2_exhaustive.py
+PROG=tools/k2_time.py
+[ "$MODE" = exh ] && PROG=tools/k2_exhaustive.py
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
@@ -16,7 +18,7 @@ i=0
 for p in "${PASSES[@]}"; do
   i=$((i+1))
   echo "== pass $i: $p" >&2
-  timeout -s KILL 90 rocprofv3 --pmc $p --output-format csv -d $OUT/p$i -o pmc -- python3 tools/k2_time.py $N > $OUT/p$i.log 2>&1
+  timeout -s KILL 90 rocprofv3 --pmc $p --output-format csv -d $OUT/p$i -o pmc -- python3 $PROG $N > $OUT/p$i.log 2>&1
   rc=$?
   echo "   rc=$rc" >&2
   if [ $rc -ne 0 ]; then tail -5 $OUT/p$i.log >&2; fi

@@ -76,6 +76,8 @@ struct SearchArgs {
     uint32_t min_split;        // steps on an item before it may donate
     unsigned long long wall_limit;  // watchdog, wall_clock64 ticks
     int kernel;                // round kernel: 2 (lock-step DFS, default) or 1 (branching DFS); 3 = persistent
+    int noprune;               // exhaustive enumeration: no bound test (kernels 2 and seed only)
+    int tails;                 // kernel 2: last four cities enumerated in registers (tail4)
     hipStream_t stream;
 };
 

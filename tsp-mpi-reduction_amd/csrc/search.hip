@@ -128,7 +128,7 @@ __global__ __launch_bounds__(kSearchThreads) void seed_kernel(SearchArgs a)
             for (int b = 0; b < 8; ++b)
                 if ((l >> 2) == b) w[b] |= (uint32_t)t << (8 * (l & 3));
             prev = t;
-            if (Num<V>::pruned((W)c + ra, inc)) live = false;
+            if (!a.noprune && Num<V>::pruned((W)c + ra, inc)) live = false;
         }
         // one atomic per wave for its live prefixes
         const unsigned long long lm = __ballot(live);
@@ -379,6 +379,17 @@ __global__ __launch_bounds__(kSearchThreads) void round_kernel_v1(SearchArgs a)
 // LDS: d (n rows of stride 32) | {a[x], d[x][0]} pairs | cost stack [n][T] |
 //      city stack [n][T] | wave item buffers.
 template <typename V>
+struct ValT2;  // a value above every tour cost
+template <>
+struct ValT2<double> {
+    __device__ static double big() { return 1.0e300; }
+};
+template <>
+struct ValT2<int32_t> {
+    __device__ static int32_t big() { return 2147483647; }
+};
+
+template <typename V>
 struct Thr;  // prune threshold from the incumbent: prune iff bound > thr
 template <>
 struct Thr<double> {
@@ -409,6 +420,96 @@ template <typename V>
 __host__ __device__ constexpr size_t v2_lds(int n)
 {
     return v2_wbuf<V>(n) + (size_t)(kSearchThreads / 64) * kChunk * sizeof(SearchItem);
+}
+
+// The last four cities of a path, all in registers: the 4 + 12 + 24 + 24
+// partial paths below the path end k (fold cost ck) are folded in the
+// reference's order ((ck + d[k][a]) + d[a][b]) + d[b][c]) + d[c][e]) + d[e][0]
+// from 20 LDS reads and 88 adds of static code — no stack, no per-node
+// select — and every tour within the incumbent is recorded.  First cities
+// outside fm (already tried) are skipped.  No bound inside: pruning is only an
+// optimisation, so the outcome (records, incumbent) is that of the DFS.
+// Returns the mask of first-city slots evaluated (16 nodes each).
+template <typename V>
+__device__ __forceinline__ uint32_t tail4(const V *dl, const APair<V> *ad, const uint8_t *myk, int T, int krow, V ck,
+                                          uint32_t rem, uint32_t fm, int L, V &inc, V &thr, const SearchArgs &a)
+{
+    int c[4];
+    uint32_t x = rem;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        c[i] = __builtin_ctz(x);
+        x &= x - 1u;
+    }
+    V dk[4], d0[4], dd[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        dk[i] = dl[krow + c[i]];
+        d0[i] = ad[c[i]].d0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            if (j != i) dd[i][j] = dl[c[i] * kRow + c[j]];
+    }
+    uint32_t valid = 0;
+    V tot[24];
+    int e = 0;
+    V best = ValT2<V>::big();
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const bool vi = (fm >> c[i]) & 1u;
+        valid |= vi ? (1u << i) : 0u;
+        const V p1 = ck + dk[i];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            if (j == i) continue;
+            const V p2 = p1 + dd[i][j];
+#pragma unroll
+            for (int l = 0; l < 4; ++l) {
+                if (l == i || l == j) continue;
+                const int m = 6 - i - j - l;
+                const V t = ((p2 + dd[j][l]) + dd[l][m]) + d0[m];
+                tot[e] = vi ? t : ValT2<V>::big();
+                best = tot[e] < best ? tot[e] : best;
+                ++e;
+            }
+        }
+    }
+    if (best <= inc) {
+        // rare: record every tour within the incumbent, in enumeration order
+        e = 0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                if (j == i) continue;
+#pragma unroll
+                for (int l = 0; l < 4; ++l) {
+                    if (l == i || l == j) continue;
+                    const int m = 6 - i - j - l;
+                    const V total = tot[e++];
+                    if (total <= inc) {
+                        const uint64_t tb = Num<V>::bits(total);
+                        const unsigned long long old = atomicMin(a.inc, (unsigned long long)tb);
+                        if (tb <= old) {
+                            const unsigned int s = atomicAdd(a.rec_count, 1u);
+                            if (s < a.rec_cap) {
+                                SearchRecord *R = a.rec + s;
+                                R->cost = tb;
+                                for (int q = 1; q <= L; ++q) R->city[q - 1] = myk[q * T];
+                                R->city[L] = (uint8_t)c[i];
+                                R->city[L + 1] = (uint8_t)c[j];
+                                R->city[L + 2] = (uint8_t)c[l];
+                                R->city[L + 3] = (uint8_t)c[m];
+                            }
+                        }
+                        const V o = Num<V>::val(old);
+                        inc = o < total ? o : total;
+                        thr = Thr<V>::of(inc);
+                    }
+                }
+            }
+    }
+    return valid;
 }
 
 template <typename V>
@@ -465,7 +566,7 @@ __global__ __launch_bounds__(kSearchThreads) void round_kernel(SearchArgs a)
             myc[l * T] = c;
             prev = t;
         }
-        if (!(c + ra > thr)) {
+        if (a.noprune || !(c + ra > thr)) {
             root = len - 1;
             L = root;
             k = prev;
@@ -482,7 +583,17 @@ __global__ __launch_bounds__(kSearchThreads) void round_kernel(SearchArgs a)
         const bool act = L >= root;
         wsteps += 64;
         wactive += (unsigned long long)__popcll(__ballot(act));
-        const uint32_t cand = act ? (rem & fm) : 0u;
+        // Four cities left: the whole subtree in registers (see tail4), then pop.
+        // (Exhaustive mode; with the bound on, the DFS's pruning inside the last
+        // four levels is worth more than the tail's static code: k2_tail_time.log.)
+        const bool tail = a.tails && act && __builtin_popcount(rem) == 4;
+        if (__ballot(tail)) {
+            uint32_t valid = 0;
+            if (tail) valid = tail4<V>(dl, ad, myk, T, krow, ck, rem, fm, L, inc, thr, a);
+            nodes += 16ull * (unsigned long long)(__popcll(__ballot(valid & 1u)) + __popcll(__ballot(valid & 2u)) +
+                                                  __popcll(__ballot(valid & 4u)) + __popcll(__ballot(valid & 8u)));
+        }
+        const uint32_t cand = act && !tail ? (rem & fm) : 0u;
         const bool has = cand != 0u;
         const int j = has ? __builtin_ctz(cand) : 0;
         const uint32_t others = rem & ~(1u << j);
@@ -519,7 +630,7 @@ __global__ __launch_bounds__(kSearchThreads) void round_kernel(SearchArgs a)
             inc = o < total ? o : total;
             thr = Thr<V>::of(inc);
         }
-        const bool desc = has && !close && !(c + rest > thr);
+        const bool desc = has && !close && (a.noprune || !(c + rest > thr));
         const bool pop = act && !has;
         myc[(L + 1) * T] = c;  // dead unless desc (L + 1 <= n - 2)
         myk[(L + 1) * T] = (uint8_t)j;

@@ -69,6 +69,7 @@ struct tspgpu_search {
     int32_t hungry = 0;
     uint32_t min_split = 64;
     double wall_s = 300.0;
+    int noprune = 0;             // exhaustive enumeration (tspgpu_search_enumerate)
     int rounds = 0;
     double ms = 0.0;             // device time of all seed/round launches
     hipEvent_t e0 = nullptr, e1 = nullptr;
@@ -387,7 +388,10 @@ static SearchArgs args_of(tspgpu_search *s)
     a.nshards = s->nshards;
     a.budget = s->budget;
     a.refill = s->refill;
-    a.kernel = s->kernel == 1 ? 1 : 2;  // the round kernels
+    a.kernel = s->kernel == 1 && !s->noprune ? 1 : 2;  // the round kernels (2 for enumeration)
+    a.noprune = s->noprune;
+    a.tails = s->noprune;  // TSPGPU_SEARCH_TAILS=0/1 overrides
+    if (const char *e = std::getenv("TSPGPU_SEARCH_TAILS")) a.tails = std::atoi(e) != 0;
     a.queue = reinterpret_cast<unsigned int *>(s->d_words);
     a.inc = s->d_words + 1;
     a.nodes = s->d_words + 2;
@@ -549,7 +553,7 @@ static int run_persist(tspgpu_search *s)
 int tspgpu_search_run_all(tspgpu_search *s)
 {
     if (!s) return -EINVAL;
-    if (s->kernel == 3) return run_persist(s);
+    if (s->kernel == 3 && !s->noprune) return run_persist(s);
     int rc = tspgpu_search_start(s);
     uint64_t pending = 1;
     while (!rc && pending) rc = tspgpu_search_step(s, &pending);
@@ -654,13 +658,14 @@ int tspgpu_select_tour(const void *dist, int dtype, int n, const tspgpu_tour_rec
                        tour_out);
 }
 
-int tspgpu_search_solve(tspgpu_ctx *c, const void *dist, int dtype, int n, double *cost_out, int32_t *tour_out,
-                        tspgpu_search_stats *stats)
+static int search_solve(tspgpu_ctx *c, const void *dist, int dtype, int n, double *cost_out, int32_t *tour_out,
+                        tspgpu_search_stats *stats, int noprune)
 {
     if (!c || !cost_out || !tour_out) return -EINVAL;
     tspgpu_search *s = nullptr;
     int rc = tspgpu_search_create(c, dist, dtype, n, 0, 1, 0, &s);
     if (rc) return rc;
+    s->noprune = noprune;
     if (const char *e = std::getenv("TSPGPU_SEARCH_RECORD_CAP")) {  // tests: force the second phase
         const long v = std::atol(e);
         if (v > 0) s->rec_cap = (unsigned int)std::min<long>(v, s->rec_cap);
@@ -733,6 +738,18 @@ int tspgpu_search_solve(tspgpu_ctx *c, const void *dist, int dtype, int n, doubl
     }
     tspgpu_search_destroy(s);
     return rc;
+}
+
+int tspgpu_search_solve(tspgpu_ctx *c, const void *dist, int dtype, int n, double *cost_out, int32_t *tour_out,
+                        tspgpu_search_stats *stats)
+{
+    return search_solve(c, dist, dtype, n, cost_out, tour_out, stats, 0);
+}
+
+int tspgpu_search_enumerate(tspgpu_ctx *c, const void *dist, int dtype, int n, double *cost_out, int32_t *tour_out,
+                            tspgpu_search_stats *stats)
+{
+    return search_solve(c, dist, dtype, n, cost_out, tour_out, stats, 1);
 }
 
 }  // extern "C"

@@ -26,7 +26,7 @@ EXPORTED_SYMBOLS = (
     "tspgpu_memcpy_dtoh", "tspgpu_stream", "tspgpu_synchronize", "tspgpu_timer_start", "tspgpu_timer_stop",
     "tspgpu_device_info",
     # K2
-    "tspgpu_search_solve", "tspgpu_search_create", "tspgpu_search_destroy", "tspgpu_search_info",
+    "tspgpu_search_solve", "tspgpu_search_enumerate", "tspgpu_search_create", "tspgpu_search_destroy", "tspgpu_search_info",
     "tspgpu_search_set_bound", "tspgpu_search_start", "tspgpu_search_step", "tspgpu_search_run_all",
     "tspgpu_search_timing", "tspgpu_search_incumbent_device",
     "tspgpu_search_counters", "tspgpu_search_reset_records", "tspgpu_search_records", "tspgpu_heuristic_tour",
@@ -118,6 +118,7 @@ def lib():
         L.tspgpu_device_info.argtypes = [vp, ctypes.POINTER(ctypes.c_int), ctypes.c_char_p, ctypes.c_int]
         u64p = ctypes.POINTER(ctypes.c_uint64)
         L.tspgpu_search_solve.argtypes = [vp, vp, ctypes.c_int, ctypes.c_int, dp, ip, ctypes.POINTER(SearchStats)]
+        L.tspgpu_search_enumerate.argtypes = [vp, vp, ctypes.c_int, ctypes.c_int, dp, ip, ctypes.POINTER(SearchStats)]
         L.tspgpu_search_create.argtypes = [vp, vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                            ctypes.c_int, ctypes.POINTER(vp)]
         L.tspgpu_search_destroy.argtypes = [vp]
@@ -486,16 +487,18 @@ class Search:
         return list(arr[:cnt.value])
 
 
-def search_solve(ctx: "Context", dist):
-    """One instance on one GPU: (cost, tour (n+1,), stats dict)."""
+def search_solve(ctx: "Context", dist, exhaustive: bool = False):
+    """One instance on one GPU: (cost, tour (n+1,), stats dict).  exhaustive:
+    enumerate every tour (no bound; tspgpu_search_enumerate)."""
     d, dt = _search_dist(dist)
     n = d.shape[0]
     cost = ctypes.c_double()
     tour = np.zeros(n + 1, dtype=np.int32)
     st = SearchStats()
-    rc = lib().tspgpu_search_solve(ctx.handle, d.ctypes.data, dt, n, ctypes.byref(cost), _ip(tour), ctypes.byref(st))
+    fn = lib().tspgpu_search_enumerate if exhaustive else lib().tspgpu_search_solve
+    rc = fn(ctx.handle, d.ctypes.data, dt, n, ctypes.byref(cost), _ip(tour), ctypes.byref(st))
     if rc:
-        raise TspGpuError(rc, "tspgpu_search_solve")
+        raise TspGpuError(rc, "tspgpu_search_enumerate" if exhaustive else "tspgpu_search_solve")
     c = cost.value if dt == F64 else int(cost.value)
     return c, tour, st.as_dict()
 
