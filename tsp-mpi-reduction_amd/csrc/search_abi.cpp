@@ -666,6 +666,9 @@ static int search_solve(tspgpu_ctx *c, const void *dist, int dtype, int n, doubl
     int rc = tspgpu_search_create(c, dist, dtype, n, 0, 1, 0, &s);
     if (rc) return rc;
     s->noprune = noprune;
+    // enumeration work is uniform and every lane reaches the register tails:
+    // long budgets (fewer, fuller rounds) win (profiles/r01/k2_exhaustive_budget.log)
+    if (noprune && !std::getenv("TSPGPU_SEARCH_BUDGET")) s->budget = 16384;
     if (const char *e = std::getenv("TSPGPU_SEARCH_RECORD_CAP")) {  // tests: force the second phase
         const long v = std::atol(e);
         if (v > 0) s->rec_cap = (unsigned int)std::min<long>(v, s->rec_cap);
