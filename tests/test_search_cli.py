@@ -112,3 +112,14 @@ def test_rccl_path_with_one_gpu():
     rc2, out2, err2 = run("--random", 23, "--seed", 4, "--solver", "k2")
     assert rc2 == 0, err2
     assert parse(out) == parse(out2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("args", [("--random", 11, "--seed", 5), ("--random", 12, "--clustered", 3, "--seed", 2)])
+def test_enum_solver_matches_k1(args):
+    """--solver enum: every (n-1)! tour enumerated on GPU 0 (config 2's
+    exhaustive mode); same cost and tie-broken tour as K1 (--verify)."""
+    rc, out, err = run(*args, "--solver", "enum", "--verify")
+    assert rc == 0, err
+    assert "K1 check: identical cost and tour" in out
+    assert "search nodes" in out

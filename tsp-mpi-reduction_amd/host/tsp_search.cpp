@@ -8,7 +8,8 @@
 //                                                         file with NODE_COORD_SECTION
 //   tsp_search --matrix FILE                              n, then n*n distances (all
 //                                                         integers -> integer mode)
-//   options: --gpus G (devices 0..G-1)  --solver auto|wide|k1|k2  --verify (n <= 20: K1 too)
+//   options: --gpus G (devices 0..G-1)  --solver auto|wide|k1|k2|enum  --verify (n <= 20: K1 too)
+//   (enum: every tour enumerated on one GPU, BASELINE config 2)
 //   auto = K1-wide (the DP with every CU on each layer) up to 31 cities on one
 //   GPU, else K2 over the GPUs.
 //
@@ -284,6 +285,24 @@ int solve_wide(const Instance &in, Result &res)
     return rc;
 }
 
+// exhaustive enumeration of all (n-1)! tours on GPU 0 (K2 with the bound off)
+int solve_enum(const Instance &in, Result &res)
+{
+    tspgpu_opts o;
+    std::memset(&o, 0, sizeof o);
+    tspgpu_ctx *ctx = nullptr;
+    int rc = tspgpu_ctx_create(&o, &ctx);
+    res.tour.assign(in.n + 1, -1);
+    tspgpu_search_stats st;
+    std::memset(&st, 0, sizeof st);
+    if (!rc) rc = tspgpu_search_enumerate(ctx, dist_ptr(in), in.dtype, in.n, &res.cost, res.tour.data(), &st);
+    res.nodes = st.nodes;
+    res.kernel_ms = st.kernel_ms;
+    res.rounds = st.rounds;
+    if (ctx) tspgpu_ctx_destroy(ctx);
+    return rc;
+}
+
 }  // namespace
 
 int main(int argc, char **argv)
@@ -310,7 +329,7 @@ int main(int argc, char **argv)
         else if (a == "--verify") verify = true;
         else {
             std::fprintf(stderr, "usage: tsp_search (--random N [--seed S] [--clustered K] | --cities FILE "
-                                 "[--tsplib-round] | --matrix FILE) [--gpus G] [--solver auto|wide|k1|k2] [--verify]\n");
+                                 "[--tsplib-round] | --matrix FILE) [--gpus G] [--solver auto|wide|k1|k2|enum] [--verify]\n");
             return 1;
         }
     }
@@ -331,11 +350,15 @@ int main(int argc, char **argv)
     // far fewer operations than branch and bound there — else the search (K2)
     // over all GPUs
     if (solver == "auto") solver = (in.n <= TSPGPU_WIDE_MAX_CITIES && gpus == 1) ? "wide" : "k2";
-    if (solver != "k1" && solver != "k2" && solver != "wide") die("--solver must be auto, wide, k1 or k2");
+    if (solver != "k1" && solver != "k2" && solver != "wide" && solver != "enum")
+        die("--solver must be auto, wide, k1, k2 or enum");
 
     Result res;
     const auto t0 = std::chrono::steady_clock::now();
-    int rc = solver == "k1" ? solve_k1(in, res) : solver == "wide" ? solve_wide(in, res) : search_multi(in, gpus, res);
+    int rc = solver == "k1"     ? solve_k1(in, res)
+             : solver == "wide" ? solve_wide(in, res)
+             : solver == "enum" ? solve_enum(in, res)
+                                : search_multi(in, gpus, res);
     if (rc == -EOVERFLOW && in.n <= TSPGPU_WIDE_MAX_CITIES) {
         // more tied optima than the record buffers hold (e.g. coincident cities):
         // the DP returns the same tour directly
@@ -354,7 +377,7 @@ int main(int argc, char **argv)
     std::printf("tour");
     for (int t : res.tour) std::printf(" %d", t);
     std::printf("\n");
-    if (solver == "k2")
+    if (solver == "k2" || solver == "enum")
         std::printf("search nodes %llu  rounds %d  kernel %.3f ms  %.3f Gnodes/s  wall %.3f ms\n",
                     (unsigned long long)res.nodes, res.rounds, res.kernel_ms,
                     res.kernel_ms > 0 ? res.nodes / res.kernel_ms / 1e6 : 0.0, wall);
