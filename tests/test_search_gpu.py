@@ -236,3 +236,57 @@ def test_exhaustive_14_golden(gpu_ctx):
     assert cost == O.hexf(case["solutions"][0]["cost_hex"]), st
     assert [cities[t][0] for t in tour] == case["solutions"][0]["ids"], st
     assert st["nodes"] > 6.0e9, st
+
+
+def _enum_nodes(n):
+    import math
+    N = n - 1
+    return sum(math.factorial(N) // math.factorial(N - l) for l in range(1, N + 1))
+
+
+@pytest.mark.parametrize("n", [7, 9, 12, 13])
+def test_enum_kernel_against_oracle_and_round_kernels(gpu_ctx, monkeypatch, n):
+    """enum.hip (7 <= n <= 16: a lane per depth-(n-7) prefix, 720 completions
+    in registers) against tsp()'s oracle, on random and tie-heavy lattice
+    cities; the round kernels with the bound off (TSPGPU_ENUM_KERNEL=0) give
+    the same answer; the node count is every partial path exactly."""
+    rng = np.random.default_rng(9100 + n)
+    for lattice in (False, True):
+        xy = rng.integers(0, 4, size=(n, 2)).astype(np.float64) if lattice else rng.uniform(0, 1000, size=(n, 2))
+        d = O.distance_matrix([(i, xy[i, 0], xy[i, 1]) for i in range(n)])
+        cost, tour, st = tspgpu.search_solve(gpu_ctx, d, exhaustive=True)
+        oc, ot = O.solve_block(d)
+        assert (cost, tour.tolist()) == (oc, ot), (n, lattice, st)
+        assert st["nodes"] == _enum_nodes(n) and st["depth"] == n - 7, st
+        if n <= 12:
+            monkeypatch.setenv("TSPGPU_ENUM_KERNEL", "0")
+            c2, t2, st2 = tspgpu.search_solve(gpu_ctx, d, exhaustive=True)
+            monkeypatch.delenv("TSPGPU_ENUM_KERNEL")
+            assert (c2, t2.tolist()) == (oc, ot), (n, lattice, st2)
+
+
+@pytest.mark.parametrize("n", [8, 12])
+def test_enum_kernel_integer_matrix(gpu_ctx, n):
+    """Integer distances (config 1 extension) through the enumeration kernel:
+    exact int32 folds, same optimum and tie-broken tour as the int64 oracle."""
+    rng = np.random.default_rng(77 + n)
+    for hi in (1000, 5):
+        m = rng.integers(1, hi + 1, size=(n, n)).astype(np.int32)
+        m = np.triu(m, 1)
+        m = m + m.T
+        cost, tour, st = tspgpu.search_solve(gpu_ctx, m, exhaustive=True)
+        oc, ot = O.solve_block(m.astype(np.int64))
+        assert (cost, tour.tolist()) == (int(oc), ot), (n, hi, st)
+
+
+def test_enum_kernel_record_overflow_second_phase(gpu_ctx, monkeypatch):
+    """Thousands of tied optima on a 3x3 lattice (n=10) with a 2-record
+    buffer: the enumeration runs a second phase with the optimum as the
+    bound and still returns tsp()'s tour."""
+    xy = [(x, y) for x in range(3) for y in range(3)] + [(1.0, 0.5)]
+    d = O.distance_matrix([(i, float(x), float(y)) for i, (x, y) in enumerate(xy)])
+    monkeypatch.setenv("TSPGPU_SEARCH_RECORD_CAP", "2")
+    cost, tour, st = tspgpu.search_solve(gpu_ctx, d, exhaustive=True)
+    monkeypatch.delenv("TSPGPU_SEARCH_RECORD_CAP")
+    oc, ot = O.solve_block(d)
+    assert (cost, tour.tolist()) == (oc, ot) and st["phases"] == 2, st

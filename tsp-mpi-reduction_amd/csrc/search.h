@@ -84,6 +84,8 @@ struct SearchArgs {
 size_t search_lds_bytes(int n, bool f64, int kernel = 2);
 hipError_t launch_seed(const SearchArgs &a, bool f64, int grid);
 hipError_t launch_round(const SearchArgs &a, bool f64, int grid);
+// exhaustive enumeration (enum.hip), 7 <= n <= 16: a.items = depth-(n-7) prefixes
+hipError_t launch_enum(const SearchArgs &a, bool f64, int grid);
 hipError_t launch_persist(const SearchArgs &a, bool f64, int grid);
 
 }  // namespace tspgpu

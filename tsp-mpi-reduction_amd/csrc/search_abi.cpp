@@ -70,6 +70,7 @@ struct tspgpu_search {
     uint32_t min_split = 64;
     double wall_s = 300.0;
     int noprune = 0;             // exhaustive enumeration (tspgpu_search_enumerate)
+    int enum_kernel = 0;         // enumeration by enum.hip (6-city register tails, 7 <= n <= 16)
     int rounds = 0;
     double ms = 0.0;             // device time of all seed/round launches
     hipEvent_t e0 = nullptr, e1 = nullptr;
@@ -550,9 +551,43 @@ static int run_persist(tspgpu_search *s)
     return 0;
 }
 
+// Exhaustive enumeration in ONE launch (enum.hip): a lane per depth-(N-6)
+// prefix, its 720 completions in registers.  nodes = the prefix levels (host,
+// exact) + 1,956 per lane (device).
+static int run_enum(tspgpu_search *s)
+{
+    (void)hipSetDevice(s->ctx->device);
+    hipStream_t st = s->ctx->stream;
+    const int N = s->n - 1, G = N - 6;
+    unsigned long long upper = 0;
+    for (int l = 1; l <= G; ++l) upper += falling(N, l);
+    SearchArgs a = args_of(s);
+    a.depth = G;
+    a.items = (uint32_t)falling(N, G);
+    const uint64_t blocks = (a.items + kSearchThreads - 1) / kSearchThreads;
+    int per_cu = 8;
+    if (const char *e = std::getenv("TSPGPU_ENUM_WG_PER_CU")) per_cu = std::max(1, std::atoi(e));
+    const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>(blocks, (uint64_t)s->ctx->cu_count * per_cu));
+    hipError_t e = hipMemcpyAsync(s->d_words + 2, &upper, 8, hipMemcpyHostToDevice, st);
+    if (e != hipSuccess) return herr(e);
+    (void)hipEventRecord(s->e0, st);
+    e = launch_enum(a, s->dtype == TSPGPU_F64, grid);
+    (void)hipEventRecord(s->e1, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (e != hipSuccess) return herr(e);
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, s->e0, s->e1) == hipSuccess) s->ms += ms;
+    s->depth = G;
+    s->items = a.items;
+    s->pending = 0;
+    ++s->rounds;
+    return 0;
+}
+
 int tspgpu_search_run_all(tspgpu_search *s)
 {
     if (!s) return -EINVAL;
+    if (s->noprune && s->enum_kernel) return run_enum(s);
     if (s->kernel == 3 && !s->noprune) return run_persist(s);
     int rc = tspgpu_search_start(s);
     uint64_t pending = 1;
@@ -669,6 +704,10 @@ static int search_solve(tspgpu_ctx *c, const void *dist, int dtype, int n, doubl
     // enumeration work is uniform and every lane reaches the register tails:
     // long budgets (fewer, fuller rounds) win (profiles/r01/k2_exhaustive_budget.log)
     if (noprune && !std::getenv("TSPGPU_SEARCH_BUDGET")) s->budget = 16384;
+    // 7 <= n <= 16, one shard: the register-tail enumeration kernel (enum.hip);
+    // TSPGPU_ENUM_KERNEL=0 keeps the round kernels (tests compare both)
+    const char *ek = std::getenv("TSPGPU_ENUM_KERNEL");
+    s->enum_kernel = noprune && n >= 7 && n <= 16 && !(ek && std::atoi(ek) == 0);
     if (const char *e = std::getenv("TSPGPU_SEARCH_RECORD_CAP")) {  // tests: force the second phase
         const long v = std::atol(e);
         if (v > 0) s->rec_cap = (unsigned int)std::min<long>(v, s->rec_cap);
