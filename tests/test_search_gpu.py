@@ -144,6 +144,49 @@ def test_search_kernels_and_hand_off_stress(gpu_ctx, monkeypatch, mode):
             assert (cost, tour.tolist()) == (oc, ot), (mode, n, kind, st)
 
 
+@pytest.mark.parametrize("mode", [("0", None, None), ("5", None, None), ("6", None, None), ("6", "8", "2"),
+                                  ("5", "8", "1"), ("6", None, "2")])
+def test_frontier_search_modes(gpu_ctx, monkeypatch, mode):
+    """Frontier search (expand_kernel level by level, then the prefixes with
+    5/6 cities left folded by tail_kernel) against the DFS rounds ("0"):
+    default seed depth, shallow seeds (depth 1-2: many expansion levels) and
+    a 256-slot tail buffer (a flush every few expansions, many small steps).
+    Same cost and tour as the oracle on tie-heavy, random and integer
+    instances, n = 8..14."""
+    tail, cap, depth = mode
+    monkeypatch.setenv("TSPGPU_SEARCH_TAIL", tail)
+    if cap is not None:
+        monkeypatch.setenv("TSPGPU_SEARCH_TAIL_CAP_LOG2", cap)
+    if depth is not None:
+        monkeypatch.setenv("TSPGPU_SEARCH_DEPTH", depth)
+    rng = np.random.default_rng(17 + int(tail) + (0 if cap is None else 7) + (0 if depth is None else 3))
+    for n in (8, 9, 11, 13, 14):
+        for kind in ("ties", "random", "int"):
+            if kind == "ties":
+                xy = rng.integers(0, 5, size=(n, 2)).astype(np.float64)
+            else:
+                xy = rng.uniform(0, 1000, size=(n, 2))
+            d = O.distance_matrix([(i, xy[i, 0], xy[i, 1]) for i in range(n)])
+            if kind == "int":
+                d = np.rint(d).astype(np.int32)
+            cost, tour, st = tspgpu.search_solve(gpu_ctx, d)
+            oc, ot = O.solve_block(d.astype(np.float64))
+            assert (float(cost), tour.tolist()) == (oc, ot), (mode, n, kind, st)
+
+
+def test_frontier_16_golden(gpu_ctx, monkeypatch):
+    """The reference's own 16-city instance through the frontier search with
+    5- and 6-city register tails: golden cost bits and tour."""
+    case = next(c for c in O.load_golden("seed0_blocks.json") if c["n"] == 16 and c["B"] == 1 and c["X"] == 1000)
+    blk = _cities(case["cities"][0])
+    d = tspgpu.distance_matrix([blk])[0]
+    for tail in ("5", "6"):
+        monkeypatch.setenv("TSPGPU_SEARCH_TAIL", tail)
+        cost, tour, st = tspgpu.search_solve(gpu_ctx, d)
+        assert cost == O.hexf(case["solutions"][0]["cost_hex"]), st
+        assert [blk[t][0] for t in tour] == case["solutions"][0]["ids"], st
+
+
 @pytest.mark.parametrize("nshards", [2, 3, 5])
 def test_sharded_on_one_gpu(gpu_ctx, nshards):
     """The multi-GPU decomposition, run shard by shard on one device: min of

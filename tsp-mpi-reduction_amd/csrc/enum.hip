@@ -62,10 +62,10 @@ __device__ __forceinline__ void static_for(F &&f, std::integer_sequence<int, I..
 }
 
 // All completions of the path ending at tail city LAST (cost p) through the
-// tail cities in LEFT (bit mask over 0..5), then back to city 0.  The
+// tail cities in LEFT (bit mask over 0..TL-1), then back to city 0.  The
 // recursion is resolved at compile time: straight-line adds and mins.
-template <typename V, int LEFT, int LAST>
-__device__ __forceinline__ void complete(const V (&s)[kTail][kTail], const V (&d0)[kTail], V p, V &best)
+template <typename V, int TL, int LEFT, int LAST>
+__device__ __forceinline__ void complete(const V (&s)[TL][TL], const V (&d0)[TL], V p, V &best)
 {
     if constexpr ((LEFT & (LEFT - 1)) == 0) {
         constexpr int r = __builtin_ctz(LEFT);
@@ -74,9 +74,9 @@ __device__ __forceinline__ void complete(const V (&s)[kTail][kTail], const V (&d
         static_for(
             [&](auto q) {
                 constexpr int Q = decltype(q)::value;
-                if constexpr ((LEFT >> Q) & 1) complete<V, (LEFT & ~(1 << Q)), Q>(s, d0, p + s[LAST][Q], best);
+                if constexpr ((LEFT >> Q) & 1) complete<V, TL, (LEFT & ~(1 << Q)), Q>(s, d0, p + s[LAST][Q], best);
             },
-            std::make_integer_sequence<int, kTail>{});
+            std::make_integer_sequence<int, TL>{});
     }
 }
 
@@ -139,7 +139,7 @@ __global__ __launch_bounds__(256) void enum_kernel(SearchArgs a)
         static_for(
             [&](auto i) {
                 constexpr int I = decltype(i)::value;
-                complete<V, (((1 << kTail) - 1) & ~(1 << I)), I>(s, d0, cp + dk[I], best);
+                complete<V, kTail, (((1 << kTail) - 1) & ~(1 << I)), I>(s, d0, cp + dk[I], best);
             },
             std::make_integer_sequence<int, kTail>{});
         V inc = ENum<V>::val(__hip_atomic_load(a.inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
@@ -215,11 +215,340 @@ hipError_t launch_v(const SearchArgs &a, int grid)
     }
 }
 
+// ---------------------------------------------------------------------------
+// Register tails of the frontier search: every prefix in a.tail_out (written
+// by expand_kernel) has exactly TL cities left; a lane refolds
+// the prefix (the same left fold, from LDS), tests it against the current
+// incumbent with the search's bound (cheapest incoming edge of every city
+// still to be entered, 2^-20 grid values, exact sums), and folds all TL!
+// completions with the straight-line code above.  Tours within the incumbent
+// are recorded exactly like the DFS records them, so the optimal set — and
+// the tie rule's answer — is unchanged; pruning inside the tail is dropped
+// because a DFS step costs ~1000x a register add.
+constexpr int kTRow = 32;  // LDS row stride (n <= 32)
+
+template <typename V>
+struct EThr;  // prune iff bound > thr (the round kernel's margin)
+template <>
+struct EThr<double> {
+    __device__ static double of(double inc) { return inc * (1.0 + 0x1p-39); }
+};
+template <>
+struct EThr<int32_t> {
+    __device__ static int32_t of(int32_t inc) { return inc; }
+};
+
+__host__ __device__ constexpr unsigned long long tail_nodes(int tl)
+{
+    unsigned long long sum = 0, f = 1;
+    for (int l = 1; l <= tl; ++l) {
+        f *= (unsigned long long)(tl - l + 1);
+        sum += f;
+    }
+    return sum;
+}
+
+// One handed-over prefix (slot idx of a.tail_out): refold, bound test, all
+// TL! completions; `act` false = a lane with nothing to do (wave-uniform code).
+template <typename V, int TL>
+__device__ __forceinline__ void tail_one(const SearchArgs &a, const V *dl, const V *am, uint32_t full, uint32_t idx,
+                                         bool act, unsigned long long &lanes)
+{
+    const uint32_t *src = reinterpret_cast<const uint32_t *>(a.tail_out + idx);
+    const int len = act ? (int)(src[8] & 255u) : 1;
+    // ---- the prefix 0, t1..t(len-1): the reference's left fold
+    V cp = 0;
+    int prev = 0;
+    uint32_t mem = 0, word = 0;
+    for (int l = 1; l < len; ++l) {
+        if ((l & 3) == 0 || l == 1) word = src[l >> 2];
+        const int c = (int)((word >> (8 * (l & 3))) & 255u);
+        cp = cp + dl[prev * kTRow + c];
+        mem |= 1u << c;
+        prev = c;
+    }
+    const uint32_t rest = full & ~mem;  // the TL cities left
+    int t[TL];
+    uint32_t tpack = 0;  // t[i] in bits 5i..5i+4 (record path)
+    V ra = am[0];
+    uint32_t x = rest;
+#pragma unroll
+    for (int i = 0; i < TL; ++i) {
+        t[i] = x ? __builtin_ctz(x) : 0;
+        x &= x - 1u;
+        ra += am[t[i]];
+        tpack |= (uint32_t)t[i] << (5 * i);
+    }
+    V inc = ENum<V>::val(__hip_atomic_load(a.inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    if (!a.noprune && cp + ra > EThr<V>::of(inc)) act = false;
+    const unsigned long long am_ = __ballot(act);
+    if (am_ == 0) return;
+    lanes += (unsigned long long)__popcll(am_);
+    V s[TL][TL], d0[TL], dk[TL];
+#pragma unroll
+    for (int i = 0; i < TL; ++i) {
+        dk[i] = dl[prev * kTRow + t[i]];
+        d0[i] = dl[t[i] * kTRow];
+#pragma unroll
+        for (int j = 0; j < TL; ++j)
+            if (j != i) s[i][j] = dl[t[i] * kTRow + t[j]];
+    }
+    // per first tail city g the best of its (TL-1)! completions
+    V bg[TL];
+    static_for(
+        [&](auto i) {
+            constexpr int I = decltype(i)::value;
+            bg[I] = ENum<V>::big();
+            complete<V, TL, (((1 << TL) - 1) & ~(1 << I)), I>(s, d0, cp + dk[I], bg[I]);
+        },
+        std::make_integer_sequence<int, TL>{});
+    V best = bg[0];
+#pragma unroll
+    for (int i = 1; i < TL; ++i) best = ENum<V>::vmin(best, bg[i]);
+    if (!(act && best <= inc)) return;
+    // rare: record every tour within the incumbent (same fold, enumeration
+    // order), only in the first-city groups whose best is within it
+    constexpr int kGroup = TL == 6 ? 120 : 24;  // (TL-1)!
+#pragma unroll 1
+    for (int g = 0; g < TL; ++g) {
+        V bgg = bg[0];
+#pragma unroll
+        for (int i = 1; i < TL; ++i) bgg = g == i ? bg[i] : bgg;
+        if (!(bgg <= inc)) continue;
+#pragma unroll 1
+        for (int p = g * kGroup; p < (g + 1) * kGroup; ++p) {
+            uint32_t lst = 0;  // indices 0..TL-1 not used yet, one per nibble
+#pragma unroll
+            for (int i = 0; i < TL; ++i) lst |= (uint32_t)i << (4 * i);
+            int ord[TL];
+            int q = p;
+#pragma unroll
+            for (int l = 0; l < TL; ++l) {
+                const int r = TL - l;
+                int fact = 1;  // (r-1)!: the l-th city is digit q / (r-1)! of the r left
+                for (int z = 2; z < r; ++z) fact *= z;
+                const int dgt = q / fact;
+                q -= dgt * fact;
+                const int sh = 4 * dgt;
+                const int ix = (int)((lst >> sh) & 15u);
+                lst = (lst & ((1u << sh) - 1u)) | ((lst >> (sh + 4)) << sh);
+                ord[l] = (int)((tpack >> (5 * ix)) & 31u);
+            }
+            V c = cp;
+            int k = prev;
+#pragma unroll
+            for (int l = 0; l < TL; ++l) {
+                c = c + dl[k * kTRow + ord[l]];
+                k = ord[l];
+            }
+            const V total = c + dl[k * kTRow];
+            if (total <= inc) {
+                const uint64_t tb = ENum<V>::bits(total);
+                const unsigned long long old = atomicMin(a.inc, (unsigned long long)tb);
+                if (tb <= old) {
+                    const unsigned int slot = atomicAdd(a.rec_count, 1u);
+                    if (slot < a.rec_cap) {
+                        SearchRecord *R = a.rec + slot;
+                        R->cost = tb;
+                        uint32_t wd = 0;
+                        for (int l = 1; l < len; ++l) {
+                            if ((l & 3) == 0 || l == 1) wd = src[l >> 2];
+                            R->city[l - 1] = (uint8_t)((wd >> (8 * (l & 3))) & 255u);
+                        }
+#pragma unroll
+                        for (int l = 0; l < TL; ++l) R->city[len - 1 + l] = (uint8_t)ord[l];
+                    }
+                }
+                const V o = ENum<V>::val(old);
+                inc = o < total ? o : total;
+            }
+        }
+    }
+}
+
+// Every wave reads 64 slots at a time, queues the non-empty ones (len > 0) in
+// LDS and folds them 64 at a time, so a producer may leave holes without
+// idling lanes here.
+template <typename V, int TL>
+__global__ __launch_bounds__(256) void tail_kernel(SearchArgs a)
+{
+    __shared__ V dl[kSearchMaxN * kTRow];
+    __shared__ V am[kSearchMaxN];
+    __shared__ uint32_t wq[4][128];
+    const int n = a.n;
+    const V *gd = static_cast<const V *>(a.dist);
+    const V *ga = static_cast<const V *>(a.amin);
+    for (int i = threadIdx.x; i < n * n; i += blockDim.x) dl[(i / n) * kTRow + i % n] = gd[i];
+    for (int i = threadIdx.x; i < n; i += blockDim.x) am[i] = ga[i];
+    __syncthreads();
+
+    const unsigned int claimed = __hip_atomic_load(a.tail_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t count = claimed < a.tail_cap ? claimed : a.tail_cap;
+    const uint32_t full = (uint32_t)((1ull << n) - 1ull) & ~1u;
+    const int lane = __lane_id();
+    uint32_t *q = wq[threadIdx.x >> 6];
+    uint32_t qn = 0;               // wave-uniform: live slots queued
+    unsigned long long lanes = 0;  // wave-uniform
+    const uint32_t wave = blockIdx.x * 4 + (threadIdx.x >> 6), waves = gridDim.x * 4;
+    for (uint32_t base = wave * 64u;; base += waves * 64u) {
+        const bool more = base < count;
+        if (more) {
+            const uint32_t idx = base + lane;
+            const bool live = idx < count && (reinterpret_cast<const uint32_t *>(a.tail_out + idx)[8] & 255u) != 0;
+            const unsigned long long m = __ballot(live);
+            if (live) q[qn + __popcll(m & ((1ull << lane) - 1ull))] = idx;
+            qn += (uint32_t)__popcll(m);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
+        while (qn >= 64u || (!more && qn > 0u)) {
+            const uint32_t take = qn < 64u ? qn : 64u;
+            const bool act = (uint32_t)lane < take;
+            const uint32_t idx = act ? q[qn - take + lane] : 0u;
+            __builtin_amdgcn_wave_barrier();
+            qn -= take;
+            tail_one<V, TL>(a, dl, am, full, idx, act, lanes);
+        }
+        if (!more) break;
+    }
+    if (lane == 0) atomicAdd(a.nodes, lanes * tail_nodes(TL));
+}
+
+// Frontier expansion, one level: a lane per item of a.in (the path 0,
+// t1..t(len-1), refolded from LDS); every child j (ascending) whose bound
+// passes becomes an item of a.tail_out when it has tail_level inner cities,
+// else of a.out.  Block-level stream compaction: one global atomic per block
+// and output (per-wave atomics on one counter serialise the grid).  The host
+// sizes both outputs for (N - depth) children per input item.
+template <typename V>
+__global__ __launch_bounds__(256) void expand_kernel(SearchArgs a)
+{
+    __shared__ V dl[kSearchMaxN * kTRow];
+    __shared__ V am[kSearchMaxN];
+    __shared__ uint32_t wtot[3][4];
+    __shared__ uint32_t bbase[2];
+    const int n = a.n;
+    const V *gd = static_cast<const V *>(a.dist);
+    const V *ga = static_cast<const V *>(a.amin);
+    for (int i = threadIdx.x; i < n * n; i += blockDim.x) dl[(i / n) * kTRow + i % n] = gd[i];
+    for (int i = threadIdx.x; i < n; i += blockDim.x) am[i] = ga[i];
+    __syncthreads();
+
+    const uint32_t idx = blockIdx.x * 256u + threadIdx.x;
+    const bool act = idx < a.in_count;
+    const uint32_t *src = reinterpret_cast<const uint32_t *>(a.in + (act ? idx : 0u));
+    const int len = act ? (int)(src[8] & 255u) : 0;
+    uint32_t w[8];
+#pragma unroll
+    for (int b = 0; b < 8; ++b) w[b] = 4 * b < len ? src[b] : 0u;
+    // ---- the path: the reference's left fold
+    V c = 0;
+    int k = 0;
+    uint32_t mem = 0;
+#pragma unroll
+    for (int b = 0; b < 8; ++b)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int lv = 4 * b + q;
+            if (lv >= 1 && lv < len) {
+                const int t = (int)((w[b] >> (8 * q)) & 255u);
+                c = c + dl[k * kTRow + t];
+                mem |= 1u << t;
+                k = t;
+            }
+        }
+    const uint32_t full = (uint32_t)((1ull << n) - 1ull) & ~1u;
+    const uint32_t rem = act ? (full & ~mem) : 0u;
+    V remA = am[0];  // every city still to be entered: its cheapest incoming edge (exact sums)
+    for (uint32_t x = rem; x; x &= x - 1u) remA += am[__builtin_ctz(x)];
+    const V inc = ENum<V>::val(__hip_atomic_load(a.inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    const V thr = EThr<V>::of(inc);
+    uint32_t live = 0;
+    for (uint32_t x = rem; x; x &= x - 1u) {
+        const int j = __builtin_ctz(x);
+        const V cj = c + dl[k * kTRow + j];
+        if (a.noprune || !(cj + (remA - am[j]) > thr)) live |= 1u << j;
+    }
+    // ---- block-level compaction: wave scans, one atomic per block and output
+    const bool tail = len == a.tail_level;  // children have len inner cities
+    const uint32_t cnt = (uint32_t)__builtin_popcount(live);
+    uint32_t v[3] = {tail ? cnt : 0u, tail ? 0u : cnt, (uint32_t)__builtin_popcount(rem)};
+    const int lane = __lane_id(), wv = threadIdx.x >> 6;
+    uint32_t incl[3] = {v[0], v[1], v[2]};
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1)
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            const uint32_t y = __shfl_up(incl[i], off);
+            if (lane >= off) incl[i] += y;
+        }
+    if (lane == 63)
+        for (int i = 0; i < 3; ++i) wtot[i][wv] = incl[i];
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const uint32_t tt = wtot[0][0] + wtot[0][1] + wtot[0][2] + wtot[0][3];
+        const uint32_t tf = wtot[1][0] + wtot[1][1] + wtot[1][2] + wtot[1][3];
+        const uint32_t tn = wtot[2][0] + wtot[2][1] + wtot[2][2] + wtot[2][3];
+        bbase[0] = tt ? atomicAdd(a.tail_count, tt) : 0u;
+        bbase[1] = tf ? atomicAdd(a.out_count, tf) : 0u;
+        if (tn) atomicAdd(a.nodes, (unsigned long long)tn);
+    }
+    __syncthreads();
+    uint32_t wofs[2] = {0u, 0u};
+    for (int u = 0; u < wv; ++u) {
+        wofs[0] += wtot[0][u];
+        wofs[1] += wtot[1][u];
+    }
+    uint32_t slot = tail ? bbase[0] + wofs[0] + incl[0] - v[0] : bbase[1] + wofs[1] + incl[1] - v[1];
+    SearchItem *dstb = tail ? a.tail_out : a.out;
+    // ---- children, ascending: parent path + j
+    const int cb = len >> 2, cs = 8 * (len & 3);
+    for (uint32_t x = live; x; x &= x - 1u, ++slot) {
+        const uint32_t j = (uint32_t)__builtin_ctz(x);
+        uint32_t *dst = reinterpret_cast<uint32_t *>(dstb + slot);
+#pragma unroll
+        for (int b = 0; b < 8; ++b) {
+            const uint32_t word = b == cb ? ((w[b] & ~(255u << cs)) | (j << cs)) : w[b];
+            if (4 * b <= len) dst[b] = word;
+        }
+        dst[8] = (uint32_t)(len + 1) | (1u << 8);
+    }
+}
+
+template <typename V>
+hipError_t launch_tail_v(const SearchArgs &a, int grid)
+{
+    if (a.n > kSearchMaxN || a.tail_level < 1 || a.tail_level + a.tail_len != a.n - 1) return hipErrorInvalidValue;
+    switch (a.tail_len) {
+    case 5: hipLaunchKernelGGL((tail_kernel<V, 5>), dim3(grid), dim3(256), 0, a.stream, a); break;
+    case 6: hipLaunchKernelGGL((tail_kernel<V, 6>), dim3(grid), dim3(256), 0, a.stream, a); break;
+    default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
 }  // namespace
 
 hipError_t launch_enum(const SearchArgs &a, bool f64, int grid)
 {
     return f64 ? launch_v<double>(a, grid) : launch_v<int32_t>(a, grid);
+}
+
+hipError_t launch_expand(const SearchArgs &a, bool f64)
+{
+    if (a.n > kSearchMaxN || a.in_count == 0) return a.in_count ? hipErrorInvalidValue : hipSuccess;
+    const int grid = (int)((a.in_count + 255u) / 256u);
+    if (f64)
+        hipLaunchKernelGGL(expand_kernel<double>, dim3(grid), dim3(256), 0, a.stream, a);
+    else
+        hipLaunchKernelGGL(expand_kernel<int32_t>, dim3(grid), dim3(256), 0, a.stream, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_tail(const SearchArgs &a, bool f64, int grid)
+{
+    return f64 ? launch_tail_v<double>(a, grid) : launch_tail_v<int32_t>(a, grid);
 }
 
 }  // namespace tspgpu

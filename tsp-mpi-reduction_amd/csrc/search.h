@@ -78,6 +78,14 @@ struct SearchArgs {
     int kernel;                // round kernel: 2 (lock-step DFS, default) or 1 (branching DFS); 3 = persistent
     int noprune;               // exhaustive enumeration: no bound test (kernels 2 and seed only)
     int tails;                 // kernel 2: last four cities enumerated in registers (tail4)
+    // frontier search (expand_kernel + tail_kernel): items are expanded one
+    // level at a time; children with tail_level inner cities (tail_len =
+    // N - tail_level cities left) go to tail_out, the others to out.
+    int tail_level;
+    int tail_len;              // 5 or 6
+    SearchItem *tail_out;
+    unsigned int *tail_count;  // items in tail_out (tail_kernel reads it on the device)
+    unsigned int tail_cap;
     hipStream_t stream;
 };
 
@@ -86,6 +94,10 @@ hipError_t launch_seed(const SearchArgs &a, bool f64, int grid);
 hipError_t launch_round(const SearchArgs &a, bool f64, int grid);
 // exhaustive enumeration (enum.hip), 7 <= n <= 16: a.items = depth-(n-7) prefixes
 hipError_t launch_enum(const SearchArgs &a, bool f64, int grid);
+// frontier search (enum.hip): one level of a.in -> a.out / a.tail_out, and
+// the register tails of a.tail_out (a.tail_len in {5, 6})
+hipError_t launch_expand(const SearchArgs &a, bool f64);
+hipError_t launch_tail(const SearchArgs &a, bool f64, int grid);
 hipError_t launch_persist(const SearchArgs &a, bool f64, int grid);
 
 }  // namespace tspgpu

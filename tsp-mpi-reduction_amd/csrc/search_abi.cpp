@@ -35,6 +35,7 @@
 using namespace tspgpu;
 
 static_assert(sizeof(SearchRecord) == sizeof(tspgpu_tour_record), "record layout");
+constexpr int kWords = 16;  // device counter words of a search (see tspgpu_search::d_words)
 
 struct tspgpu_search {
     tspgpu_ctx *ctx = nullptr;
@@ -48,7 +49,8 @@ struct tspgpu_search {
     std::vector<double> hd;    // host copy (f64 view) for the selection
     std::vector<int32_t> hi;
     void *d_dist = nullptr, *d_amin = nullptr;
-    // [0] queue (u32), [1] incumbent, [2] nodes, [3] record count (u32), [4] items out (u32)
+    // [0] queue (u32), [1] incumbent, [2] nodes, [3] record count (u32), [4] items out (u32),
+    // [5..7] utilisation counters, [8] tail items (u32)
     unsigned long long *d_words = nullptr;
     SearchRecord *d_rec = nullptr;
     unsigned int rec_cap = 0;
@@ -71,6 +73,18 @@ struct tspgpu_search {
     double wall_s = 300.0;
     int noprune = 0;             // exhaustive enumeration (tspgpu_search_enumerate)
     int enum_kernel = 0;         // enumeration by enum.hip (6-city register tails, 7 <= n <= 16)
+    // Frontier search (default for the bounded search when n - 1 - tail_len >
+    // the seed depth; TSPGPU_SEARCH_TAIL = 0 selects the DFS rounds, 5 or 6 the
+    // tail length): each step expands up to kExpandMax items of the frontier
+    // (LIFO) by one level with the bound; prefixes with tail_len cities left
+    // collect in d_tail and are folded by tail_kernel, all tail_len!
+    // completions in registers, once tail_cap / 2 of them wait or the
+    // frontier is empty.
+    int tail_len = 6;
+    bool frontier = false;
+    SearchItem *d_tail = nullptr;
+    unsigned int tail_cap = 1u << 23;
+    uint64_t tails = 0;          // items waiting in d_tail
     int rounds = 0;
     double ms = 0.0;             // device time of all seed/round launches
     hipEvent_t e0 = nullptr, e1 = nullptr;
@@ -264,6 +278,14 @@ int tspgpu_search_create(tspgpu_ctx *c, const void *dist, int dtype, int n, int 
         const long v = std::atol(e);
         if (v > 0) s->refill = (uint32_t)std::min<long>(v, 64);
     }
+    if (const char *e = std::getenv("TSPGPU_SEARCH_TAIL")) {
+        const int v = std::atoi(e);
+        s->tail_len = (v == 5 || v == 6) ? v : 0;
+    }
+    if (const char *e = std::getenv("TSPGPU_SEARCH_TAIL_CAP_LOG2")) {  // tests: many flushes, small steps
+        const int v = std::atoi(e);
+        if (v >= 8 && v <= 26) s->tail_cap = 1u << v;
+    }
     const size_t lds = search_lds_bytes(n, f64, s->kernel == 1 ? 1 : 2);
     const int per_cu = std::max(1, std::min(8, (int)((160 * 1024) / lds)));
     s->grid = c->cu_count * per_cu;
@@ -282,6 +304,7 @@ int tspgpu_search_create(tspgpu_ctx *c, const void *dist, int dtype, int n, int 
         if (v > 0) s->budget = (uint32_t)v;
     }
     s->depth = depth;
+    s->frontier = s->tail_len && s->kernel == 2 && N - s->tail_len > depth;
     s->items = falling(N, depth);
     s->local_items = s->items / nshards + (s->items % nshards > (uint64_t)shard ? 1 : 0);
     const size_t vb = f64 ? sizeof(double) : sizeof(int32_t);
@@ -310,13 +333,14 @@ int tspgpu_search_create(tspgpu_ctx *c, const void *dist, int dtype, int n, int 
     s->rec_cap = 1u << 16;
     hipError_t e = hipMalloc(&s->d_dist, vb * n * n);
     if (e == hipSuccess) e = hipMalloc(&s->d_amin, vb * n);
-    if (e == hipSuccess) e = hipMalloc((void **)&s->d_words, 8 * sizeof(unsigned long long));
+    if (e == hipSuccess) e = hipMalloc((void **)&s->d_words, kWords * sizeof(unsigned long long));
+    if (e == hipSuccess && s->frontier) e = hipMalloc((void **)&s->d_tail, sizeof(SearchItem) * s->tail_cap);
     if (e == hipSuccess) e = hipMalloc((void **)&s->d_rec, sizeof(SearchRecord) * s->rec_cap);
     if (e == hipSuccess) e = hipMemcpy(s->d_dist, dist, vb * n * n, hipMemcpyHostToDevice);
     if (e == hipSuccess)
         e = hipMemcpy(s->d_amin, f64 ? (const void *)ad.data() : (const void *)ai.data(), vb * n,
                       hipMemcpyHostToDevice);
-    unsigned long long w[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long w[kWords] = {};
     if (f64) {
         const double inf = INFINITY;
         std::memcpy(&w[1], &inf, 8);
@@ -343,6 +367,7 @@ int tspgpu_search_destroy(tspgpu_search *s)
     if (s->d_amin) (void)hipFree(s->d_amin);
     if (s->d_words) (void)hipFree(s->d_words);
     if (s->d_rec) (void)hipFree(s->d_rec);
+    if (s->d_tail) (void)hipFree(s->d_tail);
     if (s->d_ps) (void)hipFree(s->d_ps);
     if (s->d_ring) (void)hipFree(s->d_ring);
     for (auto *p : s->d_items)
@@ -399,6 +424,13 @@ static SearchArgs args_of(tspgpu_search *s)
     a.rec_count = reinterpret_cast<unsigned int *>(s->d_words + 3);
     a.out_count = reinterpret_cast<unsigned int *>(s->d_words + 4);
     a.util = s->d_words + 5;
+    a.tail_count = reinterpret_cast<unsigned int *>(s->d_words + 8);
+    if (s->frontier) {
+        a.tail_len = s->tail_len;
+        a.tail_level = s->n - 1 - s->tail_len;
+        a.tail_out = s->d_tail;
+        a.tail_cap = s->tail_cap;
+    }
     a.rec = s->d_rec;
     a.rec_cap = s->rec_cap;
     a.stream = s->ctx->stream;
@@ -451,14 +483,93 @@ int tspgpu_search_start(tspgpu_search *s)
     a.out = s->d_items[0];
     s->cur = 0;
     s->rounds = 0;
+    s->tails = 0;
+    if (s->frontier) {
+        hipError_t e = hipMemsetAsync(s->d_words + 8, 0, 8, s->ctx->stream);
+        if (e != hipSuccess) return herr(e);
+    }
     const uint64_t blocks = (s->local_items + kSearchThreads - 1) / kSearchThreads;
     const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>(blocks, (uint64_t)s->ctx->cu_count * 8));
     return launch_and_count(s, true, grid, a);
 }
 
+// Frontier search, one step: either fold the waiting tails, or expand the
+// last T frontier items (LIFO keeps the frontier small) by one level.
+static int frontier_step(tspgpu_search *s, uint64_t *pending)
+{
+    (void)hipSetDevice(s->ctx->device);
+    hipStream_t st = s->ctx->stream;
+    const bool f64 = s->dtype == TSPGPU_F64;
+    const uint64_t branch = (uint64_t)(s->n - 1 - s->depth);  // children per item, at most
+    constexpr uint64_t kExpandMax = (uint64_t)1 << 20;
+    SearchArgs a = args_of(s);
+    hipError_t e = hipSuccess;
+    if (s->pending == 0 || s->tails >= s->tail_cap / 2) {
+        if (s->tails) {
+            (void)hipEventRecord(s->e0, st);
+            e = launch_tail(a, f64, s->ctx->cu_count * 8);
+            (void)hipEventRecord(s->e1, st);
+            if (e == hipSuccess) e = hipMemsetAsync(s->d_words + 8, 0, 8, st);
+            if (e == hipSuccess) e = hipStreamSynchronize(st);
+            if (e != hipSuccess) return herr(e);
+            float ms = 0.f;
+            if (hipEventElapsedTime(&ms, s->e0, s->e1) == hipSuccess) s->ms += ms;
+            s->tails = 0;
+            ++s->rounds;
+        }
+        if (pending) *pending = s->pending;
+        return 0;
+    }
+    const uint64_t T = std::min<uint64_t>({s->pending, kExpandMax, (s->tail_cap - s->tails) / branch});
+    int rc = ensure_items(s, 1, (size_t)(T * branch + 64));
+    if (rc) return rc;
+    a.in = s->d_items[0] + (s->pending - T);
+    a.in_count = (uint32_t)T;
+    a.out = s->d_items[1];
+    e = hipMemsetAsync(s->d_words + 4, 0, 8, st);
+    if (e != hipSuccess) return herr(e);
+    (void)hipEventRecord(s->e0, st);
+    e = launch_expand(a, f64);
+    (void)hipEventRecord(s->e1, st);
+    unsigned long long cnt[5] = {};  // words 4..8: children, ..., tails
+    if (e == hipSuccess) e = hipMemcpyAsync(cnt, s->d_words + 4, sizeof cnt, hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (e != hipSuccess) return herr(e);
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, s->e0, s->e1) == hipSuccess) s->ms += ms;
+    ++s->rounds;
+    const uint64_t kids = (uint32_t)cnt[0], keep = s->pending - T;
+    s->tails = (uint32_t)cnt[4];
+    if (keep + kids > s->item_cap[0]) {  // grow the frontier, keeping its first `keep` items
+        const size_t cap = std::max<size_t>(keep + kids, 2 * s->item_cap[0]);
+        SearchItem *p = nullptr;
+        e = hipMalloc((void **)&p, cap * sizeof(SearchItem));
+        if (e == hipSuccess && keep) e = hipMemcpyAsync(p, s->d_items[0], keep * sizeof(SearchItem),
+                                                        hipMemcpyDeviceToDevice, st);
+        if (e == hipSuccess) e = hipStreamSynchronize(st);
+        if (e != hipSuccess) {
+            if (p) (void)hipFree(p);
+            return herr(e);
+        }
+        (void)hipFree(s->d_items[0]);
+        s->d_items[0] = p;
+        s->item_cap[0] = cap;
+    }
+    if (kids) {
+        e = hipMemcpyAsync(s->d_items[0] + keep, s->d_items[1], kids * sizeof(SearchItem), hipMemcpyDeviceToDevice,
+                           st);
+        if (e == hipSuccess) e = hipStreamSynchronize(st);
+        if (e != hipSuccess) return herr(e);
+    }
+    s->pending = keep + kids;
+    if (pending) *pending = s->pending + s->tails;
+    return 0;
+}
+
 int tspgpu_search_step(tspgpu_search *s, uint64_t *pending)
 {
     if (!s) return -EINVAL;
+    if (s->frontier) return frontier_step(s, pending);
     if (s->pending == 0) {
         if (pending) *pending = 0;
         return 0;
@@ -698,7 +809,9 @@ static int search_solve(tspgpu_ctx *c, const void *dist, int dtype, int n, doubl
 {
     if (!c || !cost_out || !tour_out) return -EINVAL;
     tspgpu_search *s = nullptr;
-    int rc = tspgpu_search_create(c, dist, dtype, n, 0, 1, 0, &s);
+    int depth = 0;  // automatic; TSPGPU_SEARCH_DEPTH (tests): a shallow seed, a deep frontier
+    if (const char *e = std::getenv("TSPGPU_SEARCH_DEPTH")) depth = std::max(0, std::atoi(e));
+    int rc = tspgpu_search_create(c, dist, dtype, n, 0, 1, depth, &s);
     if (rc) return rc;
     s->noprune = noprune;
     // enumeration work is uniform and every lane reaches the register tails:
