@@ -187,7 +187,7 @@ __global__ __launch_bounds__(256) void enum_kernel(SearchArgs a)
             }
         }
     }
-    if (__lane_id() == 0) atomicAdd(a.nodes, lanes * (unsigned long long)kTailNodes);
+    if (__lane_id() == 0) atomicAdd(stat_line(a), lanes * (unsigned long long)kTailNodes);
 }
 
 template <typename V, int NN>
@@ -216,7 +216,7 @@ hipError_t launch_v(const SearchArgs &a, int grid)
 }
 
 // ---------------------------------------------------------------------------
-// Register tails of the frontier search: every prefix in a.tail_out (written
+// Register tails of the frontier search: every prefix in a.ftail (written
 // by expand_kernel) has exactly TL cities left; a lane refolds
 // the prefix (the same left fold, from LDS), tests it against the current
 // incumbent with the search's bound (cheapest incoming edge of every city
@@ -248,25 +248,53 @@ __host__ __device__ constexpr unsigned long long tail_nodes(int tl)
     return sum;
 }
 
-// One handed-over prefix (slot idx of a.tail_out): refold, bound test, all
+// A frontier path in registers: two dwordx4 loads.
+__device__ __forceinline__ void load_path(const PathItem *p, bool act, uint32_t (&w)[8])
+{
+    if (act) {
+        const uint4 lo = reinterpret_cast<const uint4 *>(p)[0];
+        const uint4 hi = reinterpret_cast<const uint4 *>(p)[1];
+        w[0] = lo.x, w[1] = lo.y, w[2] = lo.z, w[3] = lo.w;
+        w[4] = hi.x, w[5] = hi.y, w[6] = hi.z, w[7] = hi.w;
+    } else {
+#pragma unroll
+        for (int b = 0; b < 8; ++b) w[b] = 0u;
+    }
+}
+
+// The left fold ((d[0][t1] + d[t1][t2]) + ...) of the path in w (len cities),
+// its end city and its members, from the matrix in LDS.
+template <typename V>
+__device__ __forceinline__ void fold_path(const V *dl, const uint32_t (&w)[8], int len, V &c, int &k, uint32_t &mem)
+{
+#pragma unroll
+    for (int b = 0; b < 8; ++b)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int lv = 4 * b + q;
+            if (lv >= 1 && lv < len) {
+                const int t = (int)((w[b] >> (8 * q)) & 255u);
+                c = c + dl[k * kTRow + t];
+                mem |= 1u << t;
+                k = t;
+            }
+        }
+}
+
+// One handed-over prefix (slot idx of a.ftail): refold, bound test, all
 // TL! completions; `act` false = a lane with nothing to do (wave-uniform code).
 template <typename V, int TL>
 __device__ __forceinline__ void tail_one(const SearchArgs &a, const V *dl, const V *am, uint32_t full, uint32_t idx,
                                          bool act, unsigned long long &lanes)
 {
-    const uint32_t *src = reinterpret_cast<const uint32_t *>(a.tail_out + idx);
-    const int len = act ? (int)(src[8] & 255u) : 1;
+    uint32_t w[8];
+    load_path(a.ftail + idx, act, w);
+    const int len = act ? (int)(w[0] & 255u) : 1;
     // ---- the prefix 0, t1..t(len-1): the reference's left fold
     V cp = 0;
     int prev = 0;
-    uint32_t mem = 0, word = 0;
-    for (int l = 1; l < len; ++l) {
-        if ((l & 3) == 0 || l == 1) word = src[l >> 2];
-        const int c = (int)((word >> (8 * (l & 3))) & 255u);
-        cp = cp + dl[prev * kTRow + c];
-        mem |= 1u << c;
-        prev = c;
-    }
+    uint32_t mem = 0;
+    fold_path<V>(dl, w, len, cp, prev, mem);
     const uint32_t rest = full & ~mem;  // the TL cities left
     int t[TL];
     uint32_t tpack = 0;  // t[i] in bits 5i..5i+4 (record path)
@@ -350,11 +378,8 @@ __device__ __forceinline__ void tail_one(const SearchArgs &a, const V *dl, const
                     if (slot < a.rec_cap) {
                         SearchRecord *R = a.rec + slot;
                         R->cost = tb;
-                        uint32_t wd = 0;
-                        for (int l = 1; l < len; ++l) {
-                            if ((l & 3) == 0 || l == 1) wd = src[l >> 2];
-                            R->city[l - 1] = (uint8_t)((wd >> (8 * (l & 3))) & 255u);
-                        }
+                        const uint8_t *pb = a.ftail[idx].b;
+                        for (int l = 1; l < len; ++l) R->city[l - 1] = pb[l];
 #pragma unroll
                         for (int l = 0; l < TL; ++l) R->city[len - 1 + l] = (uint8_t)ord[l];
                     }
@@ -394,7 +419,7 @@ __global__ __launch_bounds__(256) void tail_kernel(SearchArgs a)
         const bool more = base < count;
         if (more) {
             const uint32_t idx = base + lane;
-            const bool live = idx < count && (reinterpret_cast<const uint32_t *>(a.tail_out + idx)[8] & 255u) != 0;
+            const bool live = idx < count && a.ftail[idx].b[0] != 0;
             const unsigned long long m = __ballot(live);
             if (live) q[qn + __popcll(m & ((1ull << lane) - 1ull))] = idx;
             qn += (uint32_t)__popcll(m);
@@ -412,21 +437,56 @@ __global__ __launch_bounds__(256) void tail_kernel(SearchArgs a)
         }
         if (!more) break;
     }
-    if (lane == 0) atomicAdd(a.nodes, lanes * tail_nodes(TL));
+    if (lane == 0) atomicAdd(stat_line(a), lanes * tail_nodes(TL));
 }
 
-// Frontier expansion, one level: a lane per item of a.in (the path 0,
-// t1..t(len-1), refolded from LDS); every child j (ascending) whose bound
-// passes becomes an item of a.tail_out when it has tail_level inner cities,
-// else of a.out.  Block-level stream compaction: one global atomic per block
-// and output (per-wave atomics on one counter serialise the grid).  The host
-// sizes both outputs for (N - depth) children per input item.
+// Frontier expansion, one level: a lane per path of a.fin (0, t1..t(len-1),
+// refolded from LDS); every child j (ascending) whose bound passes becomes a
+// path of a.ftail when it has tail_level inner cities, else of a.fout.  The
+// host sizes both outputs for (N - depth) children per input path.
+//
+// Slots: device-scope atomics on one address serialise at ~20 ns each, so a
+// block owns a contiguous run of a.fin_per_block paths and takes ONE range
+// per output: pass 1 counts its live children, one atomicAdd per output,
+// pass 2 re-evaluates (cheap: LDS + registers) and writes the children at
+// block-scanned offsets.
+template <typename V>
+struct Expand {
+    uint32_t w[8];
+    int len;
+    uint32_t rem, live;
+};
+
+template <typename V>
+__device__ __forceinline__ Expand<V> expand_eval(const SearchArgs &a, const V *dl, const V *am, uint32_t full,
+                                                 uint32_t idx, uint32_t end, V thr)
+{
+    Expand<V> e;
+    const bool act = idx < end;
+    load_path(a.fin + idx, act, e.w);
+    e.len = act ? (int)(e.w[0] & 255u) : 0;
+    V c = 0;  // the reference's left fold of the path
+    int k = 0;
+    uint32_t mem = 0;
+    fold_path<V>(dl, e.w, e.len, c, k, mem);
+    e.rem = act ? (full & ~mem) : 0u;
+    V remA = am[0];  // every city still to be entered: its cheapest incoming edge (exact sums)
+    for (uint32_t x = e.rem; x; x &= x - 1u) remA += am[__builtin_ctz(x)];
+    e.live = 0;
+    for (uint32_t x = e.rem; x; x &= x - 1u) {
+        const int j = __builtin_ctz(x);
+        const V cj = c + dl[k * kTRow + j];
+        if (a.noprune || !(cj + (remA - am[j]) > thr)) e.live |= 1u << j;
+    }
+    return e;
+}
+
 template <typename V>
 __global__ __launch_bounds__(256) void expand_kernel(SearchArgs a)
 {
     __shared__ V dl[kSearchMaxN * kTRow];
     __shared__ V am[kSearchMaxN];
-    __shared__ uint32_t wtot[3][4];
+    __shared__ uint32_t wtot[2][4];
     __shared__ uint32_t bbase[2];
     const int n = a.n;
     const V *gd = static_cast<const V *>(a.dist);
@@ -435,85 +495,105 @@ __global__ __launch_bounds__(256) void expand_kernel(SearchArgs a)
     for (int i = threadIdx.x; i < n; i += blockDim.x) am[i] = ga[i];
     __syncthreads();
 
-    const uint32_t idx = blockIdx.x * 256u + threadIdx.x;
-    const bool act = idx < a.in_count;
-    const uint32_t *src = reinterpret_cast<const uint32_t *>(a.in + (act ? idx : 0u));
-    const int len = act ? (int)(src[8] & 255u) : 0;
-    uint32_t w[8];
-#pragma unroll
-    for (int b = 0; b < 8; ++b) w[b] = 4 * b < len ? src[b] : 0u;
-    // ---- the path: the reference's left fold
-    V c = 0;
-    int k = 0;
-    uint32_t mem = 0;
-#pragma unroll
-    for (int b = 0; b < 8; ++b)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int lv = 4 * b + q;
-            if (lv >= 1 && lv < len) {
-                const int t = (int)((w[b] >> (8 * q)) & 255u);
-                c = c + dl[k * kTRow + t];
-                mem |= 1u << t;
-                k = t;
-            }
-        }
     const uint32_t full = (uint32_t)((1ull << n) - 1ull) & ~1u;
-    const uint32_t rem = act ? (full & ~mem) : 0u;
-    V remA = am[0];  // every city still to be entered: its cheapest incoming edge (exact sums)
-    for (uint32_t x = rem; x; x &= x - 1u) remA += am[__builtin_ctz(x)];
-    const V inc = ENum<V>::val(__hip_atomic_load(a.inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-    const V thr = EThr<V>::of(inc);
-    uint32_t live = 0;
-    for (uint32_t x = rem; x; x &= x - 1u) {
-        const int j = __builtin_ctz(x);
-        const V cj = c + dl[k * kTRow + j];
-        if (a.noprune || !(cj + (remA - am[j]) > thr)) live |= 1u << j;
-    }
-    // ---- block-level compaction: wave scans, one atomic per block and output
-    const bool tail = len == a.tail_level;  // children have len inner cities
-    const uint32_t cnt = (uint32_t)__builtin_popcount(live);
-    uint32_t v[3] = {tail ? cnt : 0u, tail ? 0u : cnt, (uint32_t)__builtin_popcount(rem)};
+    const V thr = EThr<V>::of(ENum<V>::val(__hip_atomic_load(a.inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)));
+    const uint32_t b0 = blockIdx.x * a.fin_per_block;
+    const uint32_t b1 = b0 + a.fin_per_block < a.fin_count ? b0 + a.fin_per_block : a.fin_count;
     const int lane = __lane_id(), wv = threadIdx.x >> 6;
-    uint32_t incl[3] = {v[0], v[1], v[2]};
+
+    // ---- pass 1: this block's live children per output, nodes evaluated
+    uint32_t cT = 0, cF = 0;
+    unsigned long long nodes = 0;
+    for (uint32_t base = b0; base < b1; base += 256u) {
+        const Expand<V> e = expand_eval<V>(a, dl, am, full, base + threadIdx.x, b1, thr);
+        const uint32_t cnt = (uint32_t)__builtin_popcount(e.live);
+        if (e.len == a.tail_level) cT += cnt; else cF += cnt;  // children have len inner cities
+        nodes += (unsigned long long)__builtin_popcount(e.rem);
+    }
 #pragma unroll
-    for (int off = 1; off < 64; off <<= 1)
-#pragma unroll
-        for (int i = 0; i < 3; ++i) {
-            const uint32_t y = __shfl_up(incl[i], off);
-            if (lane >= off) incl[i] += y;
-        }
-    if (lane == 63)
-        for (int i = 0; i < 3; ++i) wtot[i][wv] = incl[i];
+    for (int off = 32; off >= 1; off >>= 1) {
+        cT += __shfl_xor(cT, off);
+        cF += __shfl_xor(cF, off);
+        nodes += __shfl_xor(nodes, off);
+    }
+    if (lane == 0) {
+        wtot[0][wv] = cT;
+        wtot[1][wv] = cF;
+        if (nodes) atomicAdd(stat_line(a), nodes);
+    }
     __syncthreads();
     if (threadIdx.x == 0) {
         const uint32_t tt = wtot[0][0] + wtot[0][1] + wtot[0][2] + wtot[0][3];
         const uint32_t tf = wtot[1][0] + wtot[1][1] + wtot[1][2] + wtot[1][3];
-        const uint32_t tn = wtot[2][0] + wtot[2][1] + wtot[2][2] + wtot[2][3];
         bbase[0] = tt ? atomicAdd(a.tail_count, tt) : 0u;
         bbase[1] = tf ? atomicAdd(a.out_count, tf) : 0u;
-        if (tn) atomicAdd(a.nodes, (unsigned long long)tn);
     }
     __syncthreads();
-    uint32_t wofs[2] = {0u, 0u};
-    for (int u = 0; u < wv; ++u) {
-        wofs[0] += wtot[0][u];
-        wofs[1] += wtot[1][u];
-    }
-    uint32_t slot = tail ? bbase[0] + wofs[0] + incl[0] - v[0] : bbase[1] + wofs[1] + incl[1] - v[1];
-    SearchItem *dstb = tail ? a.tail_out : a.out;
-    // ---- children, ascending: parent path + j
-    const int cb = len >> 2, cs = 8 * (len & 3);
-    for (uint32_t x = live; x; x &= x - 1u, ++slot) {
-        const uint32_t j = (uint32_t)__builtin_ctz(x);
-        uint32_t *dst = reinterpret_cast<uint32_t *>(dstb + slot);
+    uint32_t run[2] = {bbase[0], bbase[1]};
+
+    // ---- pass 2: the children, at block-scanned offsets
+    for (uint32_t base = b0; base < b1; base += 256u) {
+        const Expand<V> e = expand_eval<V>(a, dl, am, full, base + threadIdx.x, b1, thr);
+        const bool tail = e.len == a.tail_level;
+        const uint32_t cnt = (uint32_t)__builtin_popcount(e.live);
+        const uint32_t v[2] = {tail ? cnt : 0u, tail ? 0u : cnt};
+        uint32_t incl[2] = {v[0], v[1]};
 #pragma unroll
-        for (int b = 0; b < 8; ++b) {
-            const uint32_t word = b == cb ? ((w[b] & ~(255u << cs)) | (j << cs)) : w[b];
-            if (4 * b <= len) dst[b] = word;
+        for (int off = 1; off < 64; off <<= 1)
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                const uint32_t y = __shfl_up(incl[i], off);
+                if (lane >= off) incl[i] += y;
+            }
+        __syncthreads();  // wtot of the previous tile has been read
+        if (lane == 63) {
+            wtot[0][wv] = incl[0];
+            wtot[1][wv] = incl[1];
         }
-        dst[8] = (uint32_t)(len + 1) | (1u << 8);
+        __syncthreads();
+        uint32_t wofs[2] = {0u, 0u}, ttot[2] = {0u, 0u};
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            wofs[0] += u < wv ? wtot[0][u] : 0u;
+            wofs[1] += u < wv ? wtot[1][u] : 0u;
+            ttot[0] += wtot[0][u];
+            ttot[1] += wtot[1][u];
+        }
+        uint32_t slot = tail ? run[0] + wofs[0] + incl[0] - v[0] : run[1] + wofs[1] + incl[1] - v[1];
+        run[0] += ttot[0];
+        run[1] += ttot[1];
+        PathItem *dstb = tail ? a.ftail : a.fout;
+        // parent path + j, len + 1 (two dwordx4 stores each)
+        const int cb = e.len >> 2, cs = 8 * (e.len & 3);
+        uint32_t cw[8];
+#pragma unroll
+        for (int b = 0; b < 8; ++b) cw[b] = b == 0 ? ((e.w[0] & ~255u) | (uint32_t)(e.len + 1)) : e.w[b];
+        for (uint32_t x = e.live; x; x &= x - 1u, ++slot) {
+            const uint32_t j = (uint32_t)__builtin_ctz(x);
+            uint32_t o[8];
+#pragma unroll
+            for (int b = 0; b < 8; ++b) o[b] = b == cb ? ((cw[b] & ~(255u << cs)) | (j << cs)) : cw[b];
+            uint4 *dst = reinterpret_cast<uint4 *>(dstb + slot);
+            dst[0] = make_uint4(o[0], o[1], o[2], o[3]);
+            dst[1] = make_uint4(o[4], o[5], o[6], o[7]);
+        }
     }
+}
+
+// Seeds (SearchItem, from seed_kernel) -> frontier paths.
+__global__ __launch_bounds__(256) void to_paths_kernel(SearchArgs a)
+{
+    const uint32_t idx = blockIdx.x * 256u + threadIdx.x;
+    if (idx >= a.in_count) return;
+    const SearchItem &it = a.in[idx];
+    uint32_t o[8];
+#pragma unroll
+    for (int b = 0; b < 8; ++b) o[b] = 0u;
+    const int len = it.len;
+    for (int l = 0; l < len; ++l) o[l >> 2] |= (uint32_t)(l == 0 ? len : it.city[l]) << (8 * (l & 3));
+    uint4 *dst = reinterpret_cast<uint4 *>(a.fout + idx);
+    dst[0] = make_uint4(o[0], o[1], o[2], o[3]);
+    dst[1] = make_uint4(o[4], o[5], o[6], o[7]);
 }
 
 template <typename V>
@@ -535,10 +615,18 @@ hipError_t launch_enum(const SearchArgs &a, bool f64, int grid)
     return f64 ? launch_v<double>(a, grid) : launch_v<int32_t>(a, grid);
 }
 
+hipError_t launch_to_paths(const SearchArgs &a)
+{
+    if (a.in_count == 0) return hipSuccess;
+    hipLaunchKernelGGL(to_paths_kernel, dim3((a.in_count + 255u) / 256u), dim3(256), 0, a.stream, a);
+    return hipGetLastError();
+}
+
 hipError_t launch_expand(const SearchArgs &a, bool f64)
 {
-    if (a.n > kSearchMaxN || a.in_count == 0) return a.in_count ? hipErrorInvalidValue : hipSuccess;
-    const int grid = (int)((a.in_count + 255u) / 256u);
+    if (a.n > kSearchMaxN || a.fin_count == 0) return a.fin_count ? hipErrorInvalidValue : hipSuccess;
+    if (a.fin_per_block == 0 || a.fin_per_block % 256u) return hipErrorInvalidValue;
+    const int grid = (int)((a.fin_count + a.fin_per_block - 1u) / a.fin_per_block);
     if (f64)
         hipLaunchKernelGGL(expand_kernel<double>, dim3(grid), dim3(256), 0, a.stream, a);
     else

@@ -29,6 +29,13 @@ struct SearchItem {
     uint8_t pad[2];
 };
 
+// A frontier path (frontier search: expand_kernel, tail_kernel): byte 0 =
+// len (cities on the path, city 0 included), bytes 1..len-1 = t1..t(len-1).
+// 32 bytes, 16-byte aligned: two dwordx4 per item.
+struct alignas(16) PathItem {
+    uint8_t b[32];
+};
+
 // Device words of the persistent search (search_persist_kernel), zeroed by
 // the host before every launch except work = this shard's seed count.  Each
 // word has a 256-byte line of its own: the counters take atomics from every
@@ -64,8 +71,10 @@ struct SearchArgs {
     SearchRecord *rec;         // record buffer (device)
     unsigned int *rec_count;   // records claimed (may exceed rec_cap: overflow)
     unsigned int rec_cap;
-    unsigned long long *nodes; // search nodes evaluated (device accumulator)
-    unsigned long long *util;  // v2: [0] lane slots, [1] active lane steps, [2] item loads
+    // statistics: kStatLines lines of kStatStride u64, a block adds to line
+    // blockIdx % kStatLines (one hot address serialises device atomics):
+    // [0] search nodes evaluated, v2: [1] lane slots, [2] active lane steps, [3] item loads
+    unsigned long long *nodes;
     uint32_t refill;           // v2: a wave refills once this many lanes wait for an item
     // persistent search (kernel 3)
     PersistState *ps;
@@ -78,16 +87,26 @@ struct SearchArgs {
     int kernel;                // round kernel: 2 (lock-step DFS, default) or 1 (branching DFS); 3 = persistent
     int noprune;               // exhaustive enumeration: no bound test (kernels 2 and seed only)
     int tails;                 // kernel 2: last four cities enumerated in registers (tail4)
-    // frontier search (expand_kernel + tail_kernel): items are expanded one
-    // level at a time; children with tail_level inner cities (tail_len =
-    // N - tail_level cities left) go to tail_out, the others to out.
+    // frontier search (expand_kernel + tail_kernel): fin is expanded one
+    // level; children with tail_level inner cities (tail_len = N - tail_level
+    // cities left) go to ftail, the others to fout.
     int tail_level;
     int tail_len;              // 5 or 6
-    SearchItem *tail_out;
-    unsigned int *tail_count;  // items in tail_out (tail_kernel reads it on the device)
+    const PathItem *fin;
+    uint32_t fin_count;
+    uint32_t fin_per_block;    // expand_kernel: paths per block (multiple of 256)
+    PathItem *fout;
+    PathItem *ftail;
+    unsigned int *tail_count;  // items in ftail (tail_kernel reads it on the device)
     unsigned int tail_cap;
     hipStream_t stream;
 };
+
+constexpr int kStatLines = 64, kStatStride = 16;
+__device__ __forceinline__ unsigned long long *stat_line(const SearchArgs &a)
+{
+    return a.nodes + (blockIdx.x & (kStatLines - 1)) * kStatStride;
+}
 
 size_t search_lds_bytes(int n, bool f64, int kernel = 2);
 hipError_t launch_seed(const SearchArgs &a, bool f64, int grid);
@@ -96,6 +115,7 @@ hipError_t launch_round(const SearchArgs &a, bool f64, int grid);
 hipError_t launch_enum(const SearchArgs &a, bool f64, int grid);
 // frontier search (enum.hip): one level of a.in -> a.out / a.tail_out, and
 // the register tails of a.tail_out (a.tail_len in {5, 6})
+hipError_t launch_to_paths(const SearchArgs &a);  // a.in (seeds) -> a.fout
 hipError_t launch_expand(const SearchArgs &a, bool f64);
 hipError_t launch_tail(const SearchArgs &a, bool f64, int grid);
 hipError_t launch_persist(const SearchArgs &a, bool f64, int grid);

@@ -350,7 +350,7 @@ __global__ __launch_bounds__(kSearchThreads) void round_kernel_v1(SearchArgs a)
     }
 #undef COST
 #undef CITY
-    atomicAdd(a.nodes, nodes);
+    atomicAdd(stat_line(a), nodes);
 }
 
 
@@ -742,10 +742,11 @@ __global__ __launch_bounds__(kSearchThreads) void round_kernel(SearchArgs a)
         }
     }
     if (lane == 0) {
-        atomicAdd(a.nodes, nodes);
-        atomicAdd(a.util, wsteps);
-        atomicAdd(a.util + 1, wactive);
-        atomicAdd(a.util + 2, wloads);
+        unsigned long long *st = stat_line(a);
+        atomicAdd(st, nodes);
+        atomicAdd(st + 1, wsteps);
+        atomicAdd(st + 2, wactive);
+        atomicAdd(st + 3, wloads);
     }
 }
 
@@ -1120,10 +1121,11 @@ __global__ __launch_bounds__(kSearchThreads) void persist_kernel(SearchArgs a)
         }
     }
     if (lane == 0) {
-        atomicAdd(a.nodes, nodes);
-        atomicAdd(a.util, wsteps);
-        atomicAdd(a.util + 1, wactive);
-        atomicAdd(a.util + 2, wloads);
+        unsigned long long *st = stat_line(a);
+        atomicAdd(st, nodes);
+        atomicAdd(st + 1, wsteps);
+        atomicAdd(st + 2, wactive);
+        atomicAdd(st + 3, wloads);
     }
 }
 

@@ -36,6 +36,7 @@ using namespace tspgpu;
 
 static_assert(sizeof(SearchRecord) == sizeof(tspgpu_tour_record), "record layout");
 constexpr int kWords = 16;  // device counter words of a search (see tspgpu_search::d_words)
+constexpr size_t kStatBytes = sizeof(unsigned long long) * kStatLines * kStatStride;
 
 struct tspgpu_search {
     tspgpu_ctx *ctx = nullptr;
@@ -52,6 +53,7 @@ struct tspgpu_search {
     // [0] queue (u32), [1] incumbent, [2] nodes, [3] record count (u32), [4] items out (u32),
     // [5..7] utilisation counters, [8] tail items (u32)
     unsigned long long *d_words = nullptr;
+    unsigned long long *d_stats = nullptr;  // kStatLines x kStatStride: [0] nodes, [1..3] lane-step counters
     SearchRecord *d_rec = nullptr;
     unsigned int rec_cap = 0;
     SearchItem *d_items[2] = {nullptr, nullptr};  // round input / output (ping-pong)
@@ -82,7 +84,9 @@ struct tspgpu_search {
     // frontier is empty.
     int tail_len = 6;
     bool frontier = false;
-    SearchItem *d_tail = nullptr;
+    PathItem *d_front[2] = {nullptr, nullptr};  // frontier (LIFO) / children of the current step
+    size_t front_cap[2] = {0, 0};
+    PathItem *d_tail = nullptr;
     unsigned int tail_cap = 1u << 23;
     uint64_t tails = 0;          // items waiting in d_tail
     int rounds = 0;
@@ -334,7 +338,9 @@ int tspgpu_search_create(tspgpu_ctx *c, const void *dist, int dtype, int n, int 
     hipError_t e = hipMalloc(&s->d_dist, vb * n * n);
     if (e == hipSuccess) e = hipMalloc(&s->d_amin, vb * n);
     if (e == hipSuccess) e = hipMalloc((void **)&s->d_words, kWords * sizeof(unsigned long long));
-    if (e == hipSuccess && s->frontier) e = hipMalloc((void **)&s->d_tail, sizeof(SearchItem) * s->tail_cap);
+    if (e == hipSuccess) e = hipMalloc((void **)&s->d_stats, kStatBytes);
+    if (e == hipSuccess) e = hipMemset(s->d_stats, 0, kStatBytes);
+    if (e == hipSuccess && s->frontier) e = hipMalloc((void **)&s->d_tail, sizeof(PathItem) * s->tail_cap);
     if (e == hipSuccess) e = hipMalloc((void **)&s->d_rec, sizeof(SearchRecord) * s->rec_cap);
     if (e == hipSuccess) e = hipMemcpy(s->d_dist, dist, vb * n * n, hipMemcpyHostToDevice);
     if (e == hipSuccess)
@@ -366,8 +372,11 @@ int tspgpu_search_destroy(tspgpu_search *s)
     if (s->d_dist) (void)hipFree(s->d_dist);
     if (s->d_amin) (void)hipFree(s->d_amin);
     if (s->d_words) (void)hipFree(s->d_words);
+    if (s->d_stats) (void)hipFree(s->d_stats);
     if (s->d_rec) (void)hipFree(s->d_rec);
     if (s->d_tail) (void)hipFree(s->d_tail);
+    for (auto *p : s->d_front)
+        if (p) (void)hipFree(p);
     if (s->d_ps) (void)hipFree(s->d_ps);
     if (s->d_ring) (void)hipFree(s->d_ring);
     for (auto *p : s->d_items)
@@ -420,15 +429,14 @@ static SearchArgs args_of(tspgpu_search *s)
     if (const char *e = std::getenv("TSPGPU_SEARCH_TAILS")) a.tails = std::atoi(e) != 0;
     a.queue = reinterpret_cast<unsigned int *>(s->d_words);
     a.inc = s->d_words + 1;
-    a.nodes = s->d_words + 2;
+    a.nodes = s->d_stats;
     a.rec_count = reinterpret_cast<unsigned int *>(s->d_words + 3);
     a.out_count = reinterpret_cast<unsigned int *>(s->d_words + 4);
-    a.util = s->d_words + 5;
     a.tail_count = reinterpret_cast<unsigned int *>(s->d_words + 8);
     if (s->frontier) {
         a.tail_len = s->tail_len;
         a.tail_level = s->n - 1 - s->tail_len;
-        a.tail_out = s->d_tail;
+        a.ftail = s->d_tail;
         a.tail_cap = s->tail_cap;
     }
     a.rec = s->d_rec;
@@ -449,6 +457,40 @@ static int ensure_items(tspgpu_search *s, int which, size_t count)
     hipError_t e = hipMalloc((void **)&s->d_items[which], cap * sizeof(SearchItem));
     if (e != hipSuccess) return herr(e);
     s->item_cap[which] = cap;
+    return 0;
+}
+
+// the statistics lines, summed: [0] nodes, [1] lane slots, [2] active lane steps, [3] item loads
+static int read_stats(tspgpu_search *s, uint64_t (&out)[4])
+{
+    std::vector<unsigned long long> h(kStatLines * kStatStride);
+    hipError_t e = hipMemcpyAsync(h.data(), s->d_stats, kStatBytes, hipMemcpyDeviceToHost, s->ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(s->ctx->stream);
+    if (e != hipSuccess) return herr(e);
+    for (int i = 0; i < 4; ++i) {
+        out[i] = 0;
+        for (int l = 0; l < kStatLines; ++l) out[i] += h[l * kStatStride + i];
+    }
+    return 0;
+}
+
+// frontier buffer `which` holds at least `count` paths; its first `keep` survive a reallocation
+static int ensure_front(tspgpu_search *s, int which, size_t count, size_t keep)
+{
+    if (s->front_cap[which] >= count && s->d_front[which]) return 0;
+    const size_t cap = std::max<size_t>({count, 4096, 2 * s->front_cap[which]});
+    PathItem *p = nullptr;
+    hipError_t e = hipMalloc((void **)&p, cap * sizeof(PathItem));
+    if (e == hipSuccess && keep)
+        e = hipMemcpyAsync(p, s->d_front[which], keep * sizeof(PathItem), hipMemcpyDeviceToDevice, s->ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(s->ctx->stream);
+    if (e != hipSuccess) {
+        if (p) (void)hipFree(p);
+        return herr(e);
+    }
+    if (s->d_front[which]) (void)hipFree(s->d_front[which]);
+    s->d_front[which] = p;
+    s->front_cap[which] = cap;
     return 0;
 }
 
@@ -477,8 +519,7 @@ int tspgpu_search_start(tspgpu_search *s)
 {
     if (!s) return -EINVAL;
     (void)hipSetDevice(s->ctx->device);
-    int rc = ensure_items(s, 0, s->local_items + 1);
-    if (rc) return rc;
+    if (int rc = ensure_items(s, 0, s->local_items + 1)) return rc;
     SearchArgs a = args_of(s);
     a.out = s->d_items[0];
     s->cur = 0;
@@ -490,7 +531,17 @@ int tspgpu_search_start(tspgpu_search *s)
     }
     const uint64_t blocks = (s->local_items + kSearchThreads - 1) / kSearchThreads;
     const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>(blocks, (uint64_t)s->ctx->cu_count * 8));
-    return launch_and_count(s, true, grid, a);
+    int rc = launch_and_count(s, true, grid, a);
+    if (rc || !s->frontier || s->pending == 0) return rc;
+    // frontier search: the live seeds become the first frontier (32-byte paths)
+    rc = ensure_front(s, 0, s->pending, 0);
+    if (rc) return rc;
+    a.in = s->d_items[0];
+    a.in_count = (uint32_t)s->pending;
+    a.fout = s->d_front[0];
+    hipError_t e = launch_to_paths(a);
+    if (e == hipSuccess) e = hipStreamSynchronize(s->ctx->stream);
+    return herr(e);
 }
 
 // Frontier search, one step: either fold the waiting tails, or expand the
@@ -501,7 +552,7 @@ static int frontier_step(tspgpu_search *s, uint64_t *pending)
     hipStream_t st = s->ctx->stream;
     const bool f64 = s->dtype == TSPGPU_F64;
     const uint64_t branch = (uint64_t)(s->n - 1 - s->depth);  // children per item, at most
-    constexpr uint64_t kExpandMax = (uint64_t)1 << 20;
+    constexpr uint64_t kExpandMax = (uint64_t)1 << 21;
     SearchArgs a = args_of(s);
     hipError_t e = hipSuccess;
     if (s->pending == 0 || s->tails >= s->tail_cap / 2) {
@@ -521,11 +572,15 @@ static int frontier_step(tspgpu_search *s, uint64_t *pending)
         return 0;
     }
     const uint64_t T = std::min<uint64_t>({s->pending, kExpandMax, (s->tail_cap - s->tails) / branch});
-    int rc = ensure_items(s, 1, (size_t)(T * branch + 64));
+    const uint64_t keep = s->pending - T;
+    int rc = ensure_front(s, 1, (size_t)(T * branch + 64), 0);
     if (rc) return rc;
-    a.in = s->d_items[0] + (s->pending - T);
-    a.in_count = (uint32_t)T;
-    a.out = s->d_items[1];
+    a.fin = s->d_front[0] + keep;
+    a.fin_count = (uint32_t)T;
+    // a few blocks per CU, each over a contiguous run (one slot atomic per block and output)
+    const uint64_t blocks = std::max<uint64_t>(1, std::min<uint64_t>((T + 255) / 256, (uint64_t)s->ctx->cu_count * 4));
+    a.fin_per_block = (uint32_t)(((T + blocks - 1) / blocks + 255) / 256 * 256);
+    a.fout = s->d_front[1];
     e = hipMemsetAsync(s->d_words + 4, 0, 8, st);
     if (e != hipSuccess) return herr(e);
     (void)hipEventRecord(s->e0, st);
@@ -538,26 +593,15 @@ static int frontier_step(tspgpu_search *s, uint64_t *pending)
     float ms = 0.f;
     if (hipEventElapsedTime(&ms, s->e0, s->e1) == hipSuccess) s->ms += ms;
     ++s->rounds;
-    const uint64_t kids = (uint32_t)cnt[0], keep = s->pending - T;
+    const uint64_t kids = (uint32_t)cnt[0];
     s->tails = (uint32_t)cnt[4];
-    if (keep + kids > s->item_cap[0]) {  // grow the frontier, keeping its first `keep` items
-        const size_t cap = std::max<size_t>(keep + kids, 2 * s->item_cap[0]);
-        SearchItem *p = nullptr;
-        e = hipMalloc((void **)&p, cap * sizeof(SearchItem));
-        if (e == hipSuccess && keep) e = hipMemcpyAsync(p, s->d_items[0], keep * sizeof(SearchItem),
-                                                        hipMemcpyDeviceToDevice, st);
-        if (e == hipSuccess) e = hipStreamSynchronize(st);
-        if (e != hipSuccess) {
-            if (p) (void)hipFree(p);
-            return herr(e);
-        }
-        (void)hipFree(s->d_items[0]);
-        s->d_items[0] = p;
-        s->item_cap[0] = cap;
-    }
-    if (kids) {
-        e = hipMemcpyAsync(s->d_items[0] + keep, s->d_items[1], kids * sizeof(SearchItem), hipMemcpyDeviceToDevice,
-                           st);
+    if (keep == 0) {  // the whole frontier was expanded: the children are the frontier
+        std::swap(s->d_front[0], s->d_front[1]);
+        std::swap(s->front_cap[0], s->front_cap[1]);
+    } else if (kids) {  // behind the items not expanded yet
+        rc = ensure_front(s, 0, (size_t)(keep + kids), (size_t)keep);
+        if (rc) return rc;
+        e = hipMemcpyAsync(s->d_front[0] + keep, s->d_front[1], kids * sizeof(PathItem), hipMemcpyDeviceToDevice, st);
         if (e == hipSuccess) e = hipStreamSynchronize(st);
         if (e != hipSuccess) return herr(e);
     }
@@ -679,7 +723,7 @@ static int run_enum(tspgpu_search *s)
     int per_cu = 8;
     if (const char *e = std::getenv("TSPGPU_ENUM_WG_PER_CU")) per_cu = std::max(1, std::atoi(e));
     const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>(blocks, (uint64_t)s->ctx->cu_count * per_cu));
-    hipError_t e = hipMemcpyAsync(s->d_words + 2, &upper, 8, hipMemcpyHostToDevice, st);
+    hipError_t e = hipMemcpyAsync(s->d_stats, &upper, 8, hipMemcpyHostToDevice, st);  // line 0, nodes
     if (e != hipSuccess) return herr(e);
     (void)hipEventRecord(s->e0, st);
     e = launch_enum(a, s->dtype == TSPGPU_F64, grid);
@@ -725,8 +769,12 @@ int tspgpu_search_counters(tspgpu_search *s, uint64_t *incumbent_bits, uint64_t 
     if (e == hipSuccess) e = hipStreamSynchronize(s->ctx->stream);
     if (e != hipSuccess) return herr(e);
     if (incumbent_bits) *incumbent_bits = w[1];
-    if (nodes) *nodes = w[2];
     if (records) *records = (uint32_t)w[3];
+    if (nodes) {
+        uint64_t st[4];
+        if (int rc = read_stats(s, st)) return rc;
+        *nodes = st[0];
+    }
     return 0;
 }
 
@@ -841,7 +889,7 @@ static int search_solve(tspgpu_ctx *c, const void *dist, int dtype, int n, doubl
         unsigned long long w = inc;
         rc = tspgpu_search_reset_records(s, (unsigned int)recs);
         if (!rc) rc = herr(hipMemcpy(s->d_words + 1, &w, 8, hipMemcpyHostToDevice));
-        if (!rc) rc = herr(hipMemset(s->d_words + 2, 0, 8));
+        if (!rc) rc = herr(hipMemset(s->d_stats, 0, kStatBytes));
         if (!rc) rc = tspgpu_search_run_all(s);
         if (!rc) rc = tspgpu_search_counters(s, &inc, &nodes, &recs);
         nodes_total += nodes;
@@ -884,11 +932,11 @@ static int search_solve(tspgpu_ctx *c, const void *dist, int dtype, int n, doubl
         stats->kernel_ms = s->ms;
         stats->items = s->items;
         stats->rounds = s->rounds;
-        unsigned long long u[3] = {0, 0, 0};
-        if (hipMemcpy(u, s->d_words + 5, sizeof u, hipMemcpyDeviceToHost) == hipSuccess) {
-            stats->lane_steps = u[0];
-            stats->active_steps = u[1];
-            stats->item_loads = u[2];
+        uint64_t u[4];
+        if (read_stats(s, u) == 0) {
+            stats->lane_steps = u[1];
+            stats->active_steps = u[2];
+            stats->item_loads = u[3];
         }
     }
     tspgpu_search_destroy(s);
