@@ -37,4 +37,7 @@ struct tspgpu_ctx {
     // K1-wide per-context cache (buffers + captured launch graph of the last n), hkwide.hip
     void *wide_cache = nullptr;
     void (*wide_free)(void *) = nullptr;
+    // K2 device buffers kept between searches (search_abi.cpp)
+    void *search_pool = nullptr;
+    void (*search_pool_free)(void *) = nullptr;
 };

@@ -55,7 +55,8 @@ struct tspgpu_search {
     unsigned long long *d_words = nullptr;
     unsigned long long *d_stats = nullptr;  // kStatLines x kStatStride: [0] nodes, [1..3] lane-step counters
     SearchRecord *d_rec = nullptr;
-    unsigned int rec_cap = 0;
+    unsigned int rec_cap = 0;    // records the kernels may write
+    unsigned int rec_alloc = 0;  // records d_rec holds
     SearchItem *d_items[2] = {nullptr, nullptr};  // round input / output (ping-pong)
     size_t item_cap[2] = {0, 0};
     int cur = 0;                 // d_items[cur] holds the pending items
@@ -88,6 +89,7 @@ struct tspgpu_search {
     size_t front_cap[2] = {0, 0};
     PathItem *d_tail = nullptr;
     unsigned int tail_cap = 1u << 23;
+    unsigned int tail_alloc = 0;
     uint64_t tails = 0;          // items waiting in d_tail
     int rounds = 0;
     double ms = 0.0;             // device time of all seed/round launches
@@ -247,6 +249,100 @@ uint64_t falling(int N, int D)
 
 }  // namespace
 
+// Device buffers a context keeps between searches (hipMalloc of the tail
+// and frontier buffers cost more than a 16-city search itself).  One set per
+// context: the next search takes it, its destroy gives it back.
+namespace {
+struct SearchPool {
+    void *d_dist = nullptr, *d_amin = nullptr;
+    unsigned long long *d_words = nullptr, *d_stats = nullptr;
+    SearchRecord *d_rec = nullptr;
+    unsigned int rec_alloc = 0;
+    SearchItem *d_items[2] = {nullptr, nullptr};
+    size_t item_cap[2] = {0, 0};
+    PathItem *d_front[2] = {nullptr, nullptr};
+    size_t front_cap[2] = {0, 0};
+    PathItem *d_tail = nullptr;
+    unsigned int tail_alloc = 0;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+};
+
+template <typename A, typename B>
+void move_buffers(A &to, B &from)
+{
+    to.d_dist = from.d_dist, from.d_dist = nullptr;
+    to.d_amin = from.d_amin, from.d_amin = nullptr;
+    to.d_words = from.d_words, from.d_words = nullptr;
+    to.d_stats = from.d_stats, from.d_stats = nullptr;
+    to.d_rec = from.d_rec, from.d_rec = nullptr;
+    to.rec_alloc = from.rec_alloc, from.rec_alloc = 0;
+    for (int i = 0; i < 2; ++i) {
+        to.d_items[i] = from.d_items[i], from.d_items[i] = nullptr;
+        to.item_cap[i] = from.item_cap[i], from.item_cap[i] = 0;
+        to.d_front[i] = from.d_front[i], from.d_front[i] = nullptr;
+        to.front_cap[i] = from.front_cap[i], from.front_cap[i] = 0;
+    }
+    to.d_tail = from.d_tail, from.d_tail = nullptr;
+    to.tail_alloc = from.tail_alloc, from.tail_alloc = 0;
+    to.e0 = from.e0, from.e0 = nullptr;
+    to.e1 = from.e1, from.e1 = nullptr;
+}
+
+template <typename A>
+void free_buffers(A &b)
+{
+    if (b.d_dist) (void)hipFree(b.d_dist);
+    if (b.d_amin) (void)hipFree(b.d_amin);
+    if (b.d_words) (void)hipFree(b.d_words);
+    if (b.d_stats) (void)hipFree(b.d_stats);
+    if (b.d_rec) (void)hipFree(b.d_rec);
+    for (int i = 0; i < 2; ++i) {
+        if (b.d_items[i]) (void)hipFree(b.d_items[i]);
+        if (b.d_front[i]) (void)hipFree(b.d_front[i]);
+    }
+    if (b.d_tail) (void)hipFree(b.d_tail);
+    if (b.e0) (void)hipEventDestroy(b.e0);
+    if (b.e1) (void)hipEventDestroy(b.e1);
+    SearchPool z;
+    move_buffers(b, z);
+}
+
+void pool_free(void *p)
+{
+    auto *pool = static_cast<SearchPool *>(p);
+    free_buffers(*pool);
+    delete pool;
+}
+
+void take_pool(tspgpu_search *s)
+{
+    SearchPool *pool = nullptr;
+    {
+        std::lock_guard<std::mutex> g(s->ctx->mu);
+        pool = static_cast<SearchPool *>(s->ctx->search_pool);
+        s->ctx->search_pool = nullptr;
+    }
+    if (!pool) return;
+    move_buffers(*s, *pool);
+    delete pool;
+}
+
+void give_pool(tspgpu_search *s)
+{
+    if (s->d_words == nullptr) return;  // a failed create: nothing worth keeping
+    auto *pool = new (std::nothrow) SearchPool();
+    if (!pool) return;
+    move_buffers(*pool, *s);
+    std::lock_guard<std::mutex> g(s->ctx->mu);
+    if (!s->ctx->search_pool) {
+        s->ctx->search_pool = pool;
+        s->ctx->search_pool_free = pool_free;
+        pool = nullptr;
+    }
+    if (pool) move_buffers(*s, *pool), delete pool;  // the context has one already: free ours
+}
+}  // namespace
+
 extern "C" {
 
 int tspgpu_search_create(tspgpu_ctx *c, const void *dist, int dtype, int n, int shard, int nshards, int depth,
@@ -335,17 +431,32 @@ int tspgpu_search_create(tspgpu_ctx *c, const void *dist, int dtype, int n, int 
         }
     }
     s->rec_cap = 1u << 16;
-    hipError_t e = hipMalloc(&s->d_dist, vb * n * n);
-    if (e == hipSuccess) e = hipMalloc(&s->d_amin, vb * n);
-    if (e == hipSuccess) e = hipMalloc((void **)&s->d_words, kWords * sizeof(unsigned long long));
-    if (e == hipSuccess) e = hipMalloc((void **)&s->d_stats, kStatBytes);
-    if (e == hipSuccess) e = hipMemset(s->d_stats, 0, kStatBytes);
-    if (e == hipSuccess && s->frontier) e = hipMalloc((void **)&s->d_tail, sizeof(PathItem) * s->tail_cap);
-    if (e == hipSuccess) e = hipMalloc((void **)&s->d_rec, sizeof(SearchRecord) * s->rec_cap);
-    if (e == hipSuccess) e = hipMemcpy(s->d_dist, dist, vb * n * n, hipMemcpyHostToDevice);
+    take_pool(s);  // device buffers of the context's previous search, if any
+    hipStream_t st = c->stream;
+    hipError_t e = hipSuccess;
+    if (!s->d_dist) e = hipMalloc(&s->d_dist, sizeof(double) * kSearchMaxN * kSearchMaxN);
+    if (e == hipSuccess && !s->d_amin) e = hipMalloc(&s->d_amin, sizeof(double) * kSearchMaxN);
+    if (e == hipSuccess && !s->d_words) e = hipMalloc((void **)&s->d_words, kWords * sizeof(unsigned long long));
+    if (e == hipSuccess && !s->d_stats) e = hipMalloc((void **)&s->d_stats, kStatBytes);
+    if (e == hipSuccess && s->frontier && s->d_tail && s->tail_alloc != s->tail_cap) {
+        (void)hipFree(s->d_tail);
+        s->d_tail = nullptr;
+    }
+    if (e == hipSuccess && s->frontier && !s->d_tail) {
+        e = hipMalloc((void **)&s->d_tail, sizeof(PathItem) * s->tail_cap);
+        if (e == hipSuccess) s->tail_alloc = s->tail_cap;
+    }
+    if (e == hipSuccess && s->rec_alloc < s->rec_cap) {
+        if (s->d_rec) (void)hipFree(s->d_rec);
+        s->d_rec = nullptr;
+        e = hipMalloc((void **)&s->d_rec, sizeof(SearchRecord) * s->rec_cap);
+        if (e == hipSuccess) s->rec_alloc = s->rec_cap;
+    }
+    if (e == hipSuccess) e = hipMemsetAsync(s->d_stats, 0, kStatBytes, st);
+    if (e == hipSuccess) e = hipMemcpyAsync(s->d_dist, dist, vb * n * n, hipMemcpyHostToDevice, st);
     if (e == hipSuccess)
-        e = hipMemcpy(s->d_amin, f64 ? (const void *)ad.data() : (const void *)ai.data(), vb * n,
-                      hipMemcpyHostToDevice);
+        e = hipMemcpyAsync(s->d_amin, f64 ? (const void *)ad.data() : (const void *)ai.data(), vb * n,
+                           hipMemcpyHostToDevice, st);
     unsigned long long w[kWords] = {};
     if (f64) {
         const double inf = INFINITY;
@@ -353,9 +464,10 @@ int tspgpu_search_create(tspgpu_ctx *c, const void *dist, int dtype, int n, int 
     } else {
         w[1] = (unsigned long long)INT32_MAX;
     }
-    if (e == hipSuccess) e = hipMemcpy(s->d_words, w, sizeof w, hipMemcpyHostToDevice);
-    if (e == hipSuccess) e = hipEventCreate(&s->e0);
-    if (e == hipSuccess) e = hipEventCreate(&s->e1);
+    if (e == hipSuccess) e = hipMemcpyAsync(s->d_words, w, sizeof w, hipMemcpyHostToDevice, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (e == hipSuccess && !s->e0) e = hipEventCreate(&s->e0);
+    if (e == hipSuccess && !s->e1) e = hipEventCreate(&s->e1);
     if (e != hipSuccess) {
         tspgpu_search_destroy(s);
         return herr(e);
@@ -369,20 +481,10 @@ int tspgpu_search_destroy(tspgpu_search *s)
     if (!s) return 0;
     (void)hipSetDevice(s->ctx->device);
     (void)hipStreamSynchronize(s->ctx->stream);
-    if (s->d_dist) (void)hipFree(s->d_dist);
-    if (s->d_amin) (void)hipFree(s->d_amin);
-    if (s->d_words) (void)hipFree(s->d_words);
-    if (s->d_stats) (void)hipFree(s->d_stats);
-    if (s->d_rec) (void)hipFree(s->d_rec);
-    if (s->d_tail) (void)hipFree(s->d_tail);
-    for (auto *p : s->d_front)
-        if (p) (void)hipFree(p);
+    give_pool(s);  // the buffers stay with the context for its next search
+    free_buffers(*s);
     if (s->d_ps) (void)hipFree(s->d_ps);
     if (s->d_ring) (void)hipFree(s->d_ring);
-    for (auto *p : s->d_items)
-        if (p) (void)hipFree(p);
-    if (s->e0) (void)hipEventDestroy(s->e0);
-    if (s->e1) (void)hipEventDestroy(s->e1);
     delete s;
     return 0;
 }
@@ -784,9 +886,13 @@ int tspgpu_search_reset_records(tspgpu_search *s, unsigned int capacity)
     (void)hipSetDevice(s->ctx->device);
     hipError_t e = hipStreamSynchronize(s->ctx->stream);
     if (e == hipSuccess && capacity > s->rec_cap) {
-        (void)hipFree(s->d_rec);
-        s->d_rec = nullptr;
-        e = hipMalloc((void **)&s->d_rec, sizeof(SearchRecord) * (size_t)capacity);
+        if (capacity > s->rec_alloc) {
+            (void)hipFree(s->d_rec);
+            s->d_rec = nullptr;
+            s->rec_alloc = 0;
+            e = hipMalloc((void **)&s->d_rec, sizeof(SearchRecord) * (size_t)capacity);
+            if (e == hipSuccess) s->rec_alloc = capacity;
+        }
         if (e == hipSuccess) s->rec_cap = capacity;
     }
     if (e == hipSuccess) e = hipMemset(s->d_words + 3, 0, 8);

@@ -364,6 +364,7 @@ int tspgpu_ctx_destroy(tspgpu_ctx *c)
         if (c->d_info[i]) (void)hipFree(c->d_info[i]);
     }
     if (c->wide_free) c->wide_free(c->wide_cache);
+    if (c->search_pool_free) c->search_pool_free(c->search_pool);
     if (c->d_slots) (void)hipFree(c->d_slots);
     if (c->d_dist) (void)hipFree(c->d_dist);
     if (c->d_cost) (void)hipFree(c->d_cost);
