@@ -240,17 +240,20 @@ struct ShiftTable {
     __device__ __forceinline__ V load(uint32_t idx) const { return g.load((uint32_t)((long)idx - SHIFT)); }
     __device__ __forceinline__ void store(uint32_t idx, V v) const { g.store((uint32_t)((long)idx - SHIFT), v); }
 };
-__host__ __device__ constexpr uint32_t max_layer_elems(int N)
+// largest layer of one parity (odd layers share buffer 0, even ones buffer 1)
+__host__ __device__ constexpr uint32_t max_layer_elems(int N, int parity)
 {
     uint32_t m = 0;
-    for (int t = 1; t <= N; ++t) m = m > cbinom(N, t) * t ? m : cbinom(N, t) * t;
+    for (int t = 1; t <= N; ++t)
+        if ((t & 1) == parity) m = m > cbinom(N, t) * t ? m : cbinom(N, t) * t;
     return m;
 }
-// byte offset of the parent bytes in a VAR-4 slot (behind the two buffers)
+// byte offset of the parent bytes in a VAR-4 slot (behind the two buffers,
+// each sized for its own parity: 0.77 MB instead of 0.82 MB live at n = 16)
 template <typename V>
 __host__ __device__ constexpr uint32_t parent_base(int N)
 {
-    return 2u * max_layer_elems(N) * (uint32_t)sizeof(V);
+    return (max_layer_elems(N, 1) + max_layer_elems(N, 0)) * (uint32_t)sizeof(V);
 }
 // Parents (N <= 15): for every SOURCE row T of layer t, one 64-bit word
 // holding, per non-member k of T (q-th non-member, 4 bits at 4q), m - 1 for
@@ -258,6 +261,14 @@ __host__ __device__ constexpr uint32_t parent_base(int N)
 // of destination (T+k, k).  One coalesced 8-byte store per row (consecutive
 // threads own consecutive rows) instead of N - t scattered bytes; word index
 // = the row's place in the colex mask list (mask_off(N, t) + rank).
+// Cache-policy bits of the parent-word stores (aux: 2 = nt, 16 = sc1).  The
+// words are read back only by the backtracking (N - 1 loads per block), so
+// they are stored non-temporal: the ping-pong values keep the Infinity Cache.
+// n = 16, 16384 blocks, 3 interleaved runs each: nt 12.39-12.40 ms, default
+// policy 13.3-14.3 ms, sc1 13.6 ms (profiles/r01/k1_parent_policy_n16.log).
+#ifndef TSPGPU_PAR_AUX
+#define TSPGPU_PAR_AUX 2
+#endif
 struct ParentTable {
     static constexpr bool on = true;
     __amdgpu_buffer_rsrc_t rs;
@@ -265,7 +276,8 @@ struct ParentTable {
     __device__ __forceinline__ void store(uint32_t widx, uint64_t w) const
     {
         using u2 = decltype(__builtin_amdgcn_raw_buffer_load_b64(rs, 0, 0, 0));
-        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2, w), rs, (int)(base + widx * 8u), 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2, w), rs, (int)(base + widx * 8u), 0,
+                                              TSPGPU_PAR_AUX);
     }
     __device__ __forceinline__ uint64_t load(uint32_t widx) const
     {
@@ -291,7 +303,7 @@ struct SplitTable {
         else if constexpr (A > 0 && t >= N - A + 1)
             return LdsTableT<V>{hi, (uint32_t)layer_off(N, N - A + 1)};
         else if constexpr (PP)
-            return ShiftTable<V, (long)layer_off(N, t) - ((t & 1) ? 0L : (long)max_layer_elems(N))>{g};
+            return ShiftTable<V, (long)layer_off(N, t) - ((t & 1) ? 0L : (long)max_layer_elems(N, 1))>{g};
         else
             return g;
     }
