@@ -193,12 +193,17 @@ struct GlobalTableT<int32_t> {
         __builtin_amdgcn_raw_buffer_store_b32((uint32_t)v, rs, (int)(idx * 4u), 0, 0);
     }
 };
+// cache-policy bits of the table value loads (development knob)
+#ifndef TSPGPU_VAL_LOAD_AUX
+#define TSPGPU_VAL_LOAD_AUX 0
+#endif
 template <>
 struct GlobalTableT<double> {
     __amdgpu_buffer_rsrc_t rs;
     __device__ __forceinline__ double load(uint32_t idx) const
     {
-        return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, (int)(idx * 8u), 0, 0));
+        return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, (int)(idx * 8u), 0,
+                                                                               TSPGPU_VAL_LOAD_AUX));
     }
     // a store at an offset past num_records is dropped by the buffer range
     // check: predication without a branch
