@@ -34,7 +34,7 @@ def child():
                          + ctx.download(dt, (B, n + 1), np.int32).tobytes()).hexdigest()[:12]
         tb = tspgpu.table_bytes_per_block(n) * B
         print(f"lib={os.path.basename(os.environ.get('TSPGPU_LIB', 'default'))} n={n} B={B} {ms:.3f} ms "
-              f"{B / ms * 1e3:.3e} blocks/s {tb / ms / 1e9:.3f} TB/s(alg) hash={h}", flush=True)
+              f"{B / ms * 1e3:.3e} blocks/s {tb / ms / 1e9:.3f} TB/s(alg) hash={h} grid={ctx.last_grid()}", flush=True)
 
 
 if __name__ == "__main__":

@@ -591,12 +591,22 @@ __device__ __forceinline__ void all_layers(const Tab &tab, const double *dl, con
 // VAR: 0 member sweep, 1 compact, 2 compact + next-row prefetch, 3 compact + two rows prefetched,
 // 4 = 2 + ping-pong values + parent bytes
 __host__ __device__ constexpr int var_pf(int var) { return var == 4 ? 1 : var - 1; }
-__host__ __device__ constexpr int min_waves(int N, int var)
+// The 512-thread variant-4 kernels (the n = 16 default: one workgroup per CU)
+// target 2 waves/SIMD, i.e. up to 256 VGPRs: 171 used, the LDS reads of a row
+// overlap instead of one round trip per relaxation, and SGPR spills fall from
+// 207 to 69; 11.85 ms vs 12.44 ms for 1024 threads at 4 waves/SIMD
+// (profiles/r01/k1_512x2_n16.log).
+#ifndef TSPGPU_K1_WAVES_512V4
+#define TSPGPU_K1_WAVES_512V4 2
+#endif
+__host__ __device__ constexpr int min_waves(int N, int var, int threads = 0)
 {
-    return var == 1 ? (N <= 15 ? 8 : 4) : (N <= 15 ? 4 : 2);
+    return (TSPGPU_K1_WAVES_512V4 > 0 && threads == 512 && var == 4) ? TSPGPU_K1_WAVES_512V4
+           : var == 1                                               ? (N <= 15 ? 8 : 4)
+                                                                    : (N <= 15 ? 4 : 2);
 }
 template <typename V, int N, bool LDS_TABLE, int THREADS, int VAR>
-__global__ __launch_bounds__(THREADS, min_waves(N, VAR)) void heldkarp_kernel(
+__global__ __launch_bounds__(THREADS, min_waves(N, VAR, THREADS)) void heldkarp_kernel(
     const V *__restrict__ dist, int nblocks, V *__restrict__ slots, size_t slot_doubles,
     const uint32_t *__restrict__ masks, const LayerInfo *__restrict__ info, V *__restrict__ cost_out,
     int32_t *__restrict__ tour_out)

@@ -181,6 +181,9 @@ int solve_device_locked(tspgpu_ctx *c, const void *d_dist, int n, int nblocks, v
         // (with a full wave of blocks: one block alone is latency-bound and the
         // argmin's extra VALU only costs there)
         a.variant = c->variant >= 0 ? c->variant : (N == 15 && vbytes == 8 && nblocks >= c->cu_count ? 4 : 2);
+        // variant 4 at 16 cities: one 512-thread workgroup per CU at 2 waves/SIMD
+        // (256 VGPRs; heldkarp_impl.h TSPGPU_K1_WAVES_512V4) beats 1024 threads at 4
+        if (c->threads <= 0 && a.variant == 4 && N == 15 && vbytes == 8) a.threads = 512;
         if (a.use_lds) {
             // as many resident workgroups as the LDS allows, then persistent
             const int per_cu = (int)(160 * 1024 / lds_bytes_for(N, true, threads_for(N, true, 0), vbytes == 4 || a.variant >= 1, vbytes));
