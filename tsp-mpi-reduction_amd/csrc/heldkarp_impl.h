@@ -590,7 +590,10 @@ __device__ __forceinline__ void all_layers(const Tab &tab, const double *dl, con
 // half of that (<= 64 VGPRs, 8 waves) at the reference's sizes.
 // VAR: 0 member sweep, 1 compact, 2 compact + next-row prefetch, 3 compact + two rows prefetched,
 // 4 = 2 + ping-pong values + parent bytes
-__host__ __device__ constexpr int var_pf(int var) { return var == 4 ? 1 : var - 1; }
+#ifndef TSPGPU_K1_V4_PF
+#define TSPGPU_K1_V4_PF 1  // rows prefetched by the variant-4 pass
+#endif
+__host__ __device__ constexpr int var_pf(int var) { return var == 4 ? TSPGPU_K1_V4_PF : var - 1; }
 // The 512-thread variant-4 kernels (the n = 16 default: one workgroup per CU)
 // target 2 waves/SIMD, i.e. up to 256 VGPRs: 171 used, the LDS reads of a row
 // overlap instead of one round trip per relaxation, and SGPR spills fall from
