@@ -440,6 +440,9 @@ __device__ __forceinline__ void layer_pass_lds(const LdsTable &tab, const double
 // thread, so the kernel runs at 8 waves/SIMD without spilling.
 // PF (prefetch depth): the masks and t values of the next PF rows are in
 // flight while the current row is relaxed (software pipelining, 2t VGPRs per row).
+#ifndef TSPGPU_K1_SELMIN
+#define TSPGPU_K1_SELMIN 0  // development knob: argmin pass keeps the minimum by select, not v_min_f64
+#endif
 template <typename V, int N, int T, int THREADS, int PF, typename SrcTab, typename DstTab, typename PTab = NoParents>
 __device__ __forceinline__ void layer_pass_compact(const SrcTab &src, const DstTab &dst, const V *__restrict__ dl,
                                                    const int *__restrict__ rl, const uint32_t *__restrict__ masks,
@@ -524,8 +527,14 @@ __device__ __forceinline__ void layer_pass_compact(const SrcTab &src, const DstT
                 const V cnd = g[j] + drow[kb[q]];
                 if constexpr (PTab::on) {
                     // first strict minimum over m ascending (tsp.cpp:465): the parent
+#if TSPGPU_K1_SELMIN
+                    const bool lt = cnd < acc[q];
+                    arg[q] = lt ? (uint32_t)m : arg[q];
+                    acc[q] = lt ? cnd : acc[q];
+#else
                     arg[q] = cnd < acc[q] ? (uint32_t)m : arg[q];
                     acc[q] = ValT<V>::vmin(acc[q], cnd);
+#endif
                 } else {
                     acc[q] = ValT<V>::vmin(acc[q], cnd);
                 }
