@@ -4,19 +4,24 @@
     python bench.py [--gpus N] [--steps K] [--warmup W] [--n 16] [--blocks-per-gpu B]
 
 One STEP = one launch of the K1 Held-Karp kernel over this rank's shard of B
-blocks (inputs already resident in HBM).  Ranks (torchrun, one per GPU) each
+blocks (inputs already resident in HBM).  Ranks (one process per GPU) each
 own a contiguous shard of the instance `./tsp n B*N 1000 1000` (the
 reference's own generator, srand(0)); there is no data-path collective, so
 scaling is weak.  A gloo process group provides the barriers and the
 max-over-ranks of the timed region (measurement only).
 
-`value` = DP relaxations (the search nodes of Held-Karp: one (S,k,m) extension
-G[S\\k][m] + d[m][k] with its min, tsp.cpp:457-470; N(N-1)2^(N-2) per block) of
-all ranks / max wall time.  Rank 0 prints ONE JSON line.
+`python bench.py --gpus N` without a launcher starts the N ranks itself (a
+torch.distributed.run child; this parent never touches the GPU); under
+torchrun (WORLD_SIZE set) each process is one rank, on GPU LOCAL_RANK.
+
+`value` = Held-Karp DP relaxations (one (S,k,m) extension G[S\\k][m] + d[m][k]
+with its min, tsp.cpp:457-470; N(N-1)2^(N-2) per block) of all ranks / max
+wall time.  The K2 branch-and-bound probes report B&B search nodes in their
+own keys (never mixed with relaxations).  Rank 0 prints ONE JSON line.
 
 The GPU is driven only through libtspgpu's C ABI (device buffers, stream and
 HIP-event timer included), so the HIP events sit on the stream the kernel runs
-on.  torch is used only for torch.distributed (gloo) when WORLD_SIZE > 1.
+on.  torch is used only for torch.distributed.
 """
 from __future__ import annotations
 
@@ -24,7 +29,9 @@ import argparse
 import json
 import math
 import os
+import re
 import shutil
+import socket
 import statistics
 import subprocess
 import sys
@@ -35,11 +42,18 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 PKG = os.path.join(ROOT, "tsp-mpi-reduction_amd")
 sys.path.insert(0, PKG)
-import tspgpu  # noqa: E402
+import tspgpu  # noqa: E402  (lazy: loads libtspgpu on first use, no HIP call at import)
 
 METRIC = "search nodes/sec (whole node) + time-to-optimal tour, 16-city, 1/2/4/8 GPU"
+UNIT = "Held-Karp DP relaxations/s"
 HBM_PEAK = 8.0e12  # B/s, MI355X_MICROARCH.md chip table (spec)
-DOMINANT_KERNEL = "heldkarp_kernel"
+KERNEL_NAMES = {5: "hk_tiled_kernel"}  # K1 variant -> kernel symbol (others: heldkarp_kernel)
+UBENCH = os.path.join(PKG, "bin", "ubench")
+TSP_BIN = os.path.join(PKG, "bin", "tsp")
+
+
+def kernel_name(variant):
+    return KERNEL_NAMES.get(variant, "heldkarp_kernel")
 
 
 def host_lib():
@@ -58,7 +72,7 @@ class Shard:
         L = host_lib()
         full = (tspgpu.City * (n * blocks_total))()
         L.tsphost_generate(n, blocks_total, grid, grid, full)
-        self.n, self.B = n, hi - lo
+        self.n, self.B, self.lo, self.hi = n, hi - lo, lo, hi
         self.arr = (tspgpu.City * (n * self.B)).from_buffer_copy(
             memoryview(full).cast("B")[lo * n * 24:hi * n * 24])
 
@@ -67,7 +81,7 @@ class Shard:
                 for j in range(self.n)]
 
     def distances(self):
-        """Host libm distance matrices, bit-exact with computeDistanceMatrix."""
+        """Host libm distances, bit-exact with computeDistanceMatrix."""
         return tspgpu.distance_matrix_array(self.arr, self.n, self.B)
 
 
@@ -77,8 +91,8 @@ def shard_bounds(rank, world, per_rank):
 
 
 class Group:
-    """Barrier + max-over-ranks for the timed region (gloo; measurement only,
-    the data path has no collective)."""
+    """Barrier + max/sum/gather over ranks (gloo; measurement only, the block
+    path has no data collective)."""
 
     def __init__(self, world):
         self.dist = None
@@ -93,23 +107,27 @@ class Group:
         if self.dist is not None:
             self.dist.barrier()
 
-    def allmax(self, x):
+    def _reduce(self, x, op):
         if self.dist is None:
             return x
         import torch
 
         t = torch.tensor([x], dtype=torch.float64)
-        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        self.dist.all_reduce(t, op=op)
         return float(t.item())
+
+    def allmax(self, x):
+        return self._reduce(x, self.dist.ReduceOp.MAX) if self.dist else x
 
     def allsum(self, x):
-        if self.dist is None:
-            return x
-        import torch
+        return self._reduce(x, self.dist.ReduceOp.SUM) if self.dist else x
 
-        t = torch.tensor([x], dtype=torch.float64)
-        self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM)
-        return float(t.item())
+    def gather(self, obj):
+        if self.dist is None:
+            return [obj]
+        out = [None] * self.dist.get_world_size()
+        self.dist.all_gather_object(out, obj)
+        return out
 
 
 def timed_steps(step, sync, group, warmup, steps, begin=None, end=None):
@@ -134,31 +152,108 @@ def timed_steps(step, sync, group, warmup, steps, begin=None, end=None):
     return group.allmax(wall), wall
 
 
-def cpu_baseline(n, seconds_budget=20.0):
-    """The reference's own tsp() (oracle/_ref, built from /root/reference at -O0)
-    timed on this host: P parallel processes, one block each, like
-    `mpirun -np P ./tsp n P ...` minus MPI startup.  Falls back to the C
-    oracle port when the reference binary is absent."""
-    ref = os.path.join(ROOT, "oracle", "_ref", "ref_harness")
-    cores = max(1, min(8, len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()))
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def spawn_ranks(argv, gpus):
+    """`bench.py --gpus N` with no launcher: start the N ranks as a child
+    torch.distributed.run (one process per GPU, 127.0.0.1 rendezvous) and
+    return its exit status.  This process never initialises the GPU, and it
+    starts the launcher as a child instead of exec'ing it."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__), *argv]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"),
+               OMP_NUM_THREADS=os.environ.get("OMP_NUM_THREADS", "4"))
+    return subprocess.call(cmd, env=env)
+
+
+# --------------------------------------------------------------------------
+# CPU baselines (rank 0, N = 1): the reference itself, then the oracle port
+# --------------------------------------------------------------------------
+def host_cpus():
+    """CPUs this process may use: the affinity set, capped by a cgroup CPU quota."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, int(int(quota) // int(period))))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
+def cpu_model():
+    try:
+        for ln in open("/proc/cpuinfo"):
+            if ln.startswith("model name"):
+                return ln.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def find_mpirun():
+    for c in (shutil.which("mpirun"), "/opt/conda/bin/mpirun"):
+        if c and os.path.exists(c):
+            return c
+    return None
+
+
+def cpu_baseline(n, max_ranks=None):
+    """The reference's own program timed on this host's cores: `mpirun -np P
+    ./tsp n P 1000 1000` with P = the usable cores (one 16-city block per
+    rank, the reference's own distribution, tsp() and reduction tree; the
+    binary is built from /root/reference at -O0 by oracle/Makefile, nothing
+    else from the reference is used).  value = P blocks' DP relaxations / the
+    program's own printed milliseconds (tsp.cpp:275-276, 360-363).  Without
+    mpirun: one reference tsp() per process (oracle/_ref/ref_harness timeone)
+    on every core; without the reference binaries: the C oracle port."""
+    cores = host_cpus()
+    P = cores if max_ranks is None else min(cores, max_ranks)
     relax = tspgpu.relaxations_per_block(n)
-    if os.path.exists(ref):
+    ref_tsp = os.path.join(ROOT, "oracle", "_ref", "tsp")
+    ref_h = os.path.join(ROOT, "oracle", "_ref", "ref_harness")
+    mpirun = find_mpirun()
+    base = {"unit": UNIT, "cores": P, "cpu_model": cpu_model(), "host_cpus_usable": cores}
+    if mpirun and os.path.exists(ref_tsp):
+        try:
+            env = dict(os.environ, OMP_NUM_THREADS="1")
+            cmd = [mpirun, "-np", str(P), ref_tsp, str(n), str(P), "1000", "1000"]
+            t0 = time.perf_counter()
+            p = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env, cwd="/tmp")
+            wall = time.perf_counter() - t0
+            m = re.search(r"TSP ran in (\d+) ms for (\d+) cities and the trip cost ([0-9.]+)", p.stdout)
+            if p.returncode == 0 and m:
+                ms = int(m.group(1))
+                return dict(base, value=P * relax / (ms * 1e-3), kind="reference", launcher="mpirun",
+                            sample=f"`{os.path.basename(mpirun)} -np {P} ./tsp {n} {P} 1000 1000` (the reference "
+                                   f"program, MPICH, one {n}-city block per rank): the program's own clock "
+                                   f"{ms} ms, process wall {wall:.2f} s, cost {m.group(3)}",
+                            blocks_per_s=P / (ms * 1e-3), reference_ms=ms, wall_s=wall)
+            sys.stderr.write(f"cpu_baseline: mpirun run failed rc={p.returncode}: {p.stderr[-300:]}\n")
+        except Exception as e:  # noqa: BLE001 - fall through to the per-process harness
+            sys.stderr.write(f"cpu_baseline: mpirun failed ({e})\n")
+    if os.path.exists(ref_h):
         try:
             t0 = time.perf_counter()
-            procs = [subprocess.Popen([ref, "timeone", str(n), str(cores), "1000", "1000", str(i)],
+            procs = [subprocess.Popen([ref_h, "timeone", str(n), str(P), "1000", "1000", str(i)],
                                       stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, text=True)
-                     for i in range(cores)]
-            outs = [p.communicate(timeout=seconds_budget * 6)[0] for p in procs]
+                     for i in range(P)]
+            outs = [p.communicate(timeout=600)[0] for p in procs]
             wall = time.perf_counter() - t0
             per = [float(ln.split()[2]) for o in outs for ln in o.splitlines() if ln.startswith("T ")]
-            if len(per) == cores and all(p.returncode == 0 for p in procs):
-                return {"value": cores * relax / wall, "unit": "search nodes/s", "cores": cores, "kind": "reference",
-                        "sample": f"{cores} blocks x {n} cities of `./tsp {n} {cores} 1000 1000`, reference tsp() "
-                                  f"(-O0, std::map Held-Karp) one block per process on {cores} cores; "
-                                  f"{wall:.1f} s wall, median block {statistics.median(per):.2f} s",
-                        "blocks_per_s": cores / wall}
-        except Exception as e:  # reference binary unusable here: fall back to the port
-            sys.stderr.write(f"cpu_baseline: reference run failed ({e}); using the oracle port\n")
+            if len(per) == P and all(p.returncode == 0 for p in procs):
+                return dict(base, value=P * relax / wall, kind="reference", launcher="per-process harness (no mpirun)",
+                            sample=f"{P} blocks x {n} cities of `./tsp {n} {P} 1000 1000`, the reference's tsp() "
+                                   f"(-O0) one block per process on {P} cores; {wall:.1f} s wall, median block "
+                                   f"{statistics.median(per):.2f} s", blocks_per_s=P / wall)
+        except Exception as e:  # noqa: BLE001
+            sys.stderr.write(f"cpu_baseline: reference harness failed ({e}); using the oracle port\n")
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_py as O
 
@@ -166,27 +261,27 @@ def cpu_baseline(n, seconds_budget=20.0):
     d = shard.distances()
     t0 = time.perf_counter()
     k = 0
-    while k < shard.B and time.perf_counter() - t0 < seconds_budget:
+    while k < shard.B and time.perf_counter() - t0 < 20.0:
         O.solve_block(d[k])
         k += 1
     wall = time.perf_counter() - t0
-    return {"value": k * relax / wall, "unit": "search nodes/s", "cores": 1, "kind": "port",
-            "sample": f"{k} blocks x {n} cities, oracle array Held-Karp (-O2), 1 core, {wall:.1f} s",
-            "blocks_per_s": k / wall}
+    return dict(base, value=k * relax / wall, cores=1, kind="port", launcher="none",
+                sample=f"{k} blocks x {n} cities, oracle array Held-Karp (-O2), 1 core, {wall:.1f} s",
+                blocks_per_s=k / wall)
 
 
 def cpu_optimized(n, seconds_budget=5.0):
     """A second, optimized CPU baseline beside the reference's own path
     (SURVEY.md §8(d)): the oracle's array Held-Karp (C, -O2, the same bits)
-    on up to 8 host threads (ctypes releases the GIL), on the same generated
+    on every usable host core (ctypes releases the GIL), on the same generated
     blocks.  Reported next to cpu_baseline, never as the headline."""
     import threading
 
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_py as O
 
-    cores = max(1, min(8, len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()))
-    shard = Shard(n, 256, 0, 256)
+    cores = host_cpus()
+    shard = Shard(n, max(256, 4 * cores), 0, max(256, 4 * cores))
     d = shard.distances()
     done = [0] * cores
     t0 = time.perf_counter()
@@ -205,21 +300,46 @@ def cpu_optimized(n, seconds_budget=5.0):
         t.join()
     wall = time.perf_counter() - t0
     k = sum(done)
-    return {"value": k * tspgpu.relaxations_per_block(n) / wall, "unit": "search nodes/s", "cores": cores,
+    return {"value": k * tspgpu.relaxations_per_block(n) / wall, "unit": UNIT, "cores": cores,
             "kind": "port", "sample": f"{k} blocks x {n} cities, oracle array Held-Karp (C -O2) on {cores} threads, "
                                       f"{wall:.1f} s", "blocks_per_s": k / wall}
 
 
-VALU_PEAK = 256 * 4 * 16 * 2.4e9  # lane-ops/s: 256 CUs x 4 SIMD16 x 2.4 GHz (f64 add/min and i32 alike)
+# --------------------------------------------------------------------------
+# Time to optimal, the reference's own definition: process start -> final line
+# --------------------------------------------------------------------------
+def cli_wall(n, reps=3):
+    """`bin/tsp n 1 1000 1000` (the drop-in program) as a child process: wall
+    time from spawn to exit (process start, HIP init, generation, K1, merge,
+    final line), best of `reps`, next to the ms the program prints itself
+    (tsp.cpp:275-276, 360-363 measure from main's first line)."""
+    if not os.path.exists(TSP_BIN):
+        return {"error": "bin/tsp not built"}
+    best = None
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        p = subprocess.run([TSP_BIN, str(n), "1", "1000", "1000"], capture_output=True, text=True, timeout=120)
+        wall = (time.perf_counter() - t0) * 1e3
+        m = re.search(r"TSP ran in (\d+) ms for (\d+) cities and the trip cost ([0-9.]+)", p.stdout)
+        if p.returncode != 0 or not m:
+            return {"error": f"rc={p.returncode} {p.stderr[-200:]}"}
+        if best is None or wall < best["process_wall_ms"]:
+            best = {"command": f"./tsp {n} 1 1000 1000", "process_wall_ms": wall, "program_ms": int(m.group(1)),
+                    "cost": m.group(3)}
+    return best
+
+
+# --------------------------------------------------------------------------
+# K2 probes (branch-and-bound search nodes, their own unit)
+# --------------------------------------------------------------------------
+VALU_PEAK_SPEC = 256 * 4 * 16 * 2.4e9  # f64 lane-ops/s at 2.4 GHz (half-rate f64 on SIMD32)
 
 
 def k2_exhaustive(ctx, n=14, reps=3):
     """BASELINE config 2: `./tsp 14 1 1000 1000` by exhaustive enumeration on
     one GPU (enum.hip: a lane per depth-7 prefix, its 720 completions folded in
-    registers).  Roofline: VALU issue — the algorithmic work is one f64 add
-    per partial path (node) plus one closing add and one min per tour, against
-    39.3 T lane-ops/s; nodes/s is also given against SURVEY §8(d)'s 9.8 T
-    (the LDS-bound DFS figure, which register tails no longer touch)."""
+    registers).  Roofline: VALU issue — one f64 add per partial path (node)
+    plus one closing add and one min per tour."""
     d = Shard(n, 1, 0, 1).distances()[0]
     best = None
     for _ in range(reps):
@@ -230,38 +350,45 @@ def k2_exhaustive(ctx, n=14, reps=3):
             best = (wall, cost, tour, st)
     wall, cost, tour, st = best
     sec = max(st["kernel_ms"] * 1e-3, 1e-12)
-    nps = st["nodes"] / sec
     tours = math.factorial(n - 1)
     ops = st["nodes"] + 2 * tours
     return {"instance": f"./tsp {n} 1 1000 1000 (block 0)", "cost": cost, "tour": [int(x) for x in tour],
             "time_to_optimal_ms": wall, "kernel_ms": st["kernel_ms"], "tours": tours,
-            "tours_per_s": tours / sec, "nodes": st["nodes"], "nodes_per_s": nps,
-            "node_rate_vs_survey_lds_bound": nps / 9.8e12,
-            "roofline": {"bound": "valu", "achieved": ops / sec / 1e12, "peak": VALU_PEAK / 1e12,
-                         "unit": "T lane-ops/s", "frac": ops / sec / VALU_PEAK,
+            "tours_per_s": tours / sec, "bb_nodes": st["nodes"], "bb_nodes_per_s": st["nodes"] / sec,
+            "roofline": {"bound": "valu", "achieved": ops / sec / 1e12, "peak": VALU_PEAK_SPEC / 1e12,
+                         "unit": "T f64 lane-ops/s", "frac": ops / sec / VALU_PEAK_SPEC,
                          "note": "enum_kernel: (nodes + 2 x tours) algorithmic f64 ops / HIP-event kernel time"},
             "rounds": st["rounds"]}
 
 
-def k2_single_instance(ctx, n, world, rank, local_rank, reps=3):
-    """K2 (prefix-parallel branch and bound, one instance over the whole GPU or,
-    with N ranks, sharded over N GPUs with an all-reduce MIN of the incumbent
-    between rounds over RCCL) on the reference's own instance `./tsp n 1 1000
-    1000`: time to the optimal tour and search nodes per second."""
+def k2_instance(n, seed):
+    """Config 5's extension instance: n uniform random cities in [0,1000)^2
+    (seeded), libm distances like computeDistanceMatrix."""
+    rng = np.random.default_rng(seed)
+    xy = rng.uniform(0, 1000, size=(n, 2))
+    return tspgpu.distance_matrix([[(i, xy[i, 0], xy[i, 1]) for i in range(n)]])[0]
+
+
+def k2_group(world, local_rank):
+    if world == 1:
+        return None, "none"
+    import torch
+    import torch.distributed as dist
+
+    if torch.cuda.is_available():
+        torch.cuda.set_device(local_rank % max(1, torch.cuda.device_count()))
+        return dist.new_group(backend="nccl"), "nccl"
+    return dist.new_group(backend="gloo"), "gloo"
+
+
+def k2_single_instance(ctx, n, group, backend, world, reps=3):
+    """K2 on the reference's own instance `./tsp n 1 1000 1000` (config 3's
+    16 cities): time to the optimal tour and B&B nodes (sharded over the ranks
+    with RCCL between rounds when N > 1)."""
     import search_dist
 
-    blk = Shard(n, 1, 0, 1)
-    d = blk.distances()[0]
-    group, backend = None, "none"
-    if world > 1:
-        import torch
-        import torch.distributed as dist
+    d = Shard(n, 1, 0, 1).distances()[0]
 
-        if torch.cuda.is_available():
-            torch.cuda.set_device(local_rank)
-            group, backend = dist.new_group(backend="nccl"), "nccl"
-        else:
-            group, backend = dist.new_group(backend="gloo"), "gloo"
     def best_of(fn):
         best = None
         for _ in range(reps):
@@ -272,8 +399,6 @@ def k2_single_instance(ctx, n, world, rank, local_rank, reps=3):
                 best = (wall, cost, tour, st)
         return best
 
-    # one GPU: the native round loop (tspgpu_search_solve, what `bin/tsp_search`
-    # runs); the Python exchange loop of search_dist is timed beside it
     sharded = best_of(lambda: search_dist.solve_sharded(ctx, d, group=group))
     if world == 1:
         wall, cost, tour, st = best_of(lambda: tspgpu.search_solve(ctx, d))
@@ -282,70 +407,74 @@ def k2_single_instance(ctx, n, world, rank, local_rank, reps=3):
     else:
         wall, cost, tour, st = sharded
     return {"instance": f"./tsp {n} 1 1000 1000 (block 0)", "cost": cost, "time_to_optimal_ms": wall,
-            "kernel_ms": st["kernel_ms"], "nodes": st["nodes"],
-            "nodes_per_s": st["nodes"] / max(st["kernel_ms"] * 1e-3, 1e-12), "rounds": st["rounds"],
+            "kernel_ms": st["kernel_ms"], "bb_nodes_expanded": st["nodes"],
+            "bb_nodes_per_s": st["nodes"] / max(st["kernel_ms"] * 1e-3, 1e-12), "rounds": st["rounds"],
             "exchanges": st["exchanges"], "ranks": world, "exchange_backend": backend,
             "path": "tspgpu_search_solve (native rounds)" if world == 1 else "search_dist.solve_sharded",
             "python_exchange_loop_ms": sharded[0],
             "optimal_tours": st["optimal_tours"], "tour": [int(x) for x in tour]}
 
 
-def pmc_traffic(n, blocks, timeout=90):
-    """HBM bytes per launch of the dominant kernel from rocprofv3 PMC counters,
-    one counter group per pass (MI355X_MICROARCH.md §HBM / rocprofv3 PMC slots):
-    FETCH_SIZE and WRITE_SIZE (KiB) in separate passes; FETCH_SIZE is doubled
-    because gfx950 tallies 128-B requests at 64 B."""
+def k2_strong_scaling(ctx, n, seed, group, backend, world, rank, reps=2):
+    """Strong scaling of ONE instance over the N ranks (config 3/5 shape): the
+    prefix space is sharded statically (prefix p -> rank p mod N), every rank
+    runs its device queue in rounds and the 64-bit incumbent is all-reduced
+    (MIN) between rounds over RCCL; the optimal records are gathered at the
+    end for the DP tie rule.  time_to_optimal_ms = max over ranks of the
+    solve's wall time (distances already on the host)."""
+    import search_dist
+
+    d = k2_instance(n, seed)
+    best = None
+    for _ in range(reps):
+        if group is not None:
+            import torch.distributed as dist
+
+            dist.barrier(group=group)
+        t = time.perf_counter()
+        cost, tour, st = search_dist.solve_sharded(ctx, d, group=group)
+        wall = (time.perf_counter() - t) * 1e3
+        if best is None or wall < best[0]:
+            best = (wall, cost, tour, st)
+    wall, cost, tour, st = best
+    return {"instance": f"{n} uniform random cities in [0,1000)^2, seed {seed} (config 5 shape)", "n": n,
+            "ranks": world, "backend": backend, "cost": cost, "tour": [int(x) for x in tour],
+            "rank_wall_ms": wall, "rank_kernel_ms": st["kernel_ms"], "rank_nodes": st["rank_nodes"],
+            "bb_nodes_expanded": st["nodes"], "rounds": st.get("rounds"), "exchanges": st["exchanges"],
+            "optimal_tours": st["optimal_tours"]}
+
+
+# --------------------------------------------------------------------------
+# Roofline inputs: live VALU peak and PMC passes (rank 0, N = 1)
+# --------------------------------------------------------------------------
+def valu_peaks():
+    """Issue rates measured on this GPU by bin/ubench (the relaxation's own
+    instruction mix: v_add_f64, v_cmp_lt_f64, v_cndmask_b32, v_min_f64)."""
+    if not os.path.exists(UBENCH):
+        return None
+    p = subprocess.run(["timeout", "-k", "5", "60", UBENCH, "valu"], capture_output=True, text=True)
+    if p.returncode != 0:
+        return None
+    out = {}
+    for ln in p.stdout.splitlines():
+        r = json.loads(ln)
+        if "mix" in r:
+            out[r["mix"]] = r["lane_ops_per_s"]
+    return out
+
+
+def _rocprof_pass(counters, n, blocks, kernel, tag, timeout=90):
     rocprof = shutil.which("rocprofv3")
     if not rocprof:
         return None, "rocprofv3 not found"
-    out = {}
-    for counter in ("FETCH_SIZE", "WRITE_SIZE"):
-        d = os.path.join(ROOT, "gpurun_out", f"pmc_{counter}")
-        shutil.rmtree(d, ignore_errors=True)
-        cmd = ["timeout", "-s", "KILL", str(timeout), rocprof, "--pmc", counter, "--output-format", "csv",
-               "-d", d, "-o", "pmc", "--", sys.executable, os.path.abspath(__file__), "--pmc-child",
-               "--n", str(n), "--blocks-per-gpu", str(blocks)]
-        p = subprocess.run(cmd, capture_output=True, text=True, cwd="/tmp")
-        vals = []
-        for root, _, files in os.walk(d):
-            for f in files:
-                if f.endswith("counter_collection.csv"):
-                    import csv
-
-                    with open(os.path.join(root, f)) as fh:
-                        for row in csv.DictReader(fh):
-                            if DOMINANT_KERNEL in row.get("Kernel_Name", "") and row.get("Counter_Name") == counter:
-                                vals.append(float(row["Counter_Value"]))
-        if p.returncode != 0 or not vals:
-            return None, f"{counter}: rc={p.returncode} {p.stderr[-300:]}"
-        out[counter] = statistics.median(vals) * 1024.0  # KiB -> B per launch
-    fetch = out["FETCH_SIZE"] * 2.0
-    return fetch + out["WRITE_SIZE"], {"fetch_size_bytes_raw": out["FETCH_SIZE"], "write_size_bytes": out["WRITE_SIZE"],
-                                       "fetch_corrected_x2": fetch}
-
-
-SQ_PASS = ("SQ_WAVES", "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES", "SQ_ACTIVE_INST_VALU", "SQ_INSTS_VALU",
-           "SQ_ACTIVE_INST_LDS", "SQ_LDS_BANK_CONFLICT", "GRBM_GUI_ACTIVE")
-
-
-def pmc_counters(n, blocks, cus, timeout=90):
-    """One more rocprofv3 pass (7 SQ + 1 GRBM counters, within one pass's
-    limits) over the dominant kernel: VALU activity, LDS bank conflicts and
-    wave occupancy.  SQ_*_CYCLES / SQ_ACTIVE_INST_* count quad-cycles
-    (MI355X_MICROARCH.md); GRBM_GUI_ACTIVE is summed over the 8 XCDs."""
-    rocprof = shutil.which("rocprofv3")
-    if not rocprof:
-        return None
-    d = os.path.join(ROOT, "gpurun_out", "pmc_sq")
+    d = os.path.join(ROOT, "gpurun_out", f"pmc_{tag}")
     shutil.rmtree(d, ignore_errors=True)
-    cmd = ["timeout", "-s", "KILL", str(timeout), rocprof, "--pmc", *SQ_PASS, "--output-format", "csv",
+    cmd = ["timeout", "-s", "KILL", str(timeout), rocprof, "--pmc", *counters, "--output-format", "csv",
            "-d", d, "-o", "pmc", "--", sys.executable, os.path.abspath(__file__), "--pmc-child",
            "--n", str(n), "--blocks-per-gpu", str(blocks)]
     p = subprocess.run(cmd, capture_output=True, text=True, cwd="/tmp")
-    if p.returncode != 0:
-        return {"error": f"rc={p.returncode} {p.stderr[-300:]}"}
-    import csv
     import collections
+    import csv
 
     vals = collections.defaultdict(list)
     for root, _, files in os.walk(d):
@@ -353,22 +482,57 @@ def pmc_counters(n, blocks, cus, timeout=90):
             if f.endswith("counter_collection.csv"):
                 with open(os.path.join(root, f)) as fh:
                     for row in csv.DictReader(fh):
-                        if DOMINANT_KERNEL in row.get("Kernel_Name", ""):
+                        if kernel in row.get("Kernel_Name", ""):
                             vals[row["Counter_Name"]].append(float(row["Counter_Value"]))
-    c = {k: statistics.median(v) for k, v in vals.items()}
-    if not all(k in c for k in SQ_PASS):
-        return {"error": "missing counters", "got": sorted(c)}
-    cycles = c["GRBM_GUI_ACTIVE"] / 8.0  # per XCD = kernel cycles
-    simds = 4 * cus
-    return {
-        "valu_active_per_simd_cycle": 4.0 * c["SQ_ACTIVE_INST_VALU"] / (simds * cycles),
-        "valu_instructions_per_block": c["SQ_INSTS_VALU"] / blocks,
-        "lds_bank_conflict_cycles_over_lds_active": c["SQ_LDS_BANK_CONFLICT"] / max(c["SQ_ACTIVE_INST_LDS"], 1.0),
-        "mean_resident_waves_per_cu": 4.0 * c["SQ_WAVE_CYCLES"] / (cus * cycles),
-        "waves": c["SQ_WAVES"],
-        "raw": c,
-        "blocks_per_launch": blocks,
-    }
+    if p.returncode != 0 or not vals:
+        return None, f"rc={p.returncode} {p.stderr[-300:]}"
+    return {k: statistics.median(v) for k, v in vals.items()}, None
+
+
+SQ_PASS = ("SQ_WAVES", "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES", "SQ_ACTIVE_INST_VALU", "SQ_INSTS_VALU",
+           "SQ_ACTIVE_INST_LDS", "SQ_LDS_BANK_CONFLICT", "GRBM_GUI_ACTIVE")
+EA_PASS = ("TCC_EA0_RDREQ_sum", "TCC_EA0_RDREQ_DRAM_sum", "TCC_EA0_WRREQ_sum", "TCC_EA0_WRREQ_DRAM_sum")
+
+
+def pmc_profile(n, blocks, cus, kernel):
+    """rocprofv3 passes over the dominant kernel (one counter group per pass,
+    MI355X_MICROARCH.md §rocprofv3 PMC slots):
+      FETCH_SIZE, WRITE_SIZE — bytes at the L2's memory side (Infinity-Cache
+        hits included; FETCH_SIZE x2: calibrated on 8-B loads, profiles/r02);
+      TCC_EA0_{RD,WR}REQ[_DRAM] — the same requests split by whether DRAM
+        served them, i.e. what HBM actually moved;
+      SQ — VALU activity, instructions, LDS bank conflicts, occupancy."""
+    out = {"blocks_per_launch": blocks}
+    f, err = _rocprof_pass(("FETCH_SIZE",), n, blocks, kernel, "fetch")
+    w, err2 = _rocprof_pass(("WRITE_SIZE",), n, blocks, kernel, "write")
+    ea, err3 = _rocprof_pass(EA_PASS, n, blocks, kernel, "ea")
+    sq, err4 = _rocprof_pass(SQ_PASS, n, blocks, kernel, "sq")
+    if f and w:
+        out["fabric_read_bytes"] = f["FETCH_SIZE"] * 1024 * 2
+        out["fabric_write_bytes"] = w["WRITE_SIZE"] * 1024
+    if ea:
+        rd, rdd = ea.get("TCC_EA0_RDREQ_sum", 0), ea.get("TCC_EA0_RDREQ_DRAM_sum", 0)
+        wr, wrd = ea.get("TCC_EA0_WRREQ_sum", 0), ea.get("TCC_EA0_WRREQ_DRAM_sum", 0)
+        out["dram_read_frac"] = rdd / rd if rd else None
+        out["dram_write_frac"] = wrd / wr if wr else None
+        if "fabric_read_bytes" in out:
+            out["hbm_bytes"] = (out["fabric_read_bytes"] * (out["dram_read_frac"] or 0) +
+                                out["fabric_write_bytes"] * (out["dram_write_frac"] or 0))
+        out["ea_raw"] = ea
+    if sq and all(k in sq for k in SQ_PASS):
+        cycles = sq["GRBM_GUI_ACTIVE"] / 8.0  # per XCD = kernel cycles
+        simds = 4 * cus
+        out.update({
+            "valu_active_per_simd_cycle": 4.0 * sq["SQ_ACTIVE_INST_VALU"] / (simds * cycles),
+            "valu_instructions_per_block": sq["SQ_INSTS_VALU"] / blocks,
+            "lds_bank_conflict_cycles_over_lds_active": sq["SQ_LDS_BANK_CONFLICT"] / max(sq["SQ_ACTIVE_INST_LDS"], 1.0),
+            "mean_resident_waves_per_cu": 4.0 * sq["SQ_WAVE_CYCLES"] / (cus * cycles),
+            "sq_raw": sq,
+        })
+    errs = [e for e in (err, err2, err3, err4) if e]
+    if errs:
+        out["errors"] = errs
+    return out
 
 
 def pmc_child(args):
@@ -382,6 +546,22 @@ def pmc_child(args):
     ctx.synchronize()
 
 
+def plumbing(args, world, rank):
+    """--plumbing (CPU, no GPU): the multi-rank orchestration alone — shard
+    bounds of every rank, the barrier-bracketed region and the max over
+    ranks — printed by rank 0 (tests/test_bench_cli.py)."""
+    group = Group(world)
+    lo, hi = shard_bounds(rank, world, args.blocks_per_gpu)
+    wall_max, wall = timed_steps(lambda: None, lambda: None, group, args.warmup, args.steps)
+    shards = group.gather([lo, hi])
+    if rank == 0:
+        print(json.dumps({"plumbing": True, "metric": METRIC, "n_gpus": world, "steps": args.steps,
+                          "warmup": args.warmup, "shards": shards, "wall_max_s": wall_max,
+                          "global_blocks": args.blocks_per_gpu * world}), flush=True)
+    if group.dist is not None:
+        group.dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -389,22 +569,31 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--n", type=int, default=16, help="cities per block (config 3: 16)")
     ap.add_argument("--blocks-per-gpu", type=int, default=16384)
+    ap.add_argument("--k2-n", type=int, default=19, help="cities of the K2 strong-scaling instance")
+    ap.add_argument("--k2-seed", type=int, default=1)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pmc", action="store_true")
-    ap.add_argument("--no-tto", action="store_true", help="skip the one-block time-to-optimal probe")
-    ap.add_argument("--no-k2", action="store_true", help="skip the K2 single-instance search probe")
+    ap.add_argument("--no-tto", action="store_true", help="skip the time-to-optimal probes")
+    ap.add_argument("--no-k2", action="store_true", help="skip the K2 search probes")
+    ap.add_argument("--plumbing", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
     if args.pmc_child:
         return pmc_child(args)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(sys.argv[1:], args.gpus))
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.plumbing:
+        return plumbing(args, world, rank)
     group = Group(world)
 
     n, Bp = args.n, args.blocks_per_gpu
-    ctx = tspgpu.Context(device=local_rank, strict=False)
+    ndev = max(1, tspgpu.device_count())
+    device = local_rank % ndev
+    ctx = tspgpu.Context(device=device, strict=False)
     cu, devname = ctx.device_info()
     lo, hi = shard_bounds(rank, world, Bp)
     shard = Shard(n, Bp * world, lo, hi)
@@ -423,11 +612,14 @@ def main():
     wall_max, _ = timed_steps(step, ctx.synchronize, group, args.warmup, args.steps, begin=ctx.timer_start,
                               end=stop_events)
     kernel_ms = ev["ms"] / args.steps
+    variant = ctx.last_variant()
+    kname = kernel_name(variant)
 
-    # correctness of what was timed: every tour's left fold equals its cost
+    # correctness of what was timed: every tour is a permutation whose left fold equals its cost
     cost = ctx.download(dc, (Bp,), np.float64)
     tour = ctx.download(dt, (Bp, n + 1), np.int32)
     for b in range(0, Bp, max(1, Bp // 64)):
+        assert sorted(tour[b, :n].tolist()) == list(range(n)) and tour[b, 0] == 0 and tour[b, n] == 0
         acc = 0.0
         for i in range(n):
             acc = acc + d[b, tour[b, i], tour[b, i + 1]]
@@ -437,24 +629,27 @@ def main():
     total_blocks = Bp * world * args.steps
     value = total_blocks * relax / wall_max
 
-    # time-to-optimal: one block, host libm distances + copy + kernel + copy back
-    tto, one_kernel_ms, wide_ms = [float("nan")], float("nan"), float("nan")
+    # time to optimal: one block through the ABI (in process), and the whole
+    # program as a child process (the reference's definition)
+    tto = {}
     if not args.no_tto:
-        tto = []
+        t_one = []
         one = [shard.block(0)]
         for _ in range(10):
             t = time.perf_counter()
             ctx.solve_cities(one)
-            tto.append((time.perf_counter() - t) * 1e3)
+            t_one.append((time.perf_counter() - t) * 1e3)
         d1, c1, t1 = ctx.upload(d[:1]), ctx.alloc(8), ctx.alloc((n + 1) * 4)
         ctx.timer_start()
         for _ in range(10):
             ctx.solve_device(d1, n, 1, c1, t1, stream)
-        one_kernel_ms = ctx.timer_stop() / 10
-        # the same block with every CU on each DP layer (K1-wide)
+        tto["one_block_kernel_ms"] = ctx.timer_stop() / 10
         wide = [ctx.solve_instance(d[0]) for _ in range(5)]
         assert all(w[0] == cost[0] for w in wide), "K1-wide disagrees with K1"
-        wide_ms = min(w[2] for w in wide)
+        tto["one_block_whole_gpu_kernel_ms"] = min(w[2] for w in wide)
+        tto["one_block_in_process_ms"] = statistics.median(t_one)
+        if rank == 0:
+            tto["cli_wall_ms"] = {f"n{m}": cli_wall(m) for m in (14, 16)}
 
     # extension probe: the same launch on the rounded integer matrices (K1 i32)
     i32 = None
@@ -474,49 +669,57 @@ def main():
             for p_ in (pi, ci, ti):
                 ctx.free(p_)
             i32 = {"kernel_ms_per_launch": i32_ms, "blocks_per_s": Bp / (i32_ms * 1e-3),
-                   "relaxations_per_s": Bp * tspgpu.relaxations_per_block(n) / (i32_ms * 1e-3),
-                   "hbm_alg_GBps": tspgpu.table_bytes_per_block(n) / 2 * Bp / (i32_ms * 1e-3) / 1e9,
+                   "relaxations_per_s": Bp * relax / (i32_ms * 1e-3), "variant": ctx.last_variant(),
                    "note": "extension (no reference counterpart): rint(distances) as int32, same DP and tie rule"}
-        except Exception as e:  # the probe must never cost the headline line
+        except Exception as e:  # noqa: BLE001 - the probe must never cost the headline line
             i32 = {"error": f"{type(e).__name__}: {e}"}
 
-    exh = None
-    if not args.no_k2 and os.environ.get("BENCH_K2", "1") != "0" and rank == 0:
-        try:
-            exh = k2_exhaustive(ctx)
-        except Exception as e:  # the probe must never cost the headline line
-            exh = {"error": f"{type(e).__name__}: {e}"}
-
-    k2 = None
+    k2 = k2s = exh = None
     if not args.no_k2 and os.environ.get("BENCH_K2", "1") != "0":
         try:
-            k2 = k2_single_instance(ctx, n, world, rank, local_rank)
-        except Exception as e:  # the probe must never cost the headline line
+            kgroup, backend = k2_group(world, local_rank)
+        except Exception as e:  # noqa: BLE001
+            kgroup, backend = None, f"error: {e}"
+        if rank == 0:
+            try:
+                exh = k2_exhaustive(ctx)
+            except Exception as e:  # noqa: BLE001
+                exh = {"error": f"{type(e).__name__}: {e}"}
+        try:
+            k2 = k2_single_instance(ctx, n, kgroup, backend, world)
+        except Exception as e:  # noqa: BLE001
             k2 = {"error": f"{type(e).__name__}: {e}"}
+        try:
+            k2s = k2_strong_scaling(ctx, args.k2_n, args.k2_seed, kgroup, backend, world, rank)
+            walls = group.gather(k2s["rank_wall_ms"])
+            k2s["time_to_optimal_ms"] = max(walls)
+            k2s["bb_nodes_per_s"] = k2s["bb_nodes_expanded"] / (k2s["time_to_optimal_ms"] * 1e-3)
+            k2s["rank_walls_ms"] = walls
+        except Exception as e:  # noqa: BLE001
+            k2s = {"error": f"{type(e).__name__}: {e}"}
 
     if rank != 0:
+        if group.dist is not None:
+            group.barrier()
         return
-    alg_bytes = tspgpu.table_bytes_per_block(n) * Bp
-    achieved = alg_bytes / (kernel_ms * 1e-3)
-    traffic, traffic_note = (None, "skipped")
+    alg_bytes_per_block = tspgpu.table_bytes_per_block(n)
+    prof = None
     if world == 1 and not args.no_pmc:
-        traffic, traffic_note = pmc_traffic(n, min(Bp, 4096))
-        if traffic is not None:
-            traffic = traffic * (Bp / min(Bp, 4096))  # per launch of this run's size (same per-block bytes)
-    counters = None
-    if world == 1 and not args.no_pmc:
-        counters = pmc_counters(n, min(Bp, 4096), cu)
-    cpu, cpu_opt = None, None
+        prof = pmc_profile(n, min(Bp, 4096), cu, kname)
+    peaks = valu_peaks() if world == 1 else None
+    relax_s_kernel = Bp * relax / (kernel_ms * 1e-3)
+    roof = roofline(variant, kname, n, Bp, kernel_ms, relax_s_kernel, alg_bytes_per_block, prof, peaks)
+    cpu = cpu_opt = None
     if world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(n)
         try:
             cpu_opt = cpu_optimized(n)
-        except Exception as e:  # never costs the headline line
+        except Exception as e:  # noqa: BLE001
             cpu_opt = {"error": f"{type(e).__name__}: {e}"}
     line = {
         "metric": METRIC,
         "value": value,
-        "unit": "search nodes/s (Held-Karp DP relaxations)",
+        "unit": UNIT,
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
@@ -529,27 +732,67 @@ def main():
         "config": {"workload": f"{n}-city blocks, exact Held-Karp per block (config 3 cities/block; "
                                f"./tsp {n} {Bp * world} 1000 1000 instance)",
                    "n": n, "blocks_per_gpu": Bp, "global_blocks": Bp * world,
-                   "parallelism": f"blocks sharded over {world} rank(s), no data-path collective"},
+                   "parallelism": f"blocks sharded over {world} rank(s) (one per GPU), no data-path collective",
+                   "k1_variant": variant, "kernel": kname},
         "blocks_per_s": total_blocks / wall_max,
-        "time_to_optimal_ms": {"one_block_end_to_end_median": statistics.median(tto),
-                               "one_block_kernel": one_kernel_ms,
-                               "one_block_whole_gpu_kernel": wide_ms},
         "kernel_ms_per_launch": kernel_ms,
-        "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK, "traffic": traffic,
-                     "note": f"{DOMINANT_KERNEL} (n={n}): algorithmic bytes = 2*8*N*2^(N-1) per block "
-                             f"(each DP entry written once, read once) x {Bp} blocks per launch / HIP-event "
-                             f"launch time; traffic = PMC HBM bytes per launch ({traffic_note})"},
-        "counters": counters,
+        "time_to_optimal": tto,
+        "roofline": roof,
+        "counters": prof,
+        "valu_peaks_measured": peaks,
         "cpu_baseline": cpu,
         "cpu_optimized": cpu_opt,
         "k2_single_instance": k2,
-        "k1_i32_extension": i32,
+        "k2_strong_scaling": k2s,
         "k2_exhaustive_14": exh,
+        "k1_i32_extension": i32,
         "device": devname,
         "cus": cu,
     }
     print(json.dumps(line), flush=True)
+    if group.dist is not None:
+        group.barrier()
+
+
+def roofline(variant, kname, n, Bp, kernel_ms, relax_s, alg_bytes_per_block, prof, peaks):
+    """The dominant kernel against the ceiling that binds it.
+
+    VALU: every relaxation needs four VALU instructions (v_add_f64, v_cmp_lt_f64,
+    v_cndmask_b32 for the argmin that gives the tour, v_min_f64); the peak is
+    that same mix's issue rate measured on this GPU (bin/ubench), so frac =
+    relaxations/s / peak relaxations/s.
+    Memory: the bytes HBM actually moved per launch (PMC fabric bytes x the
+    DRAM share of the EA requests), against 8 TB/s.
+    The line reports whichever fraction is higher as `roofline` (the binding
+    one) and the other as `other`."""
+    mix = "f64 relaxation+argmin (add,cmp,cndmask,min)"
+    peak_relax = (peaks or {}).get(mix)
+    scale = Bp / (prof or {}).get("blocks_per_launch", Bp)
+    hbm = (prof or {}).get("hbm_bytes")
+    hbm = hbm * scale if hbm is not None else None
+    fabric = None
+    if prof and "fabric_read_bytes" in prof:
+        fabric = (prof["fabric_read_bytes"] + prof["fabric_write_bytes"]) * scale
+    valu = None
+    if peak_relax:
+        valu = {"bound": "valu", "achieved": 4 * relax_s / 1e12, "peak": 4 * peak_relax / 1e12,
+                "unit": "T VALU lane-instructions/s", "frac": relax_s / peak_relax, "traffic": hbm,
+                "note": f"{kname} (n={n}): 4 VALU instructions per DP relaxation x {Bp} blocks x "
+                        f"{tspgpu.relaxations_per_block(n):.0f} relaxations / HIP-event launch time; peak = the "
+                        f"same 4-instruction mix measured by bin/ubench on this GPU ({peak_relax:.3e} "
+                        f"relaxations/s); traffic = HBM bytes per launch (PMC)"}
+    mem = None
+    if hbm is not None:
+        mem = {"bound": "hbm", "achieved": hbm / (kernel_ms * 1e-3) / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
+               "frac": hbm / (kernel_ms * 1e-3) / HBM_PEAK, "traffic": hbm,
+               "note": f"bytes HBM moved per launch = PMC fabric bytes ({fabric:.4g}, Infinity-Cache hits included) "
+                       f"x DRAM share of the EA requests; the layer-by-layer algorithmic table bytes would be "
+                       f"{alg_bytes_per_block * Bp:.4g}"}
+    if valu and mem:
+        a, b = (valu, mem) if valu["frac"] >= mem["frac"] else (mem, valu)
+        return dict(a, other=b)
+    return valu or mem or {"bound": "unknown", "achieved": None, "peak": None, "unit": None, "frac": None,
+                           "traffic": None, "note": "no PMC / ubench data in this run"}
 
 
 if __name__ == "__main__":

@@ -127,6 +127,11 @@ int tspgpu_device_info(const tspgpu_ctx *ctx, int *cu_count, char *name, int nam
  * the last launch used and the DP relaxations per block for n cities,
  * N(N-1)2^(N-2) with N = n-1 (tsp.cpp:442-471). */
 int tspgpu_last_grid(const tspgpu_ctx *ctx);
+/* K1 variant the last batched launch used: 5 = sub-cube tiled (hk_tiled_kernel),
+ * 4 = ping-pong + parent words, 2 = compact + prefetch, ... (heldkarp_kernel). */
+int tspgpu_last_variant(const tspgpu_ctx *ctx);
+/* Number of visible HIP devices (0 when none). */
+int tspgpu_device_count(void);
 double tspgpu_relaxations_per_block(int n);
 /* Algorithmic table bytes per block: every DP entry written once and read
  * once, 2 * 8 * N * 2^(N-1). */

@@ -26,11 +26,19 @@ struct tspgpu_ctx {
     int32_t *d_tour = nullptr;
     size_t tour_bytes = 0;
     int last_grid = 0;
+    int last_variant = -1;
     int threads = 0;     // workgroup size of the global-table kernels; 0 = per-N default
     int wg_per_cu = 0;   // resident slots per CU (auto grid); 0 = per-N default
     int lds_table_max_n = tspgpu::kLdsTableDefaultMaxN;  // largest N whose whole table stays in LDS
-    int variant = -1;    // K1 layer pass (-1: per-n default): 4 = 2 + ping-pong values + parent words,
+    int variant = -1;    // K1 layer pass (-1: per-n default): 5 = sub-cube tiled (hk_tiled.h),
+                         // 4 = 2 + ping-pong values + parent words,
                          // 2 = compact + next-row prefetch, 1 = compact, 0 = member sweep
+    int tiled_cfg = -1;  // K1 variant 5 configuration (hkt_cfg.h); -1 = per-(n, type) default
+    void *d_tinfo[16] = {};        // TiledInfo per L (variant 5)
+    char *d_tslots = nullptr;      // variant 5 push areas (one per resident workgroup)
+    size_t tslots_bytes = 0;
+    uint64_t *d_parents = nullptr; // variant 5 parent words (one table per block of a chunk)
+    size_t parents_bytes = 0;
     hipEvent_t ev_start = nullptr, ev_stop = nullptr;
     char name[256] = {0};
     std::mutex mu;

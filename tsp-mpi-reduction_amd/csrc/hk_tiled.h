@@ -1,0 +1,450 @@
+// K1 variant 5 — "sub-cube" tiled Held-Karp for gfx950 (MI355X).
+//
+// Same recurrence, same IEEE operations and the same first-strict-minimum
+// argmin as heldkarp_impl.h (tsp.cpp:424-499), so the same cost and tour bits;
+// only the order in which DP entries are produced and where they live change.
+//
+// Split the N inner cities into L "low" ones (bits 0..L-1) and H = N-L "high"
+// ones.  A state mask S = h<<L | l has a high part h (H bits) and a low part l.
+// The transition G[S\k][m] -> G[S][k] adds ONE city k:
+//   * k low:  S\k has the same high part h          -> stays in sub-cube h
+//   * k high: S\k has high part h\k (a smaller one) -> crosses sub-cubes
+// So the DP can run sub-cube by sub-cube (h = 0, 1, ..., 2^H-1: every h\k is
+// done before h), and inside a sub-cube layer by layer over |l| = j.  The
+// entries G[S][m] with m LOW never leave the workgroup's LDS (only the two
+// live low layers of the current sub-cube are kept: 41 KB at L = 11); only
+// the entries with m HIGH go through memory, written once by sub-cube h\m
+// ("push", coalesced: same row index l on both sides) and read once by
+// sub-cube h.  At n = 16 (N = 15, L = 11, H = 4) that is 65,536 of the
+// block's 245,760 entries: 1.05 MB of table traffic per block instead of
+// 3.93 MB (SURVEY.md §8(d)'s compulsory bytes of the layer-by-layer form).
+//
+// Row-owner pass (h, j): a thread owns a source row T = h<<L | l, |l| = j,
+// t = |h|+j members, Q = N-t non-members; for every non-member k it computes
+//   acc[k] = min over members m ascending (strict <) of G[T][m] + d[m][k]
+// and its argmin city (the reference's tsp.cpp:457-470 rule) — exactly the
+// compact pass of heldkarp_impl.h — then stores acc[k] to the next LDS layer
+// (k low) or to the push area of sub-cube h|k (k high), and one 64-bit word of
+// 4-bit parents per row (per block, non-temporal) for the backtracking, which
+// a second kernel runs with one thread per block (14 dependent loads each,
+// all blocks in parallel instead of a serial tail per block).
+//
+// Distances: the N x N inner matrix is replicated R times in LDS, element e of
+// copy c at 8*(e*R + c), lane uses copy lane % R: with R = 32 the per-lane
+// gather d[m][k] of a half-wave hits 32 distinct bank pairs (conflict-free),
+// the d[m][k] gathers of the compact pass cost +48% LDS cycles in bank
+// conflicts (round-1 counters) without it.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "heldkarp_impl.h"
+
+namespace tspgpu {
+
+constexpr int kTiledMaxL = 12;
+#ifndef TSPGPU_TILED_AHEAD
+#define TSPGPU_TILED_AHEAD 8  // d loads in flight per lane in the relaxation loop
+#endif
+
+// host-built tables of one L (device copy, staged into LDS per workgroup)
+struct TiledInfo {
+    uint16_t mask[1 << kTiledMaxL];  // L-bit masks sorted by (popcount, colex rank)
+    uint16_t rank[1 << kTiledMaxL];  // colex rank of a mask among the masks of its popcount
+    int moff[kTiledMaxL + 2];        // first index of popcount class j in mask[]
+    int cnt[kTiledMaxL + 2];         // C(L, j)
+};
+
+__host__ __device__ constexpr int tiled_layer_vals(int L, int j) { return cbinom(L, j) * j; }
+// one LDS region holds the two live low layers: layer j at the bottom when j
+// is even, at the top when odd (adjacent layers never overlap)
+__host__ __device__ constexpr int tiled_region_vals(int L)
+{
+    int m = 0;
+    for (int j = 0; j < L; ++j) {
+        const int s = tiled_layer_vals(L, j) + tiled_layer_vals(L, j + 1);
+        m = s > m ? s : m;
+    }
+    return m;
+}
+__host__ __device__ constexpr size_t tiled_lds_bytes(int N, int L, int R, int vb)
+{
+    return (size_t)N * N * R * vb            // replicated inner distances
+           + (size_t)2 * 16 * vb             // d[0][k], d[m][0]
+           + (size_t)tiled_region_vals(L) * vb  // live low layers
+           + (size_t)2 * 2 * (1 << L);       // mask + rank (u16)
+}
+// push area of one slot: [h][c][idx] values (c = high city index 0..H-1,
+// idx = the row's place in the sorted L-bit mask list)
+__host__ __device__ constexpr size_t tiled_push_bytes(int N, int L, int vb)
+{
+    return (size_t)(1 << (N - L)) * (N - L) * (1 << L) * vb;
+}
+// parent words of one block: [h][idx] u64
+__host__ __device__ constexpr size_t tiled_parent_bytes(int N, int L) { return (size_t)8 << N; }
+
+template <typename V>
+struct Rsrc {
+    __amdgpu_buffer_rsrc_t rs;
+    __device__ __forceinline__ V load(uint32_t byte_off) const
+    {
+        if constexpr (sizeof(V) == 8)
+            return __builtin_bit_cast(V, __builtin_amdgcn_raw_buffer_load_b64(rs, (int)byte_off, 0, 0));
+        else
+            return (V)__builtin_amdgcn_raw_buffer_load_b32(rs, (int)byte_off, 0, 0);
+    }
+    __device__ __forceinline__ void store(uint32_t byte_off, V v, int aux = 0) const
+    {
+        if constexpr (sizeof(V) == 8) {
+            using u2 = decltype(__builtin_amdgcn_raw_buffer_load_b64(rs, 0, 0, 0));
+            if (aux)
+                __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2, v), rs, (int)byte_off, 0, 2);
+            else
+                __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2, v), rs, (int)byte_off, 0, 0);
+        } else {
+            __builtin_amdgcn_raw_buffer_store_b32((uint32_t)v, rs, (int)byte_off, 0, 0);
+        }
+    }
+};
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const void *p, uint32_t bytes)
+{
+    const uint64_t base = reinterpret_cast<uint64_t>(p);
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)base);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(base >> 32));
+    const uint32_t nb = __builtin_amdgcn_readfirstlane(bytes);
+    return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void *>(((uint64_t)hi << 32) | lo), 0, (int)nb,
+                                             0x00020000);
+}
+
+// LDS barrier: the passes inside a sub-cube hand data over through LDS only
+// (their pushes are read by later sub-cubes, behind a full __syncthreads), so
+// they wait for their own LDS operations, not for their global stores.
+__device__ __forceinline__ void lds_barrier()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
+// acc = min(acc, g + d) with arg = m where g + d < acc (the first strict
+// minimum over members ascending, tsp.cpp:465): exactly four VALU
+// instructions with the compare in VCC (compiler-scheduled compares landed in
+// SGPR pairs that were spilled, round-1 K1 counters).
+__device__ __forceinline__ void relax_argmin(double &acc, uint32_t &arg, double g, double d, uint32_t m)
+{
+    double t;
+    asm volatile(
+        "v_add_f64 %[t], %[g], %[d]\n\t"
+        "v_cmp_lt_f64 vcc, %[t], %[acc]\n\t"
+        "v_cndmask_b32 %[arg], %[arg], %[m], vcc\n\t"
+        "v_min_f64 %[acc], %[acc], %[t]"
+        : [acc] "+v"(acc), [arg] "+v"(arg), [t] "=&v"(t)
+        : [g] "v"(g), [d] "v"(d), [m] "v"(m)
+        : "vcc");
+}
+__device__ __forceinline__ void relax_argmin(int32_t &acc, uint32_t &arg, int32_t g, int32_t d, uint32_t m)
+{
+    int32_t t;
+    asm volatile(
+        "v_add_u32 %[t], %[g], %[d]\n\t"
+        "v_cmp_lt_i32 vcc, %[t], %[acc]\n\t"
+        "v_cndmask_b32 %[arg], %[arg], %[m], vcc\n\t"
+        "v_min_i32 %[acc], %[acc], %[t]"
+        : [acc] "+v"(acc), [arg] "+v"(arg), [t] "=&v"(t)
+        : [g] "v"(g), [d] "v"(d), [m] "v"(m)
+        : "vcc");
+}
+
+template <typename V, int N, int L, int R>
+struct TiledCtx {
+    const V *dr;          // LDS replicated distances
+    const uint16_t *lmask, *lrank;
+    V *region;            // LDS live low layers
+    Rsrc<V> push;         // this slot's push area
+    Rsrc<uint64_t> par;   // this block's parent words
+    const int *moff, *cnt;
+};
+
+// One pass (h, j) of a sub-cube: t = |h| + j members per source row.
+template <typename V, int N, int L, int T, int THREADS, int R>
+__device__ __forceinline__ void tiled_pass(const TiledCtx<V, N, L, R> &c, uint32_t h, int j, uint32_t tid)
+{
+    constexpr int H = N - L;
+    constexpr int Q = N - T;
+    constexpr int NL = 1 << L;
+    constexpr uint32_t FULL = (1u << N) - 1u;
+    constexpr int VB = sizeof(V);
+    const int rows = c.cnt[j];
+    const int base = c.moff[j];
+    const int rows_n = j < L ? c.cnt[j + 1] : 0;
+    const int regv = tiled_region_vals(L);
+    const V *cur = c.region + ((j & 1) ? regv - rows * j : 0);
+    V *nxt = c.region + (((j + 1) & 1) ? regv - rows_n * (j + 1) : 0);
+    const uint32_t lane_off = (tid & (uint32_t)(R - 1)) * VB;
+    const uint32_t hbase = h * (uint32_t)H;  // push row of (h, c) = (h*H + c)*NL
+    for (uint32_t r = tid; r < (uint32_t)rows; r += THREADS) {
+        const uint32_t l = c.lmask[base + r];
+        const uint32_t Tm = l | (h << L);
+        // the row's t values: low members from LDS, high members from the pushes
+        V g[T > 0 ? T : 1];
+        uint32_t hb = h;
+#pragma unroll
+        for (int p = 0; p < T; ++p) {
+            if (p < j) {
+                g[p] = cur[p * rows + r];
+            } else {
+                const uint32_t cb = __builtin_ctz(hb);
+                hb &= hb - 1u;
+                g[p] = c.push.load(((hbase + cb) * NL + base + r) * VB);
+            }
+        }
+        // members (ascending city = ascending bit) -> their d-row offsets
+        uint32_t mrow[T > 0 ? T : 1], mcity[T > 0 ? T : 1];
+        uint32_t bits = Tm;
+#pragma unroll
+        for (int p = 0; p < T; ++p) {
+            const uint32_t b = __builtin_ctz(bits);
+            bits &= bits - 1u;
+            mcity[p] = b + 1u;
+            mrow[p] = b * (uint32_t)(N * R * VB) + lane_off;
+        }
+        uint32_t kb[Q], kof[Q];
+        uint32_t nb = ~Tm & FULL;
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+            kb[q] = __builtin_ctz(nb);
+            nb &= nb - 1u;
+            kof[q] = kb[q] * (uint32_t)(R * VB);
+        }
+        V acc[Q];
+        uint32_t arg[Q];
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+            acc[q] = ValT<V>::inf;
+            arg[q] = 0;
+        }
+        // the t*Q relaxations in member-major order (members ascending for
+        // every destination), each d value loaded TSPGPU_TILED_AHEAD
+        // relaxations ahead; a scheduling barrier per relaxation keeps the
+        // compiler from hoisting all t*Q loads (and their registers) up front
+        const char *drb = reinterpret_cast<const char *>(c.dr);
+        constexpr int TQ = T * Q;
+        constexpr int AH = TSPGPU_TILED_AHEAD < TQ ? TSPGPU_TILED_AHEAD : TQ;
+        V dv[AH];
+#pragma unroll
+        for (int i = 0; i < AH; ++i) dv[i] = *reinterpret_cast<const V *>(drb + mrow[i / Q] + kof[i % Q]);
+#pragma unroll
+        for (int i = 0; i < TQ; ++i) {
+            const V d = dv[i % AH];
+            if (i + AH < TQ) dv[i % AH] = *reinterpret_cast<const V *>(drb + mrow[(i + AH) / Q] + kof[(i + AH) % Q]);
+            relax_argmin(acc[i % Q], arg[i % Q], g[i / Q], d, mcity[i / Q]);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        // destinations: the L-j low non-members come first (uniform split)
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+            if (q < L - j) {
+                const uint32_t k = kb[q];
+                const uint32_t pos = k - (uint32_t)q;  // members of l below k
+                const uint32_t rk = c.lrank[l | (1u << k)];
+                nxt[pos * rows_n + rk] = acc[q];
+            } else {
+                const uint32_t cb = kb[q] - L;
+                c.push.store((((h | (1u << cb)) * H + cb) * NL + base + r) * VB, acc[q]);
+            }
+        }
+        uint64_t w = 0;
+#pragma unroll
+        for (int q = 0; q < Q; ++q) w |= (uint64_t)((arg[q] - 1u) & 15u) << (4 * q);
+        c.par.store((h * NL + base + r) * 8u, w, 1);
+    }
+}
+
+template <typename V, int N, int L, int THREADS, int R>
+__device__ __forceinline__ void tiled_dispatch(const TiledCtx<V, N, L, R> &c, uint32_t h, int j, int t, uint32_t tid)
+{
+#define TSPGPU_TP(TT) \
+    case TT:          \
+        if constexpr (TT < N) tiled_pass<V, N, L, TT, THREADS, R>(c, h, j, tid); \
+        break;
+    switch (t) {
+        TSPGPU_TP(1) TSPGPU_TP(2) TSPGPU_TP(3) TSPGPU_TP(4) TSPGPU_TP(5) TSPGPU_TP(6) TSPGPU_TP(7)
+        TSPGPU_TP(8) TSPGPU_TP(9) TSPGPU_TP(10) TSPGPU_TP(11) TSPGPU_TP(12) TSPGPU_TP(13) TSPGPU_TP(14)
+        TSPGPU_TP(15) TSPGPU_TP(16) TSPGPU_TP(17) TSPGPU_TP(18)
+    default: break;
+    }
+#undef TSPGPU_TP
+}
+
+__host__ __device__ constexpr int tiled_waves(int threads, int wg_per_cu) { return threads * wg_per_cu / 256; }
+
+// Forward pass + closing min of blocks blockIdx.x, +gridDim.x, ...; writes
+// cost_out[blk] and the tour's last inner city (tour[n-1]); the backtracking
+// kernel below fills the rest of the tour from the parent words.
+template <typename V, int N, int L, int THREADS, int R, int WG>
+__global__ __launch_bounds__(THREADS, tiled_waves(THREADS, WG)) void hk_tiled_kernel(
+    const V *__restrict__ dist, int nblocks, int blk0, char *__restrict__ slots, uint32_t slot_bytes,
+    uint64_t *__restrict__ parents, const TiledInfo *__restrict__ info, V *__restrict__ cost_out,
+    int32_t *__restrict__ tour_out)
+{
+    constexpr int H = N - L;
+    constexpr int NH = 1 << H;
+    constexpr int NL = 1 << L;
+    constexpr int n = N + 1;
+    constexpr int VB = sizeof(V);
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    V *dr = reinterpret_cast<V *>(smem);
+    V *d0 = dr + N * N * R;    // d[0][k], k = 1..N at [k-1]
+    V *dc = d0 + 16;           // d[m][0], m = 1..N at [m-1]
+    V *region = dc + 16;
+    uint16_t *lmask = reinterpret_cast<uint16_t *>(region + tiled_region_vals(L));
+    uint16_t *lrank = lmask + NL;
+    __shared__ int s_moff[kTiledMaxL + 2], s_cnt[kTiledMaxL + 2];
+    const uint32_t tid = threadIdx.x;
+
+    for (int i = tid; i < NL; i += THREADS) {
+        lmask[i] = info->mask[i];
+        lrank[i] = info->rank[i];
+    }
+    if (tid < L + 2) {
+        s_moff[tid] = info->moff[tid];
+        s_cnt[tid] = info->cnt[tid];
+    }
+    TiledCtx<V, N, L, R> c;
+    c.dr = dr;
+    c.lmask = lmask;
+    c.lrank = lrank;
+    c.region = region;
+    c.moff = s_moff;
+    c.cnt = s_cnt;
+    c.push.rs = uniform_rsrc(slots + (size_t)blockIdx.x * slot_bytes, (uint32_t)tiled_push_bytes(N, L, VB));
+
+    for (int blk = blk0 + blockIdx.x; blk < nblocks; blk += gridDim.x) {
+        const V *dsrc = dist + (size_t)blk * n * n;
+        for (int i = tid; i < N * N * R; i += THREADS) {
+            const int e = i / R;
+            dr[i] = dsrc[(e / N + 1) * n + (e % N + 1)];
+        }
+        if (tid < N) {
+            d0[tid] = dsrc[tid + 1];
+            dc[tid] = dsrc[(tid + 1) * n];
+        }
+        c.par.rs = uniform_rsrc(parents + (size_t)(blk - blk0) * ((size_t)NH * NL), (uint32_t)tiled_parent_bytes(N, L));
+        __syncthreads();
+        // layer 1: G[{i}][i] = d[0][i] (tsp.cpp:435's d[0][i] term): low i in
+        // sub-cube 0's first LDS layer (colex rank of {i} is i), high i pushed
+        // to sub-cube {i} at row idx 0 (the empty low part)
+        // (layer 1 is odd: it sits at the top of the region, regv - C(L,1))
+        if (tid < L) region[tiled_region_vals(L) - L + tid] = d0[tid];
+        if (tid < H) c.push.store((((1u << tid) * H + tid) * NL + 0) * VB, d0[L + tid]);
+        __syncthreads();
+
+        for (uint32_t h = 0; h < (uint32_t)NH; ++h) {
+            const int hc = __builtin_popcount(h);
+            const int j0 = h == 0 ? 1 : 0;
+            const int j1 = h == (uint32_t)(NH - 1) ? L - 1 : L;
+            for (int j = j0; j <= j1; ++j) {
+                tiled_dispatch<V, N, L, THREADS, R>(c, h, j, hc + j, tid);
+                if (j < j1) lds_barrier();
+            }
+            // pushes of this sub-cube are read by later ones: full barrier
+            __syncthreads();
+        }
+
+        // closing min (tsp.cpp:483-499): G[full][m] + d[m][0], first strict min
+        if (tid < 64) {
+            const int m = tid + 1;
+            const bool valid = m <= N;
+            V gl = V(0);
+            if (valid) {
+                if (m <= L)  // low layer L: one row, position m-1
+                    gl = region[((L & 1) ? tiled_region_vals(L) - L : 0) + (m - 1)];
+                else
+                    gl = c.push.load(((uint32_t)((NH - 1) * H + (m - 1 - L)) * NL + (NL - 1)) * VB);
+            }
+            const V cand = valid ? gl + dc[m - 1] : ValT<V>::invalid;
+            const V best = ValT<V>::vmin(wave_min(cand), ValT<V>::inf);
+            const unsigned long long hit = __ballot(valid && cand == best && cand < ValT<V>::inf);
+            const int bestM = hit ? __ffsll(hit) : 0;
+            if (tid == 0) {
+                int32_t *tour = tour_out + (size_t)blk * (n + 1);
+                tour[0] = 0;
+                tour[n - 1] = bestM;
+                tour[n] = 0;
+                cost_out[blk] = bestM ? best : V(-1);
+            }
+        }
+        __syncthreads();
+    }
+}
+
+// Backtracking, one thread per block: from the last inner city, the parent
+// nibble of row T = S \ k gives the previous city (the argmin the forward
+// pass stored), N-1 steps.
+template <typename V, int N, int L>
+__global__ __launch_bounds__(256) void hk_tiled_backtrack(int nblocks, int blk0, const uint64_t *__restrict__ parents,
+                                                          const TiledInfo *__restrict__ info,
+                                                          V *__restrict__ cost_out, int32_t *__restrict__ tour_out)
+{
+    constexpr int NH = 1 << (N - L);
+    constexpr int NL = 1 << L;
+    constexpr int n = N + 1;
+    const int blk = blk0 + blockIdx.x * blockDim.x + threadIdx.x;
+    if (blk >= nblocks) return;
+    int32_t *tour = tour_out + (size_t)blk * (n + 1);
+    const uint64_t *pw = parents + (size_t)(blk - blk0) * ((size_t)NH * NL);
+    int k = tour[n - 1];
+    bool ok = k >= 1 && k <= N;
+    uint32_t S = (1u << N) - 1u;
+    for (int pos = n - 2; ok && pos >= 1; --pos) {
+        const uint32_t T = S & ~(1u << (k - 1));
+        const uint32_t hT = T >> L, lT = T & (NL - 1);
+        const uint32_t idx = (uint32_t)info->moff[__builtin_popcount(lT)] + info->rank[lT];
+        const uint64_t w = __builtin_nontemporal_load(pw + hT * NL + idx);
+        const int q = (k - 1) - __builtin_popcount(T & ((1u << (k - 1)) - 1u));
+        const int pm = (int)((w >> (4 * q)) & 15u) + 1;
+        ok = pm <= N && ((T >> (pm - 1)) & 1u);
+        tour[pos] = ok ? pm : 0;
+        S = T;
+        k = pm;
+    }
+    if (!ok) cost_out[blk] = V(-1);
+}
+
+struct TiledArgs {
+    const void *dist;
+    int n, blk0, blk1;        // blocks [blk0, blk1) of this launch pair
+    char *slots;              // grid push areas
+    uint32_t slot_bytes;
+    uint64_t *parents;        // (blk1 - blk0) parent-word tables
+    const TiledInfo *info;
+    void *cost;
+    int32_t *tour;
+    int grid;
+    hipStream_t stream;
+};
+
+template <typename V, int N, int L, int THREADS, int R, int WG>
+hipError_t launch_tiled_n(const TiledArgs &a)
+{
+    const size_t lds = tiled_lds_bytes(N, L, R, sizeof(V));
+    static bool raised = false;  // once per instantiation
+    if (!raised) {
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&hk_tiled_kernel<V, N, L, THREADS, R, WG>),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) return e;
+        raised = true;
+    }
+    hipLaunchKernelGGL((hk_tiled_kernel<V, N, L, THREADS, R, WG>), dim3(a.grid), dim3(THREADS), lds, a.stream,
+                       static_cast<const V *>(a.dist), a.blk1, a.blk0, a.slots, a.slot_bytes, a.parents, a.info,
+                       static_cast<V *>(a.cost), a.tour);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    const int nb = a.blk1 - a.blk0;
+    hipLaunchKernelGGL((hk_tiled_backtrack<V, N, L>), dim3((nb + 255) / 256), dim3(256), 0, a.stream, a.blk1, a.blk0,
+                       a.parents, a.info, static_cast<V *>(a.cost), a.tour);
+    return hipGetLastError();
+}
+
+}  // namespace tspgpu

@@ -23,6 +23,7 @@
 
 #include "ctx.h"
 #include "heldkarp.h"
+#include "hkt_cfg.h"
 
 namespace tspgpu {
 
@@ -132,6 +133,87 @@ int ensure_tables(tspgpu_ctx *c, int N)
     return 0;
 }
 
+int ensure_tiled_info(tspgpu_ctx *c, int L)
+{
+    if (c->d_tinfo[L]) return 0;
+    auto info = std::make_unique<TiledInfo>();
+    std::memset(info.get(), 0, sizeof(TiledInfo));
+    int k = 0;
+    for (int j = 0; j <= L; ++j) {
+        info->moff[j] = k;
+        info->cnt[j] = binom_host(L, j);
+        int r = 0;
+        for (uint32_t m = 0; m < (1u << L); ++m)
+            if (__builtin_popcount(m) == j) {  // numeric order of equal-popcount masks = colex order
+                info->mask[k++] = (uint16_t)m;
+                info->rank[m] = (uint16_t)r++;
+            }
+    }
+    info->moff[L + 1] = k;
+    void *d = nullptr;
+    hipError_t e = hipMalloc(&d, sizeof(TiledInfo));
+    if (e == hipSuccess) e = hipMemcpy(d, info.get(), sizeof(TiledInfo), hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+        if (d) (void)hipFree(d);
+        return hip_err(e);
+    }
+    c->d_tinfo[L] = d;
+    return 0;
+}
+
+// K1 variant 5 (sub-cube tiled, hk_tiled.h) configuration for (N, value
+// bytes): TSPGPU_TILED_CFG / c->tiled_cfg, else the measured default; null if
+// none exists for this size.
+const TiledCfg *pick_tiled(const tspgpu_ctx *c, int N, int vbytes)
+{
+    int cnt = 0;
+    const TiledCfg *t = tiled_cfgs(&cnt);
+    if (c->tiled_cfg >= 0) {
+        for (int i = 0; i < cnt; ++i)
+            if (t[i].id == c->tiled_cfg && t[i].N == N && t[i].vbytes == vbytes) return &t[i];
+        return nullptr;
+    }
+    for (int i = 0; i < cnt; ++i)  // first row of the table for this size is the default
+        if (t[i].N == N && t[i].vbytes == vbytes) return &t[i];
+    return nullptr;
+}
+
+int solve_tiled(tspgpu_ctx *c, const TiledCfg *cfg, const void *d_dist, int n, int nblocks, void *d_cost,
+                int32_t *d_tour, hipStream_t stream)
+{
+    const int N = n - 1, L = cfg->L;
+    int rc = ensure_tiled_info(c, L);
+    if (rc) return rc;
+    const int grid = std::min(nblocks, c->cu_count * cfg->wg);
+    const size_t slot = (size_t)(1 << (N - L)) * (N - L) * ((size_t)1 << L) * cfg->vbytes;
+    if ((rc = ensure(&c->d_tslots, &c->tslots_bytes, (size_t)grid * slot))) return rc;
+    // parent words: 8 B per row, one table per block; blocks go in chunks of
+    // at most 16384 (4 GiB of parent words at n = 16)
+    const size_t per_block = (size_t)8 << N;
+    const int chunk = std::min(nblocks, 16384);
+    if ((rc = ensure(&c->d_parents, &c->parents_bytes, (size_t)chunk * per_block))) return rc;
+    for (int b0 = 0; b0 < nblocks; b0 += chunk) {
+        TiledArgs a{};
+        a.dist = d_dist;
+        a.n = n;
+        a.blk0 = b0;
+        a.blk1 = std::min(nblocks, b0 + chunk);
+        a.slots = c->d_tslots;
+        a.slot_bytes = (uint32_t)slot;
+        a.parents = c->d_parents;
+        a.info = static_cast<const TiledInfo *>(c->d_tinfo[L]);
+        a.cost = d_cost;
+        a.tour = d_tour;
+        a.grid = std::min(grid, a.blk1 - a.blk0);
+        a.stream = stream;
+        hipError_t e = cfg->launch(a);
+        if (e != hipSuccess) return hip_err(e);
+    }
+    c->last_grid = grid;
+    c->last_variant = 5;
+    return 0;
+}
+
 int check_n(int n, int strict)
 {
     if (n < 2) return -EINVAL;
@@ -181,6 +263,11 @@ int solve_device_locked(tspgpu_ctx *c, const void *d_dist, int n, int nblocks, v
         // (with a full wave of blocks: one block alone is latency-bound and the
         // argmin's extra VALU only costs there)
         a.variant = c->variant >= 0 ? c->variant : (N == 15 && vbytes == 8 && nblocks >= c->cu_count ? 4 : 2);
+        if (a.variant == 5) {
+            if (const TiledCfg *cfg = pick_tiled(c, N, vbytes))
+                return solve_tiled(c, cfg, d_dist, n, nblocks, d_cost, d_tour, stream);
+            a.variant = vbytes == 8 && N == 15 ? 4 : 2;  // no tiled configuration for this size
+        }
         // variant 4 at 16 cities: one 512-thread workgroup per CU at 2 waves/SIMD
         // (256 VGPRs; heldkarp_impl.h TSPGPU_K1_WAVES_512V4) beats 1024 threads at 4
         if (c->threads <= 0 && a.variant == 4 && N == 15 && vbytes == 8) a.threads = 512;
@@ -207,6 +294,7 @@ int solve_device_locked(tspgpu_ctx *c, const void *d_dist, int n, int nblocks, v
         }
     }
     c->last_grid = grid;
+    c->last_variant = N >= 2 ? a.variant : 0;
     return hip_err(launch_heldkarp(a, grid));
 }
 
@@ -346,8 +434,9 @@ int tspgpu_ctx_create(const tspgpu_opts *opts, tspgpu_ctx **out)
     }
     if (const char *e = std::getenv("TSPGPU_K1")) {
         const int v = std::atoi(e);
-        c->variant = v < 0 ? 1 : (v >= 4 ? 4 : (v > 2 ? 2 : v));
+        c->variant = v < 0 ? 1 : (v >= 5 ? 5 : (v >= 4 ? 4 : (v > 2 ? 2 : v)));
     }
+    if (const char *e = std::getenv("TSPGPU_TILED_CFG")) c->tiled_cfg = std::atoi(e);
     if (const char *e = std::getenv("TSPGPU_WG_PER_CU")) c->wg_per_cu = std::atoi(e) > 0 ? std::atoi(e) : 0;
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
         delete c;
@@ -369,6 +458,10 @@ int tspgpu_ctx_destroy(tspgpu_ctx *c)
     if (c->wide_free) c->wide_free(c->wide_cache);
     if (c->search_pool_free) c->search_pool_free(c->search_pool);
     if (c->d_slots) (void)hipFree(c->d_slots);
+    for (void *p : c->d_tinfo)
+        if (p) (void)hipFree(p);
+    if (c->d_tslots) (void)hipFree(c->d_tslots);
+    if (c->d_parents) (void)hipFree(c->d_parents);
     if (c->d_dist) (void)hipFree(c->d_dist);
     if (c->d_cost) (void)hipFree(c->d_cost);
     if (c->d_tour) (void)hipFree(c->d_tour);
@@ -492,6 +585,14 @@ int tspgpu_solve(const double *dist, int n, int nblocks, double *cost_out, int32
 }
 
 int tspgpu_last_grid(const tspgpu_ctx *c) { return c ? c->last_grid : 0; }
+
+int tspgpu_last_variant(const tspgpu_ctx *c) { return c ? c->last_variant : -1; }
+
+int tspgpu_device_count(void)
+{
+    int n = 0;
+    return hipGetDeviceCount(&n) == hipSuccess ? n : 0;
+}
 
 int tspgpu_device_alloc(tspgpu_ctx *c, size_t bytes, void **ptr)
 {

@@ -24,7 +24,7 @@ EXPORTED_SYMBOLS = (
     "tspgpu_solve_blocks_device", "tspgpu_solve", "tspgpu_last_grid", "tspgpu_relaxations_per_block",
     "tspgpu_table_bytes_per_block", "tspgpu_device_alloc", "tspgpu_device_free", "tspgpu_memcpy_htod",
     "tspgpu_memcpy_dtoh", "tspgpu_stream", "tspgpu_synchronize", "tspgpu_timer_start", "tspgpu_timer_stop",
-    "tspgpu_device_info",
+    "tspgpu_device_info", "tspgpu_last_variant", "tspgpu_device_count",
     # K2
     "tspgpu_search_solve", "tspgpu_search_enumerate", "tspgpu_search_create", "tspgpu_search_destroy", "tspgpu_search_info",
     "tspgpu_search_set_bound", "tspgpu_search_start", "tspgpu_search_step", "tspgpu_search_run_all",
@@ -102,6 +102,8 @@ def lib():
         L.tspgpu_solve_blocks_i32_device.argtypes = [vp, vp, ctypes.c_int, ctypes.c_int, vp, vp, vp]
         L.tspgpu_solve.argtypes = [dp, ctypes.c_int, ctypes.c_int, dp, ip, ctypes.POINTER(Opts)]
         L.tspgpu_last_grid.argtypes = [vp]
+        L.tspgpu_last_variant.argtypes = [vp]
+        L.tspgpu_device_count.argtypes = []
         L.tspgpu_relaxations_per_block.argtypes = [ctypes.c_int]
         L.tspgpu_relaxations_per_block.restype = ctypes.c_double
         L.tspgpu_table_bytes_per_block.argtypes = [ctypes.c_int]
@@ -152,6 +154,11 @@ def _dp(a):
 
 def _ip(a):
     return a.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))
+
+
+def device_count() -> int:
+    """Visible HIP devices (initialises HIP in this process)."""
+    return lib().tspgpu_device_count()
 
 
 def tour_length(n: int) -> int:
@@ -285,6 +292,10 @@ class Context:
 
     def last_grid(self) -> int:
         return lib().tspgpu_last_grid(self.handle)
+
+    def last_variant(self) -> int:
+        """K1 variant of the last batched launch (5: hk_tiled_kernel, else heldkarp_kernel)."""
+        return lib().tspgpu_last_variant(self.handle)
 
     def _check(self, rc, what):
         if rc:
