@@ -1,0 +1,126 @@
+"""Every K1 variant the library can pick, checked block by block against the
+CPU oracle at the sizes where it is the default — including the variant
+switches that happen inside one call:
+
+  * n = 16, B >= 2 x CUs: the sub-cube tiled kernel (variant 5, hk_tiled.h)
+    is the default; variant 4 (ping-pong + parent words) and variant 2 are
+    forced through TSPGPU_K1 (read when a context is created);
+  * every variant-5 configuration of hkt_cfg.h (TSPGPU_TILED_CFG), f64 and i32;
+  * tie-heavy blocks (integer lattice 0..3, 0..39) mixed with random ones;
+  * one block solved alone (variant 2: fewer blocks than CUs) equals its row
+    of the large batch (variant 5).
+"""
+import os
+from concurrent.futures import ThreadPoolExecutor
+
+import numpy as np
+import pytest
+
+import oracle_py as O
+import tspgpu
+
+pytestmark = pytest.mark.gpu
+
+B_BIG = 520  # > 2 x 256 CUs: the large-batch defaults apply
+
+
+def _blocks(n, B, seed):
+    rng = np.random.default_rng(seed)
+    blocks = []
+    for b in range(B):
+        if b % 3 == 0:
+            xy = rng.integers(0, 4, size=(n, 2)).astype(np.float64)  # heavy ties
+        elif b % 3 == 1:
+            xy = rng.integers(0, 40, size=(n, 2)).astype(np.float64)
+        else:
+            xy = rng.uniform(0, 1000, size=(n, 2))
+        blocks.append([(b * n + i, xy[i, 0], xy[i, 1]) for i in range(n)])
+    return tspgpu.distance_matrix(blocks)
+
+
+_ORACLE = {}
+
+
+def _oracle_all(key, d):
+    if key not in _ORACLE:
+        with ThreadPoolExecutor(max_workers=min(16, os.cpu_count() or 4)) as ex:
+            _ORACLE[key] = list(ex.map(lambda b: O.solve_block(np.asarray(d[b], dtype=np.float64)),
+                                       range(d.shape[0])))
+    return _ORACLE[key]
+
+
+def _ctx(variant=None, cfg=None):
+    old = {k: os.environ.get(k) for k in ("TSPGPU_K1", "TSPGPU_TILED_CFG")}
+    try:
+        for k, v in (("TSPGPU_K1", variant), ("TSPGPU_TILED_CFG", cfg)):
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = str(v)
+        return tspgpu.Context(device=0)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
+def _check(ctx, d, ref, vb=8):
+    if vb == 8:
+        cost, tour = ctx.solve_blocks(d)
+    else:
+        cost, tour = ctx.solve_blocks_i32(d)
+    n = d.shape[1]
+    bad = [b for b in range(d.shape[0])
+           if float(cost[b]) != ref[b][0] or tour[b][: tspgpu.tour_length(n)].tolist() != ref[b][1]]
+    assert not bad, f"{len(bad)} blocks differ from the oracle, first {bad[:5]}"
+    return ctx.last_variant()
+
+
+@pytest.mark.parametrize("variant", [None, 5, 4, 2])
+def test_n16_large_batch_every_variant(variant):
+    d = _blocks(16, B_BIG, 16)
+    ref = _oracle_all(("f64", 16), d)
+    ctx = _ctx(variant)
+    try:
+        used = _check(ctx, d, ref)
+    finally:
+        ctx.close()
+    assert used == (5 if variant is None else variant)
+
+
+def _tiled_cfgs():
+    import re
+
+    path = os.path.join(os.path.dirname(tspgpu.PKG_DIR), "tsp-mpi-reduction_amd", "csrc", "hkt_cfg.h")
+    out = []
+    for ln in open(path):
+        m = re.match(r"\s+X\((\d+), (\w+), (\d+), (\d+),", ln)
+        if m:
+            out.append((int(m.group(1)), 8 if m.group(2) == "double" else 4, int(m.group(3)) + 1))
+    return out
+
+
+@pytest.mark.parametrize("cfg,vb,n", _tiled_cfgs())
+def test_every_tiled_configuration(cfg, vb, n):
+    d = _blocks(n, 300, 100 + n)
+    ref = _oracle_all(("f64", n, 300), d)
+    if vb == 4:
+        d = np.rint(d).astype(np.int32)
+        ref = _oracle_all(("i32", n, 300), d.astype(np.float64))
+    ctx = _ctx(5, cfg)
+    try:
+        assert _check(ctx, d, ref, vb) == 5
+    finally:
+        ctx.close()
+
+
+def test_single_block_equals_its_row_of_the_big_batch(gpu_ctx):
+    d = _blocks(16, B_BIG, 16)
+    cost, tour = gpu_ctx.solve_blocks(d)
+    assert gpu_ctx.last_variant() == 5
+    for b in (0, 1, 2, 257, B_BIG - 1):
+        c1, t1 = gpu_ctx.solve_blocks(d[b:b + 1])
+        assert gpu_ctx.last_variant() == 2
+        assert c1[0] == cost[b] and t1[0].tolist() == tour[b].tolist()

@@ -13,14 +13,17 @@ CSRC = os.path.join(ROOT, "tsp-mpi-reduction_amd", "csrc")
 
 # (id, value type, N, L, threads per workgroup, distance copies R, workgroups per CU)
 CFGS = [
-    (0, "double", 15, 11, 256, 16, 2),
-    (1, "double", 15, 11, 256, 8, 2),
     (2, "double", 15, 11, 256, 1, 3),
-    (3, "double", 15, 11, 512, 32, 1),
-    (4, "double", 15, 11, 256, 4, 2),
-    (5, "double", 14, 11, 256, 16, 2),
-    (6, "int32_t", 15, 11, 256, 32, 2),
-    (7, "int32_t", 14, 11, 256, 32, 2),
+    (0, "double", 15, 11, 512, 1, 2),
+    (1, "double", 15, 10, 256, 1, 4),
+    (3, "double", 15, 10, 512, 1, 2),
+    (4, "double", 15, 11, 512, 2, 2),
+    (5, "double", 14, 11, 512, 1, 2),
+    (6, "double", 14, 10, 256, 1, 4),
+    (7, "int32_t", 15, 11, 256, 1, 4),
+    (8, "int32_t", 15, 11, 512, 1, 2),
+    (9, "int32_t", 14, 11, 256, 1, 4),
+    (10, "double", 13, 10, 256, 1, 4),
 ]
 
 

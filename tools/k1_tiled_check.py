@@ -18,7 +18,8 @@ import oracle_py as O  # noqa: E402
 import tspgpu  # noqa: E402
 from bench import Shard  # noqa: E402
 
-CFGS = {0: (16, 8), 1: (16, 8), 2: (16, 8), 3: (16, 8), 4: (16, 8), 5: (15, 8), 6: (16, 4), 7: (15, 4)}
+CFGS = {0: (16, 8), 1: (16, 8), 2: (16, 8), 3: (16, 8), 4: (16, 8), 5: (15, 8), 6: (15, 8), 7: (16, 4), 8: (16, 4),
+        9: (15, 4), 10: (14, 8)}
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 16384
 which = [int(x) for x in sys.argv[2:]] or sorted(CFGS)
 

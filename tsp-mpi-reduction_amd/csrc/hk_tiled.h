@@ -43,6 +43,12 @@
 namespace tspgpu {
 
 constexpr int kTiledMaxL = 12;
+// Ablation knobs for timing experiments only (results are WRONG when set):
+//   1 high-member values from LDS, 2 d values from a register, 4 no barrier
+//   between the passes of a sub-cube, 8 plain minimum (no argmin)
+#ifndef TSPGPU_TILED_ABL
+#define TSPGPU_TILED_ABL 0
+#endif
 #ifndef TSPGPU_TILED_AHEAD
 #define TSPGPU_TILED_AHEAD 8  // d loads in flight per lane in the relaxation loop
 #endif
@@ -83,27 +89,39 @@ __host__ __device__ constexpr size_t tiled_push_bytes(int N, int L, int vb)
 // parent words of one block: [h][idx] u64
 __host__ __device__ constexpr size_t tiled_parent_bytes(int N, int L) { return (size_t)8 << N; }
 
+__host__ __device__ constexpr int tiled_moff(int L, int J)
+{
+    int o = 0;
+    for (int i = 0; i < J; ++i) o += cbinom(L, i);
+    return o;
+}
+
+// Buffer-resource access with the uniform part of the offset in soffset (an
+// SGPR) and the per-lane part in voffset: no VALU address arithmetic.
 template <typename V>
 struct Rsrc {
     __amdgpu_buffer_rsrc_t rs;
-    __device__ __forceinline__ V load(uint32_t byte_off) const
+    __device__ __forceinline__ V load(uint32_t voff, uint32_t soff) const
     {
         if constexpr (sizeof(V) == 8)
-            return __builtin_bit_cast(V, __builtin_amdgcn_raw_buffer_load_b64(rs, (int)byte_off, 0, 0));
+            return __builtin_bit_cast(V, __builtin_amdgcn_raw_buffer_load_b64(rs, (int)voff, (int)soff, 0));
         else
-            return (V)__builtin_amdgcn_raw_buffer_load_b32(rs, (int)byte_off, 0, 0);
+            return (V)__builtin_amdgcn_raw_buffer_load_b32(rs, (int)voff, (int)soff, 0);
     }
-    __device__ __forceinline__ void store(uint32_t byte_off, V v, int aux = 0) const
+    __device__ __forceinline__ void store(uint32_t voff, uint32_t soff, V v) const
     {
         if constexpr (sizeof(V) == 8) {
             using u2 = decltype(__builtin_amdgcn_raw_buffer_load_b64(rs, 0, 0, 0));
-            if (aux)
-                __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2, v), rs, (int)byte_off, 0, 2);
-            else
-                __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2, v), rs, (int)byte_off, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2, v), rs, (int)voff, (int)soff, 0);
         } else {
-            __builtin_amdgcn_raw_buffer_store_b32((uint32_t)v, rs, (int)byte_off, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b32((uint32_t)v, rs, (int)voff, (int)soff, 0);
         }
+    }
+    // non-temporal 8-byte store (parent words: read back only by the backtracking)
+    __device__ __forceinline__ void store_nt(uint32_t voff, uint32_t soff, uint64_t w) const
+    {
+        using u2 = decltype(__builtin_amdgcn_raw_buffer_load_b64(rs, 0, 0, 0));
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2, w), rs, (int)voff, (int)soff, 2);
     }
 };
 
@@ -158,123 +176,179 @@ __device__ __forceinline__ void relax_argmin(int32_t &acc, uint32_t &arg, int32_
 
 template <typename V, int N, int L, int R>
 struct TiledCtx {
-    const V *dr;          // LDS replicated distances
-    const uint16_t *lmask, *lrank;
-    V *region;            // LDS live low layers
-    Rsrc<V> push;         // this slot's push area
-    Rsrc<uint64_t> par;   // this block's parent words
-    const int *moff, *cnt;
+    const V *dr;               // LDS replicated distances
+    const uint16_t *lmask;     // LDS sorted L-bit masks
+    const uint16_t *lrankb;    // LDS colex rank x sizeof(V) (byte offset inside a position column)
+    V *region;                 // LDS live low layers
+    Rsrc<V> push;              // this slot's push area
+    Rsrc<uint64_t> par;        // this block's parent words
 };
 
-// One pass (h, j) of a sub-cube: t = |h| + j members per source row.
-template <typename V, int N, int L, int T, int THREADS, int R>
-__device__ __forceinline__ void tiled_pass(const TiledCtx<V, N, L, R> &c, uint32_t h, int j, uint32_t tid)
+// One pass (h, J) of a sub-cube: T = |h| + J members per source row, all
+// counts static (one instantiation per (T, J)), so the split of members and
+// non-members into low (per lane) and high (uniform) parts costs no branch.
+template <typename V, int N, int L, int T, int J, int THREADS, int R>
+__device__ __forceinline__ void tiled_pass(const TiledCtx<V, N, L, R> &c, uint32_t h, uint32_t tid)
 {
     constexpr int H = N - L;
     constexpr int Q = N - T;
+    constexpr int HC = T - J;   // high members (uniform)
+    constexpr int QL = L - J;   // low non-members (per lane), listed first
+    constexpr int QH = Q - QL;  // high non-members (uniform)
+    static_assert(HC >= 0 && HC <= H && QL >= 0 && QH >= 0 && T >= 1 && T < N, "bad pass");
     constexpr int NL = 1 << L;
-    constexpr uint32_t FULL = (1u << N) - 1u;
     constexpr int VB = sizeof(V);
-    const int rows = c.cnt[j];
-    const int base = c.moff[j];
-    const int rows_n = j < L ? c.cnt[j + 1] : 0;
-    const int regv = tiled_region_vals(L);
-    const V *cur = c.region + ((j & 1) ? regv - rows * j : 0);
-    V *nxt = c.region + (((j + 1) & 1) ? regv - rows_n * (j + 1) : 0);
-    const uint32_t lane_off = (tid & (uint32_t)(R - 1)) * VB;
-    const uint32_t hbase = h * (uint32_t)H;  // push row of (h, c) = (h*H + c)*NL
-    for (uint32_t r = tid; r < (uint32_t)rows; r += THREADS) {
-        const uint32_t l = c.lmask[base + r];
-        const uint32_t Tm = l | (h << L);
-        // the row's t values: low members from LDS, high members from the pushes
-        V g[T > 0 ? T : 1];
+    constexpr int ROWS = cbinom(L, J);
+    constexpr int BASE = tiled_moff(L, J);
+    constexpr int ROWS_N = J < L ? cbinom(L, J + 1) : 0;
+    constexpr int REGV = tiled_region_vals(L);
+    constexpr int CUR = (J & 1) ? REGV - ROWS * J : 0;
+    constexpr int NXT = ((J + 1) & 1) ? REGV - ROWS_N * (J + 1) : 0;
+    constexpr uint32_t DROW = (uint32_t)(N * R * VB);  // bytes per distance row (R copies)
+    // uniform: the high members and high non-members of h, ascending
+    uint32_t hm[HC > 0 ? HC : 1], hn[QH > 0 ? QH : 1];
+    {
         uint32_t hb = h;
 #pragma unroll
-        for (int p = 0; p < T; ++p) {
-            if (p < j) {
-                g[p] = cur[p * rows + r];
-            } else {
-                const uint32_t cb = __builtin_ctz(hb);
-                hb &= hb - 1u;
-                g[p] = c.push.load(((hbase + cb) * NL + base + r) * VB);
-            }
+        for (int i = 0; i < HC; ++i) {
+            hm[i] = __builtin_ctz(hb);
+            hb &= hb - 1u;
         }
-        // members (ascending city = ascending bit) -> their d-row offsets
-        uint32_t mrow[T > 0 ? T : 1], mcity[T > 0 ? T : 1];
-        uint32_t bits = Tm;
+        uint32_t nb = ~h & ((1u << H) - 1u);
 #pragma unroll
-        for (int p = 0; p < T; ++p) {
-            const uint32_t b = __builtin_ctz(bits);
-            bits &= bits - 1u;
-            mcity[p] = b + 1u;
-            mrow[p] = b * (uint32_t)(N * R * VB) + lane_off;
+        for (int i = 0; i < QH; ++i) {
+            hn[i] = __builtin_ctz(nb);
+            nb &= nb - 1u;
         }
+    }
+    const uint32_t lane_off = (tid & (uint32_t)(R - 1)) * VB;
+    const char *drb = reinterpret_cast<const char *>(c.dr);
+    char *lds_nxt = reinterpret_cast<char *>(c.region + NXT);
+    for (uint32_t r = tid; r < (uint32_t)ROWS; r += THREADS) {
+        const uint32_t l = c.lmask[BASE + r];
+        const uint32_t voff = (BASE + r) * VB;   // row offset in a push column
+        // the row's T values: low members from LDS, high members from the pushes
+        V g[T];
+#pragma unroll
+        for (int p = 0; p < J; ++p) g[p] = c.region[CUR + p * ROWS + r];
+#pragma unroll
+        for (int i = 0; i < HC; ++i) {
+            if constexpr (TSPGPU_TILED_ABL & 1)
+                g[J + i] = c.region[(CUR + i * 7 + r) % REGV];
+            else
+                g[J + i] = c.push.load(voff, (h * H + hm[i]) * (uint32_t)(NL * VB));
+        }
+        // members ascending (low bits of l, then the high members of h)
+        uint32_t mbit[T], mrow[T];
+        uint32_t lb = l;
+#pragma unroll
+        for (int p = 0; p < J; ++p) {
+            mbit[p] = __builtin_ctz(lb);
+            lb &= lb - 1u;
+            mrow[p] = mbit[p] * DROW + lane_off;
+        }
+#pragma unroll
+        for (int i = 0; i < HC; ++i) {
+            mbit[J + i] = L + hm[i];
+            mrow[J + i] = (L + hm[i]) * DROW + lane_off;
+        }
+        // non-members ascending (low non-members of l, then those of h)
         uint32_t kb[Q], kof[Q];
-        uint32_t nb = ~Tm & FULL;
+        uint32_t nb = ~l & (uint32_t)(NL - 1);
 #pragma unroll
-        for (int q = 0; q < Q; ++q) {
+        for (int q = 0; q < QL; ++q) {
             kb[q] = __builtin_ctz(nb);
             nb &= nb - 1u;
             kof[q] = kb[q] * (uint32_t)(R * VB);
         }
-        V acc[Q];
-        uint32_t arg[Q];
 #pragma unroll
-        for (int q = 0; q < Q; ++q) {
-            acc[q] = ValT<V>::inf;
-            arg[q] = 0;
+        for (int i = 0; i < QH; ++i) {
+            kb[QL + i] = L + hn[i];
+            kof[QL + i] = (L + hn[i]) * (uint32_t)(R * VB);
         }
-        // the t*Q relaxations in member-major order (members ascending for
-        // every destination), each d value loaded TSPGPU_TILED_AHEAD
-        // relaxations ahead; a scheduling barrier per relaxation keeps the
-        // compiler from hoisting all t*Q loads (and their registers) up front
-        const char *drb = reinterpret_cast<const char *>(c.dr);
+        // T*Q relaxations, member-major (members ascending for every
+        // destination), each d value loaded TSPGPU_TILED_AHEAD relaxations
+        // ahead; a scheduling barrier per relaxation keeps the compiler from
+        // hoisting all loads (and their registers) up front.  The first
+        // member initialises acc/arg: with validated inputs every candidate is
+        // below the reference's INT_MAX start value (tsp.cpp:453), so its
+        // first comparison always succeeds.
         constexpr int TQ = T * Q;
         constexpr int AH = TSPGPU_TILED_AHEAD < TQ ? TSPGPU_TILED_AHEAD : TQ;
         V dv[AH];
 #pragma unroll
         for (int i = 0; i < AH; ++i) dv[i] = *reinterpret_cast<const V *>(drb + mrow[i / Q] + kof[i % Q]);
+        V acc[Q];
+        uint32_t arg[Q];
 #pragma unroll
         for (int i = 0; i < TQ; ++i) {
-            const V d = dv[i % AH];
+            V d = dv[i % AH];
+            if constexpr (TSPGPU_TILED_ABL & 2) d = g[(i + 1) % T];
             if (i + AH < TQ) dv[i % AH] = *reinterpret_cast<const V *>(drb + mrow[(i + AH) / Q] + kof[(i + AH) % Q]);
-            relax_argmin(acc[i % Q], arg[i % Q], g[i / Q], d, mcity[i / Q]);
+            if (i < Q) {
+                acc[i] = g[0] + d;
+                arg[i] = mbit[0];
+            } else {
+                if constexpr (TSPGPU_TILED_ABL & 8)
+                    acc[i % Q] = ValT<V>::vmin(acc[i % Q], g[i / Q] + d);
+                else
+                    relax_argmin(acc[i % Q], arg[i % Q], g[i / Q], d, mbit[i / Q]);
+            }
             __builtin_amdgcn_sched_barrier(0);
         }
-        // destinations: the L-j low non-members come first (uniform split)
+        // destinations: low k -> next LDS layer (position k - q, colex rank of l + k)
+#pragma unroll
+        for (int q = 0; q < QL; ++q) {
+            const uint32_t k = kb[q];
+            const uint32_t rb = c.lrankb[l | (1u << k)];
+            *reinterpret_cast<V *>(lds_nxt + (k - (uint32_t)q) * (uint32_t)(ROWS_N * VB) + rb) = acc[q];
+        }
+        // high k -> the push column (h | k, k) of sub-cube h | k, same row index
+#pragma unroll
+        for (int i = 0; i < QH; ++i)
+            c.push.store(voff, ((h | (1u << hn[i])) * H + hn[i]) * (uint32_t)(NL * VB), acc[QL + i]);
+        // the row's parent word: nibble q = bit index of the argmin member
+        uint32_t wlo = 0, whi = 0;
 #pragma unroll
         for (int q = 0; q < Q; ++q) {
-            if (q < L - j) {
-                const uint32_t k = kb[q];
-                const uint32_t pos = k - (uint32_t)q;  // members of l below k
-                const uint32_t rk = c.lrank[l | (1u << k)];
-                nxt[pos * rows_n + rk] = acc[q];
-            } else {
-                const uint32_t cb = kb[q] - L;
-                c.push.store((((h | (1u << cb)) * H + cb) * NL + base + r) * VB, acc[q]);
-            }
+            if (q < 8)
+                wlo |= arg[q] << (4 * q);
+            else
+                whi |= arg[q] << (4 * (q - 8));
         }
-        uint64_t w = 0;
-#pragma unroll
-        for (int q = 0; q < Q; ++q) w |= (uint64_t)((arg[q] - 1u) & 15u) << (4 * q);
-        c.par.store((h * NL + base + r) * 8u, w, 1);
+        c.par.store_nt((BASE + r) * 8u, h * (uint32_t)(NL * 8), ((uint64_t)whi << 32) | wlo);
     }
 }
 
-template <typename V, int N, int L, int THREADS, int R>
-__device__ __forceinline__ void tiled_dispatch(const TiledCtx<V, N, L, R> &c, uint32_t h, int j, int t, uint32_t tid)
+template <typename V, int N, int L, int J, int THREADS, int R>
+__device__ __forceinline__ void tiled_dispatch_h(const TiledCtx<V, N, L, R> &c, uint32_t h, int hc, uint32_t tid)
 {
-#define TSPGPU_TP(TT) \
-    case TT:          \
-        if constexpr (TT < N) tiled_pass<V, N, L, TT, THREADS, R>(c, h, j, tid); \
+    constexpr int H = N - L;
+#define TSPGPU_TP(HC)                                                                      \
+    case HC:                                                                               \
+        if constexpr (HC <= H && J + HC >= 1 && J + HC < N)                                \
+            tiled_pass<V, N, L, J + HC, J, THREADS, R>(c, h, tid);                         \
         break;
-    switch (t) {
-        TSPGPU_TP(1) TSPGPU_TP(2) TSPGPU_TP(3) TSPGPU_TP(4) TSPGPU_TP(5) TSPGPU_TP(6) TSPGPU_TP(7)
-        TSPGPU_TP(8) TSPGPU_TP(9) TSPGPU_TP(10) TSPGPU_TP(11) TSPGPU_TP(12) TSPGPU_TP(13) TSPGPU_TP(14)
-        TSPGPU_TP(15) TSPGPU_TP(16) TSPGPU_TP(17) TSPGPU_TP(18)
+    switch (hc) {
+        TSPGPU_TP(0) TSPGPU_TP(1) TSPGPU_TP(2) TSPGPU_TP(3) TSPGPU_TP(4) TSPGPU_TP(5)
     default: break;
     }
 #undef TSPGPU_TP
+}
+
+template <typename V, int N, int L, int THREADS, int R>
+__device__ __forceinline__ void tiled_dispatch(const TiledCtx<V, N, L, R> &c, uint32_t h, int hc, int j, uint32_t tid)
+{
+#define TSPGPU_TJ(JJ)                                                                      \
+    case JJ:                                                                               \
+        if constexpr (JJ <= L) tiled_dispatch_h<V, N, L, JJ, THREADS, R>(c, h, hc, tid);   \
+        break;
+    switch (j) {
+        TSPGPU_TJ(0) TSPGPU_TJ(1) TSPGPU_TJ(2) TSPGPU_TJ(3) TSPGPU_TJ(4) TSPGPU_TJ(5) TSPGPU_TJ(6)
+        TSPGPU_TJ(7) TSPGPU_TJ(8) TSPGPU_TJ(9) TSPGPU_TJ(10) TSPGPU_TJ(11) TSPGPU_TJ(12)
+    default: break;
+    }
+#undef TSPGPU_TJ
 }
 
 __host__ __device__ constexpr int tiled_waves(int threads, int wg_per_cu) { return threads * wg_per_cu / 256; }
@@ -299,25 +373,18 @@ __global__ __launch_bounds__(THREADS, tiled_waves(THREADS, WG)) void hk_tiled_ke
     V *dc = d0 + 16;           // d[m][0], m = 1..N at [m-1]
     V *region = dc + 16;
     uint16_t *lmask = reinterpret_cast<uint16_t *>(region + tiled_region_vals(L));
-    uint16_t *lrank = lmask + NL;
-    __shared__ int s_moff[kTiledMaxL + 2], s_cnt[kTiledMaxL + 2];
+    uint16_t *lrankb = lmask + NL;
     const uint32_t tid = threadIdx.x;
 
     for (int i = tid; i < NL; i += THREADS) {
         lmask[i] = info->mask[i];
-        lrank[i] = info->rank[i];
-    }
-    if (tid < L + 2) {
-        s_moff[tid] = info->moff[tid];
-        s_cnt[tid] = info->cnt[tid];
+        lrankb[i] = (uint16_t)(info->rank[i] * VB);
     }
     TiledCtx<V, N, L, R> c;
     c.dr = dr;
     c.lmask = lmask;
-    c.lrank = lrank;
+    c.lrankb = lrankb;
     c.region = region;
-    c.moff = s_moff;
-    c.cnt = s_cnt;
     c.push.rs = uniform_rsrc(slots + (size_t)blockIdx.x * slot_bytes, (uint32_t)tiled_push_bytes(N, L, VB));
 
     for (int blk = blk0 + blockIdx.x; blk < nblocks; blk += gridDim.x) {
@@ -337,7 +404,7 @@ __global__ __launch_bounds__(THREADS, tiled_waves(THREADS, WG)) void hk_tiled_ke
         // to sub-cube {i} at row idx 0 (the empty low part)
         // (layer 1 is odd: it sits at the top of the region, regv - C(L,1))
         if (tid < L) region[tiled_region_vals(L) - L + tid] = d0[tid];
-        if (tid < H) c.push.store((((1u << tid) * H + tid) * NL + 0) * VB, d0[L + tid]);
+        if (tid < H) c.push.store(0, (((1u << tid) * H + tid) * NL) * VB, d0[L + tid]);
         __syncthreads();
 
         for (uint32_t h = 0; h < (uint32_t)NH; ++h) {
@@ -345,8 +412,8 @@ __global__ __launch_bounds__(THREADS, tiled_waves(THREADS, WG)) void hk_tiled_ke
             const int j0 = h == 0 ? 1 : 0;
             const int j1 = h == (uint32_t)(NH - 1) ? L - 1 : L;
             for (int j = j0; j <= j1; ++j) {
-                tiled_dispatch<V, N, L, THREADS, R>(c, h, j, hc + j, tid);
-                if (j < j1) lds_barrier();
+                tiled_dispatch<V, N, L, THREADS, R>(c, h, hc, j, tid);
+                if (!(TSPGPU_TILED_ABL & 4) && j < j1) lds_barrier();
             }
             // pushes of this sub-cube are read by later ones: full barrier
             __syncthreads();
@@ -361,7 +428,7 @@ __global__ __launch_bounds__(THREADS, tiled_waves(THREADS, WG)) void hk_tiled_ke
                 if (m <= L)  // low layer L: one row, position m-1
                     gl = region[((L & 1) ? tiled_region_vals(L) - L : 0) + (m - 1)];
                 else
-                    gl = c.push.load(((uint32_t)((NH - 1) * H + (m - 1 - L)) * NL + (NL - 1)) * VB);
+                    gl = c.push.load((NL - 1) * VB, ((uint32_t)((NH - 1) * H + (m - 1 - L)) * NL) * VB);
             }
             const V cand = valid ? gl + dc[m - 1] : ValT<V>::invalid;
             const V best = ValT<V>::vmin(wave_min(cand), ValT<V>::inf);
@@ -403,7 +470,7 @@ __global__ __launch_bounds__(256) void hk_tiled_backtrack(int nblocks, int blk0,
         const uint32_t idx = (uint32_t)info->moff[__builtin_popcount(lT)] + info->rank[lT];
         const uint64_t w = __builtin_nontemporal_load(pw + hT * NL + idx);
         const int q = (k - 1) - __builtin_popcount(T & ((1u << (k - 1)) - 1u));
-        const int pm = (int)((w >> (4 * q)) & 15u) + 1;
+        const int pm = (int)((w >> (4 * q)) & 15u) + 1;  // nibble = bit index of the parent city
         ok = pm <= N && ((T >> (pm - 1)) & 1u);
         tour[pos] = ok ? pm : 0;
         S = T;

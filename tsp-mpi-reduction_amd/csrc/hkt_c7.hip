@@ -1,5 +1,5 @@
 // K1 variant 5 instantiation 7 (table: hkt_cfg.h)
 #include "hk_tiled.h"
 namespace tspgpu {
-template hipError_t launch_tiled_n<int32_t, 14, 11, 256, 32, 2>(const TiledArgs &);
+template hipError_t launch_tiled_n<int32_t, 15, 11, 256, 1, 4>(const TiledArgs &);
 }  // namespace tspgpu

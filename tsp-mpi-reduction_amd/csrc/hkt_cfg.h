@@ -6,14 +6,17 @@
 #include "hk_tiled.h"
 
 #define TSPGPU_TILED_CFGS(X) \
-    X(0, double, 15, 11, 256, 16, 2) \
-    X(1, double, 15, 11, 256, 8, 2) \
     X(2, double, 15, 11, 256, 1, 3) \
-    X(3, double, 15, 11, 512, 32, 1) \
-    X(4, double, 15, 11, 256, 4, 2) \
-    X(5, double, 14, 11, 256, 16, 2) \
-    X(6, int32_t, 15, 11, 256, 32, 2) \
-    X(7, int32_t, 14, 11, 256, 32, 2)
+    X(0, double, 15, 11, 512, 1, 2) \
+    X(1, double, 15, 10, 256, 1, 4) \
+    X(3, double, 15, 10, 512, 1, 2) \
+    X(4, double, 15, 11, 512, 2, 2) \
+    X(5, double, 14, 11, 512, 1, 2) \
+    X(6, double, 14, 10, 256, 1, 4) \
+    X(7, int32_t, 15, 11, 256, 1, 4) \
+    X(8, int32_t, 15, 11, 512, 1, 2) \
+    X(9, int32_t, 14, 11, 256, 1, 4) \
+    X(10, double, 13, 10, 256, 1, 4)
 
 namespace tspgpu {
 struct TiledCfg {

@@ -262,7 +262,11 @@ int solve_device_locked(tspgpu_ctx *c, const void *d_dist, int n, int nblocks, v
         // all 256 resident blocks then stay in the Infinity Cache), not below
         // (with a full wave of blocks: one block alone is latency-bound and the
         // argmin's extra VALU only costs there)
-        a.variant = c->variant >= 0 ? c->variant : (N == 15 && vbytes == 8 && nblocks >= c->cu_count ? 4 : 2);
+        // 16 cities, f64, a full wave of blocks: the sub-cube tiled kernel
+        // (variant 5, hk_tiled.h; 9.9 vs 11.9 ms per 16384 blocks for variant 4,
+        // profiles/r02/tiled_v3.log); below 16 cities and for i32 the compact
+        // layer pass (variant 2) stays ahead
+        a.variant = c->variant >= 0 ? c->variant : (N == 15 && vbytes == 8 && nblocks >= c->cu_count ? 5 : 2);
         if (a.variant == 5) {
             if (const TiledCfg *cfg = pick_tiled(c, N, vbytes))
                 return solve_tiled(c, cfg, d_dist, n, nblocks, d_cost, d_tour, stream);
