@@ -6,23 +6,34 @@
 // is solved exactly on the MI355X in one batched call (libtspgpu); the
 // reference's distribution, local fold and reduction tree are replayed on the
 // host for the LOGICAL rank count P, which fixes the printed answer:
-//   P = PMI_SIZE / OMPI_COMM_WORLD_SIZE when started under mpirun (only rank 0
-//       prints and solves; other ranks exit 0), else TSP_NPROCS, else 1.
-// Physical GPUs (TSP_GPUS, default 1; devices 0..TSP_GPUS-1) only change speed:
-// the blocks are split into contiguous ranges, one host thread per GPU.  The
-// merges (local folds + reduction tree) run on the GPU too (K3, tspgpu_reduce);
-// TSP_HOST_MERGE=1 replays them on the host instead.
+//   P = PMI_SIZE / OMPI_COMM_WORLD_SIZE when started under mpirun, else
+//       TSP_NPROCS, else 1.
+// Under mpirun -np P (P > 1) every rank solves its own blocks, exactly the
+// reference's share (cnt[r] contiguous blocks, tsp.cpp:167-192), on GPU
+// r mod (visible devices) (TSP_GPU overrides), and hands its costs and tours
+// to rank 0 through a file in a per-job directory (no MPI library is linked:
+// TSP_GATHER_DIR, else /tmp/tspgpu-<uid>-<parent pid>-<args>, the parent
+// being mpirun's proxy, shared by the ranks of one node); rank 0 waits for all
+// of them, replays the reduction and prints.  One node only.
+// Without mpirun, physical GPUs (TSP_GPUS, default 1; device g mod visible
+// devices for g < TSP_GPUS) only change speed: the blocks are split into
+// contiguous ranges, one host thread per GPU.  The merges (local folds +
+// reduction tree) run on the GPU too (K3, tspgpu_reduce); TSP_HOST_MERGE=1
+// replays them on the host instead.
 //
 // Deviations (documented in DESIGN.md), all where the reference is undefined:
 // n < 2, numBlocks < 1 or numBlocks < P exit 2 with a message on stderr
 // instead of crashing or hanging (tsp.cpp:326-330, 355).
+#include <sys/stat.h>
 #include <time.h>
+#include <unistd.h>
 
 #include <cerrno>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <string>
 #include <thread>
 #include <vector>
 
@@ -37,36 +48,46 @@ int env_int(const char *name, int dflt)
     return (v && *v) ? std::atoi(v) : dflt;
 }
 
-int logical_ranks(int *my_rank)
+// (P, this process's rank, launched by mpirun)
+int logical_ranks(int *my_rank, bool *launched)
 {
     *my_rank = env_int("PMI_RANK", env_int("OMPI_COMM_WORLD_RANK", 0));
-    const int launched = env_int("PMI_SIZE", env_int("OMPI_COMM_WORLD_SIZE", 0));
-    if (launched > 0) return launched;
+    const int np = env_int("PMI_SIZE", env_int("OMPI_COMM_WORLD_SIZE", 0));
+    *launched = np > 0;
+    if (np > 0) return np;
     return env_int("TSP_NPROCS", 1);
 }
 
-// All blocks on `gpus` devices: contiguous ranges, one context + thread each.
-int solve_all(const std::vector<tspgpu_city> &cities, int n, int B, int gpus, std::vector<double> &cost,
-              std::vector<int32_t> &tour)
+int visible_devices()
 {
-    cost.assign(B, 0.0);
-    tour.assign((size_t)B * (n + 1), -1);
+    const int n = tspgpu_device_count();
+    return n > 0 ? n : 1;
+}
+
+// Blocks [lo, lo + count) on `gpus` devices: contiguous ranges, one context +
+// thread each; device (first_dev + g) mod visible devices.
+int solve_range(const std::vector<tspgpu_city> &cities, int n, int lo, int count, int gpus, int first_dev,
+                double *cost, int32_t *tour)
+{
+    const int B = count;
+    if (B <= 0) return 0;
     if (gpus < 1) gpus = 1;
     if (gpus > B) gpus = B;
+    const int ndev = visible_devices();
     std::vector<int> rcs(gpus, 0);
     std::vector<std::thread> th;
     for (int g = 0; g < gpus; ++g) {
         th.emplace_back([&, g] {
-            const int lo = (int)((long long)B * g / gpus), hi = (int)((long long)B * (g + 1) / gpus);
+            const int a = (int)((long long)B * g / gpus), b = (int)((long long)B * (g + 1) / gpus);
             tspgpu_opts o;
             std::memset(&o, 0, sizeof o);
-            o.device = gpus == 1 ? env_int("TSP_GPU", 0) : g;
+            o.device = (first_dev + g) % ndev;
             o.strict = 1;
             tspgpu_ctx *ctx = nullptr;
             int rc = tspgpu_ctx_create(&o, &ctx);
             if (!rc)
-                rc = tspgpu_solve_cities(ctx, cities.data() + (size_t)lo * n, n, hi - lo, cost.data() + lo,
-                                         tour.data() + (size_t)lo * (n + 1));
+                rc = tspgpu_solve_cities(ctx, cities.data() + (size_t)(lo + a) * n, n, b - a, cost + a,
+                                         tour + (size_t)a * (n + 1));
             if (ctx) tspgpu_ctx_destroy(ctx);
             rcs[g] = rc;
         });
@@ -74,6 +95,66 @@ int solve_all(const std::vector<tspgpu_city> &cities, int n, int B, int gpus, st
     for (auto &t : th) t.join();
     for (int rc : rcs)
         if (rc) return rc;
+    return 0;
+}
+
+// ---- rank-per-GPU mode: every rank's block results to rank 0 through files ----
+struct RankFileHeader {
+    uint32_t magic, rank, count, n;
+};
+constexpr uint32_t kMagic = 0x54535047;  // "TSPG"
+
+std::string gather_dir(int n, int B, int X, int Y)
+{
+    if (const char *d = std::getenv("TSP_GATHER_DIR")) return d;
+    char buf[256];
+    std::snprintf(buf, sizeof buf, "/tmp/tspgpu-%u-%d-%d-%d-%d-%d", (unsigned)getuid(), (int)getppid(), n, B, X, Y);
+    return buf;
+}
+
+int write_rank_file(const std::string &dir, int rank, int n, int count, const double *cost, const int32_t *tour)
+{
+    mkdir(dir.c_str(), 0700);  // may exist already
+    const std::string tmp = dir + "/rank" + std::to_string(rank) + ".tmp";
+    const std::string fin = dir + "/rank" + std::to_string(rank) + ".bin";
+    FILE *f = std::fopen(tmp.c_str(), "wb");
+    if (!f) return -errno;
+    RankFileHeader h{kMagic, (uint32_t)rank, (uint32_t)count, (uint32_t)n};
+    bool ok = std::fwrite(&h, sizeof h, 1, f) == 1;
+    ok = ok && (count == 0 || std::fwrite(cost, sizeof(double), (size_t)count, f) == (size_t)count);
+    ok = ok && (count == 0 || std::fwrite(tour, sizeof(int32_t), (size_t)count * (n + 1), f) == (size_t)count * (n + 1));
+    ok = (std::fclose(f) == 0) && ok;
+    if (!ok) return -EIO;
+    return std::rename(tmp.c_str(), fin.c_str()) == 0 ? 0 : -errno;  // atomic publish
+}
+
+// Rank 0: wait (up to TSP_GATHER_TIMEOUT_S, default 600 s) for every other
+// rank's file and place its blocks at their offsets.
+int read_rank_files(const std::string &dir, int P, int n, const std::vector<int> &cnt, const std::vector<int> &off,
+                    double *cost, int32_t *tour)
+{
+    const double limit = env_int("TSP_GATHER_TIMEOUT_S", 600);
+    struct timespec t0, t;
+    clock_gettime(CLOCK_MONOTONIC, &t0);
+    for (int r = 1; r < P; ++r) {
+        const std::string fin = dir + "/rank" + std::to_string(r) + ".bin";
+        FILE *f = nullptr;
+        while (!(f = std::fopen(fin.c_str(), "rb"))) {
+            clock_gettime(CLOCK_MONOTONIC, &t);
+            if ((t.tv_sec - t0.tv_sec) + 1e-9 * (t.tv_nsec - t0.tv_nsec) > limit) return -ETIMEDOUT;
+            usleep(1000);
+        }
+        RankFileHeader h{};
+        bool ok = std::fread(&h, sizeof h, 1, f) == 1 && h.magic == kMagic && (int)h.rank == r &&
+                  (int)h.count == cnt[r] && (int)h.n == n;
+        ok = ok && (cnt[r] == 0 || std::fread(cost + off[r], sizeof(double), cnt[r], f) == (size_t)cnt[r]);
+        ok = ok && (cnt[r] == 0 || std::fread(tour + (size_t)off[r] * (n + 1), sizeof(int32_t), (size_t)cnt[r] * (n + 1),
+                                              f) == (size_t)cnt[r] * (n + 1));
+        std::fclose(f);
+        std::remove(fin.c_str());
+        if (!ok) return -EIO;
+    }
+    if (!std::getenv("TSP_GATHER_DIR")) rmdir(dir.c_str());  // the per-job default directory
     return 0;
 }
 
@@ -85,7 +166,9 @@ int main(int argc, char **argv)
     clock_gettime(CLOCK_MONOTONIC_RAW, &start);  // tsp.cpp:275-276, before any setup
 
     int my_rank = 0;
-    const int P = logical_ranks(&my_rank);
+    bool launched = false;
+    const int P = logical_ranks(&my_rank, &launched);
+    const bool multi = launched && P > 1;  // one process per rank (mpirun)
     if (argc != 5) {
         // every rank prints the usage (tsp.cpp:280-284)
         const int copies = my_rank == 0 && !std::getenv("PMI_SIZE") && !std::getenv("OMPI_COMM_WORLD_SIZE") ? P : 1;
@@ -102,10 +185,32 @@ int main(int argc, char **argv)
                         "16 cities per block...\n");
         return 1337;  // exit(1337): status 57 (tsp.cpp:294)
     }
-    if (my_rank != 0) return 0;  // under mpirun, rank 0 does the whole job
+    if (my_rank != 0 && !multi) return 0;
+    const bool bad = n < 2 || B < 1 || B < P;
+    if (my_rank != 0) {
+        // a worker rank: solve this rank's share of the blocks and hand it to rank 0
+        if (bad) return 0;  // rank 0 reports the error
+        std::vector<tspgpu_city> cities((size_t)B * n);
+        tsphost_generate(n, B, X, Y, cities.data());
+        std::vector<int> cnt(P), off(P, 0);
+        tsphost_distribution_counts(B, P, cnt.data());
+        for (int r = 1; r < P; ++r) off[r] = off[r - 1] + cnt[r - 1];
+        std::vector<double> cost(cnt[my_rank]);
+        std::vector<int32_t> tour((size_t)cnt[my_rank] * (n + 1), -1);
+        const int ndev = visible_devices();
+        const int dev = env_int("TSP_GPU", my_rank % ndev);
+        int rc = solve_range(cities, n, off[my_rank], cnt[my_rank], env_int("TSP_GPUS", 1), dev, cost.data(),
+                             tour.data());
+        if (!rc) rc = write_rank_file(gather_dir(n, B, X, Y), my_rank, n, cnt[my_rank], cost.data(), tour.data());
+        if (rc) {
+            std::fprintf(stderr, "tsp: rank %d failed: %s (%d)\n", my_rank, tspgpu_strerror(rc), rc);
+            return 3;
+        }
+        return 0;
+    }
 
     std::printf("We have %i cities for each of our %i blocks\n", n, B);  // tsp.cpp:307
-    if (n < 2 || B < 1 || B < P) {
+    if (bad) {
         std::fflush(stdout);
         std::fprintf(stderr, "tsp: needs numCitiesPerBlock >= 2 and numBlocks >= max(1, ranks=%d); the reference "
                              "crashes or hangs here\n", P);
@@ -117,9 +222,19 @@ int main(int argc, char **argv)
     std::vector<tspgpu_city> cities((size_t)B * n);
     tsphost_generate(n, B, X, Y, cities.data());
 
-    std::vector<double> cost;
-    std::vector<int32_t> tour;
-    const int rc = solve_all(cities, n, B, env_int("TSP_GPUS", 1), cost, tour);
+    std::vector<double> cost(B, 0.0);
+    std::vector<int32_t> tour((size_t)B * (n + 1), -1);
+    int rc;
+    if (multi) {
+        // rank 0's own share here, the other ranks' shares from their files
+        std::vector<int> cnt(P), off(P, 0);
+        tsphost_distribution_counts(B, P, cnt.data());
+        for (int r = 1; r < P; ++r) off[r] = off[r - 1] + cnt[r - 1];
+        rc = solve_range(cities, n, 0, cnt[0], env_int("TSP_GPUS", 1), env_int("TSP_GPU", 0), cost.data(), tour.data());
+        if (!rc) rc = read_rank_files(gather_dir(n, B, X, Y), P, n, cnt, off, cost.data(), tour.data());
+    } else {
+        rc = solve_range(cities, n, 0, B, env_int("TSP_GPUS", 1), env_int("TSP_GPU", 0), cost.data(), tour.data());
+    }
     if (rc) {
         std::fflush(stdout);
         std::fprintf(stderr, "tsp: GPU block search failed: %s (%d)\n", tspgpu_strerror(rc), rc);

@@ -100,15 +100,15 @@ BlockSolution mergeBlocks(BlockSolution s1, BlockSolution s2)
     return m;
 }
 
-std::vector<int> getBlocksPerDim(int numBlocks)
+__attribute__((weak)) std::vector<int> getBlocksPerDim(int numBlocks)
 {
     int r, c;
     tsphost_blocks_per_dim(numBlocks, &r, &c);
     return {r, c};
 }
 
-std::vector<std::vector<City>> distributeCities(int numCitiesPerBlock, int numBlocksInRow, int numBlocksInCol,
-                                                int gridDimX, int gridDimY)
+__attribute__((weak)) std::vector<std::vector<City>> distributeCities(int numCitiesPerBlock, int numBlocksInRow,
+                                                                      int numBlocksInCol, int gridDimX, int gridDimY)
 {
     const int B = numBlocksInRow * numBlocksInCol;
     std::vector<tspgpu_city> flat((size_t)B * numCitiesPerBlock);

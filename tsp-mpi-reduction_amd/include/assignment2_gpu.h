@@ -16,22 +16,28 @@
 
 #include "tspgpu.h"
 
-struct City {
+// typedef'd anonymous structs exactly like the reference, so that the mangled
+// names of tsp(vector<City>) and mergeBlocks(BlockSolution, BlockSolution)
+// are the reference's own (the drop-in link of tsp.cpp relies on it)
+typedef struct
+{
     int id;
     double x;
     double y;
-};
+} City;
 
-struct PathCost {
+typedef struct
+{
     double cost;
     std::vector<int> path;
-};
+} PathCost;
 
-struct BlockSolution {
+typedef struct
+{
     int blockId;
     std::vector<City> path;
     double cost;
-};
+} BlockSolution;
 
 static_assert(sizeof(City) == sizeof(tspgpu_city), "City must keep the reference's 24-byte layout");
 
@@ -39,6 +45,13 @@ static_assert(sizeof(City) == sizeof(tspgpu_city), "City must keep the reference
 // Weak so that a program that defines its own procNum (as tsp.cpp does) wins.
 extern int procNum;
 
+// The GPU versions of the reference's tsp() and mergeBlocks().  Strong
+// symbols: linked together with the reference's tsp.cpp whose own two
+// definitions were made weak (objcopy --weaken-symbol, oracle/Makefile
+// _ref/tsp_dropin), these are the ones the reference's call sites reach.
+// distributeCities and getBlocksPerDim are weak here: the reference's own
+// definitions (tsp.cpp:136-157, 373-403) win when both are linked.
+//
 // One block on the GPU. Aborts with a message on a library error (the
 // reference has no error channel; a silent CPU fallback is never taken).
 BlockSolution tsp(std::vector<City> cities);
