@@ -86,7 +86,11 @@ int tspgpu_solve_cities(tspgpu_ctx *ctx, const tspgpu_city *cities, int n, int n
 
 /* Device-pointer form, asynchronous on `hip_stream` (hipStream_t, NULL = default).
  * The caller guarantees the data satisfy tspgpu_validate (not re-checked).
- * d_dist/d_cost/d_tour are device pointers on the context's device. */
+ * d_dist/d_cost/d_tour are device pointers on the context's device.
+ * Calls on one context may use different streams: they share the context's
+ * DP workspace, so a launch on a stream other than the previous launch's
+ * waits (hipStreamWaitEvent) for that launch first; use one context per
+ * stream for concurrent batches. */
 int tspgpu_solve_blocks_device(tspgpu_ctx *ctx, const double *d_dist, int n, int nblocks, double *d_cost,
                                int32_t *d_tour, void *hip_stream);
 
@@ -117,6 +121,11 @@ int tspgpu_device_free(tspgpu_ctx *ctx, void *ptr);
 int tspgpu_memcpy_htod(tspgpu_ctx *ctx, void *dst, const void *src, size_t bytes);
 int tspgpu_memcpy_dtoh(tspgpu_ctx *ctx, void *dst, const void *src, size_t bytes);
 void *tspgpu_stream(tspgpu_ctx *ctx);
+/* Extra non-blocking streams on the context's device (for callers without a
+ * HIP runtime of their own), and a host wait on any stream. */
+int tspgpu_stream_create(tspgpu_ctx *ctx, void **stream);
+int tspgpu_stream_destroy(tspgpu_ctx *ctx, void *stream);
+int tspgpu_stream_synchronize(tspgpu_ctx *ctx, void *stream);
 int tspgpu_synchronize(tspgpu_ctx *ctx);
 int tspgpu_timer_start(tspgpu_ctx *ctx);
 int tspgpu_timer_stop(tspgpu_ctx *ctx, float *elapsed_ms);

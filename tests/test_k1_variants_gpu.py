@@ -124,3 +124,33 @@ def test_single_block_equals_its_row_of_the_big_batch(gpu_ctx):
         c1, t1 = gpu_ctx.solve_blocks(d[b:b + 1])
         assert gpu_ctx.last_variant() == 2
         assert c1[0] == cost[b] and t1[0].tolist() == tour[b].tolist()
+
+
+def test_back_to_back_launches_on_two_streams_share_the_workspace_safely(gpu_ctx):
+    """Device entry points on one context but on two different streams, issued
+    back to back without a host sync: the second launch waits for
+    the first (they share the context's DP workspace), so both batches come out
+    exactly as when solved one after the other."""
+    da, db = _blocks(16, B_BIG, 31), _blocks(16, B_BIG, 32)
+    ref_a, ref_b = gpu_ctx.solve_blocks(da), gpu_ctx.solve_blocks(db)
+    s1, s2 = gpu_ctx.stream_create(), gpu_ctx.stream_create()
+    bufs = []
+    try:
+        pa, pb = gpu_ctx.upload(da), gpu_ctx.upload(db)
+        ca, cb = gpu_ctx.alloc(B_BIG * 8), gpu_ctx.alloc(B_BIG * 8)
+        wa, wb = gpu_ctx.alloc(B_BIG * 17 * 4), gpu_ctx.alloc(B_BIG * 17 * 4)
+        bufs = [pa, pb, ca, cb, wa, wb]
+        for _ in range(3):
+            gpu_ctx.solve_device(pa, 16, B_BIG, ca, wa, s1)
+            gpu_ctx.solve_device(pb, 16, B_BIG, cb, wb, s2)
+        gpu_ctx.synchronize(s1)
+        gpu_ctx.synchronize(s2)
+        assert np.array_equal(gpu_ctx.download(ca, (B_BIG,), np.float64), ref_a[0])
+        assert np.array_equal(gpu_ctx.download(wa, (B_BIG, 17), np.int32), ref_a[1])
+        assert np.array_equal(gpu_ctx.download(cb, (B_BIG,), np.float64), ref_b[0])
+        assert np.array_equal(gpu_ctx.download(wb, (B_BIG, 17), np.int32), ref_b[1])
+    finally:
+        for p_ in bufs:
+            gpu_ctx.free(p_)
+        gpu_ctx.stream_destroy(s1)
+        gpu_ctx.stream_destroy(s2)

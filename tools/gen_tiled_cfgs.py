@@ -13,6 +13,7 @@ CSRC = os.path.join(ROOT, "tsp-mpi-reduction_amd", "csrc")
 
 # (id, value type, N, L, threads per workgroup, distance copies R, workgroups per CU)
 CFGS = [
+    (12, "double", 15, 10, 256, 1, 5),
     (2, "double", 15, 11, 256, 1, 3),
     (0, "double", 15, 11, 512, 1, 2),
     (1, "double", 15, 10, 256, 1, 4),
@@ -24,6 +25,8 @@ CFGS = [
     (8, "int32_t", 15, 11, 512, 1, 2),
     (9, "int32_t", 14, 11, 256, 1, 4),
     (10, "double", 13, 10, 256, 1, 4),
+    (11, "double", 15, 10, 128, 1, 6),
+    (13, "double", 15, 10, 192, 1, 5),
 ]
 
 

@@ -40,6 +40,12 @@ struct tspgpu_ctx {
     uint64_t *d_parents = nullptr; // variant 5 parent words (one table per block of a chunk)
     size_t parents_bytes = 0;
     hipEvent_t ev_start = nullptr, ev_stop = nullptr;
+    // K1 workspace ordering across caller streams: the slots / push areas are
+    // per context, so a launch on a stream other than the previous one waits
+    // for the previous launch (event recorded after every K1 launch)
+    hipEvent_t ev_k1_done = nullptr;
+    hipStream_t k1_last_stream = nullptr;
+    bool k1_launched = false;
     char name[256] = {0};
     std::mutex mu;
     // K1-wide per-context cache (buffers + captured launch graph of the last n), hkwide.hip

@@ -549,7 +549,7 @@ __device__ __forceinline__ void layer_pass_compact(const SrcTab &src, const DstT
         if constexpr (PTab::on) {
             uint64_t w = 0;
 #pragma unroll
-            for (int q = 0; q < Q; ++q) w |= (uint64_t)(arg[q] - 1u) << (4 * q);
+            for (int q = 0; q < Q; ++q) w |= (uint64_t)((arg[q] - 1u) & 15u) << (4 * q);  // no argmin -> 15
             par.store(mask_off(N, T) + r, w);
         }
     }
@@ -725,21 +725,25 @@ __global__ __launch_bounds__(THREADS, min_waves(N, VAR, THREADS)) void heldkarp_
                 int32_t *tour = tour_out + (size_t)blk * (n + 1);
                 uint32_t S = (1u << N) - 1u;
                 int k = bestM;
-                for (int pos = n - 2; bestM && pos >= 1; --pos) {
+                bool ok = true;
+                for (int pos = n - 2; bestM && ok && pos >= 1; --pos) {
                     // parent word of the source row T = S \ k (layer |S| - 1), nibble of k
                     const uint32_t T = S & ~(1u << (k - 1));
                     const int tt = __builtin_popcount(T);
                     const int q = (k - 1) - __builtin_popcount(T & ((1u << (k - 1)) - 1u));
                     const uint64_t w = par.load((uint32_t)info->moff[tt] + lut_rank<N>(T, rl));
                     const int pm = (int)((w >> (4 * q)) & 15u) + 1;
-                    tour[pos] = pm;
+                    // a parent outside T (only from unvalidated input whose every
+                    // candidate reached INT_MAX) ends the walk with cost -1, like variant 2
+                    ok = pm <= N && ((T >> (pm - 1)) & 1u);
+                    tour[pos] = ok ? pm : 0;
                     S &= ~(1u << (k - 1));
                     k = pm;
                 }
                 tour[0] = 0;
                 tour[n - 1] = bestM;
                 tour[n] = 0;
-                cost_out[blk] = bestM ? best : V(-1);
+                cost_out[blk] = (bestM && ok) ? best : V(-1);
             }
         } else if (tid < 64) {
             const int lane = tid;

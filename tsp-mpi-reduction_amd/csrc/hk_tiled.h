@@ -38,6 +38,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "heldkarp_impl.h"
 
 namespace tspgpu {
@@ -49,8 +51,11 @@ constexpr int kTiledMaxL = 12;
 #ifndef TSPGPU_TILED_ABL
 #define TSPGPU_TILED_ABL 0
 #endif
+#ifndef TSPGPU_TILED_QC
+#define TSPGPU_TILED_QC 7  // destinations relaxed together (register budget of a chunk)
+#endif
 #ifndef TSPGPU_TILED_AHEAD
-#define TSPGPU_TILED_AHEAD 8  // d loads in flight per lane in the relaxation loop
+#define TSPGPU_TILED_AHEAD 6  // d loads in flight per lane in the relaxation loop
 #endif
 
 // host-built tables of one L (device copy, staged into LDS per workgroup)
@@ -75,7 +80,7 @@ __host__ __device__ constexpr int tiled_region_vals(int L)
 }
 __host__ __device__ constexpr size_t tiled_lds_bytes(int N, int L, int R, int vb)
 {
-    return (size_t)N * N * R * vb            // replicated inner distances
+    return (size_t)N * 16 * R * vb           // replicated inner distances, rows of 16
            + (size_t)2 * 16 * vb             // d[0][k], d[m][0]
            + (size_t)tiled_region_vals(L) * vb  // live low layers
            + (size_t)2 * 2 * (1 << L);       // mask + rank (u16)
@@ -88,6 +93,21 @@ __host__ __device__ constexpr size_t tiled_push_bytes(int N, int L, int vb)
 }
 // parent words of one block: [h][idx] u64
 __host__ __device__ constexpr size_t tiled_parent_bytes(int N, int L) { return (size_t)8 << N; }
+
+// f(std::integral_constant<int, 0>), ..., f(std::integral_constant<int, C-1>)
+template <int I, int C, typename F>
+__device__ __forceinline__ void static_for_impl(F &&f)
+{
+    if constexpr (I < C) {
+        f(std::integral_constant<int, I>{});
+        static_for_impl<I + 1, C>(f);
+    }
+}
+template <int C, typename F>
+__device__ __forceinline__ void static_for(F &&f)
+{
+    static_for_impl<0, C>(f);
+}
 
 __host__ __device__ constexpr int tiled_moff(int L, int J)
 {
@@ -204,7 +224,12 @@ __device__ __forceinline__ void tiled_pass(const TiledCtx<V, N, L, R> &c, uint32
     constexpr int REGV = tiled_region_vals(L);
     constexpr int CUR = (J & 1) ? REGV - ROWS * J : 0;
     constexpr int NXT = ((J + 1) & 1) ? REGV - ROWS_N * (J + 1) : 0;
-    constexpr uint32_t DROW = (uint32_t)(N * R * VB);  // bytes per distance row (R copies)
+    // distance rows of 16 entries (R copies each): a member's row offset is
+    // bit << SM, a non-member's column offset bit << SK, both shifts; the
+    // argmin is kept as the member's row offset (one register less per member)
+    constexpr int SK = __builtin_ctz((unsigned)(R * VB));
+    constexpr int SM = SK + 4;
+    static_assert((R & (R - 1)) == 0 && N <= 16, "R must be a power of two");
     // uniform: the high members and high non-members of h, ascending
     uint32_t hm[HC > 0 ? HC : 1], hn[QH > 0 ? QH : 1];
     {
@@ -239,83 +264,88 @@ __device__ __forceinline__ void tiled_pass(const TiledCtx<V, N, L, R> &c, uint32
                 g[J + i] = c.push.load(voff, (h * H + hm[i]) * (uint32_t)(NL * VB));
         }
         // members ascending (low bits of l, then the high members of h)
-        uint32_t mbit[T], mrow[T];
+        uint32_t mrow[T];
         uint32_t lb = l;
 #pragma unroll
         for (int p = 0; p < J; ++p) {
-            mbit[p] = __builtin_ctz(lb);
+            mrow[p] = ((uint32_t)__builtin_ctz(lb) << SM) | lane_off;
             lb &= lb - 1u;
-            mrow[p] = mbit[p] * DROW + lane_off;
         }
 #pragma unroll
-        for (int i = 0; i < HC; ++i) {
-            mbit[J + i] = L + hm[i];
-            mrow[J + i] = (L + hm[i]) * DROW + lane_off;
-        }
-        // non-members ascending (low non-members of l, then those of h)
-        uint32_t kb[Q], kof[Q];
-        uint32_t nb = ~l & (uint32_t)(NL - 1);
-#pragma unroll
-        for (int q = 0; q < QL; ++q) {
-            kb[q] = __builtin_ctz(nb);
-            nb &= nb - 1u;
-            kof[q] = kb[q] * (uint32_t)(R * VB);
-        }
-#pragma unroll
-        for (int i = 0; i < QH; ++i) {
-            kb[QL + i] = L + hn[i];
-            kof[QL + i] = (L + hn[i]) * (uint32_t)(R * VB);
-        }
-        // T*Q relaxations, member-major (members ascending for every
+        for (int i = 0; i < HC; ++i) mrow[J + i] = ((L + hm[i]) << SM) | lane_off;
+        // Destinations in chunks of at most TSPGPU_TILED_QC (registers: acc,
+        // arg and the column offsets of one chunk only); the non-members come
+        // ascending (low non-members of l, then those of h).  Per chunk: the
+        // T*QC relaxations, member-major (members ascending for every
         // destination), each d value loaded TSPGPU_TILED_AHEAD relaxations
         // ahead; a scheduling barrier per relaxation keeps the compiler from
         // hoisting all loads (and their registers) up front.  The first
         // member initialises acc/arg: with validated inputs every candidate is
         // below the reference's INT_MAX start value (tsp.cpp:453), so its
         // first comparison always succeeds.
-        constexpr int TQ = T * Q;
-        constexpr int AH = TSPGPU_TILED_AHEAD < TQ ? TSPGPU_TILED_AHEAD : TQ;
-        V dv[AH];
-#pragma unroll
-        for (int i = 0; i < AH; ++i) dv[i] = *reinterpret_cast<const V *>(drb + mrow[i / Q] + kof[i % Q]);
-        V acc[Q];
-        uint32_t arg[Q];
-#pragma unroll
-        for (int i = 0; i < TQ; ++i) {
-            V d = dv[i % AH];
-            if constexpr (TSPGPU_TILED_ABL & 2) d = g[(i + 1) % T];
-            if (i + AH < TQ) dv[i % AH] = *reinterpret_cast<const V *>(drb + mrow[(i + AH) / Q] + kof[(i + AH) % Q]);
-            if (i < Q) {
-                acc[i] = g[0] + d;
-                arg[i] = mbit[0];
-            } else {
-                if constexpr (TSPGPU_TILED_ABL & 8)
-                    acc[i % Q] = ValT<V>::vmin(acc[i % Q], g[i / Q] + d);
-                else
-                    relax_argmin(acc[i % Q], arg[i % Q], g[i / Q], d, mbit[i / Q]);
-            }
-            __builtin_amdgcn_sched_barrier(0);
-        }
-        // destinations: low k -> next LDS layer (position k - q, colex rank of l + k)
-#pragma unroll
-        for (int q = 0; q < QL; ++q) {
-            const uint32_t k = kb[q];
-            const uint32_t rb = c.lrankb[l | (1u << k)];
-            *reinterpret_cast<V *>(lds_nxt + (k - (uint32_t)q) * (uint32_t)(ROWS_N * VB) + rb) = acc[q];
-        }
-        // high k -> the push column (h | k, k) of sub-cube h | k, same row index
-#pragma unroll
-        for (int i = 0; i < QH; ++i)
-            c.push.store(voff, ((h | (1u << hn[i])) * H + hn[i]) * (uint32_t)(NL * VB), acc[QL + i]);
-        // the row's parent word: nibble q = bit index of the argmin member
+        uint32_t nb = ~l & (uint32_t)(NL - 1);
         uint32_t wlo = 0, whi = 0;
+        constexpr int QC = TSPGPU_TILED_QC;
+        static_for<(Q + QC - 1) / QC>([&](auto ci) {
+            constexpr int C0 = decltype(ci)::value * QC;
+            constexpr int QN = Q - C0 < QC ? Q - C0 : QC;
+            uint32_t kof[QN];
 #pragma unroll
-        for (int q = 0; q < Q; ++q) {
-            if (q < 8)
-                wlo |= arg[q] << (4 * q);
-            else
-                whi |= arg[q] << (4 * (q - 8));
-        }
+            for (int qq = 0; qq < QN; ++qq) {
+                const int q = C0 + qq;
+                if (q < QL) {
+                    kof[qq] = (uint32_t)__builtin_ctz(nb) << SK;
+                    nb &= nb - 1u;
+                } else {
+                    kof[qq] = (L + hn[q - QL]) << SK;
+                }
+            }
+            V acc[QN];
+            uint32_t arg[QN];
+            {
+                constexpr int TQ = T * QN;
+                constexpr int AH = TSPGPU_TILED_AHEAD < TQ ? TSPGPU_TILED_AHEAD : TQ;
+                V dv[AH];
+#pragma unroll
+                for (int i = 0; i < AH; ++i) dv[i] = *reinterpret_cast<const V *>(drb + mrow[i / QN] + kof[i % QN]);
+#pragma unroll
+                for (int i = 0; i < TQ; ++i) {
+                    V d = dv[i % AH];
+                    if constexpr (TSPGPU_TILED_ABL & 2) d = g[(i + 1) % T];
+                    if (i + AH < TQ)
+                        dv[i % AH] = *reinterpret_cast<const V *>(drb + mrow[(i + AH) / QN] + kof[(i + AH) % QN]);
+                    if (i < QN) {
+                        acc[i] = g[0] + d;
+                        arg[i] = mrow[0];
+                    } else {
+                        if constexpr (TSPGPU_TILED_ABL & 8)
+                            acc[i % QN] = ValT<V>::vmin(acc[i % QN], g[i / QN] + d);
+                        else
+                            relax_argmin(acc[i % QN], arg[i % QN], g[i / QN], d, mrow[i / QN]);
+                    }
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+            }
+#pragma unroll
+            for (int qq = 0; qq < QN; ++qq) {
+                const int q = C0 + qq;
+                if (q < QL) {
+                    // low k -> next LDS layer (position k - q, colex rank of l + k)
+                    const uint32_t k = kof[qq] >> SK;
+                    const uint32_t rb = c.lrankb[l | (1u << k)];
+                    *reinterpret_cast<V *>(lds_nxt + (k - (uint32_t)q) * (uint32_t)(ROWS_N * VB) + rb) = acc[qq];
+                } else {
+                    // high k -> the push column (h | k, k) of sub-cube h | k, same row index
+                    const uint32_t cb = hn[q - QL];
+                    c.push.store(voff, ((h | (1u << cb)) * H + cb) * (uint32_t)(NL * VB), acc[qq]);
+                }
+                // the row's parent word: nibble q = bit index of the argmin member
+                if (q < 8)
+                    wlo |= (arg[qq] >> SM) << (4 * q);
+                else
+                    whi |= (arg[qq] >> SM) << (4 * (q - 8));
+            }
+        });
         c.par.store_nt((BASE + r) * 8u, h * (uint32_t)(NL * 8), ((uint64_t)whi << 32) | wlo);
     }
 }
@@ -369,7 +399,7 @@ __global__ __launch_bounds__(THREADS, tiled_waves(THREADS, WG)) void hk_tiled_ke
     constexpr int VB = sizeof(V);
     extern __shared__ __attribute__((aligned(16))) char smem[];
     V *dr = reinterpret_cast<V *>(smem);
-    V *d0 = dr + N * N * R;    // d[0][k], k = 1..N at [k-1]
+    V *d0 = dr + N * 16 * R;   // d[0][k], k = 1..N at [k-1]
     V *dc = d0 + 16;           // d[m][0], m = 1..N at [m-1]
     V *region = dc + 16;
     uint16_t *lmask = reinterpret_cast<uint16_t *>(region + tiled_region_vals(L));
@@ -389,9 +419,9 @@ __global__ __launch_bounds__(THREADS, tiled_waves(THREADS, WG)) void hk_tiled_ke
 
     for (int blk = blk0 + blockIdx.x; blk < nblocks; blk += gridDim.x) {
         const V *dsrc = dist + (size_t)blk * n * n;
-        for (int i = tid; i < N * N * R; i += THREADS) {
-            const int e = i / R;
-            dr[i] = dsrc[(e / N + 1) * n + (e % N + 1)];
+        for (int i = tid; i < N * 16 * R; i += THREADS) {
+            const int e = i / R, m = e >> 4, k = e & 15;  // rows of 16, columns >= N unused
+            dr[i] = k < N ? dsrc[(m + 1) * n + (k + 1)] : V(0);
         }
         if (tid < N) {
             d0[tid] = dsrc[tid + 1];

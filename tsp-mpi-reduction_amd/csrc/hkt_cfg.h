@@ -6,6 +6,7 @@
 #include "hk_tiled.h"
 
 #define TSPGPU_TILED_CFGS(X) \
+    X(12, double, 15, 10, 256, 1, 5) \
     X(2, double, 15, 11, 256, 1, 3) \
     X(0, double, 15, 11, 512, 1, 2) \
     X(1, double, 15, 10, 256, 1, 4) \
@@ -16,7 +17,9 @@
     X(7, int32_t, 15, 11, 256, 1, 4) \
     X(8, int32_t, 15, 11, 512, 1, 2) \
     X(9, int32_t, 14, 11, 256, 1, 4) \
-    X(10, double, 13, 10, 256, 1, 4)
+    X(10, double, 13, 10, 256, 1, 4) \
+    X(11, double, 15, 10, 128, 1, 6) \
+    X(13, double, 15, 10, 192, 1, 5)
 
 namespace tspgpu {
 struct TiledCfg {

@@ -221,8 +221,33 @@ int check_n(int n, int strict)
     return 0;
 }
 
+int solve_device_unordered(tspgpu_ctx *c, const void *d_dist, int n, int nblocks, void *d_cost, int32_t *d_tour,
+                           hipStream_t stream, int vbytes);
+
+// Launches share the context's workspace (slots, push areas, parent words):
+// a launch on another stream than the previous one first waits for it, and
+// every launch records the completion event the next one may wait for.
 int solve_device_locked(tspgpu_ctx *c, const void *d_dist, int n, int nblocks, void *d_cost, int32_t *d_tour,
                         hipStream_t stream, int vbytes)
+{
+    if (nblocks > 0 && hipSetDevice(c->device) != hipSuccess) return -ENODEV;
+    if (nblocks > 0 && c->k1_launched && stream != c->k1_last_stream) {
+        hipError_t e = hipStreamWaitEvent(stream, c->ev_k1_done, 0);
+        if (e != hipSuccess) return hip_err(e);
+    }
+    int rc = solve_device_unordered(c, d_dist, n, nblocks, d_cost, d_tour, stream, vbytes);
+    if (rc || nblocks <= 0) return rc;
+    hipError_t e = hipSuccess;
+    if (!c->ev_k1_done) e = hipEventCreateWithFlags(&c->ev_k1_done, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventRecord(c->ev_k1_done, stream);
+    if (e != hipSuccess) return hip_err(e);
+    c->k1_last_stream = stream;
+    c->k1_launched = true;
+    return 0;
+}
+
+int solve_device_unordered(tspgpu_ctx *c, const void *d_dist, int n, int nblocks, void *d_cost, int32_t *d_tour,
+                           hipStream_t stream, int vbytes)
 {
     int rc = check_n(n, c->strict);
     if (rc) return rc;
@@ -471,6 +496,7 @@ int tspgpu_ctx_destroy(tspgpu_ctx *c)
     if (c->d_tour) (void)hipFree(c->d_tour);
     if (c->ev_start) (void)hipEventDestroy(c->ev_start);
     if (c->ev_stop) (void)hipEventDestroy(c->ev_stop);
+    if (c->ev_k1_done) (void)hipEventDestroy(c->ev_k1_done);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
     return 0;
@@ -636,6 +662,39 @@ int tspgpu_memcpy_dtoh(tspgpu_ctx *c, void *dst, const void *src, size_t bytes)
 }
 
 void *tspgpu_stream(tspgpu_ctx *c) { return c ? (void *)c->stream : nullptr; }
+
+int tspgpu_stream_create(tspgpu_ctx *c, void **stream)
+{
+    if (!c || !stream) return -EINVAL;
+    if (hipSetDevice(c->device) != hipSuccess) return -ENODEV;
+    hipStream_t s = nullptr;
+    hipError_t e = hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
+    *stream = e == hipSuccess ? (void *)s : nullptr;
+    return hip_err(e);
+}
+
+int tspgpu_stream_destroy(tspgpu_ctx *c, void *stream)
+{
+    if (!c) return -EINVAL;
+    if (!stream) return 0;
+    if (hipSetDevice(c->device) != hipSuccess) return -ENODEV;
+    std::lock_guard<std::mutex> g(c->mu);
+    if (c->k1_last_stream == (hipStream_t)stream) {
+        // the next launch must not wait on an event of a destroyed stream's queue:
+        // drain it and forget it
+        (void)hipStreamSynchronize((hipStream_t)stream);
+        c->k1_launched = false;
+        c->k1_last_stream = nullptr;
+    }
+    return hip_err(hipStreamDestroy((hipStream_t)stream));
+}
+
+int tspgpu_stream_synchronize(tspgpu_ctx *c, void *stream)
+{
+    if (!c) return -EINVAL;
+    if (hipSetDevice(c->device) != hipSuccess) return -ENODEV;
+    return hip_err(hipStreamSynchronize((hipStream_t)stream));
+}
 
 int tspgpu_synchronize(tspgpu_ctx *c)
 {

@@ -96,8 +96,9 @@ def solve_sharded(ctx, dist, group=None, depth: int = 0, device=None):
             S.reset_records(int(min(max(recs, 1 << 16), 1 << 22)))
             S.set_bound(tspgpu.bits_cost(opt, S.dtype))
             S.run_all()
-            _, nodes2, recs = S.counters()
-            nodes += nodes2
+            # the device node counter is cumulative over both phases (start does
+            # not reset it), so it already holds phase 1 + phase 2
+            _, nodes, recs = S.counters()
             mine, lost = local_records()
             if allmin(-lost) < 0:
                 # too many optimal tours to enumerate (coincident cities): the DP

@@ -24,7 +24,8 @@ EXPORTED_SYMBOLS = (
     "tspgpu_solve_blocks_device", "tspgpu_solve", "tspgpu_last_grid", "tspgpu_relaxations_per_block",
     "tspgpu_table_bytes_per_block", "tspgpu_device_alloc", "tspgpu_device_free", "tspgpu_memcpy_htod",
     "tspgpu_memcpy_dtoh", "tspgpu_stream", "tspgpu_synchronize", "tspgpu_timer_start", "tspgpu_timer_stop",
-    "tspgpu_device_info", "tspgpu_last_variant", "tspgpu_device_count",
+    "tspgpu_device_info", "tspgpu_last_variant", "tspgpu_device_count", "tspgpu_stream_create",
+    "tspgpu_stream_destroy", "tspgpu_stream_synchronize",
     # K2
     "tspgpu_search_solve", "tspgpu_search_enumerate", "tspgpu_search_create", "tspgpu_search_destroy", "tspgpu_search_info",
     "tspgpu_search_set_bound", "tspgpu_search_start", "tspgpu_search_step", "tspgpu_search_run_all",
@@ -115,6 +116,9 @@ def lib():
         L.tspgpu_stream.argtypes = [vp]
         L.tspgpu_stream.restype = vp
         L.tspgpu_synchronize.argtypes = [vp]
+        L.tspgpu_stream_create.argtypes = [vp, ctypes.POINTER(vp)]
+        L.tspgpu_stream_destroy.argtypes = [vp, vp]
+        L.tspgpu_stream_synchronize.argtypes = [vp, vp]
         L.tspgpu_timer_start.argtypes = [vp]
         L.tspgpu_timer_stop.argtypes = [vp, ctypes.POINTER(ctypes.c_float)]
         L.tspgpu_device_info.argtypes = [vp, ctypes.POINTER(ctypes.c_int), ctypes.c_char_p, ctypes.c_int]
@@ -324,8 +328,19 @@ class Context:
     def stream(self) -> int:
         return lib().tspgpu_stream(self.handle) or 0
 
-    def synchronize(self):
-        self._check(lib().tspgpu_synchronize(self.handle), "tspgpu_synchronize")
+    def synchronize(self, stream: int | None = None):
+        if stream is None:
+            self._check(lib().tspgpu_synchronize(self.handle), "tspgpu_synchronize")
+        else:
+            self._check(lib().tspgpu_stream_synchronize(self.handle, stream), "tspgpu_stream_synchronize")
+
+    def stream_create(self) -> int:
+        s = ctypes.c_void_p()
+        self._check(lib().tspgpu_stream_create(self.handle, ctypes.byref(s)), "tspgpu_stream_create")
+        return s.value
+
+    def stream_destroy(self, stream: int):
+        self._check(lib().tspgpu_stream_destroy(self.handle, stream), "tspgpu_stream_destroy")
 
     def timer_start(self):
         self._check(lib().tspgpu_timer_start(self.handle), "tspgpu_timer_start")
