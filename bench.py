@@ -783,13 +783,18 @@ def roofline(variant, kname, n, Bp, kernel_ms, relax_s, alg_bytes_per_block, pro
                         f"relaxations/s); traffic = HBM bytes per launch (PMC)"}
     mem = None
     if hbm is not None:
-        mem = {"bound": "hbm", "achieved": hbm / (kernel_ms * 1e-3) / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
+        mem = {"bound": "hbm (upper bound: Infinity-Cache hits included)", "achieved": hbm / (kernel_ms * 1e-3) / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                "frac": hbm / (kernel_ms * 1e-3) / HBM_PEAK, "traffic": hbm,
-               "note": f"bytes HBM moved per launch = PMC fabric bytes ({fabric:.4g}, Infinity-Cache hits included) "
-                       f"x DRAM share of the EA requests; the layer-by-layer algorithmic table bytes would be "
-                       f"{alg_bytes_per_block * Bp:.4g}"}
+               "note": f"memory-side bytes per launch = PMC FETCH_SIZE x2 + WRITE_SIZE ({fabric:.4g}; calibrated on 8-B "
+                       f"loads/stores; Infinity-Cache hits are counted too, TCC_EA0_*_DRAM does not split them), vs the "
+                       f"HBM peak; the layer-by-layer algorithmic table bytes would be {alg_bytes_per_block * Bp:.4g}"}
     if valu and mem:
-        a, b = (valu, mem) if valu["frac"] >= mem["frac"] else (mem, valu)
+        # The memory view counts every byte that left L2 toward memory (the
+        # gfx950 counters cannot separate Infinity-Cache hits from HBM reads:
+        # profiles/r02/pmc_calibration_dram_counters.txt), so it is an upper
+        # bound on HBM traffic; the kernel is priced against the VALU issue
+        # rate of its own instruction mix unless memory is clearly the wall.
+        a, b = (mem, valu) if mem["frac"] > max(0.6, valu["frac"]) else (valu, mem)
         return dict(a, other=b)
     return valu or mem or {"bound": "unknown", "achieved": None, "peak": None, "unit": None, "frac": None,
                            "traffic": None, "note": "no PMC / ubench data in this run"}
