@@ -45,6 +45,10 @@
 namespace tspgpu {
 
 constexpr int kTiledMaxL = 12;
+// distance row stride (entries): odd, so the per-lane gathers d[m][k] of a
+// half-wave with equal k and different m fall on different bank pairs (a
+// stride of 16 made every pair m, m+2 collide: 94% bank-conflict cycles)
+constexpr int kTiledDS = 17;
 // Ablation knobs for timing experiments only (results are WRONG when set):
 //   1 high-member values from LDS, 2 d values from a register, 4 no barrier
 //   between the passes of a sub-cube, 8 plain minimum (no argmin)
@@ -80,7 +84,7 @@ __host__ __device__ constexpr int tiled_region_vals(int L)
 }
 __host__ __device__ constexpr size_t tiled_lds_bytes(int N, int L, int R, int vb)
 {
-    return (size_t)N * 16 * R * vb           // replicated inner distances, rows of 16
+    return (size_t)N * kTiledDS * R * vb     // replicated inner distances, rows of kTiledDS
            + (size_t)2 * 16 * vb             // d[0][k], d[m][0]
            + (size_t)tiled_region_vals(L) * vb  // live low layers
            + (size_t)2 * 2 * (1 << L);       // mask + rank (u16)
@@ -224,12 +228,13 @@ __device__ __forceinline__ void tiled_pass(const TiledCtx<V, N, L, R> &c, uint32
     constexpr int REGV = tiled_region_vals(L);
     constexpr int CUR = (J & 1) ? REGV - ROWS * J : 0;
     constexpr int NXT = ((J + 1) & 1) ? REGV - ROWS_N * (J + 1) : 0;
-    // distance rows of 16 entries (R copies each): a member's row offset is
-    // bit << SM, a non-member's column offset bit << SK, both shifts; the
-    // argmin is kept as the member's row offset (one register less per member)
+    // distance rows of kTiledDS entries (R copies each): a member's row
+    // offset is bit * DROW, a non-member's column offset bit << SK; the argmin
+    // is kept as the member's row offset (one register less per member) and
+    // turned back into the bit by a division by the constant DROW
     constexpr int SK = __builtin_ctz((unsigned)(R * VB));
-    constexpr int SM = SK + 4;
-    static_assert((R & (R - 1)) == 0 && N <= 16, "R must be a power of two");
+    constexpr uint32_t DROW = (uint32_t)(kTiledDS * R * VB);
+    static_assert((R & (R - 1)) == 0 && N < kTiledDS, "R must be a power of two");
     // uniform: the high members and high non-members of h, ascending
     uint32_t hm[HC > 0 ? HC : 1], hn[QH > 0 ? QH : 1];
     {
@@ -268,11 +273,11 @@ __device__ __forceinline__ void tiled_pass(const TiledCtx<V, N, L, R> &c, uint32
         uint32_t lb = l;
 #pragma unroll
         for (int p = 0; p < J; ++p) {
-            mrow[p] = ((uint32_t)__builtin_ctz(lb) << SM) | lane_off;
+            mrow[p] = (uint32_t)__builtin_ctz(lb) * DROW + lane_off;
             lb &= lb - 1u;
         }
 #pragma unroll
-        for (int i = 0; i < HC; ++i) mrow[J + i] = ((L + hm[i]) << SM) | lane_off;
+        for (int i = 0; i < HC; ++i) mrow[J + i] = (L + hm[i]) * DROW + lane_off;
         // Destinations in chunks of at most TSPGPU_TILED_QC (registers: acc,
         // arg and the column offsets of one chunk only); the non-members come
         // ascending (low non-members of l, then those of h).  Per chunk: the
@@ -341,9 +346,9 @@ __device__ __forceinline__ void tiled_pass(const TiledCtx<V, N, L, R> &c, uint32
                 }
                 // the row's parent word: nibble q = bit index of the argmin member
                 if (q < 8)
-                    wlo |= (arg[qq] >> SM) << (4 * q);
+                    wlo |= (arg[qq] / DROW) << (4 * q);
                 else
-                    whi |= (arg[qq] >> SM) << (4 * (q - 8));
+                    whi |= (arg[qq] / DROW) << (4 * (q - 8));
             }
         });
         c.par.store_nt((BASE + r) * 8u, h * (uint32_t)(NL * 8), ((uint64_t)whi << 32) | wlo);
@@ -399,7 +404,7 @@ __global__ __launch_bounds__(THREADS, tiled_waves(THREADS, WG)) void hk_tiled_ke
     constexpr int VB = sizeof(V);
     extern __shared__ __attribute__((aligned(16))) char smem[];
     V *dr = reinterpret_cast<V *>(smem);
-    V *d0 = dr + N * 16 * R;   // d[0][k], k = 1..N at [k-1]
+    V *d0 = dr + N * kTiledDS * R;  // d[0][k], k = 1..N at [k-1]
     V *dc = d0 + 16;           // d[m][0], m = 1..N at [m-1]
     V *region = dc + 16;
     uint16_t *lmask = reinterpret_cast<uint16_t *>(region + tiled_region_vals(L));
@@ -419,8 +424,8 @@ __global__ __launch_bounds__(THREADS, tiled_waves(THREADS, WG)) void hk_tiled_ke
 
     for (int blk = blk0 + blockIdx.x; blk < nblocks; blk += gridDim.x) {
         const V *dsrc = dist + (size_t)blk * n * n;
-        for (int i = tid; i < N * 16 * R; i += THREADS) {
-            const int e = i / R, m = e >> 4, k = e & 15;  // rows of 16, columns >= N unused
+        for (int i = tid; i < N * kTiledDS * R; i += THREADS) {
+            const int e = i / R, m = e / kTiledDS, k = e % kTiledDS;  // columns >= N unused
             dr[i] = k < N ? dsrc[(m + 1) * n + (k + 1)] : V(0);
         }
         if (tid < N) {
