@@ -27,6 +27,9 @@ CFGS = [
     (10, "double", 13, 10, 256, 1, 4),
     (11, "double", 15, 10, 128, 1, 6),
     (13, "double", 15, 10, 192, 1, 5),
+    (14, "double", 15, 10, 256, 1, 6),
+    (15, "double", 15, 9, 256, 1, 6),
+    (16, "double", 15, 9, 256, 1, 7),
 ]
 
 

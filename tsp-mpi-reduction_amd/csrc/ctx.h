@@ -37,8 +37,6 @@ struct tspgpu_ctx {
     void *d_tinfo[16] = {};        // TiledInfo per L (variant 5)
     char *d_tslots = nullptr;      // variant 5 push areas (one per resident workgroup)
     size_t tslots_bytes = 0;
-    uint64_t *d_parents = nullptr; // variant 5 parent words (one table per block of a chunk)
-    size_t parents_bytes = 0;
     hipEvent_t ev_start = nullptr, ev_stop = nullptr;
     // K1 workspace ordering across caller streams: the slots / push areas are
     // per context, so a launch on a stream other than the previous one waits

@@ -21,13 +21,20 @@
 //
 // Row-owner pass (h, j): a thread owns a source row T = h<<L | l, |l| = j,
 // t = |h|+j members, Q = N-t non-members; for every non-member k it computes
-//   acc[k] = min over members m ascending (strict <) of G[T][m] + d[m][k]
-// and its argmin city (the reference's tsp.cpp:457-470 rule) — exactly the
-// compact pass of heldkarp_impl.h — then stores acc[k] to the next LDS layer
-// (k low) or to the push area of sub-cube h|k (k high), and one 64-bit word of
-// 4-bit parents per row (per block, non-temporal) for the backtracking, which
-// a second kernel runs with one thread per block (14 dependent loads each,
-// all blocks in parallel instead of a serial tail per block).
+//   acc[k] = min over members m of G[T][m] + d[m][k]
+// (the values of tsp.cpp:457-470) and stores acc[k] to the next LDS layer (k
+// low) or to the push area of sub-cube h|k (k high).  The argmin (the
+// reference's first strict minimum over members ascending) is kept only for
+// the top rows (>= N - TSPGPU_TILED_TA_OFF members: one 64-bit word of 4-bit
+// parents per row); everywhere else the pass is min-only — two VALU
+// instructions per relaxation instead of four.  The backtracking kernel
+// (hk_tiled_backtrack, one wave per block, all blocks at once) follows the
+// parent words down to that size, then recomputes the few rows the path still
+// needs from the block's pushed values (only subsets of the path's row, 2-8%
+// of the forward relaxations) and takes the same first strict minimum of the
+// same candidates — so the same tour bits.  At n = 16: 7.4 ms forward + 0.7 ms
+// backtracking per 16384 blocks, against 9.6 ms with the argmin everywhere
+// (profiles/r02/k1_argmin_threshold.txt).
 //
 // Distances: the N x N inner matrix is replicated R times in LDS, element e of
 // copy c at 8*(e*R + c), lane uses copy lane % R: with R = 32 the per-lane
@@ -51,9 +58,16 @@ constexpr int kTiledMaxL = 12;
 constexpr int kTiledDS = 17;
 // Ablation knobs for timing experiments only (results are WRONG when set):
 //   1 high-member values from LDS, 2 d values from a register, 4 no barrier
-//   between the passes of a sub-cube, 8 plain minimum (no argmin)
+//   between the passes of a sub-cube, 8 plain minimum (no argmin), 32 no
+//   backtracking, 64 backtracking kernel stops after staging, 128 no recompute
 #ifndef TSPGPU_TILED_ABL
 #define TSPGPU_TILED_ABL 0
+#endif
+// Rows with at least N - TSPGPU_TILED_TA_OFF members keep the argmin (a
+// 64-bit parent word each); every smaller row is relaxed without it and the
+// backtracking recomputes the few rows it needs (see tiled_backtrack).
+#ifndef TSPGPU_TILED_TA_OFF
+#define TSPGPU_TILED_TA_OFF 4
 #endif
 #ifndef TSPGPU_TILED_QC
 #define TSPGPU_TILED_QC 7  // destinations relaxed together (register budget of a chunk)
@@ -95,8 +109,20 @@ __host__ __device__ constexpr size_t tiled_push_bytes(int N, int L, int vb)
 {
     return (size_t)(1 << (N - L)) * (N - L) * (1 << L) * vb;
 }
-// parent words of one block: [h][idx] u64
-__host__ __device__ constexpr size_t tiled_parent_bytes(int N, int L) { return (size_t)8 << N; }
+// parent words of the workgroup's current block: [h][idx] u64 (only rows
+// with >= N - TSPGPU_TILED_TA_OFF members are written)
+__host__ __device__ constexpr size_t tiled_parent_bytes(int N, int L)
+{
+    return TSPGPU_TILED_TA_OFF > 0 ? (size_t)8 << N : 0;
+}
+// backtracking recompute area: G[h<<L | l][m] of one sub-cube h, [l][m], m low
+__host__ __device__ constexpr size_t tiled_recomp_bytes(int L, int vb) { return (size_t)(1 << L) * L * vb; }
+// one block's global slot: push area, parent words, recompute area (kept
+// until the backtracking kernel has run: one slot per block of a launch)
+__host__ __device__ constexpr size_t tiled_slot_bytes(int N, int L, int vb)
+{
+    return tiled_push_bytes(N, L, vb) + tiled_parent_bytes(N, L) + ((tiled_recomp_bytes(L, vb) + 255) & ~(size_t)255);
+}
 
 // f(std::integral_constant<int, 0>), ..., f(std::integral_constant<int, C-1>)
 template <int I, int C, typename F>
@@ -198,6 +224,22 @@ __device__ __forceinline__ void relax_argmin(int32_t &acc, uint32_t &arg, int32_
         : "vcc");
 }
 
+// acc = min(acc, g + d), no argmin (ablation 8 / argmin-free passes)
+__device__ __forceinline__ void relax_min(double &acc, double g, double d)
+{
+    double t;
+    asm volatile("v_add_f64 %[t], %[g], %[d]\n\tv_min_f64 %[acc], %[acc], %[t]"
+                 : [acc] "+v"(acc), [t] "=&v"(t)
+                 : [g] "v"(g), [d] "v"(d));
+}
+__device__ __forceinline__ void relax_min(int32_t &acc, int32_t g, int32_t d)
+{
+    int32_t t;
+    asm volatile("v_add_u32 %[t], %[g], %[d]\n\tv_min_i32 %[acc], %[acc], %[t]"
+                 : [acc] "+v"(acc), [t] "=&v"(t)
+                 : [g] "v"(g), [d] "v"(d));
+}
+
 template <typename V, int N, int L, int R>
 struct TiledCtx {
     const V *dr;               // LDS replicated distances
@@ -205,7 +247,9 @@ struct TiledCtx {
     const uint16_t *lrankb;    // LDS colex rank x sizeof(V) (byte offset inside a position column)
     V *region;                 // LDS live low layers
     Rsrc<V> push;              // this slot's push area
-    Rsrc<uint64_t> par;        // this block's parent words
+    Rsrc<uint64_t> par;        // this slot's parent words (the current block's)
+    Rsrc<V> rec;               // this slot's backtracking recompute area
+    const int *moff;           // first index of each popcount class (backtracking)
 };
 
 // One pass (h, J) of a sub-cube: T = |h| + J members per source row, all
@@ -228,6 +272,9 @@ __device__ __forceinline__ void tiled_pass(const TiledCtx<V, N, L, R> &c, uint32
     constexpr int REGV = tiled_region_vals(L);
     constexpr int CUR = (J & 1) ? REGV - ROWS * J : 0;
     constexpr int NXT = ((J + 1) & 1) ? REGV - ROWS_N * (J + 1) : 0;
+    // argmin and parent word only for the top rows (tiled_backtrack recomputes
+    // the rest); ablation 8 drops it everywhere (timing only)
+    constexpr bool ARG = T >= N - TSPGPU_TILED_TA_OFF && !(TSPGPU_TILED_ABL & 8);
     // distance rows of kTiledDS entries (R copies each): a member's row
     // offset is bit * DROW, a non-member's column offset bit << SK; the argmin
     // is kept as the member's row offset (one register less per member) and
@@ -306,7 +353,7 @@ __device__ __forceinline__ void tiled_pass(const TiledCtx<V, N, L, R> &c, uint32
                 }
             }
             V acc[QN];
-            uint32_t arg[QN];
+            uint32_t arg[ARG ? QN : 1];
             {
                 constexpr int TQ = T * QN;
                 constexpr int AH = TSPGPU_TILED_AHEAD < TQ ? TSPGPU_TILED_AHEAD : TQ;
@@ -321,12 +368,12 @@ __device__ __forceinline__ void tiled_pass(const TiledCtx<V, N, L, R> &c, uint32
                         dv[i % AH] = *reinterpret_cast<const V *>(drb + mrow[(i + AH) / QN] + kof[(i + AH) % QN]);
                     if (i < QN) {
                         acc[i] = g[0] + d;
-                        arg[i] = mrow[0];
+                        if constexpr (ARG) arg[i] = mrow[0];
                     } else {
-                        if constexpr (TSPGPU_TILED_ABL & 8)
-                            acc[i % QN] = ValT<V>::vmin(acc[i % QN], g[i / QN] + d);
-                        else
+                        if constexpr (ARG)
                             relax_argmin(acc[i % QN], arg[i % QN], g[i / QN], d, mrow[i / QN]);
+                        else
+                            relax_min(acc[i % QN], g[i / QN], d);
                     }
                     __builtin_amdgcn_sched_barrier(0);
                 }
@@ -345,14 +392,138 @@ __device__ __forceinline__ void tiled_pass(const TiledCtx<V, N, L, R> &c, uint32
                     c.push.store(voff, ((h | (1u << cb)) * H + cb) * (uint32_t)(NL * VB), acc[qq]);
                 }
                 // the row's parent word: nibble q = bit index of the argmin member
-                if (q < 8)
-                    wlo |= (arg[qq] / DROW) << (4 * q);
-                else
-                    whi |= (arg[qq] / DROW) << (4 * (q - 8));
+                if constexpr (ARG) {
+                    if (q < 8)
+                        wlo |= (arg[qq] / DROW) << (4 * q);
+                    else
+                        whi |= (arg[qq] / DROW) << (4 * (q - 8));
+                }
             }
         });
-        c.par.store_nt((BASE + r) * 8u, h * (uint32_t)(NL * 8), ((uint64_t)whi << 32) | wlo);
+        if constexpr (ARG) c.par.store((BASE + r) * 8u, h * (uint32_t)(NL * 8), ((uint64_t)whi << 32) | wlo);
     }
+}
+
+// Parallel bit deposit: the i-th set bit of m receives bit i of x.
+__device__ __forceinline__ uint32_t pdep_u32(uint32_t x, uint32_t m)
+{
+    uint32_t r = 0;
+    for (uint32_t b = 1; m; b <<= 1) {
+        const uint32_t low = m & (0u - m);
+        if (x & b) r |= low;
+        m ^= low;
+    }
+    return r;
+}
+
+// G[h<<L | l][m] after the forward pass: a high m from the push area, a low m
+// from the recompute area (valid for the sub-cube and the subsets the last
+// tiled_recompute covered).  Any m < N gives a valid address (the value of a
+// non-member is garbage): callers load unconditionally, then select.
+template <typename V, int N, int L, int R>
+__device__ __forceinline__ V tiled_g(const TiledCtx<V, N, L, R> &c, uint32_t h, uint32_t l, uint32_t pidx, int m)
+{
+    constexpr int H = N - L, NL = 1 << L, VB = sizeof(V);
+    if (m < L) return c.rec.load((l * L + (uint32_t)m) * VB, 0);
+    return c.push.load(pidx, (h * H + (uint32_t)(m - L)) * (uint32_t)(NL * VB));
+}
+// byte offset of row l inside a push column
+template <typename V, int N, int L, int R>
+__device__ __forceinline__ uint32_t tiled_pidx(const TiledCtx<V, N, L, R> &c, uint32_t l)
+{
+    return (uint32_t)c.moff[__builtin_popcount(l)] * (uint32_t)sizeof(V) + c.lrankb[l];
+}
+
+// Backtracking recompute (one wave): G[h<<L | l'][m] for every l' within lT and
+// every low member m, layer by layer from the pushed high-member values — the
+// forward pass's own relaxations restricted to those rows, the minimum only
+// (IEEE min is order-free, so the values are the forward pass's bits).
+template <typename V, int N, int L, int R>
+__device__ void tiled_recompute(const TiledCtx<V, N, L, R> &c, const V *d0, V *gs, uint32_t h, uint32_t lT,
+                                uint32_t lane)
+{
+    constexpr int VB = sizeof(V);
+    const int nl = __builtin_popcount(lT);
+    int j0 = 0;
+    if (h == 0) {  // no high member: layer 1 is G[{k}][k] = d[0][k] (tsp.cpp:435)
+        if (lane < (uint32_t)L && ((lT >> lane) & 1u)) c.rec.store(((1u << lane) * L + lane) * VB, 0, d0[lane]);
+        j0 = 1;
+    }
+    for (int j = j0; j < nl; ++j) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        const int cnt = cbinom(nl, j), mo = c.moff[j];
+        for (int r = (int)lane; r < cnt; r += 64) {
+            // the r-th j-subset of lT in colex order = the r-th j-subset of
+            // the low bits, deposited on lT's cities
+            const uint32_t lp = pdep_u32(c.lmask[mo + r], lT);
+            const uint32_t dst = lT & ~lp;
+            const uint32_t Tm = (h << L) | lp;
+            const uint32_t pidx = tiled_pidx(c, lp);
+            // the row's values into this lane's LDS column (all loads in flight at once)
+#pragma unroll
+            for (int m = 0; m < N; ++m) gs[m * 64 + lane] = tiled_g(c, h, lp, pidx, m);
+            for (uint32_t db = dst; db; db &= db - 1u) {
+                const int s = __builtin_ctz(db);
+                V acc = ValT<V>::inf;
+                for (uint32_t mb = Tm; mb; mb &= mb - 1u) {
+                    const int m = __builtin_ctz(mb);
+                    acc = ValT<V>::vmin(acc, gs[m * 64 + lane] + c.dr[(m * kTiledDS + s) * R]);
+                }
+                c.rec.store(((lp | (1u << s)) * L + (uint32_t)s) * VB, 0, acc);
+            }
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+// Backtracking of the block just solved (one wave, tsp.cpp:473-481's parent
+// walk): from the last inner city k_last back to the start.  A row with
+// >= N - TSPGPU_TILED_TA_OFF members has its parent word; below that the row's
+// values are recomputed (tiled_recompute, once per sub-cube the path enters)
+// and the parent is the first strict minimum over its members ascending of
+// G[T][m] + d[m][k] — the forward pass's candidates, so its argmin.
+template <typename V, int N, int L, int R>
+__device__ bool tiled_backtrack(const TiledCtx<V, N, L, R> &c, const V *d0, V *gs, int bestM,
+                                int32_t *tour, uint32_t lane)
+{
+    constexpr int NL = 1 << L, VB = sizeof(V), n = N + 1;
+    uint32_t S = (1u << N) - 1u;
+    int k = bestM - 1;
+    bool ok = bestM >= 1 && bestM <= N;
+    uint32_t hcur = ~0u, lcur = 0;
+    for (int pos = n - 2; ok && pos >= 1; --pos) {
+        const uint32_t T = S & ~(1u << k);
+        const uint32_t hT = T >> L, lT = T & (uint32_t)(NL - 1);
+        int pm;
+        if (__builtin_popcount(T) >= N - TSPGPU_TILED_TA_OFF && !(TSPGPU_TILED_ABL & 8)) {
+            const uint32_t idx = (uint32_t)c.moff[__builtin_popcount(lT)] + c.lrankb[lT] / VB;
+            const uint64_t w = c.par.load(idx * 8u, hT * (uint32_t)(NL * 8));
+            const int q = k - __builtin_popcount(T & ((1u << k) - 1u));  // k's place among T's non-members
+            pm = (int)((w >> (4 * q)) & 15u);
+        } else {
+            if (!(TSPGPU_TILED_ABL & 128) && (hT != hcur || (lT & ~lcur))) {
+                tiled_recompute(c, d0, gs, hT, lT, lane);
+                hcur = hT;
+                lcur = lT;
+            }
+            const bool mem = lane < (uint32_t)N && ((T >> lane) & 1u);
+            V cand = ValT<V>::invalid;
+            const V g = tiled_g(c, hT, lT, tiled_pidx(c, lT), lane < (uint32_t)N ? (int)lane : 0);
+            if (mem) cand = g + c.dr[(lane * kTiledDS + (uint32_t)k) * R];
+            const V best = wave_min(cand);
+            const unsigned long long hit = __ballot(mem && cand == best);
+            pm = hit ? __ffsll(hit) - 1 : N;
+        }
+        ok = pm < N && ((T >> pm) & 1u);
+        if (lane == 0) tour[pos] = ok ? pm + 1 : 0;
+        S = T;
+        k = pm;
+    }
+    return ok;
 }
 
 template <typename V, int N, int L, int J, int THREADS, int R>
@@ -365,7 +536,8 @@ __device__ __forceinline__ void tiled_dispatch_h(const TiledCtx<V, N, L, R> &c, 
             tiled_pass<V, N, L, J + HC, J, THREADS, R>(c, h, tid);                         \
         break;
     switch (hc) {
-        TSPGPU_TP(0) TSPGPU_TP(1) TSPGPU_TP(2) TSPGPU_TP(3) TSPGPU_TP(4) TSPGPU_TP(5)
+        TSPGPU_TP(0) TSPGPU_TP(1) TSPGPU_TP(2) TSPGPU_TP(3) TSPGPU_TP(4) TSPGPU_TP(5) TSPGPU_TP(6)
+        TSPGPU_TP(7)
     default: break;
     }
 #undef TSPGPU_TP
@@ -388,24 +560,24 @@ __device__ __forceinline__ void tiled_dispatch(const TiledCtx<V, N, L, R> &c, ui
 
 __host__ __device__ constexpr int tiled_waves(int threads, int wg_per_cu) { return threads * wg_per_cu / 256; }
 
-// Forward pass + closing min of blocks blockIdx.x, +gridDim.x, ...; writes
-// cost_out[blk] and the tour's last inner city (tour[n-1]); the backtracking
-// kernel below fills the rest of the tour from the parent words.
+// Forward pass + closing min of blocks blk0 + blockIdx.x, +gridDim.x, ...;
+// writes cost_out[blk] and the tour's last inner city (tour[n-1]).  Every
+// block has its own global slot, kept for hk_tiled_backtrack.
 template <typename V, int N, int L, int THREADS, int R, int WG>
 __global__ __launch_bounds__(THREADS, tiled_waves(THREADS, WG)) void hk_tiled_kernel(
     const V *__restrict__ dist, int nblocks, int blk0, char *__restrict__ slots, uint32_t slot_bytes,
-    uint64_t *__restrict__ parents, const TiledInfo *__restrict__ info, V *__restrict__ cost_out,
-    int32_t *__restrict__ tour_out)
+    const TiledInfo *__restrict__ info, V *__restrict__ cost_out, int32_t *__restrict__ tour_out)
 {
     constexpr int H = N - L;
     constexpr int NH = 1 << H;
     constexpr int NL = 1 << L;
     constexpr int n = N + 1;
     constexpr int VB = sizeof(V);
+    static_assert(H <= 7, "tiled_dispatch_h covers at most 7 high cities");
     extern __shared__ __attribute__((aligned(16))) char smem[];
     V *dr = reinterpret_cast<V *>(smem);
     V *d0 = dr + N * kTiledDS * R;  // d[0][k], k = 1..N at [k-1]
-    V *dc = d0 + 16;           // d[m][0], m = 1..N at [m-1]
+    V *dc = d0 + 16;                // d[m][0], m = 1..N at [m-1]
     V *region = dc + 16;
     uint16_t *lmask = reinterpret_cast<uint16_t *>(region + tiled_region_vals(L));
     uint16_t *lrankb = lmask + NL;
@@ -420,9 +592,12 @@ __global__ __launch_bounds__(THREADS, tiled_waves(THREADS, WG)) void hk_tiled_ke
     c.lmask = lmask;
     c.lrankb = lrankb;
     c.region = region;
-    c.push.rs = uniform_rsrc(slots + (size_t)blockIdx.x * slot_bytes, (uint32_t)tiled_push_bytes(N, L, VB));
+    c.moff = nullptr;  // (backtracking only)
 
     for (int blk = blk0 + blockIdx.x; blk < nblocks; blk += gridDim.x) {
+        char *slot = slots + (size_t)(blk - blk0) * slot_bytes;
+        c.push.rs = uniform_rsrc(slot, (uint32_t)tiled_push_bytes(N, L, VB));
+        c.par.rs = uniform_rsrc(slot + tiled_push_bytes(N, L, VB), (uint32_t)tiled_parent_bytes(N, L));
         const V *dsrc = dist + (size_t)blk * n * n;
         for (int i = tid; i < N * kTiledDS * R; i += THREADS) {
             const int e = i / R, m = e / kTiledDS, k = e % kTiledDS;  // columns >= N unused
@@ -432,7 +607,6 @@ __global__ __launch_bounds__(THREADS, tiled_waves(THREADS, WG)) void hk_tiled_ke
             d0[tid] = dsrc[tid + 1];
             dc[tid] = dsrc[(tid + 1) * n];
         }
-        c.par.rs = uniform_rsrc(parents + (size_t)(blk - blk0) * ((size_t)NH * NL), (uint32_t)tiled_parent_bytes(N, L));
         __syncthreads();
         // layer 1: G[{i}][i] = d[0][i] (tsp.cpp:435's d[0][i] term): low i in
         // sub-cube 0's first LDS layer (colex rank of {i} is i), high i pushed
@@ -481,49 +655,73 @@ __global__ __launch_bounds__(THREADS, tiled_waves(THREADS, WG)) void hk_tiled_ke
     }
 }
 
-// Backtracking, one thread per block: from the last inner city, the parent
-// nibble of row T = S \ k gives the previous city (the argmin the forward
-// pass stored), N-1 steps.
+// Backtracking (tiled_backtrack): one wave per block, four per workgroup,
+// persistent over the blocks of the launch.  A block's backtracking is a chain
+// of dependent loads (tens of microseconds), so all resident waves run their
+// chains at the same time, after the forward kernel instead of stalling it.
+constexpr int kTiledBtWaves = 4;
+namespace {  // internal linkage: every instantiation file keeps its own (timing builds differ per file)
 template <typename V, int N, int L>
-__global__ __launch_bounds__(256) void hk_tiled_backtrack(int nblocks, int blk0, const uint64_t *__restrict__ parents,
-                                                          const TiledInfo *__restrict__ info,
-                                                          V *__restrict__ cost_out, int32_t *__restrict__ tour_out)
+__global__ __launch_bounds__(64 * kTiledBtWaves) void hk_tiled_backtrack(
+    int nblocks, int blk0, const char *__restrict__ slots, uint32_t slot_bytes, const TiledInfo *__restrict__ info,
+    const V *__restrict__ dist, V *__restrict__ cost_out, int32_t *__restrict__ tour_out)
 {
-    constexpr int NH = 1 << (N - L);
-    constexpr int NL = 1 << L;
-    constexpr int n = N + 1;
-    const int blk = blk0 + blockIdx.x * blockDim.x + threadIdx.x;
-    if (blk >= nblocks) return;
-    int32_t *tour = tour_out + (size_t)blk * (n + 1);
-    const uint64_t *pw = parents + (size_t)(blk - blk0) * ((size_t)NH * NL);
-    int k = tour[n - 1];
-    bool ok = k >= 1 && k <= N;
-    uint32_t S = (1u << N) - 1u;
-    for (int pos = n - 2; ok && pos >= 1; --pos) {
-        const uint32_t T = S & ~(1u << (k - 1));
-        const uint32_t hT = T >> L, lT = T & (NL - 1);
-        const uint32_t idx = (uint32_t)info->moff[__builtin_popcount(lT)] + info->rank[lT];
-        const uint64_t w = __builtin_nontemporal_load(pw + hT * NL + idx);
-        const int q = (k - 1) - __builtin_popcount(T & ((1u << (k - 1)) - 1u));
-        const int pm = (int)((w >> (4 * q)) & 15u) + 1;  // nibble = bit index of the parent city
-        ok = pm <= N && ((T >> (pm - 1)) & 1u);
-        tour[pos] = ok ? pm : 0;
-        S = T;
-        k = pm;
+    constexpr int NL = 1 << L, n = N + 1, VB = sizeof(V), DRV = N * kTiledDS + 16;
+    __shared__ uint16_t lmask[NL], lrankb[NL];
+    __shared__ int smoff[L + 2];
+    __shared__ V drs[kTiledBtWaves][DRV];     // per wave: the block's inner distances, then d[0][k]
+    __shared__ V gss[kTiledBtWaves][N * 64];  // per wave: one recomputed row per lane, member-major
+    for (int i = threadIdx.x; i < NL; i += 64 * kTiledBtWaves) {
+        lmask[i] = info->mask[i];
+        lrankb[i] = (uint16_t)(info->rank[i] * VB);
     }
-    if (!ok) cost_out[blk] = V(-1);
+    if (threadIdx.x < (uint32_t)(L + 2)) smoff[threadIdx.x] = info->moff[threadIdx.x];
+    __syncthreads();
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    V *dr = drs[wave];
+    TiledCtx<V, N, L, 1> c;
+    c.dr = dr;
+    c.lmask = lmask;
+    c.lrankb = lrankb;
+    c.region = nullptr;
+    c.moff = smoff;
+    for (int blk = blk0 + (int)(blockIdx.x * kTiledBtWaves + wave); blk < nblocks;
+         blk += (int)(gridDim.x * kTiledBtWaves)) {
+        const V *dsrc = dist + (size_t)blk * n * n;
+        if (TSPGPU_TILED_ABL & 256) continue;
+        for (int i = lane; i < N * kTiledDS; i += 64) {
+            const int m = i / kTiledDS, k = i % kTiledDS;
+            dr[i] = k < N ? dsrc[(m + 1) * n + (k + 1)] : V(0);
+        }
+        if (lane < (uint32_t)N) dr[N * kTiledDS + lane] = dsrc[lane + 1];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        if (TSPGPU_TILED_ABL & 64) continue;
+        int32_t *tour = tour_out + (size_t)blk * (n + 1);
+        const int bestM = tour[n - 1];
+        if (bestM < 1) continue;  // no tour (cost already -1)
+        char *slot = const_cast<char *>(slots) + (size_t)(blk - blk0) * slot_bytes;
+        c.push.rs = uniform_rsrc(slot, (uint32_t)tiled_push_bytes(N, L, VB));
+        c.par.rs = uniform_rsrc(slot + tiled_push_bytes(N, L, VB), (uint32_t)tiled_parent_bytes(N, L));
+        c.rec.rs = uniform_rsrc(slot + tiled_push_bytes(N, L, VB) + tiled_parent_bytes(N, L),
+                                (uint32_t)tiled_recomp_bytes(L, VB));
+        if (!tiled_backtrack(c, dr + N * kTiledDS, gss[wave], bestM, tour, lane) && lane == 0) cost_out[blk] = V(-1);
+        __builtin_amdgcn_wave_barrier();  // dr is reloaded for the next block
+    }
 }
+}  // namespace
 
 struct TiledArgs {
     const void *dist;
     int n, blk0, blk1;        // blocks [blk0, blk1) of this launch pair
-    char *slots;              // grid push areas
+    char *slots;              // one slot per block of [blk0, blk1)
     uint32_t slot_bytes;
-    uint64_t *parents;        // (blk1 - blk0) parent-word tables
     const TiledInfo *info;
     void *cost;
     int32_t *tour;
     int grid;
+    int bt_grid;              // backtracking workgroups (kTiledBtWaves blocks each at a time)
     hipStream_t stream;
 };
 
@@ -539,13 +737,17 @@ hipError_t launch_tiled_n(const TiledArgs &a)
         raised = true;
     }
     hipLaunchKernelGGL((hk_tiled_kernel<V, N, L, THREADS, R, WG>), dim3(a.grid), dim3(THREADS), lds, a.stream,
-                       static_cast<const V *>(a.dist), a.blk1, a.blk0, a.slots, a.slot_bytes, a.parents, a.info,
+                       static_cast<const V *>(a.dist), a.blk1, a.blk0, a.slots, a.slot_bytes, a.info,
                        static_cast<V *>(a.cost), a.tour);
     hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
-    const int nb = a.blk1 - a.blk0;
-    hipLaunchKernelGGL((hk_tiled_backtrack<V, N, L>), dim3((nb + 255) / 256), dim3(256), 0, a.stream, a.blk1, a.blk0,
-                       a.parents, a.info, static_cast<V *>(a.cost), a.tour);
+    if (e != hipSuccess || (TSPGPU_TILED_ABL & 32)) return e;
+    hipLaunchKernelGGL((hk_tiled_backtrack<V, N, L>), dim3(a.bt_grid), dim3(64 * kTiledBtWaves), 0, a.stream, a.blk1, a.blk0,
+                       a.slots, a.slot_bytes, a.info, static_cast<const V *>(a.dist), static_cast<V *>(a.cost),
+                       a.tour);
+    if (TSPGPU_TILED_ABL & 512)
+        hipLaunchKernelGGL((hk_tiled_backtrack<V, N, L>), dim3(a.bt_grid), dim3(64 * kTiledBtWaves), 0, a.stream, a.blk1,
+                           a.blk0, a.slots, a.slot_bytes, a.info, static_cast<const V *>(a.dist),
+                           static_cast<V *>(a.cost), a.tour);
     return hipGetLastError();
 }
 

@@ -19,7 +19,10 @@
     X(9, int32_t, 14, 11, 256, 1, 4) \
     X(10, double, 13, 10, 256, 1, 4) \
     X(11, double, 15, 10, 128, 1, 6) \
-    X(13, double, 15, 10, 192, 1, 5)
+    X(13, double, 15, 10, 192, 1, 5) \
+    X(14, double, 15, 10, 256, 1, 6) \
+    X(15, double, 15, 9, 256, 1, 6) \
+    X(16, double, 15, 9, 256, 1, 7)
 
 namespace tspgpu {
 struct TiledCfg {

@@ -185,13 +185,14 @@ int solve_tiled(tspgpu_ctx *c, const TiledCfg *cfg, const void *d_dist, int n, i
     int rc = ensure_tiled_info(c, L);
     if (rc) return rc;
     const int grid = std::min(nblocks, c->cu_count * cfg->wg);
-    const size_t slot = (size_t)(1 << (N - L)) * (N - L) * ((size_t)1 << L) * cfg->vbytes;
-    if ((rc = ensure(&c->d_tslots, &c->tslots_bytes, (size_t)grid * slot))) return rc;
-    // parent words: 8 B per row, one table per block; blocks go in chunks of
-    // at most 16384 (4 GiB of parent words at n = 16)
-    const size_t per_block = (size_t)8 << N;
+    // one global slot per block (push area, parent words of the top rows,
+    // backtracking recompute area: 1.65 MB at n = 16, hk_tiled.h), kept until
+    // the backtracking kernel of the launch has run: blocks go in launches of
+    // at most 16384 (27 GB of the 288 GB at n = 16)
+    size_t slot = tiled_slot_bytes(N, L, cfg->vbytes);
+    if (const char *e = std::getenv("TSPGPU_SLOT_PAD")) slot += (size_t)std::atol(e);  // (layout experiments)
     const int chunk = std::min(nblocks, 16384);
-    if ((rc = ensure(&c->d_parents, &c->parents_bytes, (size_t)chunk * per_block))) return rc;
+    if ((rc = ensure(&c->d_tslots, &c->tslots_bytes, (size_t)chunk * slot))) return rc;
     for (int b0 = 0; b0 < nblocks; b0 += chunk) {
         TiledArgs a{};
         a.dist = d_dist;
@@ -200,11 +201,11 @@ int solve_tiled(tspgpu_ctx *c, const TiledCfg *cfg, const void *d_dist, int n, i
         a.blk1 = std::min(nblocks, b0 + chunk);
         a.slots = c->d_tslots;
         a.slot_bytes = (uint32_t)slot;
-        a.parents = c->d_parents;
         a.info = static_cast<const TiledInfo *>(c->d_tinfo[L]);
         a.cost = d_cost;
         a.tour = d_tour;
         a.grid = std::min(grid, a.blk1 - a.blk0);
+        a.bt_grid = std::min((a.blk1 - a.blk0 + kTiledBtWaves - 1) / kTiledBtWaves, c->cu_count * 3);
         a.stream = stream;
         hipError_t e = cfg->launch(a);
         if (e != hipSuccess) return hip_err(e);
@@ -490,7 +491,6 @@ int tspgpu_ctx_destroy(tspgpu_ctx *c)
     for (void *p : c->d_tinfo)
         if (p) (void)hipFree(p);
     if (c->d_tslots) (void)hipFree(c->d_tslots);
-    if (c->d_parents) (void)hipFree(c->d_parents);
     if (c->d_dist) (void)hipFree(c->d_dist);
     if (c->d_cost) (void)hipFree(c->d_cost);
     if (c->d_tour) (void)hipFree(c->d_tour);
