@@ -629,6 +629,21 @@ def main():
     total_blocks = Bp * world * args.steps
     value = total_blocks * relax / wall_max
 
+    # variant 5 runs two kernels per launch: time each on its stream (HIP
+    # events between them), outside the timed region
+    split = None
+    if variant == 5:
+        ctx.k1_split_timing(True)
+        fw, bt = [], []
+        for _ in range(5):
+            ctx.solve_device(dd, n, Bp, dc, dt, stream)
+            f_ms, b_ms = ctx.k1_last_split_ms()
+            fw.append(f_ms)
+            bt.append(b_ms)
+        ctx.k1_split_timing(False)
+        split = {"forward_kernel_ms": statistics.mean(fw), "backtrack_kernel_ms": statistics.mean(bt),
+                 "forward_kernel": kname, "backtrack_kernel": "hk_tiled_backtrack", "launches": 5}
+
     # time to optimal: one block through the ABI (in process), and the whole
     # program as a child process (the reference's definition)
     tto = {}
@@ -707,8 +722,9 @@ def main():
     if world == 1 and not args.no_pmc:
         prof = pmc_profile(n, min(Bp, 4096), cu, kname)
     peaks = valu_peaks() if world == 1 else None
-    relax_s_kernel = Bp * relax / (kernel_ms * 1e-3)
-    roof = roofline(variant, kname, n, Bp, kernel_ms, relax_s_kernel, alg_bytes_per_block, prof, peaks)
+    dom_ms = split["forward_kernel_ms"] if split else kernel_ms  # the dominant kernel's own time
+    relax_s_kernel = Bp * relax / (dom_ms * 1e-3)
+    roof = roofline(variant, kname, n, Bp, dom_ms, relax_s_kernel, alg_bytes_per_block, prof, peaks)
     cpu = cpu_opt = None
     if world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(n)
@@ -736,6 +752,7 @@ def main():
                    "k1_variant": variant, "kernel": kname},
         "blocks_per_s": total_blocks / wall_max,
         "kernel_ms_per_launch": kernel_ms,
+        "k1_kernel_split": split,
         "time_to_optimal": tto,
         "roofline": roof,
         "counters": prof,
@@ -757,15 +774,19 @@ def main():
 def roofline(variant, kname, n, Bp, kernel_ms, relax_s, alg_bytes_per_block, prof, peaks):
     """The dominant kernel against the ceiling that binds it.
 
-    VALU: every relaxation needs four VALU instructions (v_add_f64, v_cmp_lt_f64,
-    v_cndmask_b32 for the argmin that gives the tour, v_min_f64); the peak is
-    that same mix's issue rate measured on this GPU (bin/ubench), so frac =
-    relaxations/s / peak relaxations/s.
-    Memory: the bytes HBM actually moved per launch (PMC fabric bytes x the
-    DRAM share of the EA requests), against 8 TB/s.
+    VALU: a DP relaxation needs at least two VALU instructions (v_add_f64,
+    v_min_f64; the argmin that gives the tour is kept only for the top rows in
+    variant 5 and recomputed on the path by the backtracking kernel); the peak
+    is that min-only mix's issue rate measured on this GPU (bin/ubench), so
+    frac = relaxations/s of the forward kernel / peak relaxations/s.  For the
+    other variants (argmin in every relaxation) the 4-instruction mix is the
+    reference.
+    Memory: the bytes that left L2 toward memory per launch (PMC), against
+    8 TB/s (an upper bound on HBM: Infinity-Cache hits are included).
     The line reports whichever fraction is higher as `roofline` (the binding
     one) and the other as `other`."""
-    mix = "f64 relaxation+argmin (add,cmp,cndmask,min)"
+    mix, per = (("f64 relaxation min-only (add,min)", 2) if variant == 5
+                else ("f64 relaxation+argmin (add,cmp,cndmask,min)", 4))
     peak_relax = (peaks or {}).get(mix)
     scale = Bp / (prof or {}).get("blocks_per_launch", Bp)
     hbm = (prof or {}).get("hbm_bytes")
@@ -775,12 +796,12 @@ def roofline(variant, kname, n, Bp, kernel_ms, relax_s, alg_bytes_per_block, pro
         fabric = (prof["fabric_read_bytes"] + prof["fabric_write_bytes"]) * scale
     valu = None
     if peak_relax:
-        valu = {"bound": "valu", "achieved": 4 * relax_s / 1e12, "peak": 4 * peak_relax / 1e12,
+        valu = {"bound": "valu", "achieved": per * relax_s / 1e12, "peak": per * peak_relax / 1e12,
                 "unit": "T VALU lane-instructions/s", "frac": relax_s / peak_relax, "traffic": hbm,
-                "note": f"{kname} (n={n}): 4 VALU instructions per DP relaxation x {Bp} blocks x "
-                        f"{tspgpu.relaxations_per_block(n):.0f} relaxations / HIP-event launch time; peak = the "
-                        f"same 4-instruction mix measured by bin/ubench on this GPU ({peak_relax:.3e} "
-                        f"relaxations/s); traffic = HBM bytes per launch (PMC)"}
+                "note": f"{kname} (n={n}): {per} VALU instructions per DP relaxation ({mix}) x {Bp} blocks x "
+                        f"{tspgpu.relaxations_per_block(n):.0f} relaxations / the kernel's own HIP-event time "
+                        f"({kernel_ms:.3f} ms); peak = the same mix measured by bin/ubench on this GPU "
+                        f"({peak_relax:.3e} relaxations/s); traffic = memory-side bytes per launch (PMC)"}
     mem = None
     if hbm is not None:
         mem = {"bound": "hbm (upper bound: Infinity-Cache hits included)", "achieved": hbm / (kernel_ms * 1e-3) / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",

@@ -139,6 +139,13 @@ int tspgpu_last_grid(const tspgpu_ctx *ctx);
 /* K1 variant the last batched launch used: 5 = sub-cube tiled (hk_tiled_kernel),
  * 4 = ping-pong + parent words, 2 = compact + prefetch, ... (heldkarp_kernel). */
 int tspgpu_last_variant(const tspgpu_ctx *ctx);
+/* Measurement aid for variant 5, which runs two kernels per launch (the
+ * forward pass hk_tiled_kernel, then hk_tiled_backtrack): with split timing
+ * enabled every variant-5 launch also records a HIP event between the two, and
+ * tspgpu_k1_last_split_ms waits for the last such launch and returns both
+ * kernels' durations (-ENOENT if the last launch recorded no split). */
+int tspgpu_k1_split_timing(tspgpu_ctx *ctx, int enable);
+int tspgpu_k1_last_split_ms(tspgpu_ctx *ctx, float *forward_ms, float *backtrack_ms);
 /* Number of visible HIP devices (0 when none). */
 int tspgpu_device_count(void);
 double tspgpu_relaxations_per_block(int n);

@@ -27,7 +27,8 @@ constexpr int CHAINS = 8;
 
 // MODE 0 v_add_f64, 1 v_min_f64, 2 v_cmp_lt_f64 + v_cndmask_b32, 3 v_add_u32,
 // 4 v_min_i32, 5 the f64 relaxation with argmin (add, cmp, cndmask, min),
-// 6 the i32 relaxation with argmin, 7 v_cndmask_b32 alone
+// 6 the i32 relaxation with argmin, 7 v_cndmask_b32 alone, 8 the f64
+// relaxation without argmin (add, min: K1 variant 5's passes below the top rows)
 template <int MODE>
 __global__ __launch_bounds__(256) void valu_kernel(double *out, double seed)
 {
@@ -76,6 +77,12 @@ __global__ __launch_bounds__(256) void valu_kernel(double *out, double seed)
             }
             if constexpr (MODE == 7)
                 asm volatile("v_cndmask_b32 %0, %0, %1, vcc" : "+v"(arg[c]) : "v"(it) : "vcc");
+            if constexpr (MODE == 8) {
+                double t;
+                asm volatile("v_add_f64 %1, %2, %3\n\tv_min_f64 %0, %0, %1"
+                             : "+v"(a[c]), "=&v"(t)
+                             : "v"(b), "v"(a[(c + 1) % CHAINS]));
+            }
         }
     }
     double s = 0;
@@ -133,6 +140,7 @@ int main(int argc, char **argv)
         run_valu<4>("v_min_i32", 1, p);
         run_valu<7>("v_cndmask_b32", 1, p);
         run_valu<5>("f64 relaxation+argmin (add,cmp,cndmask,min)", 4, p);
+        run_valu<8>("f64 relaxation min-only (add,min)", 2, p);
         run_valu<6>("i32 relaxation+argmin (add,cmp,cndmask,min)", 4, p);
         return 0;
     }

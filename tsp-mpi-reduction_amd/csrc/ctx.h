@@ -42,6 +42,10 @@ struct tspgpu_ctx {
     // per context, so a launch on a stream other than the previous one waits
     // for the previous launch (event recorded after every K1 launch)
     hipEvent_t ev_k1_done = nullptr;
+    // variant-5 split timing (tspgpu_k1_split_timing): events around the
+    // forward and the backtracking kernel of the last launch
+    int split_timing = 0, split_valid = 0;
+    hipEvent_t ev_split[3] = {nullptr, nullptr, nullptr};
     hipStream_t k1_last_stream = nullptr;
     bool k1_launched = false;
     char name[256] = {0};

@@ -439,7 +439,7 @@ __device__ __forceinline__ uint32_t tiled_pidx(const TiledCtx<V, N, L, R> &c, ui
 // forward pass's own relaxations restricted to those rows, the minimum only
 // (IEEE min is order-free, so the values are the forward pass's bits).
 template <typename V, int N, int L, int R>
-__device__ void tiled_recompute(const TiledCtx<V, N, L, R> &c, const V *d0, V *gs, uint32_t h, uint32_t lT,
+__device__ void tiled_recompute(const TiledCtx<V, N, L, R> &c, const V *d0, uint32_t h, uint32_t lT,
                                 uint32_t lane)
 {
     constexpr int VB = sizeof(V);
@@ -461,17 +461,23 @@ __device__ void tiled_recompute(const TiledCtx<V, N, L, R> &c, const V *d0, V *g
             const uint32_t dst = lT & ~lp;
             const uint32_t Tm = (h << L) | lp;
             const uint32_t pidx = tiled_pidx(c, lp);
-            // the row's values into this lane's LDS column (all loads in flight at once)
+            V gv[N];  // the row's values (all loads in flight at once; non-members unused)
 #pragma unroll
-            for (int m = 0; m < N; ++m) gs[m * 64 + lane] = tiled_g(c, h, lp, pidx, m);
-            for (uint32_t db = dst; db; db &= db - 1u) {
-                const int s = __builtin_ctz(db);
-                V acc = ValT<V>::inf;
-                for (uint32_t mb = Tm; mb; mb &= mb - 1u) {
-                    const int m = __builtin_ctz(mb);
-                    acc = ValT<V>::vmin(acc, gs[m * 64 + lane] + c.dr[(m * kTiledDS + s) * R]);
+            for (int m = 0; m < N; ++m) gv[m] = tiled_g(c, h, lp, pidx, m);
+            // every destination s of lT \ lp, every member m: predicated, the
+            // distance reads are wave-uniform LDS broadcasts
+#pragma unroll
+            for (int s = 0; s < L; ++s) {
+                if ((dst >> s) & 1u) {
+                    V acc = ValT<V>::inf;
+#pragma unroll
+                    for (int m = 0; m < N; ++m) {
+                        const V t = ValT<V>::vmin(acc, gv[m] + c.dr[(m * kTiledDS + s) * R]);
+                        acc = ((Tm >> m) & 1u) ? t : acc;
+                    }
+                    c.rec.store(((lp | (1u << s)) * L + (uint32_t)s) * VB, 0, acc);
                 }
-                c.rec.store(((lp | (1u << s)) * L + (uint32_t)s) * VB, 0, acc);
+                __builtin_amdgcn_sched_barrier(0);
             }
         }
     }
@@ -487,7 +493,7 @@ __device__ void tiled_recompute(const TiledCtx<V, N, L, R> &c, const V *d0, V *g
 // and the parent is the first strict minimum over its members ascending of
 // G[T][m] + d[m][k] — the forward pass's candidates, so its argmin.
 template <typename V, int N, int L, int R>
-__device__ bool tiled_backtrack(const TiledCtx<V, N, L, R> &c, const V *d0, V *gs, int bestM,
+__device__ bool tiled_backtrack(const TiledCtx<V, N, L, R> &c, const V *d0, int bestM,
                                 int32_t *tour, uint32_t lane)
 {
     constexpr int NL = 1 << L, VB = sizeof(V), n = N + 1;
@@ -506,7 +512,7 @@ __device__ bool tiled_backtrack(const TiledCtx<V, N, L, R> &c, const V *d0, V *g
             pm = (int)((w >> (4 * q)) & 15u);
         } else {
             if (!(TSPGPU_TILED_ABL & 128) && (hT != hcur || (lT & ~lcur))) {
-                tiled_recompute(c, d0, gs, hT, lT, lane);
+                tiled_recompute(c, d0, hT, lT, lane);
                 hcur = hT;
                 lcur = lT;
             }
@@ -660,9 +666,12 @@ __global__ __launch_bounds__(THREADS, tiled_waves(THREADS, WG)) void hk_tiled_ke
 // of dependent loads (tens of microseconds), so all resident waves run their
 // chains at the same time, after the forward kernel instead of stalling it.
 constexpr int kTiledBtWaves = 4;
+#ifndef TSPGPU_TILED_BTWG
+#define TSPGPU_TILED_BTWG 6  // backtracking workgroups per CU (register budget)
+#endif
 namespace {  // internal linkage: every instantiation file keeps its own (timing builds differ per file)
 template <typename V, int N, int L>
-__global__ __launch_bounds__(64 * kTiledBtWaves) void hk_tiled_backtrack(
+__global__ __launch_bounds__(64 * kTiledBtWaves, TSPGPU_TILED_BTWG) void hk_tiled_backtrack(
     int nblocks, int blk0, const char *__restrict__ slots, uint32_t slot_bytes, const TiledInfo *__restrict__ info,
     const V *__restrict__ dist, V *__restrict__ cost_out, int32_t *__restrict__ tour_out)
 {
@@ -670,7 +679,6 @@ __global__ __launch_bounds__(64 * kTiledBtWaves) void hk_tiled_backtrack(
     __shared__ uint16_t lmask[NL], lrankb[NL];
     __shared__ int smoff[L + 2];
     __shared__ V drs[kTiledBtWaves][DRV];     // per wave: the block's inner distances, then d[0][k]
-    __shared__ V gss[kTiledBtWaves][N * 64];  // per wave: one recomputed row per lane, member-major
     for (int i = threadIdx.x; i < NL; i += 64 * kTiledBtWaves) {
         lmask[i] = info->mask[i];
         lrankb[i] = (uint16_t)(info->rank[i] * VB);
@@ -706,7 +714,7 @@ __global__ __launch_bounds__(64 * kTiledBtWaves) void hk_tiled_backtrack(
         c.par.rs = uniform_rsrc(slot + tiled_push_bytes(N, L, VB), (uint32_t)tiled_parent_bytes(N, L));
         c.rec.rs = uniform_rsrc(slot + tiled_push_bytes(N, L, VB) + tiled_parent_bytes(N, L),
                                 (uint32_t)tiled_recomp_bytes(L, VB));
-        if (!tiled_backtrack(c, dr + N * kTiledDS, gss[wave], bestM, tour, lane) && lane == 0) cost_out[blk] = V(-1);
+        if (!tiled_backtrack(c, dr + N * kTiledDS, bestM, tour, lane) && lane == 0) cost_out[blk] = V(-1);
         __builtin_amdgcn_wave_barrier();  // dr is reloaded for the next block
     }
 }
@@ -723,6 +731,7 @@ struct TiledArgs {
     int grid;
     int bt_grid;              // backtracking workgroups (kTiledBtWaves blocks each at a time)
     hipStream_t stream;
+    hipEvent_t ev_mid;        // recorded between the two kernels when non-null (split timing)
 };
 
 template <typename V, int N, int L, int THREADS, int R, int WG>
@@ -740,6 +749,7 @@ hipError_t launch_tiled_n(const TiledArgs &a)
                        static_cast<const V *>(a.dist), a.blk1, a.blk0, a.slots, a.slot_bytes, a.info,
                        static_cast<V *>(a.cost), a.tour);
     hipError_t e = hipGetLastError();
+    if (e == hipSuccess && a.ev_mid) e = hipEventRecord(a.ev_mid, a.stream);
     if (e != hipSuccess || (TSPGPU_TILED_ABL & 32)) return e;
     hipLaunchKernelGGL((hk_tiled_backtrack<V, N, L>), dim3(a.bt_grid), dim3(64 * kTiledBtWaves), 0, a.stream, a.blk1, a.blk0,
                        a.slots, a.slot_bytes, a.info, static_cast<const V *>(a.dist), static_cast<V *>(a.cost),

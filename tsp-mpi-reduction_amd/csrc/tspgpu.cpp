@@ -193,8 +193,16 @@ int solve_tiled(tspgpu_ctx *c, const TiledCfg *cfg, const void *d_dist, int n, i
     if (const char *e = std::getenv("TSPGPU_SLOT_PAD")) slot += (size_t)std::atol(e);  // (layout experiments)
     const int chunk = std::min(nblocks, 16384);
     if ((rc = ensure(&c->d_tslots, &c->tslots_bytes, (size_t)chunk * slot))) return rc;
+    const bool split = c->split_timing && nblocks <= chunk;  // one launch pair: one split
+    c->split_valid = 0;
+    if (split) {
+        for (auto &ev : c->ev_split)
+            if (!ev && hipEventCreate(&ev) != hipSuccess) return -EIO;
+        if (hipEventRecord(c->ev_split[0], stream) != hipSuccess) return -EIO;
+    }
     for (int b0 = 0; b0 < nblocks; b0 += chunk) {
         TiledArgs a{};
+        a.ev_mid = split ? c->ev_split[1] : nullptr;
         a.dist = d_dist;
         a.n = n;
         a.blk0 = b0;
@@ -205,10 +213,14 @@ int solve_tiled(tspgpu_ctx *c, const TiledCfg *cfg, const void *d_dist, int n, i
         a.cost = d_cost;
         a.tour = d_tour;
         a.grid = std::min(grid, a.blk1 - a.blk0);
-        a.bt_grid = std::min((a.blk1 - a.blk0 + kTiledBtWaves - 1) / kTiledBtWaves, c->cu_count * 3);
+        a.bt_grid = std::min((a.blk1 - a.blk0 + kTiledBtWaves - 1) / kTiledBtWaves, c->cu_count * TSPGPU_TILED_BTWG);
         a.stream = stream;
         hipError_t e = cfg->launch(a);
         if (e != hipSuccess) return hip_err(e);
+    }
+    if (split) {
+        if (hipEventRecord(c->ev_split[2], stream) != hipSuccess) return -EIO;
+        c->split_valid = 1;
     }
     c->last_grid = grid;
     c->last_variant = 5;
@@ -497,6 +509,8 @@ int tspgpu_ctx_destroy(tspgpu_ctx *c)
     if (c->ev_start) (void)hipEventDestroy(c->ev_start);
     if (c->ev_stop) (void)hipEventDestroy(c->ev_stop);
     if (c->ev_k1_done) (void)hipEventDestroy(c->ev_k1_done);
+    for (auto ev : c->ev_split)
+        if (ev) (void)hipEventDestroy(ev);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
     return 0;
@@ -617,6 +631,24 @@ int tspgpu_solve(const double *dist, int n, int nblocks, double *cost_out, int32
 int tspgpu_last_grid(const tspgpu_ctx *c) { return c ? c->last_grid : 0; }
 
 int tspgpu_last_variant(const tspgpu_ctx *c) { return c ? c->last_variant : -1; }
+
+int tspgpu_k1_split_timing(tspgpu_ctx *c, int enable)
+{
+    if (!c) return -EINVAL;
+    c->split_timing = enable ? 1 : 0;
+    return 0;
+}
+
+int tspgpu_k1_last_split_ms(tspgpu_ctx *c, float *forward_ms, float *backtrack_ms)
+{
+    if (!c || !forward_ms || !backtrack_ms) return -EINVAL;
+    if (!c->split_valid || c->last_variant != 5) return -ENOENT;
+    if (hipSetDevice(c->device) != hipSuccess) return -ENODEV;
+    hipError_t e = hipEventSynchronize(c->ev_split[2]);
+    if (e == hipSuccess) e = hipEventElapsedTime(forward_ms, c->ev_split[0], c->ev_split[1]);
+    if (e == hipSuccess) e = hipEventElapsedTime(backtrack_ms, c->ev_split[1], c->ev_split[2]);
+    return hip_err(e);
+}
 
 int tspgpu_device_count(void)
 {

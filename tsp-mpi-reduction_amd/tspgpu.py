@@ -24,7 +24,7 @@ EXPORTED_SYMBOLS = (
     "tspgpu_solve_blocks_device", "tspgpu_solve", "tspgpu_last_grid", "tspgpu_relaxations_per_block",
     "tspgpu_table_bytes_per_block", "tspgpu_device_alloc", "tspgpu_device_free", "tspgpu_memcpy_htod",
     "tspgpu_memcpy_dtoh", "tspgpu_stream", "tspgpu_synchronize", "tspgpu_timer_start", "tspgpu_timer_stop",
-    "tspgpu_device_info", "tspgpu_last_variant", "tspgpu_device_count", "tspgpu_stream_create",
+    "tspgpu_device_info", "tspgpu_last_variant", "tspgpu_k1_split_timing", "tspgpu_k1_last_split_ms", "tspgpu_device_count", "tspgpu_stream_create",
     "tspgpu_stream_destroy", "tspgpu_stream_synchronize",
     # K2
     "tspgpu_search_solve", "tspgpu_search_enumerate", "tspgpu_search_create", "tspgpu_search_destroy", "tspgpu_search_info",
@@ -104,6 +104,8 @@ def lib():
         L.tspgpu_solve.argtypes = [dp, ctypes.c_int, ctypes.c_int, dp, ip, ctypes.POINTER(Opts)]
         L.tspgpu_last_grid.argtypes = [vp]
         L.tspgpu_last_variant.argtypes = [vp]
+        L.tspgpu_k1_split_timing.argtypes = [vp, ctypes.c_int]
+        L.tspgpu_k1_last_split_ms.argtypes = [vp, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float)]
         L.tspgpu_device_count.argtypes = []
         L.tspgpu_relaxations_per_block.argtypes = [ctypes.c_int]
         L.tspgpu_relaxations_per_block.restype = ctypes.c_double
@@ -300,6 +302,17 @@ class Context:
     def last_variant(self) -> int:
         """K1 variant of the last batched launch (5: hk_tiled_kernel, else heldkarp_kernel)."""
         return lib().tspgpu_last_variant(self.handle)
+
+    def k1_split_timing(self, enable: bool = True):
+        """Record an event between variant 5's forward and backtracking kernels."""
+        self._check(lib().tspgpu_k1_split_timing(self.handle, int(enable)), "tspgpu_k1_split_timing")
+
+    def k1_last_split_ms(self):
+        """(forward_ms, backtrack_ms) of the last variant-5 launch (waits for it)."""
+        f, b = ctypes.c_float(), ctypes.c_float()
+        self._check(lib().tspgpu_k1_last_split_ms(self.handle, ctypes.byref(f), ctypes.byref(b)),
+                    "tspgpu_k1_last_split_ms")
+        return f.value, b.value
 
     def _check(self, rc, what):
         if rc:
