@@ -13,6 +13,7 @@ CSRC = os.path.join(ROOT, "tsp-mpi-reduction_amd", "csrc")
 
 # (id, value type, N, L, threads per workgroup, distance copies R, workgroups per CU)
 CFGS = [
+    (14, "double", 15, 10, 256, 1, 6),
     (12, "double", 15, 10, 256, 1, 5),
     (2, "double", 15, 11, 256, 1, 3),
     (0, "double", 15, 11, 512, 1, 2),
@@ -27,9 +28,10 @@ CFGS = [
     (10, "double", 13, 10, 256, 1, 4),
     (11, "double", 15, 10, 128, 1, 6),
     (13, "double", 15, 10, 192, 1, 5),
-    (14, "double", 15, 10, 256, 1, 6),
     (15, "double", 15, 9, 256, 1, 6),
     (16, "double", 15, 9, 256, 1, 7),
+    (17, "double", 15, 10, 256, 2, 5),
+    (18, "double", 15, 10, 256, 1, 7),
 ]
 
 

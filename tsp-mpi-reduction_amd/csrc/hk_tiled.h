@@ -80,6 +80,8 @@ constexpr int kTiledDS = 17;
 struct TiledInfo {
     uint16_t mask[1 << kTiledMaxL];  // L-bit masks sorted by (popcount, colex rank)
     uint16_t rank[1 << kTiledMaxL];  // colex rank of a mask among the masks of its popcount
+    uint16_t rankb8[1 << kTiledMaxL];  // rank x 8, rank x 4: byte offsets inside a push / layer column
+    uint16_t rankb4[1 << kTiledMaxL];
     int moff[kTiledMaxL + 2];        // first index of popcount class j in mask[]
     int cnt[kTiledMaxL + 2];         // C(L, j)
 };
@@ -96,12 +98,18 @@ __host__ __device__ constexpr int tiled_region_vals(int L)
     }
     return m;
 }
-__host__ __device__ constexpr size_t tiled_lds_bytes(int N, int L, int R, int vb)
+__host__ __device__ constexpr size_t tiled_lds_bytes(int N, int L, int R, int vb, bool tables = true)
 {
     return (size_t)N * kTiledDS * R * vb     // replicated inner distances, rows of kTiledDS
            + (size_t)2 * 16 * vb             // d[0][k], d[m][0]
            + (size_t)tiled_region_vals(L) * vb  // live low layers
-           + (size_t)2 * 2 * (1 << L);       // mask + rank (u16)
+           + (tables ? (size_t)2 * 2 * (1 << L) : 0);  // mask + rank (u16), unless read from global
+}
+// the mask/rank tables stay in global memory (L1/L2-resident) when staging
+// them in LDS would keep WG workgroups from fitting a CU's 160 KB
+__host__ __device__ constexpr bool tiled_global_tables(int N, int L, int R, int vb, int wg)
+{
+    return tiled_lds_bytes(N, L, R, vb, true) * wg > 160 * 1024;
 }
 // push area of one slot: [h][c][idx] values (c = high city index 0..H-1,
 // idx = the row's place in the sorted L-bit mask list)
@@ -243,8 +251,8 @@ __device__ __forceinline__ void relax_min(int32_t &acc, int32_t g, int32_t d)
 template <typename V, int N, int L, int R>
 struct TiledCtx {
     const V *dr;               // LDS replicated distances
-    const uint16_t *lmask;     // LDS sorted L-bit masks
-    const uint16_t *lrankb;    // LDS colex rank x sizeof(V) (byte offset inside a position column)
+    const uint16_t *lmask;     // sorted L-bit masks (LDS, or global: tiled_global_tables)
+    const uint16_t *lrankb;    // colex rank x sizeof(V) (byte offset inside a position column)
     V *region;                 // LDS live low layers
     Rsrc<V> push;              // this slot's push area
     Rsrc<uint64_t> par;        // this slot's parent words (the current block's)
@@ -585,18 +593,21 @@ __global__ __launch_bounds__(THREADS, tiled_waves(THREADS, WG)) void hk_tiled_ke
     V *d0 = dr + N * kTiledDS * R;  // d[0][k], k = 1..N at [k-1]
     V *dc = d0 + 16;                // d[m][0], m = 1..N at [m-1]
     V *region = dc + 16;
+    constexpr bool GT = tiled_global_tables(N, L, R, VB, WG);
     uint16_t *lmask = reinterpret_cast<uint16_t *>(region + tiled_region_vals(L));
     uint16_t *lrankb = lmask + NL;
     const uint32_t tid = threadIdx.x;
 
-    for (int i = tid; i < NL; i += THREADS) {
-        lmask[i] = info->mask[i];
-        lrankb[i] = (uint16_t)(info->rank[i] * VB);
+    if constexpr (!GT) {
+        for (int i = tid; i < NL; i += THREADS) {
+            lmask[i] = info->mask[i];
+            lrankb[i] = VB == 8 ? info->rankb8[i] : info->rankb4[i];
+        }
     }
     TiledCtx<V, N, L, R> c;
     c.dr = dr;
-    c.lmask = lmask;
-    c.lrankb = lrankb;
+    c.lmask = GT ? info->mask : lmask;
+    c.lrankb = GT ? (VB == 8 ? info->rankb8 : info->rankb4) : lrankb;
     c.region = region;
     c.moff = nullptr;  // (backtracking only)
 
@@ -737,7 +748,7 @@ struct TiledArgs {
 template <typename V, int N, int L, int THREADS, int R, int WG>
 hipError_t launch_tiled_n(const TiledArgs &a)
 {
-    const size_t lds = tiled_lds_bytes(N, L, R, sizeof(V));
+    const size_t lds = tiled_lds_bytes(N, L, R, sizeof(V), !tiled_global_tables(N, L, R, sizeof(V), WG));
     static bool raised = false;  // once per instantiation
     if (!raised) {
         hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&hk_tiled_kernel<V, N, L, THREADS, R, WG>),

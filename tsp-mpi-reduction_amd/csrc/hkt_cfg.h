@@ -6,6 +6,7 @@
 #include "hk_tiled.h"
 
 #define TSPGPU_TILED_CFGS(X) \
+    X(14, double, 15, 10, 256, 1, 6) \
     X(12, double, 15, 10, 256, 1, 5) \
     X(2, double, 15, 11, 256, 1, 3) \
     X(0, double, 15, 11, 512, 1, 2) \
@@ -20,9 +21,10 @@
     X(10, double, 13, 10, 256, 1, 4) \
     X(11, double, 15, 10, 128, 1, 6) \
     X(13, double, 15, 10, 192, 1, 5) \
-    X(14, double, 15, 10, 256, 1, 6) \
     X(15, double, 15, 9, 256, 1, 6) \
-    X(16, double, 15, 9, 256, 1, 7)
+    X(16, double, 15, 9, 256, 1, 7) \
+    X(17, double, 15, 10, 256, 2, 5) \
+    X(18, double, 15, 10, 256, 1, 7)
 
 namespace tspgpu {
 struct TiledCfg {

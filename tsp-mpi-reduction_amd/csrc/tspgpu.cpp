@@ -146,6 +146,8 @@ int ensure_tiled_info(tspgpu_ctx *c, int L)
         for (uint32_t m = 0; m < (1u << L); ++m)
             if (__builtin_popcount(m) == j) {  // numeric order of equal-popcount masks = colex order
                 info->mask[k++] = (uint16_t)m;
+                info->rankb8[m] = (uint16_t)(r * 8);
+                info->rankb4[m] = (uint16_t)(r * 4);
                 info->rank[m] = (uint16_t)r++;
             }
     }
