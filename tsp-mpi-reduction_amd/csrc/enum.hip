@@ -27,6 +27,7 @@
 // loop over the prefixes balances it.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <utility>
 
 #include "search.h"
@@ -450,16 +451,81 @@ __global__ __launch_bounds__(256) void tail_kernel(SearchArgs a)
 // per output: pass 1 counts its live children, one atomicAdd per output,
 // pass 2 re-evaluates (cheap: LDS + registers) and writes the children at
 // block-scanned offsets.
+// ---------------------------------------------------------------------------
+// Stronger bounds of the frontier search (SearchArgs::bnd2, ::hsuf).
+//
+// Colex rank of a set of inner-city places c_0 < c_1 < ... (place = city - 1):
+// sum_i C(c_i, i + 1); bn[m][k] = C(m, k) in LDS.
+__device__ __forceinline__ void load_binom(uint32_t (*bn)[8])
+{
+    for (int i = threadIdx.x; i < 32 * 8; i += blockDim.x) bn[i >> 3][i & 7] = search_binom(i >> 3, i & 7);
+}
+
+// Suffix table of size TL = a.hs_len, one thread per set U of TL inner cities
+// (colex rank r): H[U][x] for every x in U = the cheapest path from x over U
+// to city 0, all (TL-1)! orders folded by the same straight-line code as the
+// register tails (`complete`) — a bound only, compared with the incumbent's
+// 2^-39 margin, so its rounding order does not matter.
+template <typename V, int TL>
+__global__ __launch_bounds__(256) void suffix_kernel(SearchArgs a, uint32_t sets)
+{
+    __shared__ uint32_t bn[32][8];
+    __shared__ double dl[kSearchMaxN * kTRow];
+    const int n = a.n;
+    const V *gd = static_cast<const V *>(a.dist);
+    for (int i = threadIdx.x; i < n * n; i += blockDim.x) dl[(i / n) * kTRow + i % n] = (double)gd[i];
+    load_binom(bn);
+    __syncthreads();
+    double *H = const_cast<double *>(a.hsuf) + a.hs_off[TL];
+    for (uint32_t r0 = blockIdx.x * 256u + threadIdx.x; r0 < sets; r0 += gridDim.x * 256u) {
+        // unrank U (colex): the largest place c with C(c, i) <= r, i = TL .. 1
+        int c[TL];
+        uint32_t r = r0;
+        int hi = n - 2;  // places 0 .. N-1 (inner city = place + 1)
+#pragma unroll
+        for (int i = TL; i >= 1; --i) {
+            int m = hi;
+            while (bn[m][i] > r) --m;
+            c[i - 1] = m + 1;
+            r -= bn[m][i];
+            hi = m - 1;
+        }
+        double sm[TL][TL], d0[TL];
+#pragma unroll
+        for (int i = 0; i < TL; ++i) {
+            d0[i] = dl[c[i] * kTRow];
+#pragma unroll
+            for (int j = 0; j < TL; ++j) sm[i][j] = i == j ? 0.0 : dl[c[i] * kTRow + c[j]];
+        }
+        static_for(
+            [&](auto i) {
+                constexpr int I = decltype(i)::value;
+                double best = ENum<double>::big();
+                complete<double, TL, (((1 << TL) - 1) & ~(1 << I)), I>(sm, d0, 0.0, best);
+                H[(size_t)r0 * TL + I] = best;
+            },
+            std::make_integer_sequence<int, TL>{});
+    }
+}
+
 template <typename V>
 struct Expand {
     uint32_t w[8];
     int len;
     uint32_t rem, live;
+    uint32_t hnodes;  // suffix-table candidates evaluated (nodes one level down)
+    double ub;        // the best completion a suffix test saw, as an upper bound on the optimum
 };
 
+// The bound of child j of path (c, k, rem) (rem includes j), any of:
+//   B0: every city still to be entered pays its cheapest incoming edge;
+//   B1 (symmetric matrices): e[j] + sum over rem \ j of b + e[0];
+//   H  (the child has a.hs_len cities left): min over x in rem \ j of
+//       d[j][x] + H[rem \ j][x], the exact cheapest completion up to rounding.
 template <typename V>
-__device__ __forceinline__ Expand<V> expand_eval(const SearchArgs &a, const V *dl, const V *am, uint32_t full,
-                                                 uint32_t idx, uint32_t end, V thr)
+__device__ __forceinline__ Expand<V> expand_eval(const SearchArgs &a, const V *dl, const V *am, const V *b2,
+                                                 const uint32_t (*bn)[8], uint32_t full, uint32_t idx, uint32_t end,
+                                                 V thr)
 {
     Expand<V> e;
     const bool act = idx < end;
@@ -471,14 +537,62 @@ __device__ __forceinline__ Expand<V> expand_eval(const SearchArgs &a, const V *d
     fold_path<V>(dl, e.w, e.len, c, k, mem);
     e.rem = act ? (full & ~mem) : 0u;
     V remA = am[0];  // every city still to be entered: its cheapest incoming edge (exact sums)
-    for (uint32_t x = e.rem; x; x &= x - 1u) remA += am[__builtin_ctz(x)];
+    V remB = 0;      // B1: the rem cities' half sums (exact sums)
+    for (uint32_t x = e.rem; x; x &= x - 1u) {
+        const int t = __builtin_ctz(x);
+        remA += am[t];
+        if (a.sym) remB += b2[2 * t];
+    }
+    const bool htest = a.hs_len > 0 && a.hs_len == a.tail_len && e.len == a.tail_level && !a.noprune;
+    const double dthr = (double)thr;
     e.live = 0;
+    e.hnodes = 0;
+    e.ub = 1.0e300;
     for (uint32_t x = e.rem; x; x &= x - 1u) {
         const int j = __builtin_ctz(x);
         const V cj = c + dl[k * kTRow + j];
-        if (a.noprune || !(cj + (remA - am[j]) > thr)) e.live |= 1u << j;
+        bool ok = a.noprune || !(cj + (remA - am[j]) > thr);
+        if (ok && a.sym && !a.noprune) ok = !(cj + (((remB - b2[2 * j]) + b2[2 * j + 1]) + b2[1]) > thr);
+        if (ok && htest) {
+            // the child's completion: rank of R = rem \ j, then min over its cities
+            const uint32_t R = e.rem & ~(1u << j);
+            uint32_t rk = 0;
+            int i = 0;
+            for (uint32_t y = R; y; y &= y - 1u) rk += bn[__builtin_ctz(y) - 1][++i];
+            const double *Hs = a.hsuf + a.hs_off[a.hs_len] + (size_t)rk * (uint32_t)a.hs_len;
+            double best = 1.0e300;
+            i = 0;
+            for (uint32_t y = R; y; y &= y - 1u) {
+                const double v = (double)dl[j * kTRow + __builtin_ctz(y)] + Hs[i++];
+                best = v < best ? v : best;
+            }
+            e.hnodes += (uint32_t)a.hs_len;
+            ok = !((double)cj + best > dthr);
+            // cj + best is the cost of a real tour up to a few roundings
+            // (< 2^-47 relative): scaled up by 2^-30 it bounds the optimum
+            // from above, and the search may prune against it at once
+            const double u = ((double)cj + best) * (1.0 + 0x1p-30);
+            e.ub = u < e.ub ? u : e.ub;
+        }
+        if (ok) e.live |= 1u << j;
     }
     return e;
+}
+
+// One atomicMin per wave with the smallest suffix-test upper bound (f64
+// incumbents only: the integer search's incumbent stays a tour cost).
+template <typename V>
+__device__ __forceinline__ void publish_ub(const SearchArgs &a, double ub)
+{
+    if constexpr (sizeof(V) == 8) {
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) {
+            const double o = __shfl_xor(ub, off);
+            ub = o < ub ? o : ub;
+        }
+        if (__lane_id() == 0 && ub < 1.0e300)
+            atomicMin(a.inc, (unsigned long long)__double_as_longlong(ub));
+    }
 }
 
 template <typename V>
@@ -486,6 +600,8 @@ __global__ __launch_bounds__(256) void expand_kernel(SearchArgs a)
 {
     __shared__ V dl[kSearchMaxN * kTRow];
     __shared__ V am[kSearchMaxN];
+    __shared__ V b2[2 * kSearchMaxN];
+    __shared__ uint32_t bn[32][8];
     __shared__ uint32_t wtot[2][4];
     __shared__ uint32_t bbase[2];
     const int n = a.n;
@@ -493,6 +609,9 @@ __global__ __launch_bounds__(256) void expand_kernel(SearchArgs a)
     const V *ga = static_cast<const V *>(a.amin);
     for (int i = threadIdx.x; i < n * n; i += blockDim.x) dl[(i / n) * kTRow + i % n] = gd[i];
     for (int i = threadIdx.x; i < n; i += blockDim.x) am[i] = ga[i];
+    if (a.sym)
+        for (int i = threadIdx.x; i < 2 * n; i += blockDim.x) b2[i] = static_cast<const V *>(a.bnd2)[i];
+    load_binom(bn);
     __syncthreads();
 
     const uint32_t full = (uint32_t)((1ull << n) - 1ull) & ~1u;
@@ -505,10 +624,11 @@ __global__ __launch_bounds__(256) void expand_kernel(SearchArgs a)
     uint32_t cT = 0, cF = 0;
     unsigned long long nodes = 0;
     for (uint32_t base = b0; base < b1; base += 256u) {
-        const Expand<V> e = expand_eval<V>(a, dl, am, full, base + threadIdx.x, b1, thr);
+        const Expand<V> e = expand_eval<V>(a, dl, am, b2, bn, full, base + threadIdx.x, b1, thr);
         const uint32_t cnt = (uint32_t)__builtin_popcount(e.live);
         if (e.len == a.tail_level) cT += cnt; else cF += cnt;  // children have len inner cities
-        nodes += (unsigned long long)__builtin_popcount(e.rem);
+        nodes += (unsigned long long)__builtin_popcount(e.rem) + e.hnodes;
+        publish_ub<V>(a, e.ub);
     }
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) {
@@ -533,7 +653,7 @@ __global__ __launch_bounds__(256) void expand_kernel(SearchArgs a)
 
     // ---- pass 2: the children, at block-scanned offsets
     for (uint32_t base = b0; base < b1; base += 256u) {
-        const Expand<V> e = expand_eval<V>(a, dl, am, full, base + threadIdx.x, b1, thr);
+        const Expand<V> e = expand_eval<V>(a, dl, am, b2, bn, full, base + threadIdx.x, b1, thr);
         const bool tail = e.len == a.tail_level;
         const uint32_t cnt = (uint32_t)__builtin_popcount(e.live);
         const uint32_t v[2] = {tail ? cnt : 0u, tail ? 0u : cnt};
@@ -631,6 +751,25 @@ hipError_t launch_expand(const SearchArgs &a, bool f64)
         hipLaunchKernelGGL(expand_kernel<double>, dim3(grid), dim3(256), 0, a.stream, a);
     else
         hipLaunchKernelGGL(expand_kernel<int32_t>, dim3(grid), dim3(256), 0, a.stream, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_suffix(const SearchArgs &a, bool f64, uint32_t sets)
+{
+    if (a.n > kSearchMaxN || !a.hsuf || (a.hs_len != 5 && a.hs_len != 6)) return hipErrorInvalidValue;
+    if (sets == 0) return hipSuccess;
+    const int grid = (int)std::min<uint32_t>((sets + 255u) / 256u, 4096u);
+    if (a.hs_len == 5) {
+        if (f64)
+            hipLaunchKernelGGL((suffix_kernel<double, 5>), dim3(grid), dim3(256), 0, a.stream, a, sets);
+        else
+            hipLaunchKernelGGL((suffix_kernel<int32_t, 5>), dim3(grid), dim3(256), 0, a.stream, a, sets);
+    } else {
+        if (f64)
+            hipLaunchKernelGGL((suffix_kernel<double, 6>), dim3(grid), dim3(256), 0, a.stream, a, sets);
+        else
+            hipLaunchKernelGGL((suffix_kernel<int32_t, 6>), dim3(grid), dim3(256), 0, a.stream, a, sets);
+    }
     return hipGetLastError();
 }
 

@@ -99,6 +99,21 @@ struct SearchArgs {
     PathItem *ftail;
     unsigned int *tail_count;  // items in ftail (tail_kernel reads it on the device)
     unsigned int tail_cap;
+    // stronger bounds of the frontier search (expand_kernel):
+    //  * bnd2 (sym != 0, symmetric matrices only): per city x the pair
+    //    {b[x], e[x]} = half the sum of its two cheapest incident edges and
+    //    half its cheapest one (2^-20 grid / integer, rounded down), so a path
+    //    from j over R to 0 costs at least e[j] + sum_R b + e[0];
+    //  * hsuf (hs_len > 0): the suffix table H[U][x] = cheapest path from x
+    //    over the inner-city set U to city 0, for |U| <= hs_len (f64, any
+    //    rounding: it is only compared with the incumbent's 2^-39 margin);
+    //    size hs_len only, at hs_off[hs_len] + colex_rank(U) * hs_len +
+    //    (place of x in U).
+    const void *bnd2;
+    int sym;
+    const double *hsuf;
+    int hs_len;
+    uint32_t hs_off[8];
     hipStream_t stream;
 };
 
@@ -119,5 +134,15 @@ hipError_t launch_to_paths(const SearchArgs &a);  // a.in (seeds) -> a.fout
 hipError_t launch_expand(const SearchArgs &a, bool f64);
 hipError_t launch_tail(const SearchArgs &a, bool f64, int grid);
 hipError_t launch_persist(const SearchArgs &a, bool f64, int grid);
+// suffix table (enum.hip): size a.hs_len of a.hsuf, one thread per set
+hipError_t launch_suffix(const SearchArgs &a, bool f64, uint32_t sets);
+// colex rank helpers shared by host and device: C(n, k) for n < 32, k <= 7
+__host__ __device__ constexpr uint32_t search_binom(int nn, int k)
+{
+    if (k < 0 || k > nn) return 0;
+    uint64_t r = 1;
+    for (int i = 1; i <= k; ++i) r = r * (uint64_t)(nn - k + i) / (uint64_t)i;
+    return (uint32_t)r;
+}
 
 }  // namespace tspgpu

@@ -85,6 +85,16 @@ struct tspgpu_search {
     // frontier is empty.
     int tail_len = 6;
     bool frontier = false;
+    // stronger frontier bounds (SearchArgs::bnd2 / ::hsuf): the two-edge bound
+    // for symmetric matrices and the suffix table for the last tail_len cities
+    int sym = 0;
+    void *d_bnd2 = nullptr;
+    double *d_hsuf = nullptr;
+    size_t hsuf_alloc = 0;      // bytes
+    int hs_len = 0;             // sizes 1..hs_len built (0: none)
+    uint32_t hs_off[8] = {};
+    bool use_suffix = true;     // TSPGPU_SEARCH_SUFFIX=0: B0/B1 only
+    bool use_two_edge = true;   // TSPGPU_SEARCH_TWO_EDGE=0: no B1
     PathItem *d_front[2] = {nullptr, nullptr};  // frontier (LIFO) / children of the current step
     size_t front_cap[2] = {0, 0};
     PathItem *d_tail = nullptr;
@@ -118,39 +128,103 @@ V fold_tour(const V *d, int n, const int32_t *t)
     return c + d[prev * n];
 }
 
-// Nearest neighbour + 2-opt (on the real-valued sum), then the exact fold in
-// the better of the two directions: a valid upper bound >= OPT.
+// Local search on a closed tour (cyclic, real-valued sums): 2-opt and Or-opt
+// (a segment of 1..3 cities moved elsewhere, either direction) until neither
+// improves.
 template <typename V>
-void heuristic(const V *d, int n, std::vector<int32_t> &best, V &cost)
+void local_search(const V *d, int n, std::vector<int> &t)
 {
-    std::vector<int> t(n);
-    std::vector<char> used(n, 0);
-    t[0] = 0;
-    used[0] = 1;
-    for (int i = 1; i < n; ++i) {
-        int b = -1;
-        for (int j = 1; j < n; ++j)
-            if (!used[j] && (b < 0 || d[t[i - 1] * n + j] < d[t[i - 1] * n + b])) b = j;
-        t[i] = b;
-        used[b] = 1;
-    }
-    for (bool improved = true; improved;) {
-        improved = false;
-        for (int i = 1; i < n - 1; ++i)
-            for (int j = i + 1; j < n; ++j) {
+    auto D = [&](int a, int b) { return (double)d[a * n + b]; };
+    auto len_of = [&](const std::vector<int> &u) {
+        double c = 0;
+        for (int i = 0; i < n; ++i) c += D(u[i], u[(i + 1) % n]);
+        return c;
+    };
+    // a move is kept only if the whole cyclic length drops by more than the
+    // tolerance (asymmetric matrices: the local deltas assume symmetry), and
+    // the number of moves is capped: the loop always ends
+    double cur = len_of(t);
+    auto accept = [&](std::vector<int> &cand) {
+        const double c = len_of(cand);
+        if (c < cur - 1e-9 * (1.0 + std::fabs(cur))) {
+            t.swap(cand);
+            cur = c;
+            return true;
+        }
+        return false;
+    };
+    for (int moves = 0, improved = 1; improved && moves < 64 * n; ++moves) {
+        improved = 0;
+        for (int i = 1; i < n - 1 && !improved; ++i)
+            for (int j = i + 1; j < n && !improved; ++j) {
                 const int a = t[i - 1], b = t[i], c = t[j], e = t[(j + 1) % n];
-                const double delta = ((double)d[a * n + c] + (double)d[b * n + e]) -
-                                     ((double)d[a * n + b] + (double)d[c * n + e]);
-                if (delta < -1e-9 * (1.0 + std::fabs((double)d[a * n + b]))) {
-                    std::reverse(t.begin() + i, t.begin() + j + 1);
-                    improved = true;
+                if ((D(a, c) + D(b, e)) - (D(a, b) + D(c, e)) < 0) {
+                    std::vector<int> cand(t);
+                    std::reverse(cand.begin() + i, cand.begin() + j + 1);
+                    improved = accept(cand);
+                }
+            }
+        for (int len = 1; len <= 3 && !improved && n > len + 2; ++len)
+            for (int i = 0; i < n && !improved; ++i) {
+                // segment t[i..i+len-1] (cyclic), between p = t[i-1] and q = t[i+len]
+                const int p = t[(i - 1 + n) % n], q = t[(i + len) % n];
+                const int s0 = t[i], s1 = t[(i + len - 1) % n];
+                const double gain = D(p, s0) + D(s1, q) - D(p, q);
+                for (int k = 0; k < n && !improved; ++k) {
+                    bool touch = false;  // edge (t[k], t[k+1]) must not touch the segment
+                    for (int z = -1; z < len; ++z)
+                        if ((i + z + n) % n == k) touch = true;
+                    if (touch) continue;
+                    const int u = t[k], v = t[(k + 1) % n];
+                    const double fwd = D(u, s0) + D(s1, v) - D(u, v);
+                    const double rev = D(u, s1) + D(s0, v) - D(u, v);
+                    const bool r = rev < fwd;
+                    if ((r ? rev : fwd) - gain >= 0) continue;
+                    std::vector<int> seg, cand;
+                    for (int z = 0; z < len; ++z) seg.push_back(t[(i + z) % n]);
+                    if (r) std::reverse(seg.begin(), seg.end());
+                    for (int z = 0; z < n - len; ++z) {
+                        const int c = t[(i + len + z) % n];
+                        cand.push_back(c);
+                        if (c == u) cand.insert(cand.end(), seg.begin(), seg.end());
+                    }
+                    improved = accept(cand);
                 }
             }
     }
-    std::vector<int32_t> fw(t.begin() + 1, t.end()), bw(fw.rbegin(), fw.rend());
-    const V cf = fold_tour(d, n, fw.data()), cb = fold_tour(d, n, bw.data());
-    best = cb < cf ? bw : fw;
-    cost = cb < cf ? cb : cf;
+}
+
+// Multi-start upper bound: a nearest-neighbour tour from every city, each
+// improved by 2-opt + Or-opt, rotated to start at city 0; the best exact fold
+// (tsp.cpp's cost, either direction) is a valid bound >= OPT.  A tight start
+// matters: every node the search prunes is pruned against it.
+template <typename V>
+void heuristic(const V *d, int n, std::vector<int32_t> &best, V &cost)
+{
+    bool have = false;
+    for (int s0 = 0; s0 < n; ++s0) {
+        std::vector<int> t(n);
+        std::vector<char> used(n, 0);
+        t[0] = s0;
+        used[s0] = 1;
+        for (int i = 1; i < n; ++i) {
+            int b = -1;
+            for (int j = 0; j < n; ++j)
+                if (!used[j] && (b < 0 || d[t[i - 1] * n + j] < d[t[i - 1] * n + b])) b = j;
+            t[i] = b;
+            used[b] = 1;
+        }
+        local_search(d, n, t);
+        std::rotate(t.begin(), std::find(t.begin(), t.end(), 0), t.end());
+        std::vector<int32_t> fw(t.begin() + 1, t.end()), bw(fw.rbegin(), fw.rend());
+        const V cf = fold_tour(d, n, fw.data()), cb = fold_tour(d, n, bw.data());
+        const V c = cb < cf ? cb : cf;
+        if (!have || c < cost) {
+            best = cb < cf ? bw : fw;
+            cost = c;
+            have = true;
+        }
+    }
 }
 
 template <typename V>
@@ -265,6 +339,9 @@ struct SearchPool {
     PathItem *d_tail = nullptr;
     unsigned int tail_alloc = 0;
     hipEvent_t e0 = nullptr, e1 = nullptr;
+    void *d_bnd2 = nullptr;
+    double *d_hsuf = nullptr;
+    size_t hsuf_alloc = 0;
 };
 
 template <typename A, typename B>
@@ -286,6 +363,9 @@ void move_buffers(A &to, B &from)
     to.tail_alloc = from.tail_alloc, from.tail_alloc = 0;
     to.e0 = from.e0, from.e0 = nullptr;
     to.e1 = from.e1, from.e1 = nullptr;
+    to.d_bnd2 = from.d_bnd2, from.d_bnd2 = nullptr;
+    to.d_hsuf = from.d_hsuf, from.d_hsuf = nullptr;
+    to.hsuf_alloc = from.hsuf_alloc, from.hsuf_alloc = 0;
 }
 
 template <typename A>
@@ -303,6 +383,8 @@ void free_buffers(A &b)
     if (b.d_tail) (void)hipFree(b.d_tail);
     if (b.e0) (void)hipEventDestroy(b.e0);
     if (b.e1) (void)hipEventDestroy(b.e1);
+    if (b.d_bnd2) (void)hipFree(b.d_bnd2);
+    if (b.d_hsuf) (void)hipFree(b.d_hsuf);
     SearchPool z;
     move_buffers(b, z);
 }
@@ -382,6 +464,8 @@ int tspgpu_search_create(tspgpu_ctx *c, const void *dist, int dtype, int n, int 
         const int v = std::atoi(e);
         s->tail_len = (v == 5 || v == 6) ? v : 0;
     }
+    if (const char *e = std::getenv("TSPGPU_SEARCH_SUFFIX")) s->use_suffix = std::atoi(e) != 0;
+    if (const char *e = std::getenv("TSPGPU_SEARCH_TWO_EDGE")) s->use_two_edge = std::atoi(e) != 0;
     if (const char *e = std::getenv("TSPGPU_SEARCH_TAIL_CAP_LOG2")) {  // tests: many flushes, small steps
         const int v = std::atoi(e);
         if (v >= 8 && v <= 26) s->tail_cap = 1u << v;
@@ -430,12 +514,47 @@ int tspgpu_search_create(tspgpu_ctx *c, const void *dist, int dtype, int n, int 
             ai[x] = m;
         }
     }
+    // two-edge bound (symmetric matrices): per city x, b[x] = half the sum of
+    // its two cheapest incident edges, e[x] = half its cheapest, rounded down
+    // to the bound's grid (f64: 2^-20, exact sums; i32: integers)
+    std::vector<double> bd(2 * n, 0.0);
+    std::vector<int32_t> bi(2 * n, 0);
+    {
+        bool sym = s->use_two_edge;
+        for (int i = 0; i < n && sym; ++i)
+            for (int j = 0; j < i && sym; ++j)
+                sym = f64 ? static_cast<const double *>(dist)[i * n + j] == static_cast<const double *>(dist)[j * n + i]
+                          : static_cast<const int32_t *>(dist)[i * n + j] == static_cast<const int32_t *>(dist)[j * n + i];
+        s->sym = sym ? 1 : 0;
+        for (int x = 0; x < n && sym; ++x) {
+            double m1 = INFINITY, m2 = INFINITY;
+            for (int y = 0; y < n; ++y) {
+                if (y == x) continue;
+                const double v = f64 ? static_cast<const double *>(dist)[x * n + y]
+                                     : (double)static_cast<const int32_t *>(dist)[x * n + y];
+                if (v < m1) {
+                    m2 = m1;
+                    m1 = v;
+                } else if (v < m2) {
+                    m2 = v;
+                }
+            }
+            if (f64) {
+                bd[2 * x] = std::ldexp(std::floor(std::ldexp((m1 + m2) * 0.5, 20)), -20);
+                bd[2 * x + 1] = std::ldexp(std::floor(std::ldexp(m1 * 0.5, 20)), -20);
+            } else {
+                bi[2 * x] = (int32_t)std::floor((m1 + m2) * 0.5);
+                bi[2 * x + 1] = (int32_t)std::floor(m1 * 0.5);
+            }
+        }
+    }
     s->rec_cap = 1u << 16;
     take_pool(s);  // device buffers of the context's previous search, if any
     hipStream_t st = c->stream;
     hipError_t e = hipSuccess;
     if (!s->d_dist) e = hipMalloc(&s->d_dist, sizeof(double) * kSearchMaxN * kSearchMaxN);
     if (e == hipSuccess && !s->d_amin) e = hipMalloc(&s->d_amin, sizeof(double) * kSearchMaxN);
+    if (e == hipSuccess && !s->d_bnd2) e = hipMalloc(&s->d_bnd2, sizeof(double) * 2 * kSearchMaxN);
     if (e == hipSuccess && !s->d_words) e = hipMalloc((void **)&s->d_words, kWords * sizeof(unsigned long long));
     if (e == hipSuccess && !s->d_stats) e = hipMalloc((void **)&s->d_stats, kStatBytes);
     if (e == hipSuccess && s->frontier && s->d_tail && s->tail_alloc != s->tail_cap) {
@@ -456,6 +575,9 @@ int tspgpu_search_create(tspgpu_ctx *c, const void *dist, int dtype, int n, int 
     if (e == hipSuccess) e = hipMemcpyAsync(s->d_dist, dist, vb * n * n, hipMemcpyHostToDevice, st);
     if (e == hipSuccess)
         e = hipMemcpyAsync(s->d_amin, f64 ? (const void *)ad.data() : (const void *)ai.data(), vb * n,
+                           hipMemcpyHostToDevice, st);
+    if (e == hipSuccess && s->sym)
+        e = hipMemcpyAsync(s->d_bnd2, f64 ? (const void *)bd.data() : (const void *)bi.data(), vb * 2 * n,
                            hipMemcpyHostToDevice, st);
     unsigned long long w[kWords] = {};
     if (f64) {
@@ -543,6 +665,11 @@ static SearchArgs args_of(tspgpu_search *s)
     }
     a.rec = s->d_rec;
     a.rec_cap = s->rec_cap;
+    a.bnd2 = s->d_bnd2;
+    a.sym = s->sym;
+    a.hsuf = s->d_hsuf;
+    a.hs_len = s->hs_len;
+    for (int i = 0; i < 8; ++i) a.hs_off[i] = s->hs_off[i];
     a.stream = s->ctx->stream;
     return a;
 }
@@ -617,6 +744,41 @@ static int launch_and_count(tspgpu_search *s, bool seed, int grid, SearchArgs &a
     return 0;
 }
 
+// The suffix table of the frontier search (sizes 1..tail_len, one launch
+// each, device time counted in the search's kernel time): built once per
+// search, when the bounded frontier search will use it.
+static int build_suffix(tspgpu_search *s)
+{
+    s->hs_len = 0;
+    if (!s->frontier || s->noprune || !s->use_suffix || s->tail_len < 1) return 0;
+    const int N = s->n - 1, L = s->tail_len;
+    for (int k = 0; k < 8; ++k) s->hs_off[k] = 0;  // one size stored: L, at offset 0
+    const uint32_t sets = search_binom(N, L), off = sets * (uint32_t)L;
+    const size_t bytes = (size_t)off * sizeof(double);
+    hipStream_t st = s->ctx->stream;
+    if (s->hsuf_alloc < bytes) {
+        if (s->d_hsuf) (void)hipFree(s->d_hsuf);
+        s->d_hsuf = nullptr;
+        s->hsuf_alloc = 0;
+        hipError_t e = hipMalloc((void **)&s->d_hsuf, bytes);
+        if (e != hipSuccess) return herr(e);
+        s->hsuf_alloc = bytes;
+    }
+    SearchArgs a = args_of(s);
+    a.hsuf = s->d_hsuf;
+    a.hs_len = L;
+    for (int i = 0; i < 8; ++i) a.hs_off[i] = s->hs_off[i];
+    (void)hipEventRecord(s->e0, st);
+    if (hipError_t e = launch_suffix(a, s->dtype == TSPGPU_F64, sets); e != hipSuccess) return herr(e);
+    (void)hipEventRecord(s->e1, st);
+    hipError_t e = hipStreamSynchronize(st);
+    if (e != hipSuccess) return herr(e);
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, s->e0, s->e1) == hipSuccess) s->ms += ms;
+    s->hs_len = L;
+    return 0;
+}
+
 int tspgpu_search_start(tspgpu_search *s)
 {
     if (!s) return -EINVAL;
@@ -631,6 +793,9 @@ int tspgpu_search_start(tspgpu_search *s)
         hipError_t e = hipMemsetAsync(s->d_words + 8, 0, 8, s->ctx->stream);
         if (e != hipSuccess) return herr(e);
     }
+    if (int rc = build_suffix(s)) return rc;
+    a = args_of(s);
+    a.out = s->d_items[0];
     const uint64_t blocks = (s->local_items + kSearchThreads - 1) / kSearchThreads;
     const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>(blocks, (uint64_t)s->ctx->cu_count * 8));
     int rc = launch_and_count(s, true, grid, a);
@@ -660,7 +825,9 @@ static int frontier_step(tspgpu_search *s, uint64_t *pending)
     if (s->pending == 0 || s->tails >= s->tail_cap / 2) {
         if (s->tails) {
             (void)hipEventRecord(s->e0, st);
-            e = launch_tail(a, f64, s->ctx->cu_count * 8);
+            // a wave folds 64 tails at a time: no more blocks than that needs
+            const uint64_t tb = (s->tails + 255) / 256;
+            e = launch_tail(a, f64, (int)std::max<uint64_t>(1, std::min<uint64_t>(tb, (uint64_t)s->ctx->cu_count * 8)));
             (void)hipEventRecord(s->e1, st);
             if (e == hipSuccess) e = hipMemsetAsync(s->d_words + 8, 0, 8, st);
             if (e == hipSuccess) e = hipStreamSynchronize(st);
