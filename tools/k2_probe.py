@@ -16,6 +16,8 @@ n = int(os.environ.get("K2_N", "16"))
 d = Shard(n, 1, 0, 1).distances()[0]
 ctx = tspgpu.Context(device=0)
 reps = int(sys.argv[1]) if len(sys.argv) > 1 else 3
+if len(sys.argv) > 2:  # seed depth (the library reads TSPGPU_SEARCH_DEPTH when a search starts)
+    os.environ["TSPGPU_SEARCH_DEPTH"] = sys.argv[2]
 for _ in range(reps):
     t = time.perf_counter()
     cost, tour, st = tspgpu.search_solve(ctx, d)

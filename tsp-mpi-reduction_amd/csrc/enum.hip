@@ -334,59 +334,70 @@ __device__ __forceinline__ void tail_one(const SearchArgs &a, const V *dl, const
     V best = bg[0];
 #pragma unroll
     for (int i = 1; i < TL; ++i) best = ENum<V>::vmin(best, bg[i]);
-    if (!(act && best <= inc)) return;
     // rare: record every tour within the incumbent (same fold, enumeration
-    // order), only in the first-city groups whose best is within it
+    // order), only in the first-city groups whose best is within it.  The
+    // lanes that have such groups are served one at a time by the whole wave,
+    // each lane folding every 64th of the group's (TL-1)! orders.
+    (void)best;
     constexpr int kGroup = TL == 6 ? 120 : 24;  // (TL-1)!
-#pragma unroll 1
-    for (int g = 0; g < TL; ++g) {
-        V bgg = bg[0];
+    uint32_t gm = 0;  // groups of this lane within the incumbent
 #pragma unroll
-        for (int i = 1; i < TL; ++i) bgg = g == i ? bg[i] : bgg;
-        if (!(bgg <= inc)) continue;
-#pragma unroll 1
-        for (int p = g * kGroup; p < (g + 1) * kGroup; ++p) {
-            uint32_t lst = 0;  // indices 0..TL-1 not used yet, one per nibble
+    for (int g = 0; g < TL; ++g) gm |= (act && bg[g] <= inc) ? (1u << g) : 0u;
+    for (unsigned long long owners = __ballot(gm != 0); owners; owners &= owners - 1ull) {
+        const int o = __ffsll((long long)owners) - 1;
+        const uint32_t ogm = (uint32_t)__shfl((int)gm, o);
+        const uint32_t otp = (uint32_t)__shfl((int)tpack, o);
+        const int oprev = __shfl(prev, o), olen = __shfl(len, o);
+        const uint32_t oidx = (uint32_t)__shfl((int)idx, o);
+        V ocp;
+        if constexpr (sizeof(V) == 8)
+            ocp = __longlong_as_double(__shfl((long long)__double_as_longlong(cp), o));
+        else
+            ocp = (V)__shfl((int)cp, o);
+        for (uint32_t gg = ogm; gg; gg &= gg - 1u) {
+            const int g = __builtin_ctz(gg);
+            for (int p = g * kGroup + __lane_id(); p < (g + 1) * kGroup; p += 64) {
+                uint32_t lst = 0;  // indices 0..TL-1 not used yet, one per nibble
 #pragma unroll
-            for (int i = 0; i < TL; ++i) lst |= (uint32_t)i << (4 * i);
-            int ord[TL];
-            int q = p;
+                for (int i = 0; i < TL; ++i) lst |= (uint32_t)i << (4 * i);
+                int ord[TL];
+                int q = p;
 #pragma unroll
-            for (int l = 0; l < TL; ++l) {
-                const int r = TL - l;
-                int fact = 1;  // (r-1)!: the l-th city is digit q / (r-1)! of the r left
-                for (int z = 2; z < r; ++z) fact *= z;
-                const int dgt = q / fact;
-                q -= dgt * fact;
-                const int sh = 4 * dgt;
-                const int ix = (int)((lst >> sh) & 15u);
-                lst = (lst & ((1u << sh) - 1u)) | ((lst >> (sh + 4)) << sh);
-                ord[l] = (int)((tpack >> (5 * ix)) & 31u);
-            }
-            V c = cp;
-            int k = prev;
+                for (int l = 0; l < TL; ++l) {
+                    const int r = TL - l;
+                    int fact = 1;  // (r-1)!: the l-th city is digit q / (r-1)! of the r left
+                    for (int z = 2; z < r; ++z) fact *= z;
+                    const int dgt = q / fact;
+                    q -= dgt * fact;
+                    const int sh = 4 * dgt;
+                    const int ix = (int)((lst >> sh) & 15u);
+                    lst = (lst & ((1u << sh) - 1u)) | ((lst >> (sh + 4)) << sh);
+                    ord[l] = (int)((otp >> (5 * ix)) & 31u);
+                }
+                V c = ocp;
+                int k = oprev;
 #pragma unroll
-            for (int l = 0; l < TL; ++l) {
-                c = c + dl[k * kTRow + ord[l]];
-                k = ord[l];
-            }
-            const V total = c + dl[k * kTRow];
-            if (total <= inc) {
-                const uint64_t tb = ENum<V>::bits(total);
-                const unsigned long long old = atomicMin(a.inc, (unsigned long long)tb);
-                if (tb <= old) {
-                    const unsigned int slot = atomicAdd(a.rec_count, 1u);
-                    if (slot < a.rec_cap) {
-                        SearchRecord *R = a.rec + slot;
-                        R->cost = tb;
-                        const uint8_t *pb = a.ftail[idx].b;
-                        for (int l = 1; l < len; ++l) R->city[l - 1] = pb[l];
+                for (int l = 0; l < TL; ++l) {
+                    c = c + dl[k * kTRow + ord[l]];
+                    k = ord[l];
+                }
+                const V total = c + dl[k * kTRow];
+                const V cur = ENum<V>::val(__hip_atomic_load(a.inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+                if (total <= cur) {
+                    const uint64_t tb = ENum<V>::bits(total);
+                    const unsigned long long old = atomicMin(a.inc, (unsigned long long)tb);
+                    if (tb <= old) {
+                        const unsigned int slot = atomicAdd(a.rec_count, 1u);
+                        if (slot < a.rec_cap) {
+                            SearchRecord *R = a.rec + slot;
+                            R->cost = tb;
+                            const uint8_t *pb = a.ftail[oidx].b;
+                            for (int l = 1; l < olen; ++l) R->city[l - 1] = pb[l];
 #pragma unroll
-                        for (int l = 0; l < TL; ++l) R->city[len - 1 + l] = (uint8_t)ord[l];
+                            for (int l = 0; l < TL; ++l) R->city[olen - 1 + l] = (uint8_t)ord[l];
+                        }
                     }
                 }
-                const V o = ENum<V>::val(old);
-                inc = o < total ? o : total;
             }
         }
     }
@@ -458,7 +469,7 @@ __global__ __launch_bounds__(256) void tail_kernel(SearchArgs a)
 // sum_i C(c_i, i + 1); bn[m][k] = C(m, k) in LDS.
 __device__ __forceinline__ void load_binom(uint32_t (*bn)[8])
 {
-    for (int i = threadIdx.x; i < 32 * 8; i += blockDim.x) bn[i >> 3][i & 7] = search_binom(i >> 3, i & 7);
+    stage_search_binom(bn, threadIdx.x, blockDim.x);
 }
 
 // Suffix table of size TL = a.hs_len, one thread per set U of TL inner cities
@@ -466,8 +477,108 @@ __device__ __forceinline__ void load_binom(uint32_t (*bn)[8])
 // to city 0, all (TL-1)! orders folded by the same straight-line code as the
 // register tails (`complete`) — a bound only, compared with the incumbent's
 // 2^-39 margin, so its rounding order does not matter.
+// ---------------------------------------------------------------------------
+// Seeds of the search (both modes) and the frontier prologue.
+constexpr double kSeedShrink = 1.0 - 0x1p-40;
+template <typename V>
+struct SeedNum;
+template <>
+struct SeedNum<double> {
+    using Wide = double;
+    __device__ static double val(uint64_t b) { return __longlong_as_double((long long)b); }
+    __device__ static bool pruned(double lb, double inc) { return lb * kSeedShrink > inc; }
+};
+template <>
+struct SeedNum<int32_t> {
+    using Wide = long long;
+    __device__ static int32_t val(uint64_t b) { return (int32_t)(uint32_t)b; }
+    __device__ static bool pruned(long long lb, int32_t inc) { return lb > (long long)inc; }
+};
+
+// Seed: every depth-D prefix of this shard that survives the bound becomes an item.
+template <typename V>
+__device__ __forceinline__ void seed_body(const SearchArgs &a, uint32_t block, uint32_t nblocks)
+{
+    using W = typename SeedNum<V>::Wide;
+    __shared__ uint32_t pv[33];
+    __shared__ V dl[kSearchMaxN * kSearchMaxN];
+    __shared__ V al[kSearchMaxN];
+    const int n = a.n, N = n - 1, D = a.depth;
+    const V *gd = static_cast<const V *>(a.dist);
+    const V *ga = static_cast<const V *>(a.amin);
+    for (int i = threadIdx.x; i < n * n; i += kSearchThreads) dl[i] = gd[i];
+    for (int i = threadIdx.x; i < n; i += kSearchThreads) al[i] = ga[i];
+    if (threadIdx.x == 0) {
+        uint32_t p = 1;
+        pv[D] = 1;
+        for (int l = D; l >= 2; --l) {
+            p *= (uint32_t)(N - l + 1);
+            pv[l - 1] = p;
+        }
+    }
+    __syncthreads();
+    const uint32_t full = (uint32_t)((1ull << n) - 1ull) & ~1u;
+    W aall = 0;
+    for (int x = 0; x < n; ++x) aall += (W)al[x];
+    const V inc = SeedNum<V>::val(__hip_atomic_load(a.inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    const uint32_t local = a.items / a.nshards + (a.items % a.nshards > a.shard ? 1u : 0u);
+    const int lane = __lane_id();
+    // the loop runs the same trip count on every lane of a wave (ballots inside)
+    const uint32_t stride = nblocks * kSearchThreads;
+    for (uint32_t i0 = block * kSearchThreads + (threadIdx.x & ~63u); i0 < local; i0 += stride) {
+        const uint32_t i = i0 + (uint32_t)lane;
+        uint32_t p = i * a.nshards + a.shard;
+        uint32_t rr = full;
+        W ra = aall;
+        V c = 0;
+        int prev = 0;
+        bool live = i < local;
+        uint32_t w[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // city bytes, statically indexed below
+        for (int l = 1; l <= D && live; ++l) {
+            const uint32_t q = p / pv[l];
+            p -= q * pv[l];
+            uint32_t x = rr;
+            for (uint32_t s = 0; s < q; ++s) x &= x - 1u;
+            const int t = __builtin_ctz(x);
+            c = c + dl[prev * n + t];
+            rr &= ~(1u << t);
+            ra -= (W)al[t];
+#pragma unroll
+            for (int b = 0; b < 8; ++b)
+                if ((l >> 2) == b) w[b] |= (uint32_t)t << (8 * (l & 3));
+            prev = t;
+            if (!a.noprune && SeedNum<V>::pruned((W)c + ra, inc)) live = false;
+        }
+        // one atomic per wave for its live prefixes
+        const unsigned long long lm = __ballot(live);
+        if (!lm) continue;
+        const int leader = __ffsll((long long)lm) - 1;
+        unsigned int base = 0;
+        if (lane == leader) base = atomicAdd(a.out_count, (unsigned int)__popcll(lm));
+        base = __shfl(base, leader);
+        if (!live) continue;
+        const uint32_t slot = base + __popcll(lm & ((1ull << lane) - 1ull));
+        if (a.fout) {  // frontier search: the prefix as a path (byte 0 = len), two dwordx4
+            uint4 *dp = reinterpret_cast<uint4 *>(a.fout + slot);
+            dp[0] = make_uint4(w[0] | (uint32_t)(D + 1), w[1], w[2], w[3]);
+            dp[1] = make_uint4(w[4], w[5], w[6], w[7]);
+            continue;
+        }
+        uint32_t *dst = reinterpret_cast<uint32_t *>(a.out + slot);
+#pragma unroll
+        for (int b = 0; b < 8; ++b) dst[b] = w[b];
+        dst[8] = (uint32_t)(D + 1) | (1u << 8);  // len, from = 1
+    }
+}
+
+template <typename V>
+__global__ __launch_bounds__(kSearchThreads) void seed_kernel(SearchArgs a)
+{
+    seed_body<V>(a, blockIdx.x, gridDim.x);
+}
+
 template <typename V, int TL>
-__global__ __launch_bounds__(256) void suffix_kernel(SearchArgs a, uint32_t sets)
+__device__ __forceinline__ void suffix_body(const SearchArgs &a, uint32_t sets, uint32_t block, uint32_t nblocks)
 {
     __shared__ uint32_t bn[32][8];
     __shared__ double dl[kSearchMaxN * kTRow];
@@ -477,7 +588,7 @@ __global__ __launch_bounds__(256) void suffix_kernel(SearchArgs a, uint32_t sets
     load_binom(bn);
     __syncthreads();
     double *H = const_cast<double *>(a.hsuf) + a.hs_off[TL];
-    for (uint32_t r0 = blockIdx.x * 256u + threadIdx.x; r0 < sets; r0 += gridDim.x * 256u) {
+    for (uint32_t r0 = block * 256u + threadIdx.x; r0 < sets; r0 += nblocks * 256u) {
         // unrank U (colex): the largest place c with C(c, i) <= r, i = TL .. 1
         int c[TL];
         uint32_t r = r0;
@@ -508,6 +619,23 @@ __global__ __launch_bounds__(256) void suffix_kernel(SearchArgs a, uint32_t sets
     }
 }
 
+template <typename V, int TL>
+__global__ __launch_bounds__(256) void suffix_kernel(SearchArgs a, uint32_t sets)
+{
+    suffix_body<V, TL>(a, sets, blockIdx.x, gridDim.x);
+}
+
+// Frontier prologue: the seeds (blocks [0, seed_blocks)) and the suffix table
+// (the other blocks) are independent — one launch runs both side by side.
+template <typename V, int TL>
+__global__ __launch_bounds__(256) void prologue_kernel(SearchArgs a, uint32_t sets, uint32_t seed_blocks)
+{
+    if (blockIdx.x < seed_blocks)
+        seed_body<V>(a, blockIdx.x, seed_blocks);
+    else
+        suffix_body<V, TL>(a, sets, blockIdx.x - seed_blocks, gridDim.x - seed_blocks);
+}
+
 template <typename V>
 struct Expand {
     uint32_t w[8];
@@ -517,12 +645,66 @@ struct Expand {
     double ub;        // the best completion a suffix test saw, as an upper bound on the optimum
 };
 
+// Children of a path with exactly TL + 1 cities left (the suffix level):
+// every bound of expand_eval, with the suffix test's (TL + 1) x TL table reads
+// and distance reads unrolled and independent of the tests, so they are all
+// in flight together instead of one child after another.  Returns the live
+// mask; ub = the smallest completion seen (an upper bound on the optimum).
+template <typename V, int TL>
+__device__ __forceinline__ uint32_t hlevel_live(const SearchArgs &a, const V *dl, const V *am, const V *b2,
+                                                const uint32_t (*bn)[8], V c, int k, uint32_t rem, V remA, V remB,
+                                                V thr, double &ub)
+{
+    int m[TL + 1];
+    uint32_t x = rem;
+#pragma unroll
+    for (int i = 0; i <= TL; ++i) {
+        m[i] = __builtin_ctz(x | 0x80000000u);
+        x &= x - 1u;
+    }
+    // rank(rem \ m[i]) = sum_{q<i} C(m[q]-1, q+1) + sum_{q>i} C(m[q]-1, q)
+    uint32_t up[TL + 1], dn[TL + 1];
+#pragma unroll
+    for (int q = 0; q <= TL; ++q) {
+        up[q] = bn[m[q] - 1][q + 1];
+        dn[q] = bn[m[q] - 1][q];
+    }
+    const double *H0 = a.hsuf + a.hs_off[TL];
+    const double dthr = (double)thr;
+    uint32_t live = 0;
+#pragma unroll
+    for (int i = 0; i <= TL; ++i) {
+        uint32_t rk = 0;
+#pragma unroll
+        for (int q = 0; q <= TL; ++q) rk += q < i ? up[q] : (q > i ? dn[q] : 0u);
+        const double *Hs = H0 + (size_t)rk * TL;
+        const int j = m[i];
+        const V cj = c + dl[k * kTRow + j];
+        double best = 1.0e300;
+#pragma unroll
+        for (int r = 0; r <= TL; ++r) {
+            if (r == i) continue;
+            const double v = (double)dl[j * kTRow + m[r]] + Hs[r < i ? r : r - 1];
+            best = v < best ? v : best;
+        }
+        bool ok = !(cj + (remA - am[j]) > thr);
+        if (a.sym) ok = ok && !(cj + (((remB - b2[2 * j]) + b2[2 * j + 1]) + b2[1]) > thr);
+        ok = ok && !((double)cj + best > dthr);
+        if (ok) {
+            live |= 1u << j;
+            const double u = ((double)cj + best) * (1.0 + 0x1p-30);
+            ub = u < ub ? u : ub;
+        }
+    }
+    return live;
+}
+
 // The bound of child j of path (c, k, rem) (rem includes j), any of:
 //   B0: every city still to be entered pays its cheapest incoming edge;
 //   B1 (symmetric matrices): e[j] + sum over rem \ j of b + e[0];
 //   H  (the child has a.hs_len cities left): min over x in rem \ j of
 //       d[j][x] + H[rem \ j][x], the exact cheapest completion up to rounding.
-template <typename V>
+template <typename V, int TL>
 __device__ __forceinline__ Expand<V> expand_eval(const SearchArgs &a, const V *dl, const V *am, const V *b2,
                                                  const uint32_t (*bn)[8], uint32_t full, uint32_t idx, uint32_t end,
                                                  V thr)
@@ -543,41 +725,26 @@ __device__ __forceinline__ Expand<V> expand_eval(const SearchArgs &a, const V *d
         remA += am[t];
         if (a.sym) remB += b2[2 * t];
     }
-    const bool htest = a.hs_len > 0 && a.hs_len == a.tail_len && e.len == a.tail_level && !a.noprune;
-    const double dthr = (double)thr;
+    const bool htest = a.hs_len == TL && a.tail_len == TL && e.len == a.tail_level && !a.noprune;
     e.live = 0;
     e.hnodes = 0;
     e.ub = 1.0e300;
+    if (htest) {  // wave-divergent only when a tile mixes levels
+        e.live = act ? hlevel_live<V, TL>(a, dl, am, b2, bn, c, k, e.rem, remA, remB, thr, e.ub) : 0u;
+        e.hnodes = act ? (uint32_t)((TL + 1) * TL) : 0u;
+        return e;
+    }
     for (uint32_t x = e.rem; x; x &= x - 1u) {
         const int j = __builtin_ctz(x);
         const V cj = c + dl[k * kTRow + j];
         bool ok = a.noprune || !(cj + (remA - am[j]) > thr);
         if (ok && a.sym && !a.noprune) ok = !(cj + (((remB - b2[2 * j]) + b2[2 * j + 1]) + b2[1]) > thr);
-        if (ok && htest) {
-            // the child's completion: rank of R = rem \ j, then min over its cities
-            const uint32_t R = e.rem & ~(1u << j);
-            uint32_t rk = 0;
-            int i = 0;
-            for (uint32_t y = R; y; y &= y - 1u) rk += bn[__builtin_ctz(y) - 1][++i];
-            const double *Hs = a.hsuf + a.hs_off[a.hs_len] + (size_t)rk * (uint32_t)a.hs_len;
-            double best = 1.0e300;
-            i = 0;
-            for (uint32_t y = R; y; y &= y - 1u) {
-                const double v = (double)dl[j * kTRow + __builtin_ctz(y)] + Hs[i++];
-                best = v < best ? v : best;
-            }
-            e.hnodes += (uint32_t)a.hs_len;
-            ok = !((double)cj + best > dthr);
-            // cj + best is the cost of a real tour up to a few roundings
-            // (< 2^-47 relative): scaled up by 2^-30 it bounds the optimum
-            // from above, and the search may prune against it at once
-            const double u = ((double)cj + best) * (1.0 + 0x1p-30);
-            e.ub = u < e.ub ? u : e.ub;
-        }
         if (ok) e.live |= 1u << j;
     }
     return e;
 }
+
+constexpr int kExpandTiles = 4;  // tiles of 256 paths per expand_kernel block (a.fin_per_block <= 1024)
 
 // One atomicMin per wave with the smallest suffix-test upper bound (f64
 // incumbents only: the integer search's incumbent stays a tour cost).
@@ -595,7 +762,7 @@ __device__ __forceinline__ void publish_ub(const SearchArgs &a, double ub)
     }
 }
 
-template <typename V>
+template <typename V, int TL>
 __global__ __launch_bounds__(256) void expand_kernel(SearchArgs a)
 {
     __shared__ V dl[kSearchMaxN * kTRow];
@@ -620,11 +787,19 @@ __global__ __launch_bounds__(256) void expand_kernel(SearchArgs a)
     const uint32_t b1 = b0 + a.fin_per_block < a.fin_count ? b0 + a.fin_per_block : a.fin_count;
     const int lane = __lane_id(), wv = threadIdx.x >> 6;
 
-    // ---- pass 1: this block's live children per output, nodes evaluated
+    // ---- pass 1: this block's live children per output, nodes evaluated; the
+    // live masks stay in registers for pass 2 (at most kExpandTiles tiles of
+    // 256 paths per block: the bounds are evaluated once)
     uint32_t cT = 0, cF = 0;
     unsigned long long nodes = 0;
-    for (uint32_t base = b0; base < b1; base += 256u) {
-        const Expand<V> e = expand_eval<V>(a, dl, am, b2, bn, full, base + threadIdx.x, b1, thr);
+    uint32_t lv[kExpandTiles];
+#pragma unroll
+    for (int t = 0; t < kExpandTiles; ++t) {
+        const uint32_t base = b0 + 256u * t;
+        lv[t] = 0;
+        if (base >= b1) continue;
+        const Expand<V> e = expand_eval<V, TL>(a, dl, am, b2, bn, full, base + threadIdx.x, b1, thr);
+        lv[t] = e.live;
         const uint32_t cnt = (uint32_t)__builtin_popcount(e.live);
         if (e.len == a.tail_level) cT += cnt; else cF += cnt;  // children have len inner cities
         nodes += (unsigned long long)__builtin_popcount(e.rem) + e.hnodes;
@@ -652,8 +827,15 @@ __global__ __launch_bounds__(256) void expand_kernel(SearchArgs a)
     uint32_t run[2] = {bbase[0], bbase[1]};
 
     // ---- pass 2: the children, at block-scanned offsets
-    for (uint32_t base = b0; base < b1; base += 256u) {
-        const Expand<V> e = expand_eval<V>(a, dl, am, b2, bn, full, base + threadIdx.x, b1, thr);
+#pragma unroll
+    for (int t = 0; t < kExpandTiles; ++t) {
+        const uint32_t base = b0 + 256u * t;
+        if (base >= b1) break;  // block-uniform
+        Expand<V> e;
+        const bool act = base + threadIdx.x < b1;
+        load_path(a.fin + base + threadIdx.x, act, e.w);
+        e.len = act ? (int)(e.w[0] & 255u) : 0;
+        e.live = lv[t];
         const bool tail = e.len == a.tail_level;
         const uint32_t cnt = (uint32_t)__builtin_popcount(e.live);
         const uint32_t v[2] = {tail ? cnt : 0u, tail ? 0u : cnt};
@@ -745,12 +927,44 @@ hipError_t launch_to_paths(const SearchArgs &a)
 hipError_t launch_expand(const SearchArgs &a, bool f64)
 {
     if (a.n > kSearchMaxN || a.fin_count == 0) return a.fin_count ? hipErrorInvalidValue : hipSuccess;
-    if (a.fin_per_block == 0 || a.fin_per_block % 256u) return hipErrorInvalidValue;
+    if (a.fin_per_block == 0 || a.fin_per_block % 256u || a.fin_per_block > 256u * kExpandTiles)
+        return hipErrorInvalidValue;
     const int grid = (int)((a.fin_count + a.fin_per_block - 1u) / a.fin_per_block);
+    if (a.tail_len == 5) {
+        if (f64)
+            hipLaunchKernelGGL((expand_kernel<double, 5>), dim3(grid), dim3(256), 0, a.stream, a);
+        else
+            hipLaunchKernelGGL((expand_kernel<int32_t, 5>), dim3(grid), dim3(256), 0, a.stream, a);
+    } else {
+        if (f64)
+            hipLaunchKernelGGL((expand_kernel<double, 6>), dim3(grid), dim3(256), 0, a.stream, a);
+        else
+            hipLaunchKernelGGL((expand_kernel<int32_t, 6>), dim3(grid), dim3(256), 0, a.stream, a);
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_seed(const SearchArgs &a, bool f64, int grid)
+{
     if (f64)
-        hipLaunchKernelGGL(expand_kernel<double>, dim3(grid), dim3(256), 0, a.stream, a);
+        hipLaunchKernelGGL(seed_kernel<double>, dim3(grid), dim3(kSearchThreads), 0, a.stream, a);
     else
-        hipLaunchKernelGGL(expand_kernel<int32_t>, dim3(grid), dim3(256), 0, a.stream, a);
+        hipLaunchKernelGGL(seed_kernel<int32_t>, dim3(grid), dim3(kSearchThreads), 0, a.stream, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_prologue(const SearchArgs &a, bool f64, int seed_grid, uint32_t sets)
+{
+    if (a.n > kSearchMaxN || !a.hsuf || (a.hs_len != 5 && a.hs_len != 6)) return hipErrorInvalidValue;
+    const int grid = seed_grid + (int)std::min<uint32_t>((sets + 255u) / 256u, 4096u);
+    const uint32_t sb = (uint32_t)seed_grid;
+#define TSPGPU_PRO(VT, TLV) hipLaunchKernelGGL((prologue_kernel<VT, TLV>), dim3(grid), dim3(256), 0, a.stream, a, sets, sb)
+    if (a.hs_len == 5) {
+        if (f64) TSPGPU_PRO(double, 5); else TSPGPU_PRO(int32_t, 5);
+    } else {
+        if (f64) TSPGPU_PRO(double, 6); else TSPGPU_PRO(int32_t, 6);
+    }
+#undef TSPGPU_PRO
     return hipGetLastError();
 }
 

@@ -136,6 +136,8 @@ hipError_t launch_tail(const SearchArgs &a, bool f64, int grid);
 hipError_t launch_persist(const SearchArgs &a, bool f64, int grid);
 // suffix table (enum.hip): size a.hs_len of a.hsuf, one thread per set
 hipError_t launch_suffix(const SearchArgs &a, bool f64, uint32_t sets);
+// seeds (seed_grid blocks) and the suffix table in one launch (enum.hip)
+hipError_t launch_prologue(const SearchArgs &a, bool f64, int seed_grid, uint32_t sets);
 // colex rank helpers shared by host and device: C(n, k) for n < 32, k <= 7
 __host__ __device__ constexpr uint32_t search_binom(int nn, int k)
 {
@@ -143,6 +145,23 @@ __host__ __device__ constexpr uint32_t search_binom(int nn, int k)
     uint64_t r = 1;
     for (int i = 1; i <= k; ++i) r = r * (uint64_t)(nn - k + i) / (uint64_t)i;
     return (uint32_t)r;
+}
+// the same values as a compile-time table (kernels stage it into LDS: no
+// 64-bit divisions on the device)
+struct SearchBinom {
+    uint32_t v[32][8];
+};
+constexpr SearchBinom make_search_binom()
+{
+    SearchBinom t{};
+    for (int i = 0; i < 32; ++i)
+        for (int k = 0; k < 8; ++k) t.v[i][k] = search_binom(i, k);
+    return t;
+}
+__device__ __forceinline__ void stage_search_binom(uint32_t (*bn)[8], int tid, int nthreads)
+{
+    constexpr SearchBinom kT = make_search_binom();
+    for (int i = tid; i < 32 * 8; i += nthreads) bn[i >> 3][i & 7] = kT.v[i >> 3][i & 7];
 }
 
 }  // namespace tspgpu

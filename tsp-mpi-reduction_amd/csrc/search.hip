@@ -76,75 +76,6 @@ __host__ __device__ constexpr size_t lds_bytes(int n)
     return stack_end<V>(n) + (size_t)(kSearchThreads / 64) * kChunk * sizeof(SearchItem);
 }
 
-// Seed: every depth-D prefix of this shard that survives the bound becomes an item.
-template <typename V>
-__global__ __launch_bounds__(kSearchThreads) void seed_kernel(SearchArgs a)
-{
-    using W = typename Num<V>::Wide;
-    __shared__ uint32_t pv[33];
-    __shared__ V dl[kSearchMaxN * kSearchMaxN];
-    __shared__ V al[kSearchMaxN];
-    const int n = a.n, N = n - 1, D = a.depth;
-    const V *gd = static_cast<const V *>(a.dist);
-    const V *ga = static_cast<const V *>(a.amin);
-    for (int i = threadIdx.x; i < n * n; i += kSearchThreads) dl[i] = gd[i];
-    for (int i = threadIdx.x; i < n; i += kSearchThreads) al[i] = ga[i];
-    if (threadIdx.x == 0) {
-        uint32_t p = 1;
-        pv[D] = 1;
-        for (int l = D; l >= 2; --l) {
-            p *= (uint32_t)(N - l + 1);
-            pv[l - 1] = p;
-        }
-    }
-    __syncthreads();
-    const uint32_t full = (uint32_t)((1ull << n) - 1ull) & ~1u;
-    W aall = 0;
-    for (int x = 0; x < n; ++x) aall += (W)al[x];
-    const V inc = Num<V>::val(__hip_atomic_load(a.inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-    const uint32_t local = a.items / a.nshards + (a.items % a.nshards > a.shard ? 1u : 0u);
-    const int lane = __lane_id();
-    // the loop runs the same trip count on every lane of a wave (ballots inside)
-    const uint32_t stride = gridDim.x * kSearchThreads;
-    for (uint32_t i0 = blockIdx.x * kSearchThreads + (threadIdx.x & ~63u); i0 < local; i0 += stride) {
-        const uint32_t i = i0 + (uint32_t)lane;
-        uint32_t p = i * a.nshards + a.shard;
-        uint32_t rr = full;
-        W ra = aall;
-        V c = 0;
-        int prev = 0;
-        bool live = i < local;
-        uint32_t w[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // city bytes, statically indexed below
-        for (int l = 1; l <= D && live; ++l) {
-            const uint32_t q = p / pv[l];
-            p -= q * pv[l];
-            uint32_t x = rr;
-            for (uint32_t s = 0; s < q; ++s) x &= x - 1u;
-            const int t = __builtin_ctz(x);
-            c = c + dl[prev * n + t];
-            rr &= ~(1u << t);
-            ra -= (W)al[t];
-#pragma unroll
-            for (int b = 0; b < 8; ++b)
-                if ((l >> 2) == b) w[b] |= (uint32_t)t << (8 * (l & 3));
-            prev = t;
-            if (!a.noprune && Num<V>::pruned((W)c + ra, inc)) live = false;
-        }
-        // one atomic per wave for its live prefixes
-        const unsigned long long lm = __ballot(live);
-        if (!lm) continue;
-        const int leader = __ffsll((long long)lm) - 1;
-        unsigned int base = 0;
-        if (lane == leader) base = atomicAdd(a.out_count, (unsigned int)__popcll(lm));
-        base = __shfl(base, leader);
-        if (!live) continue;
-        uint32_t *dst = reinterpret_cast<uint32_t *>(a.out + base + __popcll(lm & ((1ull << lane) - 1ull)));
-#pragma unroll
-        for (int b = 0; b < 8; ++b) dst[b] = w[b];
-        dst[8] = (uint32_t)(D + 1) | (1u << 8);  // len, from = 1
-    }
-}
-
 // One round over the items a.in[0 .. in_count) (v1: one DFS iteration per
 // loop trip with a branch per case; kept for A/B measurements).
 template <typename V>
@@ -525,16 +456,23 @@ __global__ __launch_bounds__(kSearchThreads) void round_kernel(SearchArgs a)
     uint8_t *myk = reinterpret_cast<uint8_t *>(smem + v2_city<V>(n)) + tid;  // city of level l: myk[l*T]
     const V *gd = static_cast<const V *>(a.dist);
     const V *ga = static_cast<const V *>(a.amin);
+    // the frontier search's stronger bounds (SearchArgs::bnd2, ::hsuf), when given
+    __shared__ V b2s[2 * kSearchMaxN];
+    __shared__ uint32_t bn[32][8];
     for (int i = tid; i < n * n; i += T) dl[(i / n) * kRow + i % n] = gd[i];
     for (int i = tid; i < n; i += T) {
         ad[i].a = ga[i];
         ad[i].d0 = gd[i * n];
     }
+    const bool sym = a.sym && !a.noprune, hsuf = a.hs_len > 0 && !a.noprune;
+    for (int i = tid; i < 2 * n; i += T) b2s[i] = sym ? static_cast<const V *>(a.bnd2)[i] : V(0);
+    stage_search_binom(bn, tid, T);
     __syncthreads();
 
     const uint32_t full = (uint32_t)((1ull << n) - 1ull) & ~1u;  // cities 1..N
-    V aall = 0;
+    V aall = 0, ball = 0;
     for (int x = 0; x < n; ++x) aall += ad[x].a;                 // exact: grid values
+    for (int x = 1; x < n; ++x) ball += b2s[2 * x];             // exact: grid values
     V inc = Num<V>::val(__hip_atomic_load(a.inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
     V thr = Thr<V>::of(inc);
     unsigned long long nodes = 0;  // wave-uniform counts
@@ -542,7 +480,7 @@ __global__ __launch_bounds__(kSearchThreads) void round_kernel(SearchArgs a)
     int L = -1, root = 1;          // L < root: the lane needs an item
     int k = 0, krow = 0;           // path end and its row offset in d
     uint32_t rem = 0, fm = 0, t0 = 0;
-    V ck = 0, remA = 0;
+    V ck = 0, remA = 0, remB = 0;  // remB: sum of b over rem (two-edge bound)
     bool done = false;
     uint32_t tick = 0;
     const int lane = __lane_id();
@@ -553,7 +491,7 @@ __global__ __launch_bounds__(kSearchThreads) void round_kernel(SearchArgs a)
     auto load_item = [&](const SearchItem &it) {
         const int len = it.len;
         uint32_t rr = full;
-        V ra = aall, c = 0;
+        V ra = aall, rb = ball, c = 0;
         int prev = 0;
         myk[0] = 0;
         myc[0] = 0;
@@ -562,6 +500,7 @@ __global__ __launch_bounds__(kSearchThreads) void round_kernel(SearchArgs a)
             c = c + dl[prev * kRow + t];
             rr &= ~(1u << t);
             ra -= ad[t].a;
+            rb -= b2s[2 * t];
             myk[l * T] = (uint8_t)t;
             myc[l * T] = c;
             prev = t;
@@ -574,6 +513,7 @@ __global__ __launch_bounds__(kSearchThreads) void round_kernel(SearchArgs a)
             ck = c;
             rem = rr;
             remA = ra;
+            remB = rb;
             fm = 0xFFFFFFFEu << (it.from - 1);
             t0 = tick;
         }
@@ -630,13 +570,41 @@ __global__ __launch_bounds__(kSearchThreads) void round_kernel(SearchArgs a)
             inc = o < total ? o : total;
             thr = Thr<V>::of(inc);
         }
-        const bool desc = has && !close && (a.noprune || !(c + rest > thr));
+        bool desc = has && !close && (a.noprune || !(c + rest > thr));
+        // two-edge bound: e[j] + sum over rem \ j of b + e[0] (exact grid sums)
+        const V bj = b2s[2 * j], bk = b2s[2 * k];
+        if (sym) desc = desc && !(c + (((remB - bj) + b2s[2 * j + 1]) + b2s[1]) > thr);
+        // exact-suffix bound when j leaves hs_len cities: the cheapest completion
+        if (hsuf && desc && __builtin_popcount(rem) == a.hs_len + 1) {
+            const uint32_t R = rem & ~(1u << j);
+            uint32_t rk = 0;
+            int i = 0;
+            for (uint32_t y = R; y; y &= y - 1u) rk += bn[__builtin_ctz(y) - 1][++i];
+            const double *Hs = a.hsuf + a.hs_off[a.hs_len] + (size_t)rk * (uint32_t)a.hs_len;
+            double best = 1.0e300;
+            i = 0;
+            for (uint32_t y = R; y; y &= y - 1u) {
+                const double v = (double)dl[j * kRow + __builtin_ctz(y)] + Hs[i++];
+                best = v < best ? v : best;
+            }
+            desc = !((double)c + best > (double)thr);
+            if constexpr (sizeof(V) == 8) {
+                // a real tour's cost up to a few roundings: scaled up, an upper bound on the optimum
+                const double u = ((double)c + best) * (1.0 + 0x1p-30);
+                if (desc && u < (double)inc) {
+                    atomicMin(a.inc, (unsigned long long)__double_as_longlong(u));
+                    inc = (V)u;
+                    thr = Thr<V>::of(inc);
+                }
+            }
+        }
         const bool pop = act && !has;
         myc[(L + 1) * T] = c;  // dead unless desc (L + 1 <= n - 2)
         myk[(L + 1) * T] = (uint8_t)j;
         rem = (rem & ~(desc ? (1u << j) : 0u)) | (pop ? (1u << k) : 0u);
         fm = desc ? 0xFFFFFFFEu : (0xFFFFFFFEu << (has ? j : k));
         remA = desc ? rest : (pop ? remA + ak : remA);
+        remB = desc ? remB - bj : (pop ? remB + bk : remB);
         ck = desc ? c : (pop ? cprev : ck);
         k = desc ? j : (pop ? kprev : k);
         krow = k * kRow;
@@ -1148,15 +1116,6 @@ hipError_t launch_persist(const SearchArgs &a, bool f64, int grid)
         if (e != hipSuccess) return e;
     }
     hipLaunchKernelGGL(fn, dim3(grid), dim3(kSearchThreads), lds, a.stream, a);
-    return hipGetLastError();
-}
-
-hipError_t launch_seed(const SearchArgs &a, bool f64, int grid)
-{
-    if (f64)
-        hipLaunchKernelGGL(seed_kernel<double>, dim3(grid), dim3(kSearchThreads), 0, a.stream, a);
-    else
-        hipLaunchKernelGGL(seed_kernel<int32_t>, dim3(grid), dim3(kSearchThreads), 0, a.stream, a);
     return hipGetLastError();
 }
 

@@ -93,7 +93,7 @@ struct tspgpu_search {
     size_t hsuf_alloc = 0;      // bytes
     int hs_len = 0;             // sizes 1..hs_len built (0: none)
     uint32_t hs_off[8] = {};
-    bool use_suffix = true;     // TSPGPU_SEARCH_SUFFIX=0: B0/B1 only
+    int suffix_len = 6;         // TSPGPU_SEARCH_SUFFIX=0/5/6: table size (0: B0/B1 only)
     bool use_two_edge = true;   // TSPGPU_SEARCH_TWO_EDGE=0: no B1
     PathItem *d_front[2] = {nullptr, nullptr};  // frontier (LIFO) / children of the current step
     size_t front_cap[2] = {0, 0};
@@ -464,7 +464,10 @@ int tspgpu_search_create(tspgpu_ctx *c, const void *dist, int dtype, int n, int 
         const int v = std::atoi(e);
         s->tail_len = (v == 5 || v == 6) ? v : 0;
     }
-    if (const char *e = std::getenv("TSPGPU_SEARCH_SUFFIX")) s->use_suffix = std::atoi(e) != 0;
+    if (const char *e = std::getenv("TSPGPU_SEARCH_SUFFIX")) {
+        const int v = std::atoi(e);
+        s->suffix_len = (v == 5 || v == 6) ? v : 0;
+    }
     if (const char *e = std::getenv("TSPGPU_SEARCH_TWO_EDGE")) s->use_two_edge = std::atoi(e) != 0;
     if (const char *e = std::getenv("TSPGPU_SEARCH_TAIL_CAP_LOG2")) {  // tests: many flushes, small steps
         const int v = std::atoi(e);
@@ -477,6 +480,7 @@ int tspgpu_search_create(tspgpu_ctx *c, const void *dist, int dtype, int n, int 
     // whole grid (the rounds split whatever is still too coarse), at most
     // N-1, at least 1, and < 2^31 prefixes
     const uint64_t lanes = (uint64_t)s->grid * kSearchThreads * (uint64_t)nshards;
+    const bool auto_depth = depth <= 0;
     if (depth <= 0) {
         depth = 1;
         while (depth < N - 1 && falling(N, depth + 1) < (1ull << 31) && falling(N, depth) < lanes) ++depth;
@@ -487,8 +491,17 @@ int tspgpu_search_create(tspgpu_ctx *c, const void *dist, int dtype, int n, int 
         const long v = std::atol(e);
         if (v > 0) s->budget = (uint32_t)v;
     }
-    s->depth = depth;
     s->frontier = s->tail_len && s->kernel == 2 && N - s->tail_len > depth;
+    // the frontier search expands level by level with its own bounds: a
+    // smaller seed set (~64 prefixes per CU) costs less than the round
+    // kernels' one-per-lane (measured at n = 16: depth 4 vs 5, 0.14 vs 0.16 ms)
+    if (s->frontier && auto_depth) {
+        const uint64_t want = (uint64_t)c->cu_count * 64 * nshards;
+        int d = 1;
+        while (d < depth && falling(N, d) < want) ++d;
+        depth = d;
+    }
+    s->depth = depth;
     s->items = falling(N, depth);
     s->local_items = s->items / nshards + (s->items % nshards > (uint64_t)shard ? 1 : 0);
     const size_t vb = f64 ? sizeof(double) : sizeof(int32_t);
@@ -724,14 +737,17 @@ static int ensure_front(tspgpu_search *s, int which, size_t count, size_t keep)
 }
 
 // launch + wait + read the item count the launch produced
-static int launch_and_count(tspgpu_search *s, bool seed, int grid, SearchArgs &a)
+static int launch_and_count(tspgpu_search *s, bool seed, int grid, SearchArgs &a, uint32_t suffix_sets = 0)
 {
     hipStream_t st = s->ctx->stream;
     hipError_t e = hipMemsetAsync(s->d_words, 0, 8, st);  // queue
     if (e == hipSuccess) e = hipMemsetAsync(s->d_words + 4, 0, 8, st);  // items out
     if (e != hipSuccess) return herr(e);
     (void)hipEventRecord(s->e0, st);
-    e = seed ? launch_seed(a, s->dtype == TSPGPU_F64, grid) : launch_round(a, s->dtype == TSPGPU_F64, grid);
+    if (seed && suffix_sets)  // the frontier's seeds and its suffix table, side by side in one launch
+        e = launch_prologue(a, s->dtype == TSPGPU_F64, grid, suffix_sets);
+    else
+        e = seed ? launch_seed(a, s->dtype == TSPGPU_F64, grid) : launch_round(a, s->dtype == TSPGPU_F64, grid);
     (void)hipEventRecord(s->e1, st);
     if (e != hipSuccess) return herr(e);
     unsigned long long out = 0;
@@ -747,11 +763,14 @@ static int launch_and_count(tspgpu_search *s, bool seed, int grid, SearchArgs &a
 // The suffix table of the frontier search (sizes 1..tail_len, one launch
 // each, device time counted in the search's kernel time): built once per
 // search, when the bounded frontier search will use it.
-static int build_suffix(tspgpu_search *s)
+static int build_suffix(tspgpu_search *s, bool launch, uint32_t *sets_out)
 {
     s->hs_len = 0;
-    if (!s->frontier || s->noprune || !s->use_suffix || s->tail_len < 1) return 0;
-    const int N = s->n - 1, L = s->tail_len;
+    *sets_out = 0;
+    // the frontier's expansion tests children with tail_len cities left: the
+    // table has that size there; the lock-step DFS tests at suffix_len
+    const int N = s->n - 1, L = s->frontier ? s->tail_len : s->suffix_len;
+    if (s->noprune || s->suffix_len == 0 || L < 1 || N < L + 2 || s->kernel == 1 || s->kernel == 3) return 0;
     for (int k = 0; k < 8; ++k) s->hs_off[k] = 0;  // one size stored: L, at offset 0
     const uint32_t sets = search_binom(N, L), off = sets * (uint32_t)L;
     const size_t bytes = (size_t)off * sizeof(double);
@@ -764,10 +783,10 @@ static int build_suffix(tspgpu_search *s)
         if (e != hipSuccess) return herr(e);
         s->hsuf_alloc = bytes;
     }
+    s->hs_len = L;
+    *sets_out = sets;
+    if (!launch) return 0;  // the caller launches it (with the seeds)
     SearchArgs a = args_of(s);
-    a.hsuf = s->d_hsuf;
-    a.hs_len = L;
-    for (int i = 0; i < 8; ++i) a.hs_off[i] = s->hs_off[i];
     (void)hipEventRecord(s->e0, st);
     if (hipError_t e = launch_suffix(a, s->dtype == TSPGPU_F64, sets); e != hipSuccess) return herr(e);
     (void)hipEventRecord(s->e1, st);
@@ -775,7 +794,6 @@ static int build_suffix(tspgpu_search *s)
     if (e != hipSuccess) return herr(e);
     float ms = 0.f;
     if (hipEventElapsedTime(&ms, s->e0, s->e1) == hipSuccess) s->ms += ms;
-    s->hs_len = L;
     return 0;
 }
 
@@ -793,22 +811,17 @@ int tspgpu_search_start(tspgpu_search *s)
         hipError_t e = hipMemsetAsync(s->d_words + 8, 0, 8, s->ctx->stream);
         if (e != hipSuccess) return herr(e);
     }
-    if (int rc = build_suffix(s)) return rc;
+    uint32_t sets = 0;  // the frontier builds its suffix table in the seed launch
+    if (int rc = build_suffix(s, !s->frontier, &sets)) return rc;
     a = args_of(s);
     a.out = s->d_items[0];
+    if (s->frontier) {  // the live seeds are written as the first frontier (32-byte paths)
+        if (int rc = ensure_front(s, 0, (size_t)s->local_items + 1, 0)) return rc;
+        a.fout = s->d_front[0];
+    }
     const uint64_t blocks = (s->local_items + kSearchThreads - 1) / kSearchThreads;
     const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>(blocks, (uint64_t)s->ctx->cu_count * 8));
-    int rc = launch_and_count(s, true, grid, a);
-    if (rc || !s->frontier || s->pending == 0) return rc;
-    // frontier search: the live seeds become the first frontier (32-byte paths)
-    rc = ensure_front(s, 0, s->pending, 0);
-    if (rc) return rc;
-    a.in = s->d_items[0];
-    a.in_count = (uint32_t)s->pending;
-    a.fout = s->d_front[0];
-    hipError_t e = launch_to_paths(a);
-    if (e == hipSuccess) e = hipStreamSynchronize(s->ctx->stream);
-    return herr(e);
+    return launch_and_count(s, true, grid, a, s->frontier ? sets : 0u);
 }
 
 // Frontier search, one step: either fold the waiting tails, or expand the
@@ -847,7 +860,9 @@ static int frontier_step(tspgpu_search *s, uint64_t *pending)
     a.fin = s->d_front[0] + keep;
     a.fin_count = (uint32_t)T;
     // a few blocks per CU, each over a contiguous run (one slot atomic per block and output)
-    const uint64_t blocks = std::max<uint64_t>(1, std::min<uint64_t>((T + 255) / 256, (uint64_t)s->ctx->cu_count * 4));
+    // (at most 1024 paths per block: expand_kernel keeps their live masks in registers)
+    const uint64_t blocks = std::max<uint64_t>(
+        (T + 1023) / 1024, std::max<uint64_t>(1, std::min<uint64_t>((T + 255) / 256, (uint64_t)s->ctx->cu_count * 4)));
     a.fin_per_block = (uint32_t)(((T + blocks - 1) / blocks + 255) / 256 * 256);
     a.fout = s->d_front[1];
     e = hipMemsetAsync(s->d_words + 4, 0, 8, st);
