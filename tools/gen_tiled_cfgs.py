@@ -14,6 +14,9 @@ CSRC = os.path.join(ROOT, "tsp-mpi-reduction_amd", "csrc")
 # (id, value type, N, L, threads per workgroup, distance copies R, workgroups per CU)
 CFGS = [
     (14, "double", 15, 10, 256, 1, 6),
+    (20, "int32_t", 15, 10, 256, 1, 8),
+    (22, "double", 14, 10, 256, 1, 6),
+    (23, "double", 13, 10, 256, 1, 6),
     (12, "double", 15, 10, 256, 1, 5),
     (2, "double", 15, 11, 256, 1, 3),
     (0, "double", 15, 11, 512, 1, 2),
@@ -32,6 +35,9 @@ CFGS = [
     (16, "double", 15, 9, 256, 1, 7),
     (17, "double", 15, 10, 256, 2, 5),
     (18, "double", 15, 10, 256, 1, 7),
+    (19, "int32_t", 15, 10, 256, 1, 6),
+    (21, "int32_t", 15, 11, 256, 1, 5),
+    (24, "int32_t", 14, 10, 256, 1, 6),
 ]
 
 

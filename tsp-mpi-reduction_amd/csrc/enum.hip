@@ -31,6 +31,7 @@
 #include <utility>
 
 #include "search.h"
+#include "wave.h"
 
 namespace tspgpu {
 namespace {
@@ -752,11 +753,7 @@ template <typename V>
 __device__ __forceinline__ void publish_ub(const SearchArgs &a, double ub)
 {
     if constexpr (sizeof(V) == 8) {
-#pragma unroll
-        for (int off = 32; off >= 1; off >>= 1) {
-            const double o = __shfl_xor(ub, off);
-            ub = o < ub ? o : ub;
-        }
+        ub = wave_min_dpp(ub);
         if (__lane_id() == 0 && ub < 1.0e300)
             atomicMin(a.inc, (unsigned long long)__double_as_longlong(ub));
     }

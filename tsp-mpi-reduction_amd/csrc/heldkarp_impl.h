@@ -39,6 +39,7 @@
 #include <type_traits>
 
 #include "heldkarp.h"
+#include "wave.h"
 
 namespace tspgpu {
 
@@ -160,12 +161,11 @@ __device__ __forceinline__ int colex_rank(uint32_t mask, const int *binom)
     return rank;
 }
 
+// minimum over the wave (all 64 lanes active): DPP row reduction + readlane (wave.h)
 template <typename V>
 __device__ __forceinline__ V wave_min(V v)
 {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) v = ValT<V>::vmin(v, __shfl_xor(v, off));
-    return v;
+    return wave_min_dpp(v);
 }
 
 // dl row m holds d[m][1..N] at [0, N) and d[m][0] at N: the N values a row

@@ -55,11 +55,15 @@ constexpr int kTiledMaxL = 12;
 // distance row stride (entries): odd, so the per-lane gathers d[m][k] of a
 // half-wave with equal k and different m fall on different bank pairs (a
 // stride of 16 made every pair m, m+2 collide: 94% bank-conflict cycles)
-constexpr int kTiledDS = 17;
+#ifndef TSPGPU_TILED_DS
+#define TSPGPU_TILED_DS 17
+#endif
+constexpr int kTiledDS = TSPGPU_TILED_DS;
 // Ablation knobs for timing experiments only (results are WRONG when set):
 //   1 high-member values from LDS, 2 d values from a register, 4 no barrier
 //   between the passes of a sub-cube, 8 plain minimum (no argmin), 32 no
-//   backtracking, 64 backtracking kernel stops after staging, 128 no recompute
+//   backtracking, 64 backtracking kernel stops after staging, 128 no recompute,
+//   1024 no sub-cube reordering of the distance table (TSPGPU_TILED_PERM)
 #ifndef TSPGPU_TILED_ABL
 #define TSPGPU_TILED_ABL 0
 #endif
@@ -74,6 +78,20 @@ constexpr int kTiledDS = 17;
 #endif
 #ifndef TSPGPU_TILED_AHEAD
 #define TSPGPU_TILED_AHEAD 6  // d loads in flight per lane in the relaxation loop
+#endif
+// High cities in sub-cube order: the forward kernel keeps the high rows and
+// columns of its LDS distance table in the order sigma_h = (members of h
+// ascending, then non-members ascending), so a pass (whose member/non-member
+// split of the high cities is static) addresses them with immediate offsets:
+// no VALU address add for a relaxation with a high member or destination, and
+// the high-high distances are wave-uniform reads.  Wave 0 permutes the table
+// from sigma_h to sigma_{h+1} after the last pass of sub-cube h (that pass has
+// one row, so wave 0 is the only reader left).  Measured at n = 16 (cfg 14,
+// 16384 blocks, profiles/r02/k1_tiled_v16_perm.log): the passes get 3% faster
+// (7.37 ms with the reordering skipped, results wrong) but the reordering on
+// wave 0's path costs more (7.79-7.81 ms vs 7.58-7.61 without): off.
+#ifndef TSPGPU_TILED_PERM
+#define TSPGPU_TILED_PERM 0
 #endif
 
 // host-built tables of one L (device copy, staged into LDS per workgroup)
@@ -306,6 +324,15 @@ __device__ __forceinline__ void tiled_pass(const TiledCtx<V, N, L, R> &c, uint32
             nb &= nb - 1u;
         }
     }
+    // table row -> city of every member row (argmin rows, sub-cube order):
+    // nibble p = p for the low rows, L + hm[i] for high row L + i
+    uint64_t pmap = 0;
+    if constexpr (ARG && TSPGPU_TILED_PERM) {
+#pragma unroll
+        for (int p = 0; p < L; ++p) pmap |= (uint64_t)p << (4 * p);
+#pragma unroll
+        for (int i = 0; i < HC; ++i) pmap |= (uint64_t)(L + hm[i]) << (4 * (L + i));
+    }
     const uint32_t lane_off = (tid & (uint32_t)(R - 1)) * VB;
     const char *drb = reinterpret_cast<const char *>(c.dr);
     char *lds_nxt = reinterpret_cast<char *>(c.region + NXT);
@@ -332,7 +359,8 @@ __device__ __forceinline__ void tiled_pass(const TiledCtx<V, N, L, R> &c, uint32
             lb &= lb - 1u;
         }
 #pragma unroll
-        for (int i = 0; i < HC; ++i) mrow[J + i] = (L + hm[i]) * DROW + lane_off;
+        for (int i = 0; i < HC; ++i)  // high member i: table row L + i in sub-cube order
+            mrow[J + i] = (TSPGPU_TILED_PERM ? (uint32_t)(L + i) : (L + hm[i])) * DROW + lane_off;
         // Destinations in chunks of at most TSPGPU_TILED_QC (registers: acc,
         // arg and the column offsets of one chunk only); the non-members come
         // ascending (low non-members of l, then those of h).  Per chunk: the
@@ -356,8 +384,8 @@ __device__ __forceinline__ void tiled_pass(const TiledCtx<V, N, L, R> &c, uint32
                 if (q < QL) {
                     kof[qq] = (uint32_t)__builtin_ctz(nb) << SK;
                     nb &= nb - 1u;
-                } else {
-                    kof[qq] = (L + hn[q - QL]) << SK;
+                } else {  // high non-member q - QL: table column L + HC + (q - QL) in sub-cube order
+                    kof[qq] = (TSPGPU_TILED_PERM ? (uint32_t)(L + HC + (q - QL)) : (L + hn[q - QL])) << SK;
                 }
             }
             V acc[QN];
@@ -401,10 +429,13 @@ __device__ __forceinline__ void tiled_pass(const TiledCtx<V, N, L, R> &c, uint32
                 }
                 // the row's parent word: nibble q = bit index of the argmin member
                 if constexpr (ARG) {
+                    uint32_t pos = arg[qq] / DROW;  // table row of the argmin member
+                    if constexpr (TSPGPU_TILED_PERM && HC > 0)
+                        pos = (uint32_t)(pmap >> (4 * pos)) & 15u;  // -> its city
                     if (q < 8)
-                        wlo |= (arg[qq] / DROW) << (4 * q);
+                        wlo |= pos << (4 * q);
                     else
-                        whi |= (arg[qq] / DROW) << (4 * (q - 8));
+                        whi |= pos << (4 * (q - 8));
                 }
             }
         });
@@ -422,6 +453,63 @@ __device__ __forceinline__ uint32_t pdep_u32(uint32_t x, uint32_t m)
         m ^= low;
     }
     return r;
+}
+
+// TSPGPU_TILED_PERM: one wave rewrites the high rows and columns of the
+// forward kernel's LDS distance table from sub-cube order sigma_hf to
+// sigma_ht (sigma_h: members of h ascending, then non-members ascending; h = 0
+// is the natural order).  Every lane loads its entries first, then stores.
+template <typename V, int N, int L, int R>
+__device__ __forceinline__ void tiled_perm_high(V *dr, uint32_t hf, uint32_t ht, uint32_t lane)
+{
+    constexpr int H = N - L, E = H * N + L * H, PER = (E * R + 63) / 64;
+    // uniform: sig = the city at each position under ht, inv = the position of
+    // each city under hf (nibbles; members ascending, then non-members)
+    uint32_t sig = 0, inv = 0;
+    {
+        int ps = 0, pi = 0;
+#pragma unroll
+        for (int x = 0; x < H; ++x)
+            if ((ht >> x) & 1u) sig |= (uint32_t)x << (4 * ps++);
+#pragma unroll
+        for (int x = 0; x < H; ++x)
+            if (!((ht >> x) & 1u)) sig |= (uint32_t)x << (4 * ps++);
+#pragma unroll
+        for (int x = 0; x < H; ++x)
+            if ((hf >> x) & 1u) inv |= (uint32_t)(pi++) << (4 * x);
+#pragma unroll
+        for (int x = 0; x < H; ++x)
+            if (!((hf >> x) & 1u)) inv |= (uint32_t)(pi++) << (4 * x);
+    }
+    auto src_pos = [&](int t) -> int {  // table position under hf of the city at position t under ht
+        if (t < L) return t;
+        const uint32_t x = (sig >> (4 * (t - L))) & 15u;
+        return L + (int)((inv >> (4 * x)) & 15u);
+    };
+    V v[PER];
+    int dst[PER];
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+        const int e = (int)lane + 64 * k;
+        dst[k] = -1;
+        v[k] = V(0);
+        if (e < E * R) {
+            const int c = e % R, ee = e / R;
+            int a, b;
+            if (ee < H * N) {
+                a = L + ee / N;
+                b = ee % N;
+            } else {
+                a = (ee - H * N) / H;
+                b = L + (ee - H * N) % H;
+            }
+            dst[k] = (a * kTiledDS + b) * R + c;
+            v[k] = dr[(src_pos(a) * kTiledDS + src_pos(b)) * R + c];
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < PER; ++k)
+        if (dst[k] >= 0) dr[dst[k]] = v[k];
 }
 
 // G[h<<L | l][m] after the forward pass: a high m from the push area, a low m
@@ -641,6 +729,10 @@ __global__ __launch_bounds__(THREADS, tiled_waves(THREADS, WG)) void hk_tiled_ke
                 tiled_dispatch<V, N, L, THREADS, R>(c, h, hc, j, tid);
                 if (!(TSPGPU_TILED_ABL & 4) && j < j1) lds_barrier();
             }
+            // the last pass (j = L, one row: thread 0) leaves wave 0 the only
+            // reader of the distance table: it reorders the high cities for h + 1
+            if (TSPGPU_TILED_PERM && !(TSPGPU_TILED_ABL & 1024) && h + 1 < (uint32_t)NH && tid < 64u)
+                tiled_perm_high<V, N, L, R>(dr, h, h + 1, tid);
             // pushes of this sub-cube are read by later ones: full barrier
             __syncthreads();
         }

@@ -7,6 +7,9 @@
 
 #define TSPGPU_TILED_CFGS(X) \
     X(14, double, 15, 10, 256, 1, 6) \
+    X(20, int32_t, 15, 10, 256, 1, 8) \
+    X(22, double, 14, 10, 256, 1, 6) \
+    X(23, double, 13, 10, 256, 1, 6) \
     X(12, double, 15, 10, 256, 1, 5) \
     X(2, double, 15, 11, 256, 1, 3) \
     X(0, double, 15, 11, 512, 1, 2) \
@@ -24,7 +27,10 @@
     X(15, double, 15, 9, 256, 1, 6) \
     X(16, double, 15, 9, 256, 1, 7) \
     X(17, double, 15, 10, 256, 2, 5) \
-    X(18, double, 15, 10, 256, 1, 7)
+    X(18, double, 15, 10, 256, 1, 7) \
+    X(19, int32_t, 15, 10, 256, 1, 6) \
+    X(21, int32_t, 15, 11, 256, 1, 5) \
+    X(24, int32_t, 14, 10, 256, 1, 6)
 
 namespace tspgpu {
 struct TiledCfg {

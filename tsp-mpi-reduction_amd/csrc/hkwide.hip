@@ -24,6 +24,7 @@
 #include <vector>
 
 #include "ctx.h"
+#include "wave.h"
 #include "tspgpu.h"
 
 namespace {
@@ -194,7 +195,7 @@ __global__ void wide_close(const double *__restrict__ dist, int N, const WideInf
     const double glast = valid ? tab[info->off[N] + (unsigned long long)(m - 1) * info->cnt[N]] : 0.0;
     const double cand = valid ? glast + dist[m * n] : 1.0e300;
     double best = cand;
-    for (int off = 32; off > 0; off >>= 1) best = fmin(best, __shfl_xor(best, off));
+    best = tspgpu::wave_min_dpp(best);
     best = fmin(best, kIntMaxD);
     const unsigned long long hit = __ballot(valid && cand == best && cand < kIntMaxD);
     const int bestM = hit ? __ffsll(hit) : 0;

@@ -35,6 +35,7 @@
 #include <vector>
 
 #include "ctx.h"
+#include "wave.h"
 #include "tspgpu.h"
 
 namespace {
@@ -142,11 +143,7 @@ __global__ __launch_bounds__(kMergeThreads) void argmin_kernel(const tspgpu_city
             });
         __syncthreads();  // before the next chunk overwrites the stage
     }
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-        const unsigned long long o = __shfl_xor(best, off);
-        best = o < best ? o : best;
-    }
+    best = tspgpu::wave_min_dpp(best);
     if (__lane_id() == 0) wmin[threadIdx.x / 64] = best;
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -182,11 +179,7 @@ __global__ __launch_bounds__(kMergeThreads) void fold_pick_kernel(const tspgpu_c
             const unsigned long long k = order_key(sc);
             best = k < best ? k : best;
         });
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-        const unsigned long long o = __shfl_xor(best, off);
-        best = o < best ? o : best;
-    }
+    best = tspgpu::wave_min_dpp(best);
     if (__lane_id() == 0) wmin[threadIdx.x / 64] = best;
     __syncthreads();
     if (threadIdx.x == 0) {
