@@ -215,10 +215,14 @@ def test_solve_sharded_single_process(gpu_ctx):
     rng = np.random.default_rng(5)
     xy = rng.uniform(0, 1000, size=(15, 2))
     d = O.distance_matrix([(i, xy[i, 0], xy[i, 1]) for i in range(15)])
-    cost, tour, st = search_dist.solve_sharded(gpu_ctx, d)
     oc, ot = O.solve_block(d)
+    cost, tour, st = search_dist.solve_sharded(gpu_ctx, d, exchange_every=1)
     assert cost == oc and tour.tolist() == ot, st
     assert st["exchanges"] == st["rounds"] >= 1
+    # the default batches 4 steps per exchange: same answer, fewer exchanges
+    cost, tour, st4 = search_dist.solve_sharded(gpu_ctx, d)
+    assert cost == oc and tour.tolist() == ot, st4
+    assert st4["exchange_every"] == 4 and 1 <= st4["exchanges"] <= st4["rounds"] // 4 + 1
 
 
 def test_overflow_falls_back_to_second_phase(gpu_ctx):

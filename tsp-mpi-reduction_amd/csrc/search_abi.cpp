@@ -98,8 +98,13 @@ struct tspgpu_search {
     PathItem *d_front[2] = {nullptr, nullptr};  // frontier (LIFO) / children of the current step
     size_t front_cap[2] = {0, 0};
     PathItem *d_tail = nullptr;
-    unsigned int tail_cap = 1u << 23;
+    // one frontier step expands at most min(expand_max, free tail slots / branch)
+    // items; bigger steps mean fewer host round trips (n = 30 random, seed 2:
+    // 2^23 tails / 2^21 items 2903 steps, 192 ms; 2^26 / 2^24 373 steps, 58 ms;
+    // profiles/r02/k2_knobs.log).  Buffers grow on demand.
+    unsigned int tail_cap = 1u << 26;
     unsigned int tail_alloc = 0;
+    uint64_t expand_max = (uint64_t)1 << 24;  // frontier items one step expands, at most (TSPGPU_SEARCH_EXPAND_LOG2)
     uint64_t tails = 0;          // items waiting in d_tail
     int rounds = 0;
     double ms = 0.0;             // device time of all seed/round launches
@@ -471,7 +476,11 @@ int tspgpu_search_create(tspgpu_ctx *c, const void *dist, int dtype, int n, int 
     if (const char *e = std::getenv("TSPGPU_SEARCH_TWO_EDGE")) s->use_two_edge = std::atoi(e) != 0;
     if (const char *e = std::getenv("TSPGPU_SEARCH_TAIL_CAP_LOG2")) {  // tests: many flushes, small steps
         const int v = std::atoi(e);
-        if (v >= 8 && v <= 26) s->tail_cap = 1u << v;
+        if (v >= 8 && v <= 27) s->tail_cap = 1u << v;
+    }
+    if (const char *e = std::getenv("TSPGPU_SEARCH_EXPAND_LOG2")) {
+        const int v = std::atoi(e);
+        if (v >= 8 && v <= 26) s->expand_max = (uint64_t)1 << v;
     }
     const size_t lds = search_lds_bytes(n, f64, s->kernel == 1 ? 1 : 2);
     const int per_cu = std::max(1, std::min(8, (int)((160 * 1024) / lds)));
@@ -832,7 +841,6 @@ static int frontier_step(tspgpu_search *s, uint64_t *pending)
     hipStream_t st = s->ctx->stream;
     const bool f64 = s->dtype == TSPGPU_F64;
     const uint64_t branch = (uint64_t)(s->n - 1 - s->depth);  // children per item, at most
-    constexpr uint64_t kExpandMax = (uint64_t)1 << 21;
     SearchArgs a = args_of(s);
     hipError_t e = hipSuccess;
     if (s->pending == 0 || s->tails >= s->tail_cap / 2) {
@@ -853,7 +861,7 @@ static int frontier_step(tspgpu_search *s, uint64_t *pending)
         if (pending) *pending = s->pending;
         return 0;
     }
-    const uint64_t T = std::min<uint64_t>({s->pending, kExpandMax, (s->tail_cap - s->tails) / branch});
+    const uint64_t T = std::min<uint64_t>({s->pending, s->expand_max, (s->tail_cap - s->tails) / branch});
     const uint64_t keep = s->pending - T;
     int rc = ensure_front(s, 1, (size_t)(T * branch + 64), 0);
     if (rc) return rc;
@@ -885,8 +893,8 @@ static int frontier_step(tspgpu_search *s, uint64_t *pending)
     } else if (kids) {  // behind the items not expanded yet
         rc = ensure_front(s, 0, (size_t)(keep + kids), (size_t)keep);
         if (rc) return rc;
+        // stream-ordered before the next step's launch: no host wait
         e = hipMemcpyAsync(s->d_front[0] + keep, s->d_front[1], kids * sizeof(PathItem), hipMemcpyDeviceToDevice, st);
-        if (e == hipSuccess) e = hipStreamSynchronize(st);
         if (e != hipSuccess) return herr(e);
     }
     s->pending = keep + kids;

@@ -171,7 +171,8 @@ struct Result {
     int rounds = 0;
 };
 
-// K2 over G GPUs of this process, RCCL all-reduce MIN of the incumbent between rounds.
+// K2 over G GPUs of this process, RCCL all-reduce MIN of the incumbent every
+// `every` frontier steps.
 int search_multi(const Instance &in, int G, Result &res)
 {
     // one RCCL communicator per GPU (a single GPU needs none)
@@ -187,6 +188,9 @@ int search_multi(const Instance &in, int G, Result &res)
     std::vector<double> ms(G, 0.0);
     std::vector<int> rounds(G, 0);
     std::atomic<int> busy{0}, failed{0};
+    // frontier steps between two incumbent exchanges (TSPGPU_EXCHANGE_EVERY, default 4)
+    int every = 4;
+    if (const char *e = std::getenv("TSPGPU_EXCHANGE_EVERY")) every = std::max(1, std::atoi(e));
     std::barrier sync(G);
     std::vector<std::thread> th;
     for (int g = 0; g < G; ++g) {
@@ -206,7 +210,9 @@ int search_multi(const Instance &in, int G, Result &res)
             sync.arrive_and_wait();
             uint64_t pending = 1;
             for (; !failed.load();) {
-                if (!rc && pending) rc = tspgpu_search_step(s, &pending);
+                // up to `every` steps of this shard, then one exchange (the same
+                // count on every shard, so the all-reduces pair up)
+                for (int k = 0; k < every && !rc && pending; ++k) rc = tspgpu_search_step(s, &pending);
                 busy.fetch_add(!rc && pending ? 1 : 0);
                 // incumbent exchange: in-place RCCL all-reduce MIN on the device word
                 void *w = s ? tspgpu_search_incumbent_device(s) : nullptr;

@@ -21,6 +21,7 @@ needs a reduction: picking the global best tour.
 from __future__ import annotations
 
 import errno
+import os
 import time
 
 import numpy as np
@@ -34,9 +35,15 @@ def _word_tensor(value: int, device):
     return torch.tensor([value], dtype=torch.int64, device=device)
 
 
-def solve_sharded(ctx, dist, group=None, depth: int = 0, device=None):
+def solve_sharded(ctx, dist, group=None, depth: int = 0, device=None, exchange_every: int | None = None):
     """Search one instance over the ranks of `group` (None: the default group,
     or a single process when torch.distributed is not initialised).
+
+    Every rank runs `exchange_every` steps of its own shard (fewer once it runs
+    out of work), then all ranks exchange once: ONE all-reduce(MIN) of the pair
+    (incumbent word, -busy).  The count is the same on every rank, so the
+    collectives always pair up; a rank without work only joins the exchanges.
+    Default: TSPGPU_EXCHANGE_EVERY or 4.
 
     Returns (cost, tour (n+1,), stats dict); identical on every rank."""
     import torch
@@ -56,6 +63,20 @@ def solve_sharded(ctx, dist, group=None, depth: int = 0, device=None):
         tdist.all_reduce(t, op=tdist.ReduceOp.MIN, group=group)
         return int(t.item())
 
+    def allmin2(a: int, b: int):
+        if world == 1:
+            return a, b
+        import torch
+
+        t = torch.tensor([a, b], dtype=torch.int64, device=device)
+        tdist.all_reduce(t, op=tdist.ReduceOp.MIN, group=group)
+        v = t.tolist()
+        return int(v[0]), int(v[1])
+
+    if exchange_every is None:
+        exchange_every = int(os.environ.get("TSPGPU_EXCHANGE_EVERY", "4"))
+    exchange_every = max(1, int(exchange_every))
+
     S = tspgpu.Search(ctx, dist, shard=rank, nshards=world, depth=depth)
     try:
         ub, _ = tspgpu.heuristic_tour(dist)  # deterministic: the same bound on every rank
@@ -65,16 +86,19 @@ def solve_sharded(ctx, dist, group=None, depth: int = 0, device=None):
         S.start()
         busy = 1
         while True:
-            # one round on this rank (if it still has work), then the exchange:
-            # incumbent MIN and "anyone still busy" as MIN of the negated flag
-            pending = S.step() if busy else 0
+            # up to exchange_every steps on this rank (while it has work), then
+            # the exchange: incumbent MIN and "anyone still busy" (MIN of the
+            # negated flag) in one all-reduce
+            for _ in range(exchange_every):
+                if not busy:
+                    break
+                busy = 1 if S.step() else 0
             inc, _, _ = S.counters()
-            best = allmin(inc)
+            best, anybusy = allmin2(inc, -busy)
             exchanges += 1
             if best < inc:
                 S.set_bound(tspgpu.bits_cost(best, S.dtype))
-            busy = 1 if pending else 0
-            if allmin(-busy) == 0:
+            if anybusy == 0:
                 break
         inc, nodes, recs = S.counters()
         opt = allmin(inc)
@@ -133,7 +157,7 @@ def solve_sharded(ctx, dist, group=None, depth: int = 0, device=None):
         stats = {"nodes": total_nodes, "rank_nodes": int(nodes), "optimal_tours": len(allrec), "depth": S.depth,
                  "items": S.items, "phases": phases, "fallback": 0, "kernel_ms": kernel_ms, "rounds": rounds,
                  "wall_s": wall,
-                 "exchanges": exchanges, "world": world, "backend": backend}
+                 "exchanges": exchanges, "exchange_every": exchange_every, "world": world, "backend": backend}
         return cost, tour, stats
     finally:
         S.close()
