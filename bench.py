@@ -375,9 +375,13 @@ def k2_group(world, local_rank):
     import torch
     import torch.distributed as dist
 
-    if torch.cuda.is_available():
-        torch.cuda.set_device(local_rank % max(1, torch.cuda.device_count()))
+    ndev = torch.cuda.device_count() if torch.cuda.is_available() else 0
+    if ndev >= world:
+        # one GPU per rank: the incumbent exchange is an RCCL all-reduce over xGMI
+        torch.cuda.set_device(local_rank % ndev)
         return dist.new_group(backend="nccl"), "nccl"
+    # ranks share a GPU (a rehearsal on a smaller box; RCCL wants one rank per
+    # device) or no GPU: the same exchange over gloo
     return dist.new_group(backend="gloo"), "gloo"
 
 
