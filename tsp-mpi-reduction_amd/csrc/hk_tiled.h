@@ -52,11 +52,16 @@
 namespace tspgpu {
 
 constexpr int kTiledMaxL = 12;
-// distance row stride (entries): odd, so the per-lane gathers d[m][k] of a
-// half-wave with equal k and different m fall on different bank pairs (a
-// stride of 16 made every pair m, m+2 collide: 94% bank-conflict cycles)
+// distance row stride (entries): the per-lane gathers d[m][k] of a half-wave
+// fall on bank pair (m * stride + k) mod 32.  16 made every pair m, m+2
+// collide (94% bank-conflict cycles); a bank model over every pass's
+// (member, destination) positions gives 0.44 extra cycles per low-low gather
+// at 17, 0.065 at 19; measured at n = 16 (cfg 14, 4096 blocks,
+// profiles/r02/lds_conflicts_stride.txt): conflict cycles 29.7 K -> 20.2 K
+// per block (0.575 -> 0.391 of LDS-active cycles), time equal or 0.5% less.
+// The rest are the scattered next-layer stores and rank lookups.
 #ifndef TSPGPU_TILED_DS
-#define TSPGPU_TILED_DS 17
+#define TSPGPU_TILED_DS 19
 #endif
 constexpr int kTiledDS = TSPGPU_TILED_DS;
 // Ablation knobs for timing experiments only (results are WRONG when set):
