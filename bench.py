@@ -726,6 +726,14 @@ def main():
     if world == 1 and not args.no_pmc:
         prof = pmc_profile(n, min(Bp, 4096), cu, kname)
     peaks = valu_peaks() if world == 1 else None
+    if i32 and "relaxations_per_s" in i32 and (peaks or {}).get("i32 relaxation min-only (add,min)"):
+        # K1 on int32 distances against the integer VALU issue rate of its own
+        # min-only relaxation (v_add_u32 + v_min_i32, registers only, this GPU);
+        # launch time includes the backtracking kernel (variant 5), so this
+        # understates the forward kernel's fraction
+        pk = peaks["i32 relaxation min-only (add,min)"]
+        i32["valu_roofline"] = {"bound": "valu (int32)", "achieved_relax_per_s": i32["relaxations_per_s"],
+                                "peak_relax_per_s": pk, "frac": i32["relaxations_per_s"] / pk}
     dom_ms = split["forward_kernel_ms"] if split else kernel_ms  # the dominant kernel's own time
     relax_s_kernel = Bp * relax / (dom_ms * 1e-3)
     roof = roofline(variant, kname, n, Bp, dom_ms, relax_s_kernel, alg_bytes_per_block, prof, peaks)

@@ -1,0 +1,41 @@
+"""bench.py's multi-rank path on a real GPU: `bench.py --gpus 2` starts two
+ranks itself (torch.distributed.run child); on a one-GPU box both ranks share
+device 0 and the K2 incumbent exchange runs over gloo (RCCL wants one rank
+per device), on an 8-GPU node the same code takes the RCCL group.  Checks
+the line the driver reads: n_gpus, the global block count, both ranks' K2
+shards and the strong-scaling instance's optimum (= K1-wide on one GPU)."""
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+import tspgpu
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_bench_two_ranks_end_to_end(gpu_ctx):
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1",
+           "--blocks-per-gpu", "512", "--no-pmc", "--no-cpu-baseline", "--no-tto", "--k2-n", "18", "--k2-seed", "1"]
+    env = dict(os.environ, BENCH_I32="0")
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
+    assert p.returncode == 0, p.stderr[-2000:]
+    line = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
+    assert line["n_gpus"] == 2 and line["config"]["global_blocks"] == 1024
+    assert line["value"] > 0 and line["scaling"] == "weak"
+    k2s = line["k2_strong_scaling"]
+    assert "error" not in k2s, k2s
+    assert k2s["ranks"] == 2 and len(k2s["rank_walls_ms"]) == 2
+    sys.path.insert(0, ROOT)
+    from bench import k2_instance
+
+    d = k2_instance(18, 1)
+    wide_cost, wide_tour, _ = gpu_ctx.solve_instance(np.asarray(d, dtype=np.float64))
+    assert k2s["cost"] == wide_cost and k2s["tour"] == [int(x) for x in wide_tour]
+    k2 = line["k2_single_instance"]
+    assert "error" not in k2 and k2["ranks"] == 2 and k2["cost"] == 3871.1947567096445

@@ -28,7 +28,8 @@ constexpr int CHAINS = 8;
 // MODE 0 v_add_f64, 1 v_min_f64, 2 v_cmp_lt_f64 + v_cndmask_b32, 3 v_add_u32,
 // 4 v_min_i32, 5 the f64 relaxation with argmin (add, cmp, cndmask, min),
 // 6 the i32 relaxation with argmin, 7 v_cndmask_b32 alone, 8 the f64
-// relaxation without argmin (add, min: K1 variant 5's passes below the top rows)
+// relaxation without argmin (add, min: K1 variant 5's passes below the top rows),
+// 9 the i32 relaxation without argmin
 template <int MODE>
 __global__ __launch_bounds__(256) void valu_kernel(double *out, double seed)
 {
@@ -82,6 +83,12 @@ __global__ __launch_bounds__(256) void valu_kernel(double *out, double seed)
                 asm volatile("v_add_f64 %1, %2, %3\n\tv_min_f64 %0, %0, %1"
                              : "+v"(a[c]), "=&v"(t)
                              : "v"(b), "v"(a[(c + 1) % CHAINS]));
+            }
+            if constexpr (MODE == 9) {
+                int t;
+                asm volatile("v_add_u32 %1, %2, %3\n\tv_min_i32 %0, %0, %1"
+                             : "+v"(ia[c]), "=&v"(t)
+                             : "v"(ib), "v"(ia[(c + 1) % CHAINS]));
             }
         }
     }
@@ -142,6 +149,7 @@ int main(int argc, char **argv)
         run_valu<5>("f64 relaxation+argmin (add,cmp,cndmask,min)", 4, p);
         run_valu<8>("f64 relaxation min-only (add,min)", 2, p);
         run_valu<6>("i32 relaxation+argmin (add,cmp,cndmask,min)", 4, p);
+        run_valu<9>("i32 relaxation min-only (add,min)", 2, p);
         return 0;
     }
     if (argc >= 4 && !strcmp(argv[1], "mem")) {
