@@ -259,6 +259,11 @@ int tspgpu_search_records(tspgpu_search *s, uint64_t cost_bits, tspgpu_tour_reco
  * the chosen suffix and whose best prefix fold + d[m][next] equals the state
  * value (tsp.cpp:457-470, 483-499) — the tour tsp() returns. */
 int tspgpu_heuristic_tour(const void *dist, int dtype, int n, double *cost_out, int32_t *tour_out);
+/* the same over the start cities first, first + step, ... < n only (-ENOENT
+ * when first >= n): R ranks taking first = r, step = R and the MIN of their
+ * costs get the bound of all starts, each doing 1/R of the work */
+int tspgpu_heuristic_tour_starts(const void *dist, int dtype, int n, int first, int step, double *cost_out,
+                                 int32_t *tour_out);
 int tspgpu_select_tour(const void *dist, int dtype, int n, const tspgpu_tour_record *records, int count,
                        uint64_t cost_bits, int32_t *tour_out);
 

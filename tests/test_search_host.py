@@ -109,6 +109,24 @@ def test_heuristic_is_an_upper_bound(n):
         assert cost >= O.solve_block(d)[0]
 
 
+@pytest.mark.parametrize("n", [6, 17, 30])
+def test_heuristic_split_over_ranks_gives_the_same_bound(n):
+    """tspgpu_heuristic_tour_starts: W ranks taking the start cities r, r+W, ...
+    and the MIN of their costs get exactly the all-starts bound (what
+    search_dist.solve_sharded exchanges before the search)."""
+    rng = np.random.default_rng(100 + n)
+    xy = rng.uniform(0, 1000, size=(n, 2))
+    d = O.distance_matrix([(i, xy[i, 0], xy[i, 1]) for i in range(n)])
+    full, _ = tspgpu.heuristic_tour(d)
+    for W in (1, 2, 3, 8):
+        parts = [tspgpu.heuristic_tour(d, first=r, step=W)[0] for r in range(W)]
+        assert min(c for c in parts if c is not None) == full
+    assert tspgpu.heuristic_tour(d, first=n, step=1) == (None, None)
+    di = np.rint(d).astype(np.int32)
+    full_i, _ = tspgpu.heuristic_tour(di)
+    assert min(tspgpu.heuristic_tour(di, first=r, step=4)[0] for r in range(4)) == full_i
+
+
 def test_search_validation():
     """Host-side argument checks of the K2 entry points (no device needed)."""
     with pytest.raises(tspgpu.TspGpuError):

@@ -251,6 +251,17 @@ __host__ __device__ constexpr unsigned long long tail_nodes(int tl)
 }
 
 // A frontier path in registers: two dwordx4 loads.
+// path i of a frontier step's input (up to four segments, SearchArgs::fseg)
+__device__ __forceinline__ const PathItem *fin_at(const SearchArgs &a, uint32_t i)
+{
+    const PathItem *p = a.fseg[0];
+    uint32_t st = 0;
+    if (a.nseg > 1 && i >= a.fseg_start[1]) p = a.fseg[1], st = a.fseg_start[1];
+    if (a.nseg > 2 && i >= a.fseg_start[2]) p = a.fseg[2], st = a.fseg_start[2];
+    if (a.nseg > 3 && i >= a.fseg_start[3]) p = a.fseg[3], st = a.fseg_start[3];
+    return p + (i - st);
+}
+
 __device__ __forceinline__ void load_path(const PathItem *p, bool act, uint32_t (&w)[8])
 {
     if (act) {
@@ -712,7 +723,7 @@ __device__ __forceinline__ Expand<V> expand_eval(const SearchArgs &a, const V *d
 {
     Expand<V> e;
     const bool act = idx < end;
-    load_path(a.fin + idx, act, e.w);
+    load_path(fin_at(a, idx), act, e.w);
     e.len = act ? (int)(e.w[0] & 255u) : 0;
     V c = 0;  // the reference's left fold of the path
     int k = 0;
@@ -830,7 +841,7 @@ __global__ __launch_bounds__(256) void expand_kernel(SearchArgs a)
         if (base >= b1) break;  // block-uniform
         Expand<V> e;
         const bool act = base + threadIdx.x < b1;
-        load_path(a.fin + base + threadIdx.x, act, e.w);
+        load_path(fin_at(a, base + threadIdx.x), act, e.w);
         e.len = act ? (int)(e.w[0] & 255u) : 0;
         e.live = lv[t];
         const bool tail = e.len == a.tail_level;

@@ -92,8 +92,14 @@ struct SearchArgs {
     // cities left) go to ftail, the others to fout.
     int tail_level;
     int tail_len;              // 5 or 6
-    const PathItem *fin;
-    uint32_t fin_count;
+    const PathItem *fin;       // (the first input segment)
+    uint32_t fin_count;        // paths of the step, over all its input segments
+    // a step's input may span up to kFinSegs frontier segments (the top of the
+    // LIFO stack): path i is fseg[k][i - fseg_start[k]] for the last k < nseg
+    // with fseg_start[k] <= i
+    const PathItem *fseg[4];
+    uint32_t fseg_start[4];
+    int nseg;
     uint32_t fin_per_block;    // expand_kernel: paths per block (multiple of 256)
     PathItem *fout;
     PathItem *ftail;

@@ -95,8 +95,15 @@ struct tspgpu_search {
     uint32_t hs_off[8] = {};
     int suffix_len = 6;         // TSPGPU_SEARCH_SUFFIX=0/5/6: table size (0: B0/B1 only)
     bool use_two_edge = true;   // TSPGPU_SEARCH_TWO_EDGE=0: no B1
-    PathItem *d_front[2] = {nullptr, nullptr};  // frontier (LIFO) / children of the current step
-    size_t front_cap[2] = {0, 0};
+    // The frontier is a LIFO stack of segments, each a run of paths in its own
+    // buffer (fb): a step expands the top T items of the top segment and its
+    // children become a new segment on top, written straight into a spare
+    // buffer (no device copy of the children behind the items left below:
+    // those copies were 11 ms of a 61 ms 30-city search).
+    std::vector<PathItem *> fb;       // frontier buffers (kept in the context's pool between searches)
+    std::vector<size_t> fb_cap;
+    std::vector<int> seg_buf;         // buffer index of each segment, bottom first
+    std::vector<uint64_t> seg_n;      // paths in each segment
     PathItem *d_tail = nullptr;
     // one frontier step expands at most min(expand_max, free tail slots / branch)
     // items; bigger steps mean fewer host round trips (n = 30 random, seed 2:
@@ -203,11 +210,13 @@ void local_search(const V *d, int n, std::vector<int> &t)
 // improved by 2-opt + Or-opt, rotated to start at city 0; the best exact fold
 // (tsp.cpp's cost, either direction) is a valid bound >= OPT.  A tight start
 // matters: every node the search prunes is pruned against it.
+// Starts first, first + step, ... (several ranks split the starts and take the
+// MIN of their costs: the same bound as all starts in one process).
 template <typename V>
-void heuristic(const V *d, int n, std::vector<int32_t> &best, V &cost)
+bool heuristic(const V *d, int n, std::vector<int32_t> &best, V &cost, int first = 0, int step = 1)
 {
     bool have = false;
-    for (int s0 = 0; s0 < n; ++s0) {
+    for (int s0 = first; s0 < n; s0 += step) {
         std::vector<int> t(n);
         std::vector<char> used(n, 0);
         t[0] = s0;
@@ -230,6 +239,7 @@ void heuristic(const V *d, int n, std::vector<int32_t> &best, V &cost)
             have = true;
         }
     }
+    return have;
 }
 
 template <typename V>
@@ -339,8 +349,8 @@ struct SearchPool {
     unsigned int rec_alloc = 0;
     SearchItem *d_items[2] = {nullptr, nullptr};
     size_t item_cap[2] = {0, 0};
-    PathItem *d_front[2] = {nullptr, nullptr};
-    size_t front_cap[2] = {0, 0};
+    std::vector<PathItem *> fb;
+    std::vector<size_t> fb_cap;
     PathItem *d_tail = nullptr;
     unsigned int tail_alloc = 0;
     hipEvent_t e0 = nullptr, e1 = nullptr;
@@ -361,9 +371,11 @@ void move_buffers(A &to, B &from)
     for (int i = 0; i < 2; ++i) {
         to.d_items[i] = from.d_items[i], from.d_items[i] = nullptr;
         to.item_cap[i] = from.item_cap[i], from.item_cap[i] = 0;
-        to.d_front[i] = from.d_front[i], from.d_front[i] = nullptr;
-        to.front_cap[i] = from.front_cap[i], from.front_cap[i] = 0;
     }
+    to.fb.swap(from.fb);
+    to.fb_cap.swap(from.fb_cap);
+    from.fb.clear();
+    from.fb_cap.clear();
     to.d_tail = from.d_tail, from.d_tail = nullptr;
     to.tail_alloc = from.tail_alloc, from.tail_alloc = 0;
     to.e0 = from.e0, from.e0 = nullptr;
@@ -383,8 +395,11 @@ void free_buffers(A &b)
     if (b.d_rec) (void)hipFree(b.d_rec);
     for (int i = 0; i < 2; ++i) {
         if (b.d_items[i]) (void)hipFree(b.d_items[i]);
-        if (b.d_front[i]) (void)hipFree(b.d_front[i]);
     }
+    for (PathItem *p : b.fb)
+        if (p) (void)hipFree(p);
+    b.fb.clear();
+    b.fb_cap.clear();
     if (b.d_tail) (void)hipFree(b.d_tail);
     if (b.e0) (void)hipEventDestroy(b.e0);
     if (b.e1) (void)hipEventDestroy(b.e1);
@@ -429,6 +444,8 @@ void give_pool(tspgpu_search *s)
     if (pool) move_buffers(*s, *pool), delete pool;  // the context has one already: free ours
 }
 }  // namespace
+
+static void front_release(tspgpu_search *s);
 
 extern "C" {
 
@@ -630,6 +647,7 @@ int tspgpu_search_destroy(tspgpu_search *s)
     if (!s) return 0;
     (void)hipSetDevice(s->ctx->device);
     (void)hipStreamSynchronize(s->ctx->stream);
+    front_release(s);
     give_pool(s);  // the buffers stay with the context for its next search
     free_buffers(*s);
     if (s->d_ps) (void)hipFree(s->d_ps);
@@ -730,24 +748,38 @@ static int read_stats(tspgpu_search *s, uint64_t (&out)[4])
     return 0;
 }
 
-// frontier buffer `which` holds at least `count` paths; its first `keep` survive a reallocation
-static int ensure_front(tspgpu_search *s, int which, size_t count, size_t keep)
+// A frontier buffer that no segment uses, holding at least `count` paths:
+// the smallest spare one that is big enough, else a new allocation (rounded up
+// to 2^20 paths); buffers are only freed when the search ends.
+// -> index into s->fb, or < 0 (*rc set).
+static int front_spare(tspgpu_search *s, size_t count, int *rc)
 {
-    if (s->front_cap[which] >= count && s->d_front[which]) return 0;
-    const size_t cap = std::max<size_t>({count, 4096, 2 * s->front_cap[which]});
+    int best = -1;
+    for (int i = 0; i < (int)s->fb.size(); ++i) {
+        bool used = false;
+        for (int b : s->seg_buf) used = used || b == i;
+        if (used || !s->fb[i] || s->fb_cap[i] < count) continue;
+        if (best < 0 || s->fb_cap[i] < s->fb_cap[best]) best = i;
+    }
+    if (best >= 0) return best;
+    const size_t gran = (size_t)1 << 20;
+    const size_t cap = std::max<size_t>(4096, count <= 4096 ? 4096 : (count + gran - 1) / gran * gran);
     PathItem *p = nullptr;
     hipError_t e = hipMalloc((void **)&p, cap * sizeof(PathItem));
-    if (e == hipSuccess && keep)
-        e = hipMemcpyAsync(p, s->d_front[which], keep * sizeof(PathItem), hipMemcpyDeviceToDevice, s->ctx->stream);
-    if (e == hipSuccess) e = hipStreamSynchronize(s->ctx->stream);
     if (e != hipSuccess) {
-        if (p) (void)hipFree(p);
-        return herr(e);
+        *rc = herr(e);
+        return -1;
     }
-    if (s->d_front[which]) (void)hipFree(s->d_front[which]);
-    s->d_front[which] = p;
-    s->front_cap[which] = cap;
-    return 0;
+    s->fb.push_back(p);
+    s->fb_cap.push_back(cap);
+    return (int)s->fb.size() - 1;
+}
+
+// the search ends: its segments go, its frontier buffers stay for the pool
+static void front_release(tspgpu_search *s)
+{
+    s->seg_buf.clear();
+    s->seg_n.clear();
 }
 
 // launch + wait + read the item count the launch produced
@@ -829,13 +861,23 @@ int tspgpu_search_start(tspgpu_search *s)
     if (int rc = build_suffix(s, !s->frontier, &sets)) return rc;
     a = args_of(s);
     a.out = s->d_items[0];
-    if (s->frontier) {  // the live seeds are written as the first frontier (32-byte paths)
-        if (int rc = ensure_front(s, 0, (size_t)s->local_items + 1, 0)) return rc;
-        a.fout = s->d_front[0];
+    int seed_buf = -1;
+    if (s->frontier) {  // the live seeds are written as the first frontier segment (32-byte paths)
+        s->seg_buf.clear();
+        s->seg_n.clear();
+        int rc = 0;
+        seed_buf = front_spare(s, (size_t)s->local_items + 1, &rc);
+        if (seed_buf < 0) return rc;
+        a.fout = s->fb[seed_buf];
     }
     const uint64_t blocks = (s->local_items + kSearchThreads - 1) / kSearchThreads;
     const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>(blocks, (uint64_t)s->ctx->cu_count * 8));
-    return launch_and_count(s, true, grid, a, s->frontier ? sets : 0u);
+    int rc = launch_and_count(s, true, grid, a, s->frontier ? sets : 0u);
+    if (!rc && s->frontier && s->pending) {
+        s->seg_buf.push_back(seed_buf);
+        s->seg_n.push_back(s->pending);
+    }
+    return rc;
 }
 
 // Frontier search, one step: either fold the waiting tails, or expand the
@@ -866,18 +908,29 @@ static int frontier_step(tspgpu_search *s, uint64_t *pending)
         if (pending) *pending = s->pending;
         return 0;
     }
-    const uint64_t T = std::min<uint64_t>({s->pending, s->expand_max, (s->tail_cap - s->tails) / branch});
-    const uint64_t keep = s->pending - T;
-    int rc = ensure_front(s, 1, (size_t)(T * branch + 64), 0);
-    if (rc) return rc;
-    a.fin = s->d_front[0] + keep;
+    // the step's input: the top `want` paths of the stack, over at most four segments
+    const uint64_t want = std::min<uint64_t>({s->pending, s->expand_max, (s->tail_cap - s->tails) / branch});
+    uint64_t T = 0, take[4] = {};
+    int used = 0;
+    for (int k = (int)s->seg_n.size() - 1; k >= 0 && T < want && used < 4; --k, ++used) {
+        const uint64_t c = std::min<uint64_t>(s->seg_n[k], want - T);
+        a.fseg[used] = s->fb[s->seg_buf[k]] + (s->seg_n[k] - c);
+        a.fseg_start[used] = (uint32_t)T;
+        take[used] = c;
+        T += c;
+    }
+    a.nseg = used;
+    int rc = 0;
+    const int ob = front_spare(s, (size_t)(T * branch + 64), &rc);
+    if (ob < 0) return rc;
+    a.fin = a.fseg[0];
     a.fin_count = (uint32_t)T;
     // a few blocks per CU, each over a contiguous run (one slot atomic per block and output)
     // (at most 1024 paths per block: expand_kernel keeps their live masks in registers)
     const uint64_t blocks = std::max<uint64_t>(
         (T + 1023) / 1024, std::max<uint64_t>(1, std::min<uint64_t>((T + 255) / 256, (uint64_t)s->ctx->cu_count * 4)));
     a.fin_per_block = (uint32_t)(((T + blocks - 1) / blocks + 255) / 256 * 256);
-    a.fout = s->d_front[1];
+    a.fout = s->fb[ob];
     e = hipMemsetAsync(s->d_words + 4, 0, 8, st);
     if (e != hipSuccess) return herr(e);
     (void)hipEventRecord(s->e0, st);
@@ -892,17 +945,25 @@ static int frontier_step(tspgpu_search *s, uint64_t *pending)
     ++s->rounds;
     const uint64_t kids = (uint32_t)cnt[0];
     s->tails = (uint32_t)cnt[4];
-    if (keep == 0) {  // the whole frontier was expanded: the children are the frontier
-        std::swap(s->d_front[0], s->d_front[1]);
-        std::swap(s->front_cap[0], s->front_cap[1]);
-    } else if (kids) {  // behind the items not expanded yet
-        rc = ensure_front(s, 0, (size_t)(keep + kids), (size_t)keep);
-        if (rc) return rc;
-        // stream-ordered before the next step's launch: no host wait
-        e = hipMemcpyAsync(s->d_front[0] + keep, s->d_front[1], kids * sizeof(PathItem), hipMemcpyDeviceToDevice, st);
-        if (e != hipSuccess) return herr(e);
+    // the expanded paths leave the top segments (all but the deepest one used
+    // are now empty); their children go on top: appended to the top segment
+    // when few (a small copy), as a segment of their own (no copy) when many
+    for (int u = 0; u < used; ++u) s->seg_n[s->seg_n.size() - 1 - u] -= take[u];
+    while (!s->seg_n.empty() && s->seg_n.back() == 0) {
+        s->seg_buf.pop_back();
+        s->seg_n.pop_back();
     }
-    s->pending = keep + kids;
+    constexpr uint64_t kAppendMax = (uint64_t)1 << 20;
+    if (kids && !s->seg_n.empty() && kids <= kAppendMax && s->fb_cap[s->seg_buf.back()] >= s->seg_n.back() + kids) {
+        e = hipMemcpyAsync(s->fb[s->seg_buf.back()] + s->seg_n.back(), s->fb[ob], kids * sizeof(PathItem),
+                           hipMemcpyDeviceToDevice, st);
+        if (e != hipSuccess) return herr(e);
+        s->seg_n.back() += kids;  // stream-ordered before the next step's launch
+    } else if (kids) {
+        s->seg_buf.push_back(ob);
+        s->seg_n.push_back(kids);
+    }
+    s->pending = s->pending - T + kids;
     if (pending) *pending = s->pending + s->tails;
     return 0;
 }
@@ -1118,16 +1179,24 @@ int tspgpu_search_records(tspgpu_search *s, uint64_t cost_bits, tspgpu_tour_reco
 
 int tspgpu_heuristic_tour(const void *dist, int dtype, int n, double *cost_out, int32_t *tour_out)
 {
+    return tspgpu_heuristic_tour_starts(dist, dtype, n, 0, 1, cost_out, tour_out);
+}
+
+int tspgpu_heuristic_tour_starts(const void *dist, int dtype, int n, int first, int step, double *cost_out,
+                                 int32_t *tour_out)
+{
     int rc = validate_search(dist, dtype, n);
     if (rc) return rc;
+    if (first < 0 || step < 1) return -EINVAL;
+    if (first >= n) return -ENOENT;  // no start city in this range
     std::vector<int32_t> t;
     if (dtype == TSPGPU_F64) {
         double c;
-        heuristic(static_cast<const double *>(dist), n, t, c);
+        heuristic(static_cast<const double *>(dist), n, t, c, first, step);
         if (cost_out) *cost_out = c;
     } else {
         int32_t c;
-        heuristic(static_cast<const int32_t *>(dist), n, t, c);
+        heuristic(static_cast<const int32_t *>(dist), n, t, c, first, step);
         if (cost_out) *cost_out = c;
     }
     if (tour_out) {

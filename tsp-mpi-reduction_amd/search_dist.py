@@ -79,7 +79,14 @@ def solve_sharded(ctx, dist, group=None, depth: int = 0, device=None, exchange_e
 
     S = tspgpu.Search(ctx, dist, shard=rank, nshards=world, depth=depth)
     try:
-        ub, _ = tspgpu.heuristic_tour(dist)  # deterministic: the same bound on every rank
+        if world > 1:
+            # the multi-start tour split over the ranks (start cities r, r+W, ...),
+            # then the MIN of their costs: all starts' bound at 1/W of the host time
+            ub_r, _ = tspgpu.heuristic_tour(dist, first=rank, step=world)
+            word = tspgpu.cost_bits(ub_r, S.dtype) if ub_r is not None else (1 << 63) - 1
+            ub = tspgpu.bits_cost(allmin2(word, 0)[0], S.dtype)
+        else:
+            ub, _ = tspgpu.heuristic_tour(dist)
         S.set_bound(ub)
         t0 = time.perf_counter()
         exchanges = 0

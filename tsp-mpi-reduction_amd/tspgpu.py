@@ -31,6 +31,7 @@ EXPORTED_SYMBOLS = (
     "tspgpu_search_set_bound", "tspgpu_search_start", "tspgpu_search_step", "tspgpu_search_run_all",
     "tspgpu_search_timing", "tspgpu_search_incumbent_device",
     "tspgpu_search_counters", "tspgpu_search_reset_records", "tspgpu_search_records", "tspgpu_heuristic_tour",
+    "tspgpu_heuristic_tour_starts",
     "tspgpu_select_tour",
     # K3
     "tspgpu_merge", "tspgpu_reduce",
@@ -143,6 +144,7 @@ def lib():
         L.tspgpu_search_records.argtypes = [vp, ctypes.c_uint64, ctypes.POINTER(TourRecord), ctypes.c_int,
                                             ctypes.POINTER(ctypes.c_int)]
         L.tspgpu_heuristic_tour.argtypes = [vp, ctypes.c_int, ctypes.c_int, dp, ip]
+        L.tspgpu_heuristic_tour_starts.argtypes = [vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, dp, ip]
         L.tspgpu_select_tour.argtypes = [vp, ctypes.c_int, ctypes.c_int, ctypes.POINTER(TourRecord), ctypes.c_int,
                                          ctypes.c_uint64, ip]
         cp = ctypes.POINTER(City)
@@ -425,14 +427,18 @@ def bits_cost(bits: int, dtype: int):
     return int(np.uint32(bits).view(np.int32))
 
 
-def heuristic_tour(dist):
+def heuristic_tour(dist, first: int = 0, step: int = 1):
+    """Multi-start tour (an upper bound): the start cities first, first+step, ...
+    -> (cost, tour), or (None, None) when the range holds no start city."""
     d, dt = _search_dist(dist)
     n = d.shape[0]
     cost = ctypes.c_double()
     tour = np.zeros(n + 1, dtype=np.int32)
-    rc = lib().tspgpu_heuristic_tour(d.ctypes.data, dt, n, ctypes.byref(cost), _ip(tour))
+    rc = lib().tspgpu_heuristic_tour_starts(d.ctypes.data, dt, n, first, step, ctypes.byref(cost), _ip(tour))
+    if rc == -errno.ENOENT:
+        return None, None
     if rc:
-        raise TspGpuError(rc, "tspgpu_heuristic_tour")
+        raise TspGpuError(rc, "tspgpu_heuristic_tour_starts")
     return cost.value, tour
 
 
