@@ -789,6 +789,8 @@ __global__ __launch_bounds__(256) void expand_kernel(SearchArgs a)
     load_binom(bn);
     __syncthreads();
 
+    // the next step counts its children into the other counter word (no host memset per step)
+    if (a.out_next && blockIdx.x == 0 && threadIdx.x == 0) *a.out_next = 0u;
     const uint32_t full = (uint32_t)((1ull << n) - 1ull) & ~1u;
     const V thr = EThr<V>::of(ENum<V>::val(__hip_atomic_load(a.inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)));
     const uint32_t b0 = blockIdx.x * a.fin_per_block;

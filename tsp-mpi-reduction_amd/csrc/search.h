@@ -104,6 +104,7 @@ struct SearchArgs {
     PathItem *fout;
     PathItem *ftail;
     unsigned int *tail_count;  // items in ftail (tail_kernel reads it on the device)
+    unsigned int *out_next;    // expand_kernel: zeroes the next step's out_count (double-buffered counters)
     unsigned int tail_cap;
     // stronger bounds of the frontier search (expand_kernel):
     //  * bnd2 (sym != 0, symmetric matrices only): per city x the pair

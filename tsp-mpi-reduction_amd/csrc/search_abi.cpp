@@ -111,7 +111,8 @@ struct tspgpu_search {
     // profiles/r02/k2_knobs.log).  Buffers grow on demand.
     unsigned int tail_cap = 1u << 26;
     unsigned int tail_alloc = 0;
-    uint64_t expand_max = (uint64_t)1 << 24;  // frontier items one step expands, at most (TSPGPU_SEARCH_EXPAND_LOG2)
+    uint64_t expand_max = (uint64_t)1 << 24;
+    uint64_t expand_steps = 0;  // frontier expansions so far (parity of the double-buffered child counter)  // frontier items one step expands, at most (TSPGPU_SEARCH_EXPAND_LOG2)
     uint64_t tails = 0;          // items waiting in d_tail
     int rounds = 0;
     double ms = 0.0;             // device time of all seed/round launches
@@ -853,9 +854,10 @@ int tspgpu_search_start(tspgpu_search *s)
     s->cur = 0;
     s->rounds = 0;
     s->tails = 0;
-    if (s->frontier) {
-        hipError_t e = hipMemsetAsync(s->d_words + 8, 0, 8, s->ctx->stream);
+    if (s->frontier) {  // tails (word 8) and the odd steps' child counter (word 9)
+        hipError_t e = hipMemsetAsync(s->d_words + 8, 0, 16, s->ctx->stream);
         if (e != hipSuccess) return herr(e);
+        s->expand_steps = 0;
     }
     uint32_t sets = 0;  // the frontier builds its suffix table in the seed launch
     if (int rc = build_suffix(s, !s->frontier, &sets)) return rc;
@@ -931,19 +933,24 @@ static int frontier_step(tspgpu_search *s, uint64_t *pending)
         (T + 1023) / 1024, std::max<uint64_t>(1, std::min<uint64_t>((T + 255) / 256, (uint64_t)s->ctx->cu_count * 4)));
     a.fin_per_block = (uint32_t)(((T + blocks - 1) / blocks + 255) / 256 * 256);
     a.fout = s->fb[ob];
-    e = hipMemsetAsync(s->d_words + 4, 0, 8, st);
-    if (e != hipSuccess) return herr(e);
+    // children counted in word 9 or 4 by step parity; the kernel zeroes the
+    // other one for the next step (word 9 is zeroed when the frontier starts,
+    // word 4 still holds the seed count then)
+    const int cw = (s->expand_steps & 1) ? 4 : 9;
+    a.out_count = reinterpret_cast<unsigned int *>(s->d_words + cw);
+    a.out_next = reinterpret_cast<unsigned int *>(s->d_words + (13 - cw));
     (void)hipEventRecord(s->e0, st);
     e = launch_expand(a, f64);
     (void)hipEventRecord(s->e1, st);
-    unsigned long long cnt[5] = {};  // words 4..8: children, ..., tails
+    unsigned long long cnt[6] = {};  // words 4..9: children (even steps), ..., tails (8), children (odd steps)
     if (e == hipSuccess) e = hipMemcpyAsync(cnt, s->d_words + 4, sizeof cnt, hipMemcpyDeviceToHost, st);
     if (e == hipSuccess) e = hipStreamSynchronize(st);
     if (e != hipSuccess) return herr(e);
     float ms = 0.f;
     if (hipEventElapsedTime(&ms, s->e0, s->e1) == hipSuccess) s->ms += ms;
     ++s->rounds;
-    const uint64_t kids = (uint32_t)cnt[0];
+    ++s->expand_steps;
+    const uint64_t kids = (uint32_t)cnt[cw - 4];
     s->tails = (uint32_t)cnt[4];
     // the expanded paths leave the top segments (all but the deepest one used
     // are now empty); their children go on top: appended to the top segment
