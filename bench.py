@@ -361,6 +361,31 @@ def k2_exhaustive(ctx, n=14, reps=3):
             "rounds": st["rounds"]}
 
 
+TSPLIB_OPTIMA = {"gr17.tsp": 2085, "ulysses16.tsp": 6859}  # published TSPLIB optima
+
+
+def config4_tsplib(ctx, reps=3):
+    """BASELINE config 4 on the real TSPLIB instances (tests/golden/tsplib):
+    K2 in integer mode, time to the optimal tour and B&B nodes, the cost
+    checked against the published optimum."""
+    out = {}
+    for name, opt in TSPLIB_OPTIMA.items():
+        _, d = tspgpu.read_tsplib(os.path.join(ROOT, "tests", "golden", "tsplib", name))
+        best = None
+        for _ in range(reps):
+            t = time.perf_counter()
+            cost, tour, st = tspgpu.search_solve(ctx, d)
+            wall = (time.perf_counter() - t) * 1e3
+            if best is None or wall < best[0]:
+                best = (wall, cost, tour, st)
+        wall, cost, tour, st = best
+        assert cost == opt, f"{name}: {cost} != published optimum {opt}"
+        out[name] = {"n": int(d.shape[0]), "cost": int(cost), "published_optimum": opt,
+                     "time_to_optimal_ms": wall, "kernel_ms": st["kernel_ms"], "bb_nodes_expanded": st["nodes"],
+                     "tour": [int(x) for x in tour]}
+    return out
+
+
 def k2_instance(n, seed):
     """Config 5's extension instance: n uniform random cities in [0,1000)^2
     (seeded), libm distances like computeDistanceMatrix."""
@@ -693,7 +718,7 @@ def main():
         except Exception as e:  # noqa: BLE001 - the probe must never cost the headline line
             i32 = {"error": f"{type(e).__name__}: {e}"}
 
-    k2 = k2s = exh = None
+    k2 = k2s = exh = tsplib = None
     if not args.no_k2 and os.environ.get("BENCH_K2", "1") != "0":
         try:
             kgroup, backend = k2_group(world, local_rank)
@@ -704,6 +729,10 @@ def main():
                 exh = k2_exhaustive(ctx)
             except Exception as e:  # noqa: BLE001
                 exh = {"error": f"{type(e).__name__}: {e}"}
+            try:
+                tsplib = config4_tsplib(ctx)
+            except Exception as e:  # noqa: BLE001
+                tsplib = {"error": f"{type(e).__name__}: {e}"}
         try:
             k2 = k2_single_instance(ctx, n, kgroup, backend, world)
         except Exception as e:  # noqa: BLE001
@@ -774,6 +803,7 @@ def main():
         "k2_single_instance": k2,
         "k2_strong_scaling": k2s,
         "k2_exhaustive_14": exh,
+        "config4_tsplib": tsplib,
         "k1_i32_extension": i32,
         "device": devname,
         "cus": cu,

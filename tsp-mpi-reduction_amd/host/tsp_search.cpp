@@ -8,6 +8,10 @@
 //                                                         file with NODE_COORD_SECTION
 //   tsp_search --matrix FILE                              n, then n*n distances (all
 //                                                         integers -> integer mode)
+//   tsp_search --tsplib FILE                              a TSPLIB instance (EUC_2D,
+//                                                         CEIL_2D, ATT, GEO or EXPLICIT
+//                                                         weights: integer mode), e.g.
+//                                                         tests/golden/tsplib/gr17.tsp
 //   options: --gpus G (devices 0..G-1)  --solver auto|wide|k1|k2|enum  --verify (n <= 20: K1 too)
 //   (enum: every tour enumerated on one GPU, BASELINE config 2)
 //   auto = K1-wide (the DP with every CU on each layer) up to 31 cities on one
@@ -135,6 +139,101 @@ Instance from_cities(const std::vector<tspgpu_city> &c, bool tsplib_round)
         in.di.resize(in.d.size());
         for (size_t i = 0; i < in.d.size(); ++i) in.di[i] = (int32_t)std::lround(in.d[i]);  // TSPLIB nint
     }
+    return in;
+}
+
+// TSPLIB95 instance -> integer matrix (the same reader as tspgpu.read_tsplib):
+// EDGE_WEIGHT_TYPE EUC_2D / CEIL_2D / ATT / GEO (TSPLIB's integer distance
+// functions; GEO degrees truncated like Concorde) or EXPLICIT with
+// EDGE_WEIGHT_FORMAT FULL_MATRIX / UPPER_ROW / LOWER_ROW / UPPER_DIAG_ROW /
+// LOWER_DIAG_ROW.
+Instance read_tsplib(const char *path)
+{
+    std::ifstream f(path);
+    if (!f) die("cannot open the TSPLIB file");
+    std::string line, kind = "EUC_2D", fmt = "FULL_MATRIX", name = path, section;
+    int n = 0;
+    std::vector<double> xs, ys;
+    std::vector<long> w;
+    auto trim = [](std::string t) {
+        const size_t a = t.find_first_not_of(" \t\r"), b = t.find_last_not_of(" \t\r");
+        return a == std::string::npos ? std::string() : t.substr(a, b - a + 1);
+    };
+    while (std::getline(f, line)) {
+        const std::string t = trim(line);
+        if (t.empty()) continue;
+        if (t == "EOF") break;
+        if (t.rfind("NODE_COORD_SECTION", 0) == 0) { section = "coord"; continue; }
+        if (t.rfind("EDGE_WEIGHT_SECTION", 0) == 0) { section = "weight"; continue; }
+        const std::string first = t.substr(0, t.find_first_of(" \t:"));
+        if (first.size() > 8 && first.compare(first.size() - 8, 8, "_SECTION") == 0) { section = "skip"; continue; }
+        if (section.empty() && t.find(':') != std::string::npos) {
+            const std::string k = trim(t.substr(0, t.find(':'))), v = trim(t.substr(t.find(':') + 1));
+            if (k == "DIMENSION") n = std::atoi(v.c_str());
+            else if (k == "EDGE_WEIGHT_TYPE") kind = v;
+            else if (k == "EDGE_WEIGHT_FORMAT") fmt = v;
+            else if (k == "NAME") name = v;
+            continue;
+        }
+        std::istringstream ss(t);
+        if (section == "coord") {
+            double id, x, y;
+            if (ss >> id >> x >> y) xs.push_back(x), ys.push_back(y);
+        } else if (section == "weight") {
+            double v;
+            while (ss >> v) w.push_back((long)v);
+        }
+    }
+    if (n < 3) die("TSPLIB: DIMENSION must be >= 3");
+    Instance in;
+    in.n = n;
+    in.dtype = TSPGPU_I32;
+    in.di.assign((size_t)n * n, 0);
+    in.what = name;
+    if (kind == "EXPLICIT") {
+        size_t k = 0;
+        for (int i = 0; i < n; ++i) {
+            int j0 = 0, j1 = n;  // columns of row i in the file
+            if (fmt == "UPPER_ROW") j0 = i + 1;
+            else if (fmt == "LOWER_ROW") j1 = i;
+            else if (fmt == "UPPER_DIAG_ROW") j0 = i;
+            else if (fmt == "LOWER_DIAG_ROW") j1 = i + 1;
+            else if (fmt != "FULL_MATRIX") die("TSPLIB: EDGE_WEIGHT_FORMAT not supported");
+            for (int j = j0; j < j1; ++j) {
+                if (k >= w.size()) die("TSPLIB: EDGE_WEIGHT_SECTION too short");
+                in.di[(size_t)i * n + j] = (int32_t)w[k++];
+                if (fmt != "FULL_MATRIX") in.di[(size_t)j * n + i] = (int32_t)w[k - 1];
+            }
+        }
+        return in;
+    }
+    if ((int)xs.size() != n) die("TSPLIB: NODE_COORD_SECTION does not hold DIMENSION cities");
+    auto geo = [](double v) {
+        const double deg = (double)(long)v;
+        return 3.141592 * (deg + 5.0 * (v - deg) / 3.0) / 180.0;
+    };
+    for (int i = 0; i < n; ++i)
+        for (int j = 0; j < n; ++j) {
+            if (i == j) continue;
+            const double dx = xs[i] - xs[j], dy = ys[i] - ys[j];
+            long v;
+            if (kind == "GEO") {
+                const double q1 = std::cos(geo(ys[i]) - geo(ys[j])), q2 = std::cos(geo(xs[i]) - geo(xs[j])),
+                             q3 = std::cos(geo(xs[i]) + geo(xs[j]));
+                v = (long)(6378.388 * std::acos(0.5 * ((1.0 + q1) * q2 - (1.0 - q1) * q3)) + 1.0);
+            } else if (kind == "ATT") {
+                const double r = std::sqrt((dx * dx + dy * dy) / 10.0);
+                const long t = (long)(r + 0.5);
+                v = t < r ? t + 1 : t;
+            } else if (kind == "CEIL_2D") {
+                v = (long)std::ceil(std::sqrt(dx * dx + dy * dy));
+            } else if (kind == "EUC_2D") {
+                v = (long)(std::sqrt(dx * dx + dy * dy) + 0.5);
+            } else {
+                die("TSPLIB: EDGE_WEIGHT_TYPE not supported");
+            }
+            in.di[(size_t)i * n + j] = (int32_t)v;
+        }
     return in;
 }
 
@@ -314,10 +413,10 @@ int solve_enum(const Instance &in, Result &res)
 int main(int argc, char **argv)
 {
     Instance in;
-    bool have = false, verify = false, tsplib_round = false;
+    bool have = false, verify = false, tsplib_round = false, dump = false;
     int gpus = 1, random_n = 0, clusters = 0;
     uint64_t seed = 1;
-    std::string solver = "auto", cities_file, matrix_file;
+    std::string solver = "auto", cities_file, matrix_file, tsplib_file;
     for (int i = 1; i < argc; ++i) {
         const std::string a = argv[i];
         auto next = [&]() -> const char * {
@@ -329,13 +428,15 @@ int main(int argc, char **argv)
         else if (a == "--clustered") clusters = std::atoi(next());
         else if (a == "--cities") cities_file = next();
         else if (a == "--matrix") matrix_file = next();
+        else if (a == "--tsplib") tsplib_file = next();
         else if (a == "--tsplib-round") tsplib_round = true;
         else if (a == "--gpus") gpus = std::atoi(next());
         else if (a == "--solver") solver = next();
         else if (a == "--verify") verify = true;
+        else if (a == "--dump-matrix") dump = true;  // print the instance's matrix and exit (no GPU)
         else {
             std::fprintf(stderr, "usage: tsp_search (--random N [--seed S] [--clustered K] | --cities FILE "
-                                 "[--tsplib-round] | --matrix FILE) [--gpus G] [--solver auto|wide|k1|k2|enum] [--verify]\n");
+                                 "[--tsplib-round] | --matrix FILE | --tsplib FILE) [--gpus G] [--solver auto|wide|k1|k2|enum] [--verify]\n");
             return 1;
         }
     }
@@ -349,8 +450,24 @@ int main(int argc, char **argv)
     } else if (!matrix_file.empty()) {
         in = read_matrix(matrix_file.c_str());
         have = true;
+    } else if (!tsplib_file.empty()) {
+        in = read_tsplib(tsplib_file.c_str());
+        have = true;
     }
-    if (!have) die("no instance (--random, --cities or --matrix)");
+    if (!have) die("no instance (--random, --cities, --matrix or --tsplib)");
+    if (dump) {
+        std::printf("%d\n", in.n);
+        for (int i = 0; i < in.n; ++i) {
+            for (int j = 0; j < in.n; ++j) {
+                if (in.dtype == TSPGPU_I32)
+                    std::printf(j ? " %d" : "%d", in.di[(size_t)i * in.n + j]);
+                else
+                    std::printf(j ? " %.17g" : "%.17g", in.d[(size_t)i * in.n + j]);
+            }
+            std::printf("\n");
+        }
+        return 0;
+    }
     if (gpus < 1) gpus = 1;
     // auto: the DP over the whole GPU (K1-wide) up to 31 cities on one GPU —
     // far fewer operations than branch and bound there — else the search (K2)

@@ -442,6 +442,93 @@ def heuristic_tour(dist, first: int = 0, step: int = 1):
     return cost.value, tour
 
 
+def read_tsplib(path):
+    """A TSPLIB file -> (name, int32 distance matrix): EDGE_WEIGHT_TYPE EUC_2D,
+    CEIL_2D, ATT, GEO (TSPLIB95's integer distance functions; GEO degrees
+    truncated like Concorde) or EXPLICIT (FULL_MATRIX, UPPER_ROW, LOWER_ROW,
+    UPPER_DIAG_ROW, LOWER_DIAG_ROW).  The same reader as bin/tsp_search --tsplib
+    (host/tsp_search.cpp); integer matrices run the exact integer mode."""
+    import math
+
+    hdr, coords, weights, section = {}, [], [], None
+    for line in open(path):
+        t = line.strip()
+        if not t or t == "EOF":
+            if t == "EOF":
+                break
+            continue
+        if t.startswith("NODE_COORD_SECTION"):
+            section = "coord"
+            continue
+        if t.startswith("EDGE_WEIGHT_SECTION"):
+            section = "weight"
+            continue
+        if t.split()[0].endswith("_SECTION"):
+            section = "skip"
+            continue
+        if section is None and ":" in t:
+            k, v = t.split(":", 1)
+            hdr[k.strip().upper()] = v.strip()
+            continue
+        if section == "coord":
+            f = t.split()
+            coords.append((float(f[1]), float(f[2])))
+        elif section == "weight":
+            weights.extend(int(float(x)) for x in t.split())
+    n = int(hdr["DIMENSION"])
+    kind = hdr.get("EDGE_WEIGHT_TYPE", "EUC_2D").upper()
+    d = np.zeros((n, n), dtype=np.int64)
+    if kind == "EXPLICIT":
+        fmt = hdr.get("EDGE_WEIGHT_FORMAT", "FULL_MATRIX").upper()
+        it = iter(weights)
+        for i in range(n):
+            if fmt == "FULL_MATRIX":
+                cols = range(n)
+            elif fmt == "UPPER_ROW":
+                cols = range(i + 1, n)
+            elif fmt == "LOWER_ROW":
+                cols = range(i)
+            elif fmt == "UPPER_DIAG_ROW":
+                cols = range(i, n)
+            elif fmt == "LOWER_DIAG_ROW":
+                cols = range(i + 1)
+            else:
+                raise ValueError(f"EDGE_WEIGHT_FORMAT {fmt} not supported")
+            for j in cols:
+                d[i, j] = next(it)
+                if fmt != "FULL_MATRIX":
+                    d[j, i] = d[i, j]
+    else:
+        if len(coords) != n:
+            raise ValueError("NODE_COORD_SECTION does not hold DIMENSION cities")
+
+        def geo(v):
+            deg = float(int(v))
+            return 3.141592 * (deg + 5.0 * (v - deg) / 3.0) / 180.0
+
+        for i in range(n):
+            for j in range(n):
+                if i == j:
+                    continue
+                (xi, yi), (xj, yj) = coords[i], coords[j]
+                if kind == "GEO":
+                    q1 = math.cos(geo(yi) - geo(yj))
+                    q2 = math.cos(geo(xi) - geo(xj))
+                    q3 = math.cos(geo(xi) + geo(xj))
+                    d[i, j] = int(6378.388 * math.acos(0.5 * ((1.0 + q1) * q2 - (1.0 - q1) * q3)) + 1.0)
+                elif kind == "ATT":
+                    r = math.sqrt(((xi - xj) ** 2 + (yi - yj) ** 2) / 10.0)
+                    t_ = int(r + 0.5)
+                    d[i, j] = t_ + 1 if t_ < r else t_
+                elif kind == "CEIL_2D":
+                    d[i, j] = int(math.ceil(math.sqrt((xi - xj) ** 2 + (yi - yj) ** 2)))
+                elif kind == "EUC_2D":
+                    d[i, j] = int(math.sqrt((xi - xj) ** 2 + (yi - yj) ** 2) + 0.5)
+                else:
+                    raise ValueError(f"EDGE_WEIGHT_TYPE {kind} not supported")
+    return hdr.get("NAME", os.path.basename(path)), d.astype(np.int32)
+
+
 def select_tour(dist, records, cost):
     """The DP's tie rule over the optimal set (tspgpu_select_tour)."""
     d, dt = _search_dist(dist)
