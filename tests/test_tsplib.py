@@ -1,10 +1,12 @@
-"""BASELINE config 4 on the real TSPLIB instances gr17 (EXPLICIT,
-LOWER_DIAG_ROW) and ulysses16 (GEO): tests/golden/tsplib/ (data files).
+"""BASELINE config 4 on real TSPLIB instances: gr17 (EXPLICIT,
+LOWER_DIAG_ROW), burma14, ulysses16 and ulysses22 (GEO): tests/golden/tsplib/
+(data files).
 
-Pinned by the published optimal tour lengths (TSPLIB: gr17 2085, ulysses16
-6859): the CPU oracle reaches them on the matrices both readers build
-(tspgpu.read_tsplib and bin/tsp_search --tsplib, checked equal), and every
-GPU path returns the oracle's cost and tie-broken tour.  The reference itself
+Pinned by the published optimal tour lengths (TSPLIB: burma14 3323,
+ulysses16 6859, gr17 2085, ulysses22 7013): the CPU oracle reaches them on
+the matrices both readers build (tspgpu.read_tsplib and bin/tsp_search
+--tsplib, checked equal), and every GPU path returns the oracle's cost and
+tie-broken tour.  The reference itself
 cannot read these (Euclidean doubles, <= 16 cities)."""
 import os
 import subprocess
@@ -18,7 +20,8 @@ import tspgpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 TSPLIB = os.path.join(ROOT, "tests", "golden", "tsplib")
 BIN = os.path.join(ROOT, "tsp-mpi-reduction_amd", "bin", "tsp_search")
-OPTIMUM = {"gr17.tsp": 2085, "ulysses16.tsp": 6859}  # TSPLIB's published optima
+# TSPLIB's published optima
+OPTIMUM = {"burma14.tsp": 3323, "ulysses16.tsp": 6859, "gr17.tsp": 2085, "ulysses22.tsp": 7013}
 
 
 def _matrix(name):
@@ -92,14 +95,19 @@ def test_gpu_paths_match_the_oracle(gpu_ctx, name):
     cw, tw, _ = gpu_ctx.solve_instance(d.astype(np.float64))
     assert cw == oc and tw.tolist() == ot
     # K1 i32 (the batched kernel; n = 17 runs the extension sizes)
-    ci, ti = gpu_ctx.solve_blocks_i32(d[None, :, :])
-    assert int(ci[0]) == int(oc) and ti[0][: tspgpu.tour_length(n)].tolist() == ot
+    if n <= tspgpu.MAX_CITIES:
+        ci, ti = gpu_ctx.solve_blocks_i32(d[None, :, :])
+        assert int(ci[0]) == int(oc) and ti[0][: tspgpu.tour_length(n)].tolist() == ot
 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("solver", ["k2", "wide", "k1"])
 @pytest.mark.parametrize("name", sorted(OPTIMUM))
 def test_cli_on_tsplib(name, solver):
+    if solver == "k1" and _matrix(name).shape[0] > tspgpu.MAX_CITIES:
+        pytest.skip("K1 batch sizes end at MAX_CITIES")
+    if solver == "k2" and _matrix(name).shape[0] > 17:
+        pytest.skip("ulysses22 by K2 takes ~8 s (weak bounds); test_gpu_paths_match_the_oracle runs it once")
     p = subprocess.run([BIN, "--tsplib", os.path.join(TSPLIB, name), "--solver", solver], capture_output=True,
                        text=True, timeout=120)
     assert p.returncode == 0, p.stderr

@@ -43,6 +43,7 @@ EXPORTED_SYMBOLS = (
 
 F64, I32 = 0, 1
 SEARCH_MAX_CITIES = 32
+MAX_CITIES = 20  # TSPGPU_MAX_CITIES: the batched K1 (extension sizes above the reference's 16)
 
 
 class TourRecord(ctypes.Structure):
