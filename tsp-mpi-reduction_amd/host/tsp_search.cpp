@@ -14,7 +14,7 @@
 //                                                         tests/golden/tsplib/gr17.tsp
 //   options: --gpus G (devices 0..G-1)  --solver auto|wide|k1|k2|enum  --verify (n <= 20: K1 too)
 //   (enum: every tour enumerated on one GPU, BASELINE config 2)
-//   auto = K1-wide (the DP with every CU on each layer) up to 31 cities on one
+//   auto = K1-wide (the DP with every CU on each layer) up to 25 cities on one
 //   GPU, else K2 over the GPUs.
 //
 // City distances are the reference's computeDistanceMatrix (assignment2.h:
@@ -469,10 +469,12 @@ int main(int argc, char **argv)
         return 0;
     }
     if (gpus < 1) gpus = 1;
-    // auto: the DP over the whole GPU (K1-wide) up to 31 cities on one GPU —
-    // far fewer operations than branch and bound there — else the search (K2)
-    // over all GPUs
-    if (solver == "auto") solver = (in.n <= TSPGPU_WIDE_MAX_CITIES && gpus == 1) ? "wide" : "k2";
+    // auto: the DP over the whole GPU (K1-wide) up to 25 cities on one GPU,
+    // else the search (K2) over all GPUs
+    // (with the Lagrangian two-edge bound K2 overtakes the DP from ~25 cities:
+    // n = 28 2.0-2.5 ms vs ~10 ms, n = 30 2.3-5.8 ms vs ~40 ms;
+    // profiles/r02/k2_lagrange.log)
+    if (solver == "auto") solver = (in.n <= 25 && gpus == 1) ? "wide" : "k2";
     if (solver != "k1" && solver != "k2" && solver != "wide" && solver != "enum")
         die("--solver must be auto, wide, k1, k2 or enum");
 
