@@ -616,8 +616,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--n", type=int, default=16, help="cities per block (config 3: 16)")
     ap.add_argument("--blocks-per-gpu", type=int, default=16384)
-    ap.add_argument("--k2-n", type=int, default=30, help="cities of the K2 strong-scaling instance")
-    ap.add_argument("--k2-seed", type=int, default=2)
+    ap.add_argument("--k2-n", type=int, default=32, help="cities of the K2 strong-scaling instance")
+    ap.add_argument("--k2-seed", type=int, default=35)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pmc", action="store_true")
     ap.add_argument("--no-tto", action="store_true", help="skip the time-to-optimal probes")

@@ -112,7 +112,11 @@ struct tspgpu_search {
     // profiles/r02/k2_knobs.log).  Buffers grow on demand.
     unsigned int tail_cap = 1u << 26;
     unsigned int tail_alloc = 0;
-    uint64_t expand_max = (uint64_t)1 << 24;
+    // 2^21: the output buffer of a step holds T x branch paths, and a step's
+    // children can become a segment of their own: at 2^24 a cold 32-city
+    // search spent 1.3 s in hipMalloc (1714 vs 524 ms warm), at 2^21 564 vs
+    // 545 ms (profiles/r02/k2_expand_cap.log)
+    uint64_t expand_max = (uint64_t)1 << 21;
     uint64_t expand_steps = 0;  // frontier expansions so far (parity of the double-buffered child counter)  // frontier items one step expands, at most (TSPGPU_SEARCH_EXPAND_LOG2)
     uint64_t tails = 0;          // items waiting in d_tail
     int rounds = 0;
