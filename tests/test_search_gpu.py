@@ -337,3 +337,26 @@ def test_enum_kernel_record_overflow_second_phase(gpu_ctx, monkeypatch):
     monkeypatch.delenv("TSPGPU_SEARCH_RECORD_CAP")
     oc, ot = O.solve_block(d)
     assert (cost, tour.tolist()) == (oc, ot) and st["phases"] == 2, st
+
+
+@pytest.mark.parametrize("kind", ["random", "clustered", "ties"])
+def test_lagrangian_two_edge_bound_keeps_the_answer(gpu_ctx, monkeypatch, kind):
+    """The Lagrangian city weights only change which nodes are pruned: with
+    and without them (TSPGPU_SEARCH_LAGRANGE) the search returns the DP's cost
+    and tour (K1-wide) on random and clustered instances of 17-21 cities and
+    tie-heavy ones of 13-17."""
+    rng = np.random.default_rng({"random": 1, "clustered": 2, "ties": 3}[kind])
+    for n in ((13, 15, 17) if kind == "ties" else (17, 19, 21)):
+        if kind == "random":
+            xy = rng.uniform(0, 1000, size=(n, 2))
+        elif kind == "clustered":
+            c = rng.uniform(100, 900, size=(3, 2))
+            xy = c[np.arange(n) % 3] + rng.normal(0, 40, size=(n, 2))
+        else:
+            xy = rng.integers(0, 6, size=(n, 2)).astype(np.float64)
+        d = tspgpu.distance_matrix([[(i, xy[i, 0], xy[i, 1]) for i in range(n)]])[0]
+        wc, wt, _ = gpu_ctx.solve_instance(d)
+        for lag in ("1", "0"):
+            monkeypatch.setenv("TSPGPU_SEARCH_LAGRANGE", lag)
+            cost, tour, st = tspgpu.search_solve(gpu_ctx, d)
+            assert cost == wc and tour.tolist() == wt.tolist(), (kind, n, lag, st)
