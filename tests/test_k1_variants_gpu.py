@@ -90,9 +90,9 @@ def test_n16_large_batch_every_variant(variant):
     assert used == (5 if variant is None else variant)
 
 
-@pytest.mark.parametrize("n,vb,expect", [(14, 8, 5), (15, 8, 5), (13, 8, 2), (16, 4, 5), (15, 4, 2)])
+@pytest.mark.parametrize("n,vb,expect", [(13, 8, 5), (14, 8, 5), (15, 8, 5), (12, 8, 2), (16, 4, 5), (15, 4, 2)])
 def test_large_batch_default_per_size(n, vb, expect):
-    """The large-batch default at each size (tspgpu.cpp: tiled at 14-16
+    """The large-batch default at each size (tspgpu.cpp: tiled at 13-16
     cities f64 and 16 cities i32, the compact layer pass elsewhere), every
     block against the oracle."""
     d = _blocks(n, B_BIG, 40 + n)

@@ -38,6 +38,10 @@ CFGS = [
     (19, "int32_t", 15, 10, 256, 1, 6),
     (21, "int32_t", 15, 11, 256, 1, 5),
     (24, "int32_t", 14, 10, 256, 1, 6),
+    (26, "double", 12, 10, 256, 1, 6),
+    (25, "double", 12, 9, 256, 1, 8),
+    (27, "int32_t", 14, 10, 256, 1, 8),
+    (28, "int32_t", 13, 10, 256, 1, 8),
 ]
 
 

@@ -20,7 +20,8 @@ from bench import Shard  # noqa: E402
 
 CFGS = {0: (16, 8), 1: (16, 8), 2: (16, 8), 3: (16, 8), 4: (16, 8), 5: (15, 8), 6: (15, 8), 7: (16, 4), 8: (16, 4),
         9: (15, 4), 10: (14, 8), 11: (16, 8), 12: (16, 8), 13: (16, 8), 14: (16, 8), 15: (16, 8), 16: (16, 8), 17: (16, 8), 18: (16, 8), 19: (16, 4),
-        20: (16, 4), 21: (16, 4), 22: (15, 8), 23: (14, 8), 24: (15, 4)}
+        20: (16, 4), 21: (16, 4), 22: (15, 8), 23: (14, 8), 24: (15, 4), 25: (13, 8), 26: (13, 8),
+        27: (15, 4), 28: (14, 4)}
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 16384
 which = [int(x) for x in sys.argv[2:]] or sorted(CFGS)
 

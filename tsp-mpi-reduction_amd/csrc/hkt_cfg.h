@@ -30,7 +30,11 @@
     X(18, double, 15, 10, 256, 1, 7) \
     X(19, int32_t, 15, 10, 256, 1, 6) \
     X(21, int32_t, 15, 11, 256, 1, 5) \
-    X(24, int32_t, 14, 10, 256, 1, 6)
+    X(24, int32_t, 14, 10, 256, 1, 6) \
+    X(26, double, 12, 10, 256, 1, 6) \
+    X(25, double, 12, 9, 256, 1, 8) \
+    X(27, int32_t, 14, 10, 256, 1, 8) \
+    X(28, int32_t, 13, 10, 256, 1, 8)
 
 namespace tspgpu {
 struct TiledCfg {

@@ -303,12 +303,13 @@ int solve_device_unordered(tspgpu_ctx *c, const void *d_dist, int n, int nblocks
         // (with a full wave of blocks: one block alone is latency-bound and the
         // argmin's extra VALU only costs there)
         // a full wave of blocks: the sub-cube tiled kernel (variant 5,
-        // hk_tiled.h) at 14-16 cities f64 and 16 cities i32; per 16384 blocks
-        // (profiles/r02/k1_tiled_v17_cfgs.log): n = 16 f64 7.6 vs 12.0 ms
-        // (variant 4), n = 15 3.75 vs 4.59, n = 14 1.80 vs 2.20, n = 16 i32
-        // 5.72 vs 7.63 (variant 2); the compact layer pass (variant 2) stays
-        // ahead below 14 cities and for i32 at 15 (2.95 vs 2.70 ms)
-        const bool tiled = vbytes == 8 ? (N >= 13 && N <= 15) : N == 15;
+        // hk_tiled.h) at 13-16 cities f64 and 16 cities i32; per 16384 blocks
+        // (profiles/r02/k1_tiled_v17_cfgs.log, k1_tiled_v19_small.log): n = 16
+        // f64 7.6 vs 12.0 ms (variant 4), n = 15 3.75 vs 4.59, n = 14 1.80 vs
+        // 2.20, n = 13 0.88 vs 1.06, n = 16 i32 5.72 vs 7.63 (variant 2); the
+        // compact layer pass (variant 2) stays ahead below 13 cities and for
+        // i32 at 14-15 (1.34 vs 1.38, 2.78 vs 2.74 ms)
+        const bool tiled = vbytes == 8 ? (N >= 12 && N <= 15) : N == 15;
         a.variant = c->variant >= 0 ? c->variant : (tiled && nblocks >= c->cu_count ? 5 : 2);
         if (a.variant == 5) {
             if (const TiledCfg *cfg = pick_tiled(c, N, vbytes))
