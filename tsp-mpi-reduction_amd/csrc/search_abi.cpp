@@ -122,6 +122,7 @@ struct tspgpu_search {
     int rounds = 0;
     double ms = 0.0;             // device time of all seed/round launches
     hipEvent_t e0 = nullptr, e1 = nullptr;
+    unsigned long long *h_cnt = nullptr;  // pinned host words: the frontier step's counter readback
 };
 
 namespace {
@@ -429,6 +430,7 @@ struct SearchPool {
     PathItem *d_tail = nullptr;
     unsigned int tail_alloc = 0;
     hipEvent_t e0 = nullptr, e1 = nullptr;
+    unsigned long long *h_cnt = nullptr;
     void *d_bnd2 = nullptr;
     double *d_hsuf = nullptr;
     size_t hsuf_alloc = 0;
@@ -455,6 +457,7 @@ void move_buffers(A &to, B &from)
     to.tail_alloc = from.tail_alloc, from.tail_alloc = 0;
     to.e0 = from.e0, from.e0 = nullptr;
     to.e1 = from.e1, from.e1 = nullptr;
+    to.h_cnt = from.h_cnt, from.h_cnt = nullptr;
     to.d_bnd2 = from.d_bnd2, from.d_bnd2 = nullptr;
     to.d_hsuf = from.d_hsuf, from.d_hsuf = nullptr;
     to.hsuf_alloc = from.hsuf_alloc, from.hsuf_alloc = 0;
@@ -478,6 +481,7 @@ void free_buffers(A &b)
     if (b.d_tail) (void)hipFree(b.d_tail);
     if (b.e0) (void)hipEventDestroy(b.e0);
     if (b.e1) (void)hipEventDestroy(b.e1);
+    if (b.h_cnt) (void)hipHostFree(b.h_cnt);
     if (b.d_bnd2) (void)hipFree(b.d_bnd2);
     if (b.d_hsuf) (void)hipFree(b.d_hsuf);
     SearchPool z;
@@ -721,6 +725,8 @@ int tspgpu_search_create(tspgpu_ctx *c, const void *dist, int dtype, int n, int 
     if (e == hipSuccess) e = hipStreamSynchronize(st);
     if (e == hipSuccess && !s->e0) e = hipEventCreate(&s->e0);
     if (e == hipSuccess && !s->e1) e = hipEventCreate(&s->e1);
+    if (e == hipSuccess && !s->h_cnt && !std::getenv("TSPGPU_SEARCH_PAGEABLE"))
+        e = hipHostMalloc((void **)&s->h_cnt, 8 * sizeof(unsigned long long), hipHostMallocDefault);
     if (e != hipSuccess) {
         tspgpu_search_destroy(s);
         return herr(e);
@@ -1028,8 +1034,11 @@ static int frontier_step(tspgpu_search *s, uint64_t *pending)
     (void)hipEventRecord(s->e0, st);
     e = launch_expand(a, f64);
     (void)hipEventRecord(s->e1, st);
-    unsigned long long cnt[6] = {};  // words 4..9: children (even steps), ..., tails (8), children (odd steps)
-    if (e == hipSuccess) e = hipMemcpyAsync(cnt, s->d_words + 4, sizeof cnt, hipMemcpyDeviceToHost, st);
+    // words 4..9: children (even steps), ..., tails (8), children (odd steps);
+    // read into pinned host memory (a direct DMA, no staging copy)
+    unsigned long long local[6] = {};
+    unsigned long long *cnt = s->h_cnt ? s->h_cnt : local;
+    if (e == hipSuccess) e = hipMemcpyAsync(cnt, s->d_words + 4, 6 * sizeof(unsigned long long), hipMemcpyDeviceToHost, st);
     if (e == hipSuccess) e = hipStreamSynchronize(st);
     if (e != hipSuccess) return herr(e);
     float ms = 0.f;
