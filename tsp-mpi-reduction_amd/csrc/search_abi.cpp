@@ -449,8 +449,10 @@ void move_buffers(A &to, B &from)
         to.d_items[i] = from.d_items[i], from.d_items[i] = nullptr;
         to.item_cap[i] = from.item_cap[i], from.item_cap[i] = 0;
     }
-    to.fb.swap(from.fb);
-    to.fb_cap.swap(from.fb_cap);
+    for (PathItem *p : to.fb)  // (never non-empty at the call sites; freed rather than leaked)
+        if (p) (void)hipFree(p);
+    to.fb = std::move(from.fb);
+    to.fb_cap = std::move(from.fb_cap);
     from.fb.clear();
     from.fb_cap.clear();
     to.d_tail = from.d_tail, from.d_tail = nullptr;
