@@ -68,7 +68,8 @@ constexpr int kTiledDS = TSPGPU_TILED_DS;
 //   1 high-member values from LDS, 2 d values from a register, 4 no barrier
 //   between the passes of a sub-cube, 8 plain minimum (no argmin), 32 no
 //   backtracking, 64 backtracking kernel stops after staging, 128 no recompute,
-//   1024 no sub-cube reordering of the distance table (TSPGPU_TILED_PERM)
+//   1024 no sub-cube reordering of the distance table (TSPGPU_TILED_PERM),
+//   2048 / 4096 skip the passes with j <= 1 or >= L-1 / j <= 2 or >= L-2
 #ifndef TSPGPU_TILED_ABL
 #define TSPGPU_TILED_ABL 0
 #endif
@@ -97,6 +98,20 @@ constexpr int kTiledDS = TSPGPU_TILED_DS;
 // wave 0's path costs more (7.79-7.81 ms vs 7.58-7.61 without): off.
 #ifndef TSPGPU_TILED_PERM
 #define TSPGPU_TILED_PERM 0
+#endif
+// Destination-parallel passes: a pass whose (row, destination) pairs fit the
+// workgroup's threads at once (j <= 1 and j >= L - 1 at L = 10: 1-10 rows)
+// gives every pair its own lane — T relaxations per lane instead of a T x Q
+// chain on one lane while the other waves wait at the barrier.  Those four
+// passes hold 13% of the relaxations but took 20% of the kernel time
+// (skipping them: 7.57 -> 6.04 ms, profiles/r02/k1_tiled_small_pass_ablation.log).
+// Measured slower, so off: parity holds but cfg 14 goes 7.61 -> 9.02 ms (bit 1,
+// passes j <= 1), 10.31 (bit 2, j >= L - 1), 11.41 ms (both), because the
+// extra pass bodies push the whole fused kernel's register allocation into
+// spills (VGPR spills 19 -> 28 / 54 / 61, scratch ops 47 -> 125 / 186;
+// profiles/r02/k1_tiled_dp_sweep.log).
+#ifndef TSPGPU_TILED_DP
+#define TSPGPU_TILED_DP 0
 #endif
 
 // host-built tables of one L (device copy, staged into LDS per workgroup)
@@ -448,6 +463,137 @@ __device__ __forceinline__ void tiled_pass(const TiledCtx<V, N, L, R> &c, uint32
     }
 }
 
+__host__ __device__ constexpr int pow2_at_least(int q)
+{
+    int p = 1;
+    while (p < q) p *= 2;
+    return p;
+}
+
+// Destination-parallel form of tiled_pass (TSPGPU_TILED_DP): thread t owns the
+// pair (row r = t / QP, destination q = t % QP), QP = Q rounded up to a power
+// of two so that a row's lanes never straddle a wave.  The lane loads its
+// row's values, finds its destination k (the q-th non-member: low ones
+// ascending, then the high ones) and takes the same T relaxations, in the
+// same member order (the first strict minimum), as the row-owner pass does
+// for k; stores go to the same places.  In the top rows (the argmin kept)
+// the row's parent word is OR-reduced over its QP lanes and stored by lane 0.
+template <typename V, int N, int L, int T, int J, int THREADS, int R>
+__device__ __forceinline__ void tiled_pass_dp(const TiledCtx<V, N, L, R> &c, uint32_t h, uint32_t tid)
+{
+    constexpr int H = N - L;
+    constexpr int Q = N - T;
+    constexpr int HC = T - J;
+    constexpr int QL = L - J;
+    constexpr int QH = Q - QL;
+    constexpr int QP = pow2_at_least(Q);
+    constexpr int NL = 1 << L;
+    constexpr int VB = sizeof(V);
+    constexpr int ROWS = cbinom(L, J);
+    constexpr int BASE = tiled_moff(L, J);
+    constexpr int ROWS_N = J < L ? cbinom(L, J + 1) : 0;
+    constexpr int REGV = tiled_region_vals(L);
+    constexpr int CUR = (J & 1) ? REGV - ROWS * J : 0;
+    constexpr int NXT = ((J + 1) & 1) ? REGV - ROWS_N * (J + 1) : 0;
+    constexpr bool ARG = T >= N - TSPGPU_TILED_TA_OFF && !(TSPGPU_TILED_ABL & 8);
+    constexpr int SK = __builtin_ctz((unsigned)(R * VB));
+    constexpr uint32_t DROW = (uint32_t)(kTiledDS * R * VB);
+    static_assert(QP <= 64 && ROWS * QP <= THREADS, "destination-parallel pass: one pair per thread");
+    const uint32_t lane_off = (tid & (uint32_t)(R - 1)) * VB;
+    const char *drb = reinterpret_cast<const char *>(c.dr);
+    char *lds_nxt = reinterpret_cast<char *>(c.region + NXT);
+    const uint32_t r = tid / QP, q = tid % QP;
+    if (r >= (uint32_t)ROWS) return;  // (whole groups of QP lanes: the reduction below stays inside active lanes)
+    const bool act = q < (uint32_t)Q;
+    const uint32_t l = c.lmask[BASE + r];
+    const uint32_t voff = (BASE + r) * VB;
+    // this lane's destination: the q-th non-member of the row (low ones first)
+    uint32_t k = 0, cb = 0;
+    {
+        uint32_t nb = ~l & (uint32_t)(NL - 1);
+#pragma unroll
+        for (int i = 0; i < QL; ++i) {
+            if ((uint32_t)i == q) k = (uint32_t)__builtin_ctz(nb);
+            nb &= nb - 1u;
+        }
+        uint32_t hb = ~h & ((1u << H) - 1u);
+#pragma unroll
+        for (int i = 0; i < QH; ++i) {
+            if ((uint32_t)(QL + i) == q) cb = (uint32_t)__builtin_ctz(hb), k = L + cb;
+            hb &= hb - 1u;
+        }
+    }
+    const char *dk = drb + lane_off + (k << SK);
+    // members streamed in the row-owner pass's order (low ascending, then the
+    // high ones), each value and distance used once: no per-row arrays
+    V acc = V(0);
+    uint32_t arg = 0;
+    if (act) {
+        uint32_t lb = l;
+#pragma unroll
+        for (int p = 0; p < J; ++p) {
+            const uint32_t m = (uint32_t)__builtin_ctz(lb) * DROW;
+            lb &= lb - 1u;
+            const V g = c.region[CUR + p * ROWS + r];
+            const V d = *reinterpret_cast<const V *>(dk + m);
+            if (p == 0) {
+                acc = g + d;
+                arg = m;
+            } else if constexpr (ARG) {
+                relax_argmin(acc, arg, g, d, m);
+            } else {
+                relax_min(acc, g, d);
+            }
+            __builtin_amdgcn_sched_barrier(0);  // (as in tiled_pass: no hoisting of every load)
+        }
+        uint32_t hb = h;
+#pragma unroll
+        for (int i = 0; i < HC; ++i) {
+            const uint32_t hm = (uint32_t)__builtin_ctz(hb);
+            hb &= hb - 1u;
+            const uint32_t m = (L + hm) * DROW;
+            const V g = c.push.load(voff, (h * H + hm) * (uint32_t)(NL * VB));
+            const V d = *reinterpret_cast<const V *>(dk + m);
+            if (J == 0 && i == 0) {
+                acc = g + d;
+                arg = m;
+            } else if constexpr (ARG) {
+                relax_argmin(acc, arg, g, d, m);
+            } else {
+                relax_min(acc, g, d);
+            }
+            __builtin_amdgcn_sched_barrier(0);  // (as in tiled_pass: no hoisting of every load)
+        }
+        if (q < (uint32_t)QL) {  // low k -> the next LDS layer (position k - q)
+            const uint32_t rb = c.lrankb[l | (1u << k)];
+            *reinterpret_cast<V *>(lds_nxt + (k - q) * (uint32_t)(ROWS_N * VB) + rb) = acc;
+        } else {  // high k -> the push column of sub-cube h | k
+            c.push.store(voff, ((h | (1u << cb)) * H + cb) * (uint32_t)(NL * VB), acc);
+        }
+    }
+    if constexpr (ARG) {
+        uint64_t w = act ? (uint64_t)(arg / DROW) << (4 * q) : 0ull;
+#pragma unroll
+        for (int off = 1; off < QP; off *= 2) {
+            const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)w, off);
+            const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(w >> 32), off);
+            w |= ((uint64_t)hi << 32) | lo;
+        }
+        if (q == 0) c.par.store((BASE + r) * 8u, h * (uint32_t)(NL * 8), w);
+    }
+}
+
+template <typename V, int N, int L, int T, int J, int THREADS, int R>
+__device__ __forceinline__ void tiled_pass_any(const TiledCtx<V, N, L, R> &c, uint32_t h, uint32_t tid)
+{
+    constexpr int Q = N - T;
+    constexpr int DPB = J <= 1 ? 1 : 2;  // TSPGPU_TILED_DP bit 1: the first passes, bit 2: the last ones
+    if constexpr ((TSPGPU_TILED_DP & DPB) && !TSPGPU_TILED_PERM && Q >= 2 && cbinom(L, J) * pow2_at_least(Q) <= THREADS)
+        tiled_pass_dp<V, N, L, T, J, THREADS, R>(c, h, tid);
+    else
+        tiled_pass<V, N, L, T, J, THREADS, R>(c, h, tid);
+}
+
 // Parallel bit deposit: the i-th set bit of m receives bit i of x.
 __device__ __forceinline__ uint32_t pdep_u32(uint32_t x, uint32_t m)
 {
@@ -640,7 +786,7 @@ __device__ __forceinline__ void tiled_dispatch_h(const TiledCtx<V, N, L, R> &c, 
 #define TSPGPU_TP(HC)                                                                      \
     case HC:                                                                               \
         if constexpr (HC <= H && J + HC >= 1 && J + HC < N)                                \
-            tiled_pass<V, N, L, J + HC, J, THREADS, R>(c, h, tid);                         \
+            tiled_pass_any<V, N, L, J + HC, J, THREADS, R>(c, h, tid);                     \
         break;
     switch (hc) {
         TSPGPU_TP(0) TSPGPU_TP(1) TSPGPU_TP(2) TSPGPU_TP(3) TSPGPU_TP(4) TSPGPU_TP(5) TSPGPU_TP(6)
@@ -731,6 +877,8 @@ __global__ __launch_bounds__(THREADS, tiled_waves(THREADS, WG)) void hk_tiled_ke
             const int j0 = h == 0 ? 1 : 0;
             const int j1 = h == (uint32_t)(NH - 1) ? L - 1 : L;
             for (int j = j0; j <= j1; ++j) {
+                if ((TSPGPU_TILED_ABL & 2048) && (j <= 1 || j >= L - 1)) continue;
+                if ((TSPGPU_TILED_ABL & 4096) && (j <= 2 || j >= L - 2)) continue;
                 tiled_dispatch<V, N, L, THREADS, R>(c, h, hc, j, tid);
                 if (!(TSPGPU_TILED_ABL & 4) && j < j1) lds_barrier();
             }
