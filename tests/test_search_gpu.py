@@ -360,3 +360,56 @@ def test_lagrangian_two_edge_bound_keeps_the_answer(gpu_ctx, monkeypatch, kind):
             monkeypatch.setenv("TSPGPU_SEARCH_LAGRANGE", lag)
             cost, tour, st = tspgpu.search_solve(gpu_ctx, d)
             assert cost == wc and tour.tolist() == wt.tolist(), (kind, n, lag, st)
+
+
+@pytest.mark.parametrize("kind", ["random", "clustered", "ties", "integer"])
+def test_tree_bound_keeps_the_answer(gpu_ctx, monkeypatch, kind):
+    """The Held-Karp tree bound (TSPGPU_SEARCH_MST, on at paths with >= 12
+    cities left by default, TSPGPU_SEARCH_MST_MINREM=0: at every level) only
+    changes which paths are pruned: off, default and everywhere, the search
+    returns the DP's cost and tie-broken tour (K1-wide) on random, clustered,
+    tie-heavy and integer (i32 search) instances of 13-25 cities."""
+    rng = np.random.default_rng({"random": 11, "clustered": 12, "ties": 13, "integer": 14}[kind])
+    for n in ((13, 16, 19) if kind in ("ties", "integer") else (18, 22, 25)):
+        if kind == "clustered":
+            c = rng.uniform(100, 900, size=(3, 2))
+            xy = c[np.arange(n) % 3] + rng.normal(0, 40, size=(n, 2))
+        elif kind == "ties":
+            xy = rng.integers(0, 6, size=(n, 2)).astype(np.float64)
+        else:
+            xy = rng.uniform(0, 1000, size=(n, 2))
+        d = tspgpu.distance_matrix([[(i, xy[i, 0], xy[i, 1]) for i in range(n)]])[0]
+        if kind == "integer":
+            d = np.rint(d).astype(np.int32)
+        wc, wt, _ = gpu_ctx.solve_instance(np.asarray(d, dtype=np.float64))
+        for mst, minrem in (("0", None), ("1", None), ("1", "0")):
+            monkeypatch.setenv("TSPGPU_SEARCH_MST", mst)
+            if minrem is None:
+                monkeypatch.delenv("TSPGPU_SEARCH_MST_MINREM", raising=False)
+            else:
+                monkeypatch.setenv("TSPGPU_SEARCH_MST_MINREM", minrem)
+            cost, tour, st = tspgpu.search_solve(gpu_ctx, d)
+            assert cost == wc and tour.tolist() == wt.tolist(), (kind, n, mst, minrem, st)
+
+
+def test_tree_bound_on_the_hard_32_city_seeds(gpu_ctx, monkeypatch):
+    """bench.k2_instance(32, s) for the seeds whose two-edge bound left a
+    heavy tail (35: 0.5 s without the tree bound; 14 and 20: 11-14 s): with
+    the tree bound each is solved in well under a second, the same answer at
+    every gating level, and seed 35 also equals the search without it."""
+    from bench import k2_instance
+
+    for seed in (35, 14, 20):
+        d = k2_instance(32, seed)
+        got = []
+        for minrem in ("12", "0"):
+            monkeypatch.setenv("TSPGPU_SEARCH_MST_MINREM", minrem)
+            cost, tour, st = tspgpu.search_solve(gpu_ctx, d)
+            assert st["kernel_ms"] < 500, st
+            got.append((cost, tour.tolist()))
+        assert got[0] == got[1], seed
+        if seed == 35:
+            monkeypatch.setenv("TSPGPU_SEARCH_MST", "0")
+            cost, tour, _ = tspgpu.search_solve(gpu_ctx, d)
+            monkeypatch.delenv("TSPGPU_SEARCH_MST")
+            assert (cost, tour.tolist()) == got[0]

@@ -106,8 +106,6 @@ def test_gpu_paths_match_the_oracle(gpu_ctx, name):
 def test_cli_on_tsplib(name, solver):
     if solver == "k1" and _matrix(name).shape[0] > tspgpu.MAX_CITIES:
         pytest.skip("K1 batch sizes end at MAX_CITIES")
-    if solver == "k2" and _matrix(name).shape[0] > 17:
-        pytest.skip("ulysses22 by K2 takes ~8 s (weak bounds); test_gpu_paths_match_the_oracle runs it once")
     p = subprocess.run([BIN, "--tsplib", os.path.join(TSPLIB, name), "--solver", solver], capture_output=True,
                        text=True, timeout=120)
     assert p.returncode == 0, p.stderr

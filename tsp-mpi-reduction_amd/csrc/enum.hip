@@ -711,6 +711,49 @@ __device__ __forceinline__ uint32_t hlevel_live(const SearchArgs &a, const V *dl
     return live;
 }
 
+// Held-Karp tree bound of the rest of a path (SearchArgs::mst): the path from
+// tail city k over the cities rem back to 0, on d' = d + pi_x + pi_y, is a
+// first edge k -> x, a Hamiltonian path over rem (a spanning tree of rem)
+// and a last edge y -> 0, and its d'-cost is its d-cost + pi_k + pi_0 +
+// 2 sum_rem pi; so its d-cost is at least MST'(rem) + min_x d'[k][x] +
+// min_y d'[y][0] - pi_k - pi_0 - 2 sum_rem pi (k = 0 at the root: the same
+// for the whole tour).  Prim's algorithm per lane, the keys of the (at most
+// 31) cities in registers, indexed by city; rem non-empty.
+__device__ __forceinline__ double tree_bound(const double *dm, const double *pim, int k, uint32_t rem)
+{
+    double ek = 1.0e300, e0 = 1.0e300, ps = pim[k] + pim[0];
+    for (uint32_t x = rem; x; x &= x - 1u) {
+        const int t = __builtin_ctz(x);
+        ps += 2.0 * pim[t];
+        const double a = dm[k * kTRow + t], b = dm[t];
+        ek = a < ek ? a : ek;
+        e0 = b < e0 ? b : e0;
+    }
+    double key[kSearchMaxN];
+#pragma unroll
+    for (int v = 0; v < kSearchMaxN; ++v) key[v] = 1.0e300;
+    uint32_t todo = rem & (rem - 1u);
+    int u = __builtin_ctz(rem);
+    double tot = 0.0;
+    while (todo) {
+        double best = 1.0e300;
+        int bi = 0;
+#pragma unroll
+        for (int v = 1; v < kSearchMaxN; ++v) {  // (city 0 is never in rem)
+            if ((todo >> v) & 1u) {
+                const double w = dm[u * kTRow + v];
+                const double kv = w < key[v] ? w : key[v];
+                key[v] = kv;
+                if (kv < best) best = kv, bi = v;
+            }
+        }
+        tot += best;
+        todo &= ~(1u << bi);
+        u = bi;
+    }
+    return tot + ek + e0 - ps;
+}
+
 // The bound of child j of path (c, k, rem) (rem includes j), any of:
 //   B0: every city still to be entered pays its cheapest incoming edge;
 //   B1 (symmetric matrices): e[j] + sum over rem \ j of b + e[0];
@@ -718,8 +761,8 @@ __device__ __forceinline__ uint32_t hlevel_live(const SearchArgs &a, const V *dl
 //       d[j][x] + H[rem \ j][x], the exact cheapest completion up to rounding.
 template <typename V, int TL>
 __device__ __forceinline__ Expand<V> expand_eval(const SearchArgs &a, const V *dl, const V *am, const V *b2,
-                                                 const uint32_t (*bn)[8], uint32_t full, uint32_t idx, uint32_t end,
-                                                 V thr)
+                                                 const uint32_t (*bn)[8], const double *dm, uint32_t full,
+                                                 uint32_t idx, uint32_t end, V thr)
 {
     Expand<V> e;
     const bool act = idx < end;
@@ -745,6 +788,13 @@ __device__ __forceinline__ Expand<V> expand_eval(const SearchArgs &a, const V *d
         e.live = act ? hlevel_live<V, TL>(a, dl, am, b2, bn, c, k, e.rem, remA, remB, thr, e.ub) : 0u;
         e.hnodes = act ? (uint32_t)((TL + 1) * TL) : 0u;
         return e;
+    }
+    // the tree bound of the whole rest (all children at once); its margin
+    // dm[kSearchMaxN * kTRow + kSearchMaxN] covers the device's rounding
+    if (a.mst && !a.noprune && act && e.rem && __builtin_popcount(e.rem) >= a.mst_min_rem) {
+        const double lb = (double)c + tree_bound(dm, dm + kSearchMaxN * kTRow, k, e.rem) -
+                          dm[kSearchMaxN * kTRow + kSearchMaxN];
+        if (lb > (double)thr) return e;  // e.live = 0: no child survives
     }
     for (uint32_t x = e.rem; x; x &= x - 1u) {
         const int j = __builtin_ctz(x);
@@ -787,6 +837,13 @@ __global__ __launch_bounds__(256) void expand_kernel(SearchArgs a)
     if (a.sym)
         for (int i = threadIdx.x; i < 2 * n; i += blockDim.x) b2[i] = static_cast<const V *>(a.bnd2)[i];
     load_binom(bn);
+    // the tree bound's d' (kTRow rows), pi and margin
+    __shared__ double dm[kSearchMaxN * kTRow + kSearchMaxN + 1];
+    if (a.mst) {
+        for (int i = threadIdx.x; i < n * n; i += blockDim.x) dm[(i / n) * kTRow + i % n] = a.mst[i];
+        for (int i = threadIdx.x; i < n; i += blockDim.x) dm[kSearchMaxN * kTRow + i] = a.mst[n * n + i];
+        if (threadIdx.x == 0) dm[kSearchMaxN * kTRow + kSearchMaxN] = a.mst[n * n + n];
+    }
     __syncthreads();
 
     // the next step counts its children into the other counter word (no host memset per step)
@@ -808,7 +865,7 @@ __global__ __launch_bounds__(256) void expand_kernel(SearchArgs a)
         const uint32_t base = b0 + 256u * t;
         lv[t] = 0;
         if (base >= b1) continue;
-        const Expand<V> e = expand_eval<V, TL>(a, dl, am, b2, bn, full, base + threadIdx.x, b1, thr);
+        const Expand<V> e = expand_eval<V, TL>(a, dl, am, b2, bn, dm, full, base + threadIdx.x, b1, thr);
         lv[t] = e.live;
         const uint32_t cnt = (uint32_t)__builtin_popcount(e.live);
         if (e.len == a.tail_level) cT += cnt; else cF += cnt;  // children have len inner cities

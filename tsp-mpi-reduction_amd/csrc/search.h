@@ -118,6 +118,14 @@ struct SearchArgs {
     //    (place of x in U).
     const void *bnd2;
     int sym;
+    //  * mst (symmetric matrices, may be null): the Held-Karp (1-tree)
+    //    city weights pi and d'[x][y] = d[x][y] + pi_x + pi_y, as doubles:
+    //    mst[0 .. n*n) = d', mst[n*n .. n*n+n) = pi, mst[n*n+n] = a margin for
+    //    the rounding of the device's sums.  A path from k over R to 0 costs
+    //    at least MST'(R) + min_{x in R} d'[k][x] + min_{y in R} d'[y][0]
+    //    - pi_k - pi_0 - 2 sum_R pi (expand_kernel: the tree bound).
+    const double *mst;
+    int mst_min_rem;  // the tree bound only for paths with at least this many cities left
     const double *hsuf;
     int hs_len;
     uint32_t hs_off[8];

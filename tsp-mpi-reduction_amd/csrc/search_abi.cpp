@@ -89,6 +89,7 @@ struct tspgpu_search {
     // for symmetric matrices and the suffix table for the last tail_len cities
     int sym = 0;
     void *d_bnd2 = nullptr;
+    double *d_mst = nullptr;
     double *d_hsuf = nullptr;
     size_t hsuf_alloc = 0;      // bytes
     int hs_len = 0;             // sizes 1..hs_len built (0: none)
@@ -96,6 +97,9 @@ struct tspgpu_search {
     int suffix_len = 6;         // TSPGPU_SEARCH_SUFFIX=0/5/6: table size (0: B0/B1 only)
     bool use_two_edge = true;   // TSPGPU_SEARCH_TWO_EDGE=0: no B1
     bool use_lagrange = true;   // TSPGPU_SEARCH_LAGRANGE=0: B1 without the Lagrangian city weights
+    bool use_mst = true;        // TSPGPU_SEARCH_MST=0: no Held-Karp tree bound in the expand kernel
+    bool mst_on = false;        // (symmetric matrices only)
+    int mst_min_rem = 12;       // TSPGPU_SEARCH_MST_MINREM: paths with fewer cities left skip it (measured: profiles/r02/k2_tree_minrem.log)
     // The frontier is a LIFO stack of segments, each a run of paths in its own
     // buffer (fb): a step expands the top T items of the top segment and its
     // children become a new segment on top, written straight into a spare
@@ -282,6 +286,83 @@ static void lagrange_pi(const std::vector<double> &D, int n, std::vector<double>
     }
 }
 
+// Held-Karp city weights: subgradient ascent on the 1-tree bound (a minimum
+// spanning tree of cities 1..n-1 plus the two cheapest edges at city 0, on
+// d' = d + pi_x + pi_y, minus 2 sum pi), the same Polyak steps towards a
+// nearest-neighbour tour's cost as lagrange_pi, 300 iterations of an O(n^2)
+// Prim.  On the hardest 32-city seeds (bench.py's k2_instance 14, 30, 35) the
+// bound reaches the optimum to 5 digits, where the two-edge bound stops at
+// 0.83-0.88 (tools/k2_tree_bound_proto.py).  These weights serve the tree
+// bound of the expand kernel (SearchArgs::mst); the bound is valid for any pi.
+static void held_karp_pi(const std::vector<double> &D, int n, std::vector<double> &best_pi)
+{
+    double ub = 0.0;
+    {
+        std::vector<char> used(n, 0);
+        int k = 0;
+        used[0] = 1;
+        for (int i = 1; i < n; ++i) {
+            int b = -1;
+            for (int j = 0; j < n; ++j)
+                if (!used[j] && (b < 0 || D[(size_t)k * n + j] < D[(size_t)k * n + b])) b = j;
+            ub += D[(size_t)k * n + b];
+            used[b] = 1;
+            k = b;
+        }
+        ub += D[(size_t)k * n];
+    }
+    std::vector<double> pi(n, 0.0), key(n);
+    std::vector<int> deg(n), par(n);
+    std::vector<char> in(n);
+    double best = -INFINITY, lam = 2.0;
+    int stall = 0;
+    best_pi.assign(n, 0.0);
+    auto dp = [&](int x, int y) { return D[(size_t)x * n + y] + pi[x] + pi[y]; };
+    for (int it = 0; it < 300 && n >= 3; ++it) {
+        std::fill(deg.begin(), deg.end(), 0);
+        std::fill(in.begin(), in.end(), 0);
+        double lb = 0.0;
+        for (int v = 1; v < n; ++v) key[v] = dp(1, v), par[v] = 1;
+        in[1] = 1;
+        for (int step = 2; step < n; ++step) {
+            int u = -1;
+            for (int v = 2; v < n; ++v)
+                if (!in[v] && (u < 0 || key[v] < key[u])) u = v;
+            in[u] = 1;
+            lb += key[u];
+            ++deg[u];
+            ++deg[par[u]];
+            for (int v = 2; v < n; ++v)
+                if (!in[v] && dp(u, v) < key[v]) key[v] = dp(u, v), par[v] = u;
+        }
+        int a = -1, b = -1;
+        for (int v = 1; v < n; ++v) {
+            if (a < 0 || dp(0, v) < dp(0, a))
+                b = a, a = v;
+            else if (b < 0 || dp(0, v) < dp(0, b))
+                b = v;
+        }
+        lb += dp(0, a) + dp(0, b);
+        deg[0] = 2;
+        ++deg[a];
+        ++deg[b];
+        for (int x = 0; x < n; ++x) lb -= 2.0 * pi[x];
+        if (lb > best) {
+            best = lb;
+            best_pi = pi;
+            stall = 0;
+        } else if (++stall >= 10) {
+            lam *= 0.7;
+            stall = 0;
+        }
+        double nn = 0.0;
+        for (int x = 0; x < n; ++x) nn += (double)(deg[x] - 2) * (deg[x] - 2);
+        if (nn == 0.0 || !(ub > lb)) break;
+        const double t = lam * (ub - lb) / nn;
+        for (int x = 0; x < n; ++x) pi[x] += t * (deg[x] - 2);
+    }
+}
+
 // Multi-start upper bound: a nearest-neighbour tour from every city, each
 // improved by 2-opt + Or-opt, rotated to start at city 0; the best exact fold
 // (tsp.cpp's cost, either direction) is a valid bound >= OPT.  A tight start
@@ -432,6 +513,7 @@ struct SearchPool {
     hipEvent_t e0 = nullptr, e1 = nullptr;
     unsigned long long *h_cnt = nullptr;
     void *d_bnd2 = nullptr;
+    double *d_mst = nullptr;
     double *d_hsuf = nullptr;
     size_t hsuf_alloc = 0;
 };
@@ -461,6 +543,7 @@ void move_buffers(A &to, B &from)
     to.e1 = from.e1, from.e1 = nullptr;
     to.h_cnt = from.h_cnt, from.h_cnt = nullptr;
     to.d_bnd2 = from.d_bnd2, from.d_bnd2 = nullptr;
+    to.d_mst = from.d_mst, from.d_mst = nullptr;
     to.d_hsuf = from.d_hsuf, from.d_hsuf = nullptr;
     to.hsuf_alloc = from.hsuf_alloc, from.hsuf_alloc = 0;
 }
@@ -485,6 +568,7 @@ void free_buffers(A &b)
     if (b.e1) (void)hipEventDestroy(b.e1);
     if (b.h_cnt) (void)hipHostFree(b.h_cnt);
     if (b.d_bnd2) (void)hipFree(b.d_bnd2);
+    if (b.d_mst) (void)hipFree(b.d_mst);
     if (b.d_hsuf) (void)hipFree(b.d_hsuf);
     SearchPool z;
     move_buffers(b, z);
@@ -573,6 +657,8 @@ int tspgpu_search_create(tspgpu_ctx *c, const void *dist, int dtype, int n, int 
     }
     if (const char *e = std::getenv("TSPGPU_SEARCH_TWO_EDGE")) s->use_two_edge = std::atoi(e) != 0;
     if (const char *e = std::getenv("TSPGPU_SEARCH_LAGRANGE")) s->use_lagrange = std::atoi(e) != 0;
+    if (const char *e = std::getenv("TSPGPU_SEARCH_MST")) s->use_mst = std::atoi(e) != 0;
+    if (const char *e = std::getenv("TSPGPU_SEARCH_MST_MINREM")) s->mst_min_rem = std::atoi(e);
     if (const char *e = std::getenv("TSPGPU_SEARCH_TAIL_CAP_LOG2")) {  // tests: many flushes, small steps
         const int v = std::atoi(e);
         if (v >= 8 && v <= 27) s->tail_cap = 1u << v;
@@ -685,6 +771,25 @@ int tspgpu_search_create(tspgpu_ctx *c, const void *dist, int dtype, int n, int 
             }
         }
     }
+    // tree bound (symmetric matrices): d' and pi as doubles, and a margin far
+    // above the rounding of the device's sums of <= 2n + 2 such terms
+    std::vector<double> mt;
+    s->mst_on = s->sym && s->use_mst && !s->noprune && n >= 4;
+    if (s->mst_on) {
+        std::vector<double> D((size_t)n * n), pi;
+        for (int i = 0; i < n * n; ++i)
+            D[i] = f64 ? static_cast<const double *>(dist)[i] : (double)static_cast<const int32_t *>(dist)[i];
+        held_karp_pi(D, n, pi);
+        mt.assign((size_t)n * n + n + 1, 0.0);
+        double mx = 0.0, ps = 0.0;
+        for (int x = 0; x < n; ++x)
+            for (int y = 0; y < n; ++y) {
+                mt[(size_t)x * n + y] = D[(size_t)x * n + y] + pi[x] + pi[y];
+                mx = std::max(mx, std::fabs(mt[(size_t)x * n + y]));
+            }
+        for (int x = 0; x < n; ++x) mt[(size_t)n * n + x] = pi[x], ps += std::fabs(pi[x]);
+        mt[(size_t)n * n + n] = 1e-9 * ((n + 2) * mx + 2.0 * ps + 1.0);
+    }
     s->rec_cap = 1u << 16;
     take_pool(s);  // device buffers of the context's previous search, if any
     hipStream_t st = c->stream;
@@ -692,6 +797,8 @@ int tspgpu_search_create(tspgpu_ctx *c, const void *dist, int dtype, int n, int 
     if (!s->d_dist) e = hipMalloc(&s->d_dist, sizeof(double) * kSearchMaxN * kSearchMaxN);
     if (e == hipSuccess && !s->d_amin) e = hipMalloc(&s->d_amin, sizeof(double) * kSearchMaxN);
     if (e == hipSuccess && !s->d_bnd2) e = hipMalloc(&s->d_bnd2, sizeof(double) * 2 * kSearchMaxN);
+    if (e == hipSuccess && s->mst_on && !s->d_mst)
+        e = hipMalloc((void **)&s->d_mst, sizeof(double) * (kSearchMaxN * kSearchMaxN + kSearchMaxN + 1));
     if (e == hipSuccess && !s->d_words) e = hipMalloc((void **)&s->d_words, kWords * sizeof(unsigned long long));
     if (e == hipSuccess && !s->d_stats) e = hipMalloc((void **)&s->d_stats, kStatBytes);
     if (e == hipSuccess && s->frontier && s->d_tail && s->tail_alloc != s->tail_cap) {
@@ -716,6 +823,8 @@ int tspgpu_search_create(tspgpu_ctx *c, const void *dist, int dtype, int n, int 
     if (e == hipSuccess && s->sym)
         e = hipMemcpyAsync(s->d_bnd2, f64 ? (const void *)bd.data() : (const void *)bi.data(), vb * 2 * n,
                            hipMemcpyHostToDevice, st);
+    if (e == hipSuccess && s->mst_on)
+        e = hipMemcpyAsync(s->d_mst, mt.data(), sizeof(double) * mt.size(), hipMemcpyHostToDevice, st);
     unsigned long long w[kWords] = {};
     if (f64) {
         const double inf = INFINITY;
@@ -807,6 +916,8 @@ static SearchArgs args_of(tspgpu_search *s)
     a.rec_cap = s->rec_cap;
     a.bnd2 = s->d_bnd2;
     a.sym = s->sym;
+    a.mst = s->mst_on ? s->d_mst : nullptr;
+    a.mst_min_rem = s->mst_min_rem;
     a.hsuf = s->d_hsuf;
     a.hs_len = s->hs_len;
     for (int i = 0; i < 8; ++i) a.hs_off[i] = s->hs_off[i];
