@@ -369,10 +369,9 @@ def config4_tsplib(ctx, reps=3):
     """BASELINE config 4 on the real TSPLIB instances (tests/golden/tsplib):
     the DP over the whole GPU (K1-wide) and K2 in integer mode, time to the
     optimal tour (and B&B nodes), the cost checked against the published
-    optimum.  K2 runs up to 17 cities: on ulysses22 its bounds are weak
-    (4.2e12 nodes, 7.9 s, profiles/r02/config4_tsplib.json) where the DP
-    takes well under a millisecond — `bin/tsp_search --solver auto` picks the
-    DP there."""
+    optimum.  K2 runs on all four: before its Held-Karp tree bound ulysses22
+    took it 4.2e12 nodes and 7.9 s (profiles/r02/config4_tsplib.json) where
+    the DP takes well under a millisecond."""
     out = {}
     for name, opt in TSPLIB_OPTIMA.items():
         _, d = tspgpu.read_tsplib(os.path.join(ROOT, "tests", "golden", "tsplib", name))
@@ -388,18 +387,17 @@ def config4_tsplib(ctx, reps=3):
         assert best[1] == opt, f"{name}: DP {best[1]} != published optimum {opt}"
         rec["dp_k1_wide"] = {"cost": int(best[1]), "time_to_optimal_ms": best[0], "kernel_ms": best[3],
                              "tour": [int(x) for x in best[2]]}
-        if n <= 17:
-            best = None
-            for _ in range(reps):
-                t = time.perf_counter()
-                cost, tour, st = tspgpu.search_solve(ctx, d)
-                wall = (time.perf_counter() - t) * 1e3
-                if best is None or wall < best[0]:
-                    best = (wall, cost, tour, st)
-            wall, cost, tour, st = best
-            assert cost == opt, f"{name}: K2 {cost} != published optimum {opt}"
-            rec["k2_search"] = {"cost": int(cost), "time_to_optimal_ms": wall, "kernel_ms": st["kernel_ms"],
-                                "bb_nodes_expanded": st["nodes"], "tour": [int(x) for x in tour]}
+        best = None
+        for _ in range(reps):
+            t = time.perf_counter()
+            cost, tour, st = tspgpu.search_solve(ctx, d)
+            wall = (time.perf_counter() - t) * 1e3
+            if best is None or wall < best[0]:
+                best = (wall, cost, tour, st)
+        wall, cost, tour, st = best
+        assert cost == opt, f"{name}: K2 {cost} != published optimum {opt}"
+        rec["k2_search"] = {"cost": int(cost), "time_to_optimal_ms": wall, "kernel_ms": st["kernel_ms"],
+                            "bb_nodes_expanded": st["nodes"], "tour": [int(x) for x in tour]}
         out[name] = rec
     return out
 
