@@ -761,6 +761,7 @@ int tspgpu_search_create(tspgpu_ctx *c, const void *dist, int dtype, int n, int 
     // to the bound's grid (f64: 2^-20, exact sums; i32: integers)
     std::vector<double> bd(2 * n, 0.0);
     std::vector<int32_t> bi(2 * n, 0);
+    std::vector<double> hk_pi;  // Held-Karp weights of the tree bound (symmetric matrices)
     {
         bool sym = s->use_two_edge;
         for (int i = 0; i < n && sym; ++i)
@@ -773,7 +774,23 @@ int tspgpu_search_create(tspgpu_ctx *c, const void *dist, int dtype, int n, int 
             for (int i = 0; i < n * n; ++i)
                 D[i] = f64 ? static_cast<const double *>(dist)[i] : (double)static_cast<const int32_t *>(dist)[i];
             std::vector<double> pi(n, 0.0);
+            // the tree bound's weights on a second thread meanwhile (host time
+            // at n = 32: 1.3 ms beside lagrange_pi's 0.45 ms)
+            const bool want_tree = s->use_mst && n >= 4;
+            std::thread ht;
+            bool threaded = false;
+            if (want_tree && n >= 20) {  // (smaller: a thread costs more than it saves)
+                try {
+                    ht = std::thread([&] { held_karp_pi(D, n, hk_pi); });
+                    threaded = true;
+                } catch (...) {
+                }
+            }
             if (s->use_lagrange) lagrange_pi(D, n, pi);
+            if (threaded)
+                ht.join();
+            else if (want_tree)
+                held_karp_pi(D, n, hk_pi);
             for (int x = 0; x < n; ++x) {
                 double m1 = INFINITY, m2 = INFINITY;  // the two cheapest d'[x][y] = d + pi_x + pi_y
                 for (int y = 0; y < n; ++y) {
@@ -804,12 +821,12 @@ int tspgpu_search_create(tspgpu_ctx *c, const void *dist, int dtype, int n, int 
     // tree bound (symmetric matrices): d' and pi as doubles, and a margin far
     // above the rounding of the device's sums of <= 2n + 2 such terms
     std::vector<double> mt;
-    s->mst_on = s->sym && s->use_mst && !s->noprune && n >= 4;
+    s->mst_on = s->sym && s->use_mst && !s->noprune && n >= 4 && (int)hk_pi.size() == n;
     if (s->mst_on) {
-        std::vector<double> D((size_t)n * n), pi;
+        std::vector<double> D((size_t)n * n);
+        const std::vector<double> &pi = hk_pi;
         for (int i = 0; i < n * n; ++i)
             D[i] = f64 ? static_cast<const double *>(dist)[i] : (double)static_cast<const int32_t *>(dist)[i];
-        held_karp_pi(D, n, pi);
         mt.assign((size_t)n * n + n + 1, 0.0);
         double mx = 0.0, ps = 0.0;
         for (int x = 0; x < n; ++x)
@@ -1474,7 +1491,24 @@ static int search_solve(tspgpu_ctx *c, const void *dist, int dtype, int n, doubl
     tspgpu_search *s = nullptr;
     int depth = 0;  // automatic; TSPGPU_SEARCH_DEPTH (tests): a shallow seed, a deep frontier
     if (const char *e = std::getenv("TSPGPU_SEARCH_DEPTH")) depth = std::max(0, std::atoi(e));
+    // the multi-start bound (host) while the search is created (host tables,
+    // device buffers): both take ~1 ms at 32 cities
+    double ub = 0.0;
+    int hrc = 0;
+    std::thread ht;
+    bool threaded = false;
+    if (n >= 20) {  // (smaller: a thread costs more than it saves)
+        try {
+            ht = std::thread([&] { hrc = tspgpu_heuristic_tour(dist, dtype, n, &ub, nullptr); });
+            threaded = true;
+        } catch (...) {
+        }
+    }
     int rc = tspgpu_search_create(c, dist, dtype, n, 0, 1, depth, &s);
+    if (threaded)
+        ht.join();
+    else
+        hrc = tspgpu_heuristic_tour(dist, dtype, n, &ub, nullptr);
     if (rc) return rc;
     s->noprune = noprune;
     // enumeration work is uniform and every lane reaches the register tails:
@@ -1488,8 +1522,7 @@ static int search_solve(tspgpu_ctx *c, const void *dist, int dtype, int n, doubl
         const long v = std::atol(e);
         if (v > 0) s->rec_cap = (unsigned int)std::min<long>(v, s->rec_cap);
     }
-    double ub = 0.0;
-    rc = tspgpu_heuristic_tour(dist, dtype, n, &ub, nullptr);
+    rc = hrc;
     if (!rc) rc = tspgpu_search_set_bound(s, ub);
     int phases = 1, fallback = 0;
     uint64_t inc = 0, nodes = 0, nodes_total = 0, recs = 0;

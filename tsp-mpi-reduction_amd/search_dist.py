@@ -22,6 +22,7 @@ from __future__ import annotations
 
 import errno
 import os
+import threading
 import time
 
 import numpy as np
@@ -77,16 +78,32 @@ def solve_sharded(ctx, dist, group=None, depth: int = 0, device=None, exchange_e
         exchange_every = int(os.environ.get("TSPGPU_EXCHANGE_EVERY", "4"))
     exchange_every = max(1, int(exchange_every))
 
-    S = tspgpu.Search(ctx, dist, shard=rank, nshards=world, depth=depth)
+    # the multi-start tour (host, split over the ranks: start cities r, r+W,
+    # ...) on a thread while the search is created (ctypes releases the GIL)
+    heur = {}
+
+    def _heuristic():
+        heur["v"] = tspgpu.heuristic_tour(dist, first=rank, step=world) if world > 1 else \
+            tspgpu.heuristic_tour(dist)
+
+    th = threading.Thread(target=_heuristic) if len(dist) >= 20 else None  # (smaller: not worth a thread)
+    if th is not None:
+        th.start()
+    try:
+        S = tspgpu.Search(ctx, dist, shard=rank, nshards=world, depth=depth)
+    finally:
+        if th is not None:
+            th.join()
+    if "v" not in heur:
+        _heuristic()  # (no thread, or it raised: here, so an error surfaces)
     try:
         if world > 1:
-            # the multi-start tour split over the ranks (start cities r, r+W, ...),
-            # then the MIN of their costs: all starts' bound at 1/W of the host time
-            ub_r, _ = tspgpu.heuristic_tour(dist, first=rank, step=world)
+            # then the MIN of the ranks' costs: all starts' bound at 1/W of the host time
+            ub_r, _ = heur["v"]
             word = tspgpu.cost_bits(ub_r, S.dtype) if ub_r is not None else (1 << 63) - 1
             ub = tspgpu.bits_cost(allmin2(word, 0)[0], S.dtype)
         else:
-            ub, _ = tspgpu.heuristic_tour(dist)
+            ub, _ = heur["v"]
         S.set_bound(ub)
         t0 = time.perf_counter()
         exchanges = 0
