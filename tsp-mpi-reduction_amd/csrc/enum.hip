@@ -789,19 +789,20 @@ __device__ __forceinline__ Expand<V> expand_eval(const SearchArgs &a, const V *d
         e.hnodes = act ? (uint32_t)((TL + 1) * TL) : 0u;
         return e;
     }
-    // the tree bound of the whole rest (all children at once); its margin
-    // dm[kSearchMaxN * kTRow + kSearchMaxN] covers the device's rounding
-    if (a.mst && !a.noprune && act && e.rem && __builtin_popcount(e.rem) >= a.mst_min_rem) {
-        const double lb = (double)c + tree_bound(dm, dm + kSearchMaxN * kTRow, k, e.rem) -
-                          dm[kSearchMaxN * kTRow + kSearchMaxN];
-        if (lb > (double)thr) return e;  // e.live = 0: no child survives
-    }
     for (uint32_t x = e.rem; x; x &= x - 1u) {
         const int j = __builtin_ctz(x);
         const V cj = c + dl[k * kTRow + j];
         bool ok = a.noprune || !(cj + (remA - am[j]) > thr);
         if (ok && a.sym && !a.noprune) ok = !(cj + (((remB - b2[2 * j]) + b2[2 * j + 1]) + b2[1]) > thr);
         if (ok) e.live |= 1u << j;
+    }
+    // the tree bound of the whole rest (all children at once), only for paths
+    // the cheaper bounds left children of; its margin
+    // dm[kSearchMaxN * kTRow + kSearchMaxN] covers the device's rounding
+    if (e.live && a.mst && !a.noprune && __builtin_popcount(e.rem) >= a.mst_min_rem) {
+        const double lb = (double)c + tree_bound(dm, dm + kSearchMaxN * kTRow, k, e.rem) -
+                          dm[kSearchMaxN * kTRow + kSearchMaxN];
+        if (lb > (double)thr) e.live = 0;  // no child survives
     }
     return e;
 }
