@@ -727,7 +727,16 @@ int tspgpu_search_create(tspgpu_ctx *c, const void *dist, int dtype, int n, int 
         // the optimum spread over the shards (n = 30 random, 8 shards: node
         // imbalance max/mean 1.91 at depth 4, 1.20 at depth 5;
         // profiles/r02/k2_shard_balance_depth.log)
-        if (nshards > 1 && d + 1 < N - s->tail_len && falling(N, d + 1) < (1ull << 31)) ++d;
+        // Not with the tree bound (symmetric matrices): it leaves no heavy
+        // subtree to spread, and the deeper seed level, bounded only by B0/B1,
+        // costs more than it balances (n = 32 seed 35, 2 shards: 5.0e7 nodes
+        // per shard vs 7.1e5 for one GPU; profiles/r02/k2_shard_depth_tree.log)
+        bool tree = s->use_mst && s->use_two_edge;
+        for (int i = 0; i < n && tree; ++i)
+            for (int j = 0; j < i && tree; ++j)
+                tree = f64 ? static_cast<const double *>(dist)[i * n + j] == static_cast<const double *>(dist)[j * n + i]
+                           : static_cast<const int32_t *>(dist)[i * n + j] == static_cast<const int32_t *>(dist)[j * n + i];
+        if (nshards > 1 && !tree && d + 1 < N - s->tail_len && falling(N, d + 1) < (1ull << 31)) ++d;
         depth = d;
     }
     s->depth = depth;
