@@ -127,6 +127,23 @@ def test_heuristic_split_over_ranks_gives_the_same_bound(n):
     assert min(tspgpu.heuristic_tour(di, first=r, step=4)[0] for r in range(4)) == full_i
 
 
+@pytest.mark.parametrize("n", [20, 27, 32])
+def test_heuristic_threads_give_the_serial_tour(monkeypatch, n):
+    """From 20 cities the multi-start runs on up to 8 host threads
+    (TSPGPU_HEURISTIC_THREADS overrides); the results are combined in start
+    order, so cost and tour equal the serial run's, f64 and i32."""
+    rng = np.random.default_rng(500 + n)
+    xy = rng.uniform(0, 1000, size=(n, 2))
+    d = tspgpu.distance_matrix([[(i, xy[i, 0], xy[i, 1]) for i in range(n)]])[0]
+    for m in (d, np.rint(d).astype(np.int32)):
+        got = []
+        for t in ("1", "3", "8"):
+            monkeypatch.setenv("TSPGPU_HEURISTIC_THREADS", t)
+            c, tour = tspgpu.heuristic_tour(m)
+            got.append((c, tour.tolist()))
+        assert got[0] == got[1] == got[2]
+
+
 def test_search_validation():
     """Host-side argument checks of the K2 entry points (no device needed)."""
     with pytest.raises(tspgpu.TspGpuError):
