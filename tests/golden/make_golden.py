@@ -133,6 +133,57 @@ def random_instances():
     return blocks
 
 
+def k1_batch_instances(n, count, seed):
+    """Batches for K1's large-batch kernel (variant 5 at n = 13..16): a third
+    on the 0..3 lattice (coincident cities, tie storms), a third on the 0..39
+    lattice (many tied optima), a third uniform doubles in [0, 1000)."""
+    rng = np.random.default_rng(seed)
+    blocks = []
+    for b in range(count):
+        kind = b % 3
+        if kind == 0:
+            xy = rng.integers(0, 4, size=(n, 2)).astype(np.float64)
+        elif kind == 1:
+            xy = rng.integers(0, 40, size=(n, 2)).astype(np.float64)
+        else:
+            xy = rng.uniform(0, 1000, size=(n, 2))
+        blocks.append([(1000 * b + i, float(xy[i, 0]), float(xy[i, 1])) for i in range(n)])
+    return blocks
+
+
+def gen_k1_batches(count=522, workers=8):
+    """tsp() (the reference, -O0) on 522 blocks at each of n = 13..16, solved
+    in parallel harness processes (chunks of 6 blocks)."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    out = []
+    for n in (13, 14, 15, 16):
+        blocks = k1_batch_instances(n, count, 20261017 + n)
+        chunks = [blocks[i:i + 6] for i in range(0, len(blocks), 6)]
+
+        def solve(ci):
+            tmp = os.path.join(REF, f"_k1b_{n}_{ci}.txt")
+            write_blockfile(tmp, chunks[ci])
+            try:
+                return parse_solutions(harness("solvefile", tmp))
+            finally:
+                os.remove(tmp)
+
+        with ThreadPoolExecutor(workers) as ex:
+            sols = [s for part in ex.map(solve, range(len(chunks))) for s in part]
+        assert len(sols) == len(blocks)
+        rows = []
+        for blk, s in zip(blocks, sols):
+            xy = [[c[1], c[2]] for c in blk]
+            integral = all(v == int(v) for p in xy for v in p)
+            rows.append({"id0": blk[0][0], "xy": [[int(a), int(b)] for a, b in xy] if integral
+                         else [[float(a).hex(), float(b).hex()] for a, b in xy],
+                         "cost_hex": s["cost_hex"], "ids": s["ids"]})
+        out.append({"n": n, "blocks": rows})
+        print(f"k1 batch n={n}: {len(rows)} blocks", flush=True)
+    return out
+
+
 def gen_fold():
     out = []
     for (n, B, X, Y) in [(5, 7, 500, 500), (6, 8, 1000, 1000), (8, 12, 1000, 1000), (4, 16, 1000, 1000), (3, 5, 100, 100)]:
@@ -171,6 +222,11 @@ def gen_cli():
         (3, 30, 1000, 1000): (1, 3, 6),
         (11, 5, 1000, 1000): (5,),
         (9, 32, 1000, 1000): (8,),
+        # SURVEY Appendix B's 16-city multi-block runs (the reference's own
+        # strong-scaling axis): one fixed B over P ranks
+        (16, 8, 1000, 1000): (1, 2, 4, 8),
+        (16, 16, 1000, 1000): (8,),
+        (14, 64, 1000, 1000): (8,),
     }
     for (n, B, X, Y), Ps in mat.items():
         for P in Ps:
@@ -187,7 +243,7 @@ def gen_cli():
 def main():
     if not os.path.exists(HARNESS):
         sys.exit("build the reference first: make -C oracle (needs /root/reference)")
-    which = set(sys.argv[1:]) or {"seed0", "dist", "ties", "random", "fold", "cli"}
+    which = set(sys.argv[1:]) or {"seed0", "dist", "ties", "random", "fold", "cli", "k1batch"}
     jobs = {
         "seed0": ("seed0_blocks.json", gen_seed0_blocks),
         "dist": ("seed0_dist.json", gen_dist),
@@ -195,6 +251,7 @@ def main():
         "random": ("random_blocks.json", lambda: gen_file_instances("random", random_instances())),
         "fold": ("fold.json", gen_fold),
         "cli": ("cli.json", gen_cli),
+        "k1batch": ("k1_batches.json", gen_k1_batches),
     }
     for key in sorted(which):
         fname, fn = jobs[key]

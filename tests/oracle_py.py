@@ -120,3 +120,13 @@ def load_golden(name):
 
 def hexf(s: str) -> float:
     return float.fromhex(s)
+
+
+def k1_batch_blocks(case):
+    """City lists of one n of tests/golden/k1_batches.json (lattice coordinates
+    stored as integers, uniform ones as C99 hex)."""
+    out = []
+    for blk in case["blocks"]:
+        conv = (lambda v: float(v)) if isinstance(blk["xy"][0][0], int) else hexf
+        out.append([(blk["id0"] + i, conv(x), conv(y)) for i, (x, y) in enumerate(blk["xy"])])
+    return out

@@ -79,7 +79,11 @@ def test_two_gpus_split_in_one_process(case):
 
 
 MPI_CASES = [c for c in CASES if (c["args"], c["P"]) in (([6, 8, 1000, 1000], 3), ([12, 4, 1000, 1000], 4),
-                                                         ([8, 12, 1000, 1000], 5), ([10, 16, 1000, 1000], 8))]
+                                                         ([8, 12, 1000, 1000], 5), ([10, 16, 1000, 1000], 8),
+                                                         # SURVEY Appendix B's 16-city multi-block runs
+                                                         ([16, 8, 1000, 1000], 1), ([16, 8, 1000, 1000], 2),
+                                                         ([16, 8, 1000, 1000], 4), ([16, 8, 1000, 1000], 8),
+                                                         ([16, 16, 1000, 1000], 8), ([14, 64, 1000, 1000], 8))]
 
 
 @pytest.mark.skipif(MPIRUN is None, reason="no mpirun on this machine")

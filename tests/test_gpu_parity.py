@@ -183,3 +183,18 @@ def test_torch_tensors_and_stream_interop():
     p = subprocess.run([sys.executable, "-c", TORCH_INTEROP, tspgpu.PKG_DIR], capture_output=True, text=True,
                        timeout=300)
     assert p.returncode == 0 and "OK" in p.stdout, p.stderr[-2000:]
+
+
+@pytest.mark.parametrize("case", O.load_golden("k1_batches.json"), ids=lambda c: f"n{c['n']}")
+def test_k1_batches_reference_goldens_default_kernel(gpu_ctx, case):
+    """The reference's own tsp() outputs for 522 blocks per n = 13..16 (tie-heavy
+    lattices and uniform cities), solved in ONE batch through the default path:
+    a batch of more than one block per CU runs the large-batch kernel (variant
+    5 or later), the configuration ./tsp 16 16384 times."""
+    blocks = O.k1_batch_blocks(case)
+    n = case["n"]
+    _, cost, tour = _solve_blocks_of_cities(gpu_ctx, blocks)
+    assert gpu_ctx.last_variant() >= 5, gpu_ctx.last_variant()
+    bad = [b for b, ref in enumerate(case["blocks"])
+           if cost[b] != O.hexf(ref["cost_hex"]) or _ids(blocks[b], tour[b], n) != ref["ids"]]
+    assert not bad, f"n={n}: mismatching blocks {bad[:10]}"
