@@ -47,7 +47,7 @@ import tspgpu  # noqa: E402  (lazy: loads libtspgpu on first use, no HIP call at
 METRIC = "search nodes/sec (whole node) + time-to-optimal tour, 16-city, 1/2/4/8 GPU"
 UNIT = "Held-Karp DP relaxations/s"
 HBM_PEAK = 8.0e12  # B/s, MI355X_MICROARCH.md chip table (spec)
-KERNEL_NAMES = {5: "hk_tiled_kernel"}  # K1 variant -> kernel symbol (others: heldkarp_kernel)
+KERNEL_NAMES = {5: "hk_tiled_kernel", 6: "hk_sub_kernel"}  # K1 variant -> kernel symbol (others: heldkarp_kernel)
 UBENCH = os.path.join(PKG, "bin", "ubench")
 TSP_BIN = os.path.join(PKG, "bin", "tsp")
 
@@ -674,10 +674,10 @@ def main():
     total_blocks = Bp * world * args.steps
     value = total_blocks * relax / wall_max
 
-    # variant 5 runs two kernels per launch: time each on its stream (HIP
+    # variants 5/6 run two kernels per launch: time each on its stream (HIP
     # events between them), outside the timed region
     split = None
-    if variant == 5:
+    if variant in (5, 6):
         ctx.k1_split_timing(True)
         fw, bt = [], []
         for _ in range(5):
@@ -843,7 +843,7 @@ def roofline(variant, kname, n, Bp, kernel_ms, relax_s, alg_bytes_per_block, pro
     8 TB/s (an upper bound on HBM: Infinity-Cache hits are included).
     The line reports whichever fraction is higher as `roofline` (the binding
     one) and the other as `other`."""
-    mix, per = (("f64 relaxation min-only (add,min)", 2) if variant == 5
+    mix, per = (("f64 relaxation min-only (add,min)", 2) if variant in (5, 6)
                 else ("f64 relaxation+argmin (add,cmp,cndmask,min)", 4))
     peak_relax = (peaks or {}).get(mix)
     scale = Bp / (prof or {}).get("blocks_per_launch", Bp)

@@ -105,3 +105,49 @@ def test_reference_tsp_cpp_linked_against_gpu_shim(case):
                        text=True, env=_clean_env(), timeout=300, cwd="/tmp")
     assert p.returncode == case["rc"], p.stderr[-2000:]
     assert _norm(p.stdout) == _expect(case)
+
+
+def _two_rank_case():
+    return next(c for c in CASES if c["args"] == [6, 8, 1000, 1000] and c["P"] == 2)
+
+
+def test_stale_rank_file_of_an_earlier_run_is_ignored():
+    """a rank file left in the gather directory by an earlier run
+    (another job key) must not be taken for this run's: rank 0 drops it and
+    waits for this job's own file."""
+    import struct
+
+    case = _two_rank_case()
+    with tempfile.TemporaryDirectory() as gd:
+        # header of the current format (magic "TSP2"), same rank/n/B/X/Y, foreign job key, no payload
+        n, B, X, Y = case["args"]
+        with open(os.path.join(gd, "rank1.bin"), "wb") as f:
+            f.write(struct.pack("<4I4iQ", 0x32505354, 1, 4, n, B, X, Y, 0, 0x1234))
+        procs = []
+        for r in range(2):
+            env = dict(_clean_env(), PMI_SIZE="2", PMI_RANK=str(r), TSP_GATHER_DIR=gd)
+            procs.append(subprocess.Popen([tspgpu.TSP_BIN, *map(str, case["args"])], stdout=subprocess.PIPE,
+                                          stderr=subprocess.PIPE, text=True, env=env))
+        outs = [p.communicate(timeout=300) for p in procs]
+        assert procs[0].returncode == 0, outs[0][1]
+        assert _norm(outs[0][0]) == _expect(case)
+        assert os.listdir(gd) == []
+
+
+def test_failed_worker_rank_ends_the_wait_at_once():
+    """A worker rank that fails publishes a failure record: rank 0 exits with
+    that rank's error within seconds instead of polling for 600 s."""
+    import time
+
+    case = _two_rank_case()
+    with tempfile.TemporaryDirectory() as gd:
+        t0 = time.monotonic()
+        procs = []
+        for r in range(2):
+            env = dict(_clean_env(), PMI_SIZE="2", PMI_RANK=str(r), TSP_GATHER_DIR=gd, TSP_INJECT_FAIL_RANK="1")
+            procs.append(subprocess.Popen([tspgpu.TSP_BIN, *map(str, case["args"])], stdout=subprocess.PIPE,
+                                          stderr=subprocess.PIPE, text=True, env=env))
+        outs = [p.communicate(timeout=120) for p in procs]
+        assert procs[1].returncode == 3 and procs[0].returncode == 3, [o[1] for o in outs]
+        assert "rank 1 failed" in outs[0][1]
+        assert time.monotonic() - t0 < 60

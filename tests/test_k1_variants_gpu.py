@@ -2,10 +2,12 @@
 CPU oracle at the sizes where it is the default — including the variant
 switches that happen inside one call:
 
-  * n = 16, B >= 2 x CUs: the sub-cube tiled kernel (variant 5, hk_tiled.h)
-    is the default; variant 4 (ping-pong + parent words) and variant 2 are
-    forced through TSPGPU_K1 (read when a context is created);
-  * every variant-5 configuration of hkt_cfg.h (TSPGPU_TILED_CFG), f64 and i32;
+  * n = 16, B >= 2 x CUs: the restructured sub-cube kernel (variant 6,
+    hk_sub.h) is the default; variant 5 (hk_tiled.h), variant 4 (ping-pong +
+    parent words) and variant 2 are forced through TSPGPU_K1 (read when a
+    context is created);
+  * every variant-5/6 configuration compiled in (k1_cfg.h, TSPGPU_TILED_CFG),
+    f64 and i32;
   * tie-heavy blocks (integer lattice 0..3, 0..39) mixed with random ones;
   * one block solved alone (variant 2: fewer blocks than CUs) equals its row
     of the large batch (variant 5).
@@ -78,7 +80,7 @@ def _check(ctx, d, ref, vb=8):
     return ctx.last_variant()
 
 
-@pytest.mark.parametrize("variant", [None, 5, 4, 2])
+@pytest.mark.parametrize("variant", [None, 6, 5, 4, 2])
 def test_n16_large_batch_every_variant(variant):
     d = _blocks(16, B_BIG, 16)
     ref = _oracle_all(("f64", 16), d)
@@ -87,14 +89,15 @@ def test_n16_large_batch_every_variant(variant):
         used = _check(ctx, d, ref)
     finally:
         ctx.close()
-    assert used == (5 if variant is None else variant)
+    assert used == (6 if variant is None else variant)
 
 
-@pytest.mark.parametrize("n,vb,expect", [(13, 8, 5), (14, 8, 5), (15, 8, 5), (12, 8, 2), (16, 4, 5), (15, 4, 2)])
+@pytest.mark.parametrize("n,vb,expect", [(13, 8, 6), (14, 8, 6), (15, 8, 6), (16, 8, 6), (12, 8, 2), (16, 4, 6),
+                                         (15, 4, 2)])
 def test_large_batch_default_per_size(n, vb, expect):
-    """The large-batch default at each size (tspgpu.cpp: tiled at 13-16
-    cities f64 and 16 cities i32, the compact layer pass elsewhere), every
-    block against the oracle."""
+    """The large-batch default at each size (tspgpu.cpp: the sub-cube kernel
+    at 13-16 cities f64 and 16 cities i32, the compact layer pass elsewhere),
+    every block against the oracle."""
     d = _blocks(n, B_BIG, 40 + n)
     ref = _oracle_all(("f64", n, B_BIG, 40 + n), d)
     if vb == 4:
@@ -107,28 +110,31 @@ def test_large_batch_default_per_size(n, vb, expect):
         ctx.close()
 
 
-def _tiled_cfgs():
+def _k1_cfgs():
+    """(variant, id, value bytes, n) of every configuration compiled into the
+    library: the product rows of k1_cfg.h (sweep rows only in K1_SWEEP builds)."""
     import re
 
-    path = os.path.join(os.path.dirname(tspgpu.PKG_DIR), "tsp-mpi-reduction_amd", "csrc", "hkt_cfg.h")
+    path = os.path.join(os.path.dirname(tspgpu.PKG_DIR), "tsp-mpi-reduction_amd", "csrc", "k1_cfg.h")
+    text = open(path).read()
     out = []
-    for ln in open(path):
-        m = re.match(r"\s+X\((\d+), (\w+), (\d+), (\d+),", ln)
-        if m:
-            out.append((int(m.group(1)), 8 if m.group(2) == "double" else 4, int(m.group(3)) + 1))
+    for variant, macro in ((5, "TSPGPU_TILED_PRODUCT_CFGS"), (6, "TSPGPU_SUB_PRODUCT_CFGS")):
+        body = text[text.index(f"#define {macro}(X)"):].split("\n\n", 1)[0]
+        for m in re.finditer(r"X\((\d+), (\w+), (\d+), (\d+),", body):
+            out.append((variant, int(m.group(1)), 8 if m.group(2) == "double" else 4, int(m.group(3)) + 1))
     return out
 
 
-@pytest.mark.parametrize("cfg,vb,n", _tiled_cfgs())
-def test_every_tiled_configuration(cfg, vb, n):
+@pytest.mark.parametrize("variant,cfg,vb,n", _k1_cfgs())
+def test_every_k1_configuration(variant, cfg, vb, n):
     d = _blocks(n, 300, 100 + n)
     ref = _oracle_all(("f64", n, 300), d)
     if vb == 4:
         d = np.rint(d).astype(np.int32)
         ref = _oracle_all(("i32", n, 300), d.astype(np.float64))
-    ctx = _ctx(5, cfg)
+    ctx = _ctx(variant, cfg)
     try:
-        assert _check(ctx, d, ref, vb) == 5
+        assert _check(ctx, d, ref, vb) == variant
     finally:
         ctx.close()
 
@@ -136,7 +142,7 @@ def test_every_tiled_configuration(cfg, vb, n):
 def test_single_block_equals_its_row_of_the_big_batch(gpu_ctx):
     d = _blocks(16, B_BIG, 16)
     cost, tour = gpu_ctx.solve_blocks(d)
-    assert gpu_ctx.last_variant() == 5
+    assert gpu_ctx.last_variant() == 6
     for b in (0, 1, 2, 257, B_BIG - 1):
         c1, t1 = gpu_ctx.solve_blocks(d[b:b + 1])
         assert gpu_ctx.last_variant() == 2

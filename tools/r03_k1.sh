@@ -1,0 +1,30 @@
+#!/bin/bash
+# Round 3 K1 session on the GPU box: variant 6 timing vs 5, then the K1 parity
+# tests.  Every GPU step has its own time limit; a failure ends the script.
+set -u
+cd "$(dirname "$0")/.."
+OUT=gpurun_out/r03
+mkdir -p $OUT
+export TMPDIR=/tmp
+step() {  # name seconds cmd...
+    local name=$1 secs=$2
+    shift 2
+    echo "== $name" >&2
+    timeout -k 10 "$secs" "$@" > "$OUT/$name.log" 2>&1
+    local rc=$?
+    echo "== $name rc=$rc" >&2
+    tail -n 30 "$OUT/$name.log" >&2
+    if [ $rc -ne 0 ]; then exit $rc; fi
+}
+for s in ${STEPS:-time16 tests}; do
+    case $s in
+    time16) step k1_time_n16 240 python -u tools/k1_time.py 16 16384 8 6 5 ;;
+    timeall) step k1_time_n15 120 python -u tools/k1_time.py 15 16384 8 6 5
+             step k1_time_n14 120 python -u tools/k1_time.py 14 16384 8 6 5
+             step k1_time_n13 120 python -u tools/k1_time.py 13 16384 8 6 5
+             step k1_time_i32 120 python -u tools/k1_time.py 16 16384 4 6 5 ;;
+    tests) step k1_tests 400 python -u -m pytest tests/test_k1_variants_gpu.py tests/test_gpu_parity.py -x -q --timeout 200 --timeout-method thread ;;
+    trace) rm -rf $OUT/trace_timed
+           BENCH_I32=0 step trace_timed 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace_timed -o run -- python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-pmc --no-tto --no-k2 ;;
+    esac
+done

@@ -30,12 +30,14 @@ struct tspgpu_ctx {
     int threads = 0;     // workgroup size of the global-table kernels; 0 = per-N default
     int wg_per_cu = 0;   // resident slots per CU (auto grid); 0 = per-N default
     int lds_table_max_n = tspgpu::kLdsTableDefaultMaxN;  // largest N whose whole table stays in LDS
-    int variant = -1;    // K1 layer pass (-1: per-n default): 5 = sub-cube tiled (hk_tiled.h),
+    int variant = -1;    // K1 layer pass (-1: per-n default): 6 = sub-cube, restructured (hk_sub.h),
+                         // 5 = sub-cube tiled (hk_tiled.h),
                          // 4 = 2 + ping-pong values + parent words,
                          // 2 = compact + next-row prefetch, 1 = compact, 0 = member sweep
-    int tiled_cfg = -1;  // K1 variant 5 configuration (hkt_cfg.h); -1 = per-(n, type) default
-    void *d_tinfo[16] = {};        // TiledInfo per L (variant 5)
-    char *d_tslots = nullptr;      // variant 5 push areas (one per resident workgroup)
+    int tiled_cfg = -1;  // K1 variant 5/6 configuration id (k1_cfg.h); -1 = per-(n, type) default
+    void *d_tinfo[16] = {};        // TiledInfo per L (variants 5, 6)
+    void *d_subrows[16] = {};      // SubRow table per L (variant 6)
+    char *d_tslots = nullptr;      // variant 5/6 slots (one per block of a launch)
     size_t tslots_bytes = 0;
     hipEvent_t ev_start = nullptr, ev_stop = nullptr;
     // K1 workspace ordering across caller streams: the slots / push areas are

@@ -1,0 +1,756 @@
+// K1 variant 6 — sub-cube Held-Karp, restructured for gfx950 (MI355X).
+//
+// Same recurrence, same IEEE operations, same first-strict-minimum argmin and
+// the same global slot layout (push area, parent words, recompute area) as
+// variant 5 (hk_tiled.h), whose backtracking kernel it reuses — so the same
+// cost and tour bits (tsp.cpp:424-499).  What changes is how a sub-cube's
+// passes are scheduled and where a relaxation's distance comes from:
+//
+// * Distances touching a high city need no address arithmetic.  The inner
+//   distance image in LDS has H extra rows and columns that hold, for the
+//   current sub-cube h, the high rows d[hm_i][*] and columns d[*][hn_u] in
+//   sub-cube order (members ascending, then non-members): a pass knows i and
+//   u at compile time, so d[hm_i][k] is one ds_read with an immediate offset
+//   on the lane's k, d[m][hn_u] one on the lane's m, and d[hm_i][hn_u] is
+//   wave-uniform (an SGPR operand of v_add).  Only the low-low relaxations
+//   (43% at n = 16) keep a per-lane v_add_u32 for the address.  The extra
+//   rows/columns of sub-cube h + 1 are written by idle threads during the
+//   last pass of sub-cube h (which reads only the natural image).
+// * Fewer, fuller passes.  The 1- and 10-row passes at both ends of a
+//   sub-cube (j = 0, 1, L-1, L: 13% of the relaxations, 20% of variant 5's
+//   time) become destination-parallel: a lane per (row, destination), the
+//   row's T relaxations each.  j = 0 is folded into j = 1 (each lane of row
+//   {a} recomputes its own G[h+a][a] from the |h| pushed values), and j = L of
+//   sub-cube h runs in the same barrier interval as j = 0/1 of sub-cube h + 1
+//   (independent work).  L - 1 = 9 intervals per sub-cube instead of 11.
+// * Row tables instead of bit loops.  A row's members, non-members and the
+//   colex ranks of its destination rows come from one 16-byte host-built
+//   entry (global, L2-resident), prefetched one pass ahead; decoding is
+//   independent v_bfe ops instead of a dependent ctz chain.
+#pragma once
+#include "hk_tiled.h"
+
+namespace tspgpu {
+
+// row stride (entries) of the LDS distance image: N natural columns + H
+// sub-cube-ordered high columns, odd so that the low-low gathers of a
+// half-wave spread over the banks
+#ifndef TSPGPU_SUB_DS
+#define TSPGPU_SUB_DS 21
+#endif
+constexpr int kSubDS = TSPGPU_SUB_DS;
+
+// one entry per L-bit mask (indexed like TiledInfo::mask, L <= 10): nibbles
+// 0..L-1 = the members ascending, then the non-members ascending; bytes
+// 5..14 = colex rank of mask | (1 << k_q) among the masks of one more member,
+// for the q-th non-member k_q
+struct SubRow {
+    uint32_t w[4];
+};
+
+__host__ __device__ constexpr size_t sub_img_bytes(int N, int L, int vb)
+{
+    return (size_t)(N + (N - L)) * kSubDS * vb;
+}
+__host__ __device__ constexpr size_t sub_lds_bytes(int N, int L, int vb)
+{
+    return sub_img_bytes(N, L, vb) + (size_t)2 * 16 * vb + (size_t)tiled_region_vals(L) * vb + (size_t)16 * vb;
+}
+
+template <typename V, int N, int L>
+struct SubCtx {
+    char *img;         // LDS distance image (bytes): natural rows/columns 0..N-1, sub-cube-ordered N..N+H-1
+    const V *d0;       // d[0][k], k = 1..N at [k-1]
+    V *region;         // live low layers (as variant 5)
+    V *layerL;         // G[h | full low][m], m low: written by pass L-1, read by pass L
+    Rsrc<V> push;      // this block's push area
+    Rsrc<uint64_t> par;  // this block's parent words
+};
+
+template <typename V>
+__device__ __forceinline__ V lds_val(const char *base, uint32_t byte_off)
+{
+    return *reinterpret_cast<const V *>(base + byte_off);
+}
+// wave-uniform LDS value -> SGPR(s)
+template <typename V>
+__device__ __forceinline__ V uniform_val(const char *base, uint32_t byte_off)
+{
+    const V v = lds_val<V>(base, byte_off);
+    if constexpr (sizeof(V) == 8) {
+        const uint64_t u = __builtin_bit_cast(uint64_t, v);
+        const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)u);
+        const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(u >> 32));
+        return __builtin_bit_cast(V, ((uint64_t)hi << 32) | lo);
+    } else {
+        return (V)__builtin_amdgcn_readfirstlane((uint32_t)v);
+    }
+}
+
+// relaxations whose distance is an SGPR operand (wave-uniform)
+__device__ __forceinline__ void relax_min_s(double &acc, double g, double d)
+{
+    double t;
+    asm volatile("v_add_f64 %[t], %[g], %[d]\n\tv_min_f64 %[acc], %[acc], %[t]"
+                 : [acc] "+v"(acc), [t] "=&v"(t)
+                 : [g] "v"(g), [d] "s"(d));
+}
+__device__ __forceinline__ void relax_min_s(int32_t &acc, int32_t g, int32_t d)
+{
+    int32_t t;
+    asm volatile("v_add_u32 %[t], %[d], %[g]\n\tv_min_i32 %[acc], %[acc], %[t]"
+                 : [acc] "+v"(acc), [t] "=&v"(t)
+                 : [g] "v"(g), [d] "s"(d));
+}
+__device__ __forceinline__ void relax_argmin_s(double &acc, uint32_t &arg, double g, double d, uint32_t m)
+{
+    double t;
+    asm volatile(
+        "v_add_f64 %[t], %[g], %[d]\n\t"
+        "v_cmp_lt_f64 vcc, %[t], %[acc]\n\t"
+        "v_cndmask_b32 %[arg], %[arg], %[m], vcc\n\t"
+        "v_min_f64 %[acc], %[acc], %[t]"
+        : [acc] "+v"(acc), [arg] "+v"(arg), [t] "=&v"(t)
+        : [g] "v"(g), [d] "s"(d), [m] "v"(m)
+        : "vcc");
+}
+__device__ __forceinline__ void relax_argmin_s(int32_t &acc, uint32_t &arg, int32_t g, int32_t d, uint32_t m)
+{
+    int32_t t;
+    asm volatile(
+        "v_add_u32 %[t], %[d], %[g]\n\t"
+        "v_cmp_lt_i32 vcc, %[t], %[acc]\n\t"
+        "v_cndmask_b32 %[arg], %[arg], %[m], vcc\n\t"
+        "v_min_i32 %[acc], %[acc], %[t]"
+        : [acc] "+v"(acc), [arg] "+v"(arg), [t] "=&v"(t)
+        : [g] "v"(g), [d] "s"(d), [m] "v"(m)
+        : "vcc");
+}
+
+// generic relaxation with a first-member initialisation (edge passes)
+template <bool ARG, typename V>
+__device__ __forceinline__ void relax_any(bool first, V &acc, uint32_t &arg, V g, V d, uint32_t m)
+{
+    if (first) {
+        acc = g + d;
+        arg = m;
+    } else if constexpr (ARG) {
+        relax_argmin(acc, arg, g, d, m);
+    } else {
+        relax_min(acc, g, d);
+    }
+}
+
+// a copy of x the compiler must treat as unknown at this point: keeps it from
+// hoisting every pass's thread-index arithmetic out of the block and
+// sub-cube loops (which would keep all of it live, i.e. spilled, throughout)
+__device__ __forceinline__ uint32_t opaque_u32(uint32_t x)
+{
+    asm volatile("" : "+v"(x));
+    return x;
+}
+
+// the idx-th set bit of the low `bits` bits of x (idx wave-uniform or not)
+__device__ __forceinline__ uint32_t nth_bit(uint32_t x, uint32_t idx)
+{
+    return (uint32_t)__builtin_ctz(pdep_u32(1u << idx, x));
+}
+
+// OR of a 64-bit word over aligned groups of QP lanes (QP a power of two)
+template <int QP>
+__device__ __forceinline__ uint64_t group_or(uint64_t w)
+{
+#pragma unroll
+    for (int off = 1; off < QP; off *= 2) {
+        const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)w, off);
+        const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(w >> 32), off);
+        w |= ((uint64_t)hi << 32) | lo;
+    }
+    return w;
+}
+
+__device__ __forceinline__ uint32_t sub_nib(const uint4 &e, int i)
+{
+    return i < 8 ? (e.x >> (4 * i)) & 15u : (e.y >> (4 * (i - 8))) & 15u;
+}
+__device__ __forceinline__ uint32_t sub_rank(const uint4 &e, int q)
+{
+    const int b = 5 + q;  // byte index
+    const uint32_t w = b < 4 ? e.x : (b < 8 ? e.y : (b < 12 ? e.z : e.w));
+    return (w >> (8 * (b & 3))) & 255u;
+}
+
+// ---------------------------------------------------------------------------
+// Middle pass (h, J), 2 <= J <= L-2: a thread owns row r = tid (colex rank of
+// its low part l among the J-subsets), T = |h| + J members, Q = N - T
+// destinations; for every destination the first strict minimum over the
+// members ascending of G[T][m] + d[m][k] (tsp.cpp:457-470), argmin kept only
+// in the top rows (T >= N - TSPGPU_TILED_TA_OFF).
+// ---------------------------------------------------------------------------
+// relaxation order of a destination chunk [C0, C0 + QN): every (member,
+// destination) pair whose distance comes from LDS, member-major, then the
+// high-high pairs (SGPR distances) — per destination still members ascending
+template <int T, int J, int QL, int C0, int QN>
+__host__ __device__ constexpr int sub_lds_count()
+{
+    int n = 0;
+    for (int p = 0; p < T; ++p)
+        for (int qq = 0; qq < QN; ++qq)
+            if (!(p >= J && C0 + qq >= QL)) ++n;
+    return n;
+}
+template <int T, int J, int QL, int C0, int QN>
+__host__ __device__ constexpr int sub_lds_pair(int k)
+{
+    int n = 0;
+    for (int p = 0; p < T; ++p)
+        for (int qq = 0; qq < QN; ++qq)
+            if (!(p >= J && C0 + qq >= QL)) {
+                if (n == k) return p * 64 + qq;
+                ++n;
+            }
+    return -1;
+}
+
+#ifndef TSPGPU_SUB_QC
+#define TSPGPU_SUB_QC 7  // destinations relaxed together (register budget)
+#endif
+#ifndef TSPGPU_SUB_AHEAD
+#define TSPGPU_SUB_AHEAD 6  // distance loads in flight per lane
+#endif
+
+template <typename V, int N, int L, int T, int J>
+__device__ __forceinline__ void sub_mid(const SubCtx<V, N, L> &c, uint32_t h, uint32_t tid, const uint4 &ent)
+{
+    constexpr int H = N - L;
+    constexpr int Q = N - T;
+    constexpr int HC = T - J;   // high members (uniform)
+    constexpr int QL = L - J;   // low non-members (per lane), first
+    constexpr int QH = Q - QL;  // high non-members (uniform)
+    static_assert(J >= 2 && J <= L - 2 && HC >= 0 && HC <= H && QH >= 0, "bad middle pass");
+    constexpr int NL = 1 << L;
+    constexpr int VB = sizeof(V);
+    constexpr int ROWS = cbinom(L, J);
+    constexpr int BASE = tiled_moff(L, J);
+    constexpr int ROWS_N = cbinom(L, J + 1);
+    constexpr int REGV = tiled_region_vals(L);
+    constexpr int CUR = (J & 1) ? REGV - ROWS * J : 0;
+    constexpr int NXT = ((J + 1) & 1) ? REGV - ROWS_N * (J + 1) : 0;
+    constexpr bool ARG = T >= N - TSPGPU_TILED_TA_OFF;
+    constexpr uint32_t DSB = (uint32_t)(kSubDS * VB);
+    constexpr uint32_t HR0 = (uint32_t)N * DSB;  // image row N: the first sub-cube-ordered high row
+    constexpr uint32_t HC0 = (uint32_t)N * VB;   // image column N
+    uint32_t hm[HC > 0 ? HC : 1], hn[QH > 0 ? QH : 1];
+    {
+        uint32_t hb = h;
+#pragma unroll
+        for (int i = 0; i < HC; ++i) {
+            hm[i] = __builtin_ctz(hb);
+            hb &= hb - 1u;
+        }
+        uint32_t nb = ~h & ((1u << H) - 1u);
+#pragma unroll
+        for (int i = 0; i < QH; ++i) {
+            hn[i] = __builtin_ctz(nb);
+            nb &= nb - 1u;
+        }
+    }
+    // high-high distances of this sub-cube: wave-uniform
+    V hh[HC * QH > 0 ? HC * QH : 1];
+#pragma unroll
+    for (int i = 0; i < HC; ++i)
+#pragma unroll
+        for (int u = 0; u < QH; ++u) hh[i * QH + u] = uniform_val<V>(c.img, HR0 + i * DSB + HC0 + u * VB);
+    if (tid >= (uint32_t)ROWS) return;
+    const uint32_t r = tid;
+    const uint32_t voff = (BASE + r) * VB;  // the row's offset in a push column
+    V g[T];
+#pragma unroll
+    for (int p = 0; p < J; ++p) g[p] = c.region[CUR + p * ROWS + r];
+#pragma unroll
+    for (int i = 0; i < HC; ++i) g[J + i] = c.push.load(voff, (h * H + hm[i]) * (uint32_t)(NL * VB));
+    uint32_t mrow[J], kof[QL];
+#pragma unroll
+    for (int p = 0; p < J; ++p) mrow[p] = sub_nib(ent, p) * DSB;
+#pragma unroll
+    for (int q = 0; q < QL; ++q) kof[q] = sub_nib(ent, J + q) * VB;
+    // argmin operand: the member's image row offset (low: mrow, high: L + hm)
+    uint32_t hrow[HC > 0 ? HC : 1];
+#pragma unroll
+    for (int i = 0; i < HC; ++i) hrow[i] = (L + hm[i]) * DSB;
+    uint32_t wlo = 0, whi = 0;
+    constexpr int QC = TSPGPU_SUB_QC;
+    static_for<(Q + QC - 1) / QC>([&](auto ci) {
+        constexpr int C0 = decltype(ci)::value * QC;
+        constexpr int QN = Q - C0 < QC ? Q - C0 : QC;
+        constexpr int CNT = sub_lds_count<T, J, QL, C0, QN>();
+        constexpr int AH = TSPGPU_SUB_AHEAD < CNT ? TSPGPU_SUB_AHEAD : CNT;
+        V acc[QN];
+        uint32_t arg[ARG ? QN : 1];
+        // distance of LDS relaxation k (compile-time pair)
+        auto dload = [&](auto kk) -> V {
+            constexpr int pq = sub_lds_pair<T, J, QL, C0, QN>(decltype(kk)::value);
+            constexpr int p = pq / 64, q = C0 + pq % 64;
+            if constexpr (p < J && q < QL)
+                return lds_val<V>(c.img, mrow[p] + kof[q]);
+            else if constexpr (p < J)
+                return lds_val<V>(c.img, mrow[p] + HC0 + (q - QL) * VB);
+            else
+                return lds_val<V>(c.img, HR0 + (p - J) * DSB + kof[q]);
+        };
+        V dv[AH > 0 ? AH : 1];
+        static_for<AH>([&](auto kk) { dv[decltype(kk)::value] = dload(kk); });
+        static_for<CNT>([&](auto kk) {
+            constexpr int k = decltype(kk)::value;
+            constexpr int pq = sub_lds_pair<T, J, QL, C0, QN>(k);
+            constexpr int p = pq / 64, qq = pq % 64;
+            const V d = dv[k % AH];
+            if constexpr (k + AH < CNT) dv[k % AH] = dload(std::integral_constant<int, k + AH>{});
+            const uint32_t mo = p < J ? mrow[p < J ? p : 0] : hrow[p >= J ? p - J : 0];
+            if constexpr (p == 0) {
+                acc[qq] = g[0] + d;
+                if constexpr (ARG) arg[qq] = mo;
+            } else if constexpr (ARG) {
+                relax_argmin(acc[qq], arg[qq], g[p], d, mo);
+            } else {
+                relax_min(acc[qq], g[p], d);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        });
+        // high members x high destinations: SGPR distances
+#pragma unroll
+        for (int i = 0; i < HC; ++i)
+#pragma unroll
+            for (int qq = 0; qq < QN; ++qq) {
+                const int q = C0 + qq;
+                if (q >= QL) {
+                    if constexpr (ARG)
+                        relax_argmin_s(acc[qq], arg[qq], g[J + i], hh[i * QH + (q - QL)], hrow[i]);
+                    else
+                        relax_min_s(acc[qq], g[J + i], hh[i * QH + (q - QL)]);
+                }
+            }
+#pragma unroll
+        for (int qq = 0; qq < QN; ++qq) {
+            const int q = C0 + qq;
+            if (q < QL) {
+                // low k -> next LDS layer: position k - q, colex rank of l + k
+                const uint32_t k = kof[q] / VB;
+                const uint32_t slot = (k - (uint32_t)q) * (uint32_t)ROWS_N + sub_rank(ent, q);
+                c.region[NXT + slot] = acc[qq];
+            } else {
+                // high k -> push column (h | k, k) of sub-cube h | k, same row index
+                const uint32_t cb = hn[q - QL];
+                c.push.store(voff, ((h | (1u << cb)) * H + cb) * (uint32_t)(NL * VB), acc[qq]);
+            }
+            if constexpr (ARG) {
+                const uint32_t pos = arg[qq] / DSB;  // image row of the argmin member = its city bit
+                if (q < 8)
+                    wlo |= pos << (4 * q);
+                else
+                    whi |= pos << (4 * (q - 8));
+            }
+        }
+    });
+    if constexpr (ARG) c.par.store((BASE + r) * 8u, h * (uint32_t)(NL * 8), ((uint64_t)whi << 32) | wlo);
+}
+
+// ---------------------------------------------------------------------------
+// First interval of sub-cube h (|h| = C): passes j = 0 and j = 1 in
+// destination-parallel form.  Lane (a, q) < L * Q1: row {a} of sub-cube h,
+// destination = its q-th non-member (low ones first); it first recomputes the
+// row's own G[h + a][a] (j = 0's relaxation for destination a; at h = 0 that
+// is d[0][a], tsp.cpp:435), then the row's C + 1 relaxations.  Lanes
+// L * Q1 + u: j = 0's high destinations (pushes of row 0).  Min-only (T <= 6).
+// ---------------------------------------------------------------------------
+template <typename V, int N, int L, int C>
+__device__ __forceinline__ void sub_first(const SubCtx<V, N, L> &c, uint32_t h, uint32_t tid)
+{
+    constexpr int H = N - L, QH = H - C, Q1 = N - 1 - C;
+    constexpr int NL = 1 << L, VB = sizeof(V);
+    constexpr uint32_t DSB = (uint32_t)(kSubDS * VB);
+    constexpr int ROWS2 = cbinom(L, 2);
+    static_assert(C + 1 < N - TSPGPU_TILED_TA_OFF, "first passes are min-only");
+    if (tid >= (uint32_t)(L * Q1 + (C > 0 ? QH : 0))) return;
+    uint32_t hm[C > 0 ? C : 1];
+    {
+        uint32_t hb = h;
+#pragma unroll
+        for (int i = 0; i < C; ++i) {
+            hm[i] = __builtin_ctz(hb);
+            hb &= hb - 1u;
+        }
+    }
+    const uint32_t nh = ~h & ((1u << H) - 1u);
+    V g0[C > 0 ? C : 1];  // G[h][hm_i]: row 0 of sub-cube h (wave-uniform)
+#pragma unroll
+    for (int i = 0; i < C; ++i) g0[i] = c.push.load(0, (h * H + hm[i]) * (uint32_t)(NL * VB));
+    if (tid < (uint32_t)(L * Q1)) {
+        const uint32_t a = tid / Q1, q = tid % Q1;
+        const uint32_t kk = q < (uint32_t)(L - 1) ? q + (q >= a ? 1u : 0u) : L + nth_bit(nh, q - (L - 1));
+        V gA;
+        if constexpr (C == 0) {
+            gA = c.d0[a];
+        } else {
+            gA = g0[0] + lds_val<V>(c.img, (L + hm[0]) * DSB + a * VB);
+#pragma unroll
+            for (int i = 1; i < C; ++i)
+                gA = ValT<V>::vmin(gA, g0[i] + lds_val<V>(c.img, (L + hm[i]) * DSB + a * VB));
+        }
+        V acc = gA + lds_val<V>(c.img, a * DSB + kk * VB);
+        const uint32_t voff = (1u + a) * VB;  // row {a}: index 1 + a in the mask list
+#pragma unroll
+        for (int i = 0; i < C; ++i) {
+            const V g1 = c.push.load(voff, (h * H + hm[i]) * (uint32_t)(NL * VB));
+            relax_min(acc, g1, lds_val<V>(c.img, (L + hm[i]) * DSB + kk * VB));
+        }
+        if (kk < (uint32_t)L) {
+            // layer 2 (even: bottom of the region): position of kk in {a, kk}, colex rank
+            const uint32_t lo = a < kk ? a : kk, hi = a < kk ? kk : a;
+            c.region[(kk > a ? ROWS2 : 0) + hi * (hi - 1) / 2 + lo] = acc;
+        } else {
+            const uint32_t x = kk - L;
+            c.push.store(voff, ((h | (1u << x)) * H + x) * (uint32_t)(NL * VB), acc);
+        }
+    } else if constexpr (C > 0) {
+        // pass j = 0, high destination: G[h + x][x] -> push row 0 of sub-cube h | x
+        const uint32_t x = nth_bit(nh, tid - L * Q1);
+        V acc = g0[0] + lds_val<V>(c.img, (L + hm[0]) * DSB + (L + x) * VB);
+#pragma unroll
+        for (int i = 1; i < C; ++i) relax_min(acc, g0[i], lds_val<V>(c.img, (L + hm[i]) * DSB + (L + x) * VB));
+        c.push.store(0, ((h | (1u << x)) * H + x) * (uint32_t)(NL * VB), acc);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Pass j = L of sub-cube h (|h| = C): the full low set, high destinations
+// only, a lane per destination (lanes 0..QP-1 of the calling group).
+// ---------------------------------------------------------------------------
+template <typename V, int N, int L, int C>
+__device__ __forceinline__ void sub_last(const SubCtx<V, N, L> &c, uint32_t h, uint32_t lane)
+{
+    constexpr int H = N - L, Q = H - C, T = L + C;
+    static_assert(Q >= 1 && T < N, "pass L needs a high destination");
+    constexpr bool ARG = T >= N - TSPGPU_TILED_TA_OFF;
+    constexpr int QP = pow2_at_least(Q);
+    constexpr int NL = 1 << L, VB = sizeof(V);
+    constexpr uint32_t DSB = (uint32_t)(kSubDS * VB);
+    if (lane >= (uint32_t)QP) return;
+    uint32_t hm[C > 0 ? C : 1];
+    {
+        uint32_t hb = h;
+#pragma unroll
+        for (int i = 0; i < C; ++i) {
+            hm[i] = __builtin_ctz(hb);
+            hb &= hb - 1u;
+        }
+    }
+    const bool act = lane < (uint32_t)Q;
+    const uint32_t x = nth_bit(~h & ((1u << H) - 1u), act ? lane : 0u);
+    const uint32_t kk = L + x;
+    V acc = V(0);
+    uint32_t arg = 0;
+#pragma unroll
+    for (int m = 0; m < L; ++m) relax_any<ARG>(m == 0, acc, arg, c.layerL[m], lds_val<V>(c.img, m * DSB + kk * VB), (uint32_t)m);
+#pragma unroll
+    for (int i = 0; i < C; ++i) {
+        const V g = c.push.load((NL - 1) * VB, (h * H + hm[i]) * (uint32_t)(NL * VB));
+        relax_any<ARG>(false, acc, arg, g, lds_val<V>(c.img, (L + hm[i]) * DSB + kk * VB), L + hm[i]);
+    }
+    if (act) c.push.store((NL - 1) * VB, ((h | (1u << x)) * H + x) * (uint32_t)(NL * VB), acc);
+    if constexpr (ARG) {
+        const uint64_t w = group_or<QP>(act ? (uint64_t)arg << (4 * lane) : 0ull);
+        if (lane == 0) c.par.store((NL - 1) * 8u, h * (uint32_t)(NL * 8), w);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Pass j = L - 1 of sub-cube h (|h| = C): rows full \ {b} (rank r = L-1-b),
+// destinations b (-> layerL[b]) and the high non-members; a lane per (row,
+// destination), QP lanes per row.
+// ---------------------------------------------------------------------------
+template <typename V, int N, int L, int C>
+__device__ __forceinline__ void sub_penult(const SubCtx<V, N, L> &c, uint32_t h, uint32_t tid)
+{
+    constexpr int H = N - L, QH = H - C, Q = 1 + QH, T = L - 1 + C, J = L - 1;
+    constexpr bool ARG = T >= N - TSPGPU_TILED_TA_OFF;
+    constexpr int QP = pow2_at_least(Q);
+    constexpr int NL = 1 << L, VB = sizeof(V);
+    constexpr uint32_t DSB = (uint32_t)(kSubDS * VB);
+    constexpr int ROWS = L, BASE = tiled_moff(L, J), REGV = tiled_region_vals(L);
+    constexpr int CUR = (J & 1) ? REGV - ROWS * J : 0;
+    if (tid >= (uint32_t)(L * QP)) return;
+    uint32_t hm[C > 0 ? C : 1];
+    {
+        uint32_t hb = h;
+#pragma unroll
+        for (int i = 0; i < C; ++i) {
+            hm[i] = __builtin_ctz(hb);
+            hb &= hb - 1u;
+        }
+    }
+    const uint32_t r = tid / QP, q = tid % QP, b = L - 1 - r;
+    const bool act = q < (uint32_t)Q;
+    const uint32_t x = (act && q > 0) ? nth_bit(~h & ((1u << H) - 1u), q - 1) : 0u;
+    const uint32_t kk = q == 0 ? b : L + x;
+    const uint32_t voff = (BASE + r) * VB;
+    V acc = V(0);
+    uint32_t arg = 0;
+#pragma unroll
+    for (int p = 0; p < L - 1; ++p) {
+        const uint32_t m = (uint32_t)p + ((uint32_t)p >= b ? 1u : 0u);
+        relax_any<ARG>(p == 0, acc, arg, c.region[CUR + p * ROWS + r], lds_val<V>(c.img, m * DSB + kk * VB), m);
+    }
+#pragma unroll
+    for (int i = 0; i < C; ++i) {
+        const V g = c.push.load(voff, (h * H + hm[i]) * (uint32_t)(NL * VB));
+        relax_any<ARG>(false, acc, arg, g, lds_val<V>(c.img, (L + hm[i]) * DSB + kk * VB), L + hm[i]);
+    }
+    if (act) {
+        if (q == 0)
+            c.layerL[b] = acc;
+        else
+            c.push.store(voff, ((h | (1u << x)) * H + x) * (uint32_t)(NL * VB), acc);
+    }
+    if constexpr (ARG) {
+        const uint64_t w = group_or<QP>(act ? (uint64_t)arg << (4 * q) : 0ull);
+        if (q == 0) c.par.store((BASE + r) * 8u, h * (uint32_t)(NL * 8), w);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Sub-cube-ordered high rows/columns of sub-cube h in the image (rows and
+// columns N..N+H-1): position x of sigma_h = (members ascending, then
+// non-members ascending).  e in [0, H*L): x = e / L, low k = e % L; then the
+// high-high block.  Each entry is one LDS read and one LDS write.
+// ---------------------------------------------------------------------------
+template <typename V, int N, int L>
+__device__ __forceinline__ void sub_build_high(const SubCtx<V, N, L> &c, uint32_t h, uint32_t e)
+{
+    constexpr int H = N - L, VB = sizeof(V);
+    constexpr uint32_t DSB = (uint32_t)(kSubDS * VB);
+    const uint32_t cc = (uint32_t)__builtin_popcount(h);
+    const uint32_t nh = ~h & ((1u << H) - 1u);
+    char *img = c.img;
+    if (e < (uint32_t)(H * L)) {
+        const uint32_t x = e / L, k = e % L;
+        if (x < cc) {
+            const uint32_t s = nth_bit(h, x);
+            *reinterpret_cast<V *>(img + (N + x) * DSB + k * VB) = lds_val<V>(img, (L + s) * DSB + k * VB);
+        } else {
+            const uint32_t s = nth_bit(nh, x - cc);
+            *reinterpret_cast<V *>(img + k * DSB + (N + x - cc) * VB) = lds_val<V>(img, k * DSB + (L + s) * VB);
+        }
+    } else if (e < (uint32_t)(H * L) + cc * ((uint32_t)H - cc)) {
+        const uint32_t f = e - H * L, i = f / ((uint32_t)H - cc), u = f % ((uint32_t)H - cc);
+        const uint32_t si = nth_bit(h, i), su = nth_bit(nh, u);
+        *reinterpret_cast<V *>(img + (N + i) * DSB + (N + u) * VB) = lds_val<V>(img, (L + si) * DSB + (L + su) * VB);
+    }
+}
+
+template <typename V, int N, int L, int J>
+__device__ __forceinline__ void sub_dispatch_mid_j(const SubCtx<V, N, L> &c, uint32_t h, int hc, uint32_t tid,
+                                                   const uint4 &ent)
+{
+    constexpr int H = N - L;
+#define TSPGPU_SM(HC)                                                                       \
+    case HC:                                                                                \
+        if constexpr (HC <= H) sub_mid<V, N, L, J + (HC <= H ? HC : 0), J>(c, h, tid, ent);  \
+        break;
+    switch (hc) {
+        TSPGPU_SM(0) TSPGPU_SM(1) TSPGPU_SM(2) TSPGPU_SM(3) TSPGPU_SM(4) TSPGPU_SM(5) TSPGPU_SM(6) TSPGPU_SM(7)
+    default: break;
+    }
+#undef TSPGPU_SM
+}
+
+#define TSPGPU_SUB_SWITCH_C(CVAR, FN, ...)                                                  \
+    switch (CVAR) {                                                                         \
+    case 0: if constexpr (0 <= H) FN<V, N, L, 0>(__VA_ARGS__); break;                       \
+    case 1: if constexpr (1 <= H) FN<V, N, L, (1 <= H ? 1 : 0)>(__VA_ARGS__); break;        \
+    case 2: if constexpr (2 <= H) FN<V, N, L, (2 <= H ? 2 : 0)>(__VA_ARGS__); break;        \
+    case 3: if constexpr (3 <= H) FN<V, N, L, (3 <= H ? 3 : 0)>(__VA_ARGS__); break;        \
+    case 4: if constexpr (4 <= H) FN<V, N, L, (4 <= H ? 4 : 0)>(__VA_ARGS__); break;        \
+    case 5: if constexpr (5 <= H) FN<V, N, L, (5 <= H ? 5 : 0)>(__VA_ARGS__); break;        \
+    case 6: if constexpr (6 <= H) FN<V, N, L, (6 <= H ? 6 : 0)>(__VA_ARGS__); break;        \
+    default: break;                                                                         \
+    }
+
+template <typename V, int N, int L>
+__device__ __forceinline__ void sub_dispatch_first(const SubCtx<V, N, L> &c, uint32_t h, int hc, uint32_t tid)
+{
+    constexpr int H = N - L;
+    TSPGPU_SUB_SWITCH_C(hc, sub_first, c, h, tid)
+}
+template <typename V, int N, int L>
+__device__ __forceinline__ void sub_dispatch_penult(const SubCtx<V, N, L> &c, uint32_t h, int hc, uint32_t tid)
+{
+    constexpr int H = N - L;
+    TSPGPU_SUB_SWITCH_C(hc, sub_penult, c, h, tid)
+}
+template <typename V, int N, int L>
+__device__ __forceinline__ void sub_dispatch_last(const SubCtx<V, N, L> &c, uint32_t h, int hc, uint32_t lane)
+{
+    constexpr int H = N - L;
+    // (|h| = H has no pass L: the full set has no destination)
+    switch (hc) {
+    case 0: if constexpr (0 < H) sub_last<V, N, L, 0>(c, h, lane); break;
+    case 1: if constexpr (1 < H) sub_last<V, N, L, (1 < H ? 1 : 0)>(c, h, lane); break;
+    case 2: if constexpr (2 < H) sub_last<V, N, L, (2 < H ? 2 : 0)>(c, h, lane); break;
+    case 3: if constexpr (3 < H) sub_last<V, N, L, (3 < H ? 3 : 0)>(c, h, lane); break;
+    case 4: if constexpr (4 < H) sub_last<V, N, L, (4 < H ? 4 : 0)>(c, h, lane); break;
+    case 5: if constexpr (5 < H) sub_last<V, N, L, (5 < H ? 5 : 0)>(c, h, lane); break;
+    default: break;
+    }
+}
+
+// Forward pass + closing min of blocks blk0 + blockIdx.x, +gridDim.x, ...;
+// writes cost_out[blk] and the tour's last inner city (tour[n-1]) like
+// hk_tiled_kernel; hk_tiled_backtrack completes the tour from the slot.
+template <typename V, int N, int L, int THREADS, int WG>
+__global__ __launch_bounds__(THREADS, tiled_waves(THREADS, WG)) void hk_sub_kernel(
+    const V *__restrict__ dist, int nblocks, int blk0, char *__restrict__ slots, uint32_t slot_bytes,
+    const SubRow *__restrict__ rows, V *__restrict__ cost_out, int32_t *__restrict__ tour_out)
+{
+    constexpr int H = N - L;
+    constexpr int NH = 1 << H;
+    constexpr int NL = 1 << L;
+    constexpr int n = N + 1;
+    constexpr int VB = sizeof(V);
+    constexpr uint32_t DSB = (uint32_t)(kSubDS * VB);
+    static_assert(H >= 1 && H <= 6 && L >= 5 && L <= 10, "variant 6 sizes");
+    static_assert(kSubDS >= N + H, "image stride");
+    static_assert(THREADS >= 256 && L * (N - 1) + H <= 192, "edge passes: lanes 0..191, pass L at 192..");
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    SubCtx<V, N, L> c;
+    c.img = smem;
+    V *d0 = reinterpret_cast<V *>(smem + sub_img_bytes(N, L, VB));
+    V *dc = d0 + 16;
+    c.d0 = d0;
+    c.region = dc + 16;
+    c.layerL = c.region + tiled_region_vals(L);
+    const uint32_t tid = threadIdx.x;
+    const uint4 *rowtab = reinterpret_cast<const uint4 *>(rows);
+
+    for (int blk = blk0 + blockIdx.x; blk < nblocks; blk += gridDim.x) {
+        char *slot = slots + (size_t)(blk - blk0) * slot_bytes;
+        c.push.rs = uniform_rsrc(slot, (uint32_t)tiled_push_bytes(N, L, VB));
+        c.par.rs = uniform_rsrc(slot + tiled_push_bytes(N, L, VB), (uint32_t)tiled_parent_bytes(N, L));
+        const V *dsrc = dist + (size_t)blk * n * n;
+        // natural image (inner distances) and, for sub-cube 0 (no high
+        // member), the high columns in order
+        for (int i = tid; i < N * N; i += THREADS) {
+            const int m = i / N, k = i % N;
+            const V v = dsrc[(m + 1) * n + (k + 1)];
+            *reinterpret_cast<V *>(smem + m * DSB + k * VB) = v;
+            if (m < L && k >= L) *reinterpret_cast<V *>(smem + m * DSB + (N + k - L) * VB) = v;
+        }
+        if (tid < N) {
+            d0[tid] = dsrc[tid + 1];
+            dc[tid] = dsrc[(tid + 1) * n];
+        }
+        // layer 1 of the high cities: G[{x}][x] = d[0][x] (tsp.cpp:435), pushed to sub-cube {x}, row 0
+        if (tid < H) c.push.store(0, (((1u << tid) * H + tid) * NL) * VB, dsrc[L + tid + 1]);
+        __syncthreads();
+
+        uint4 ent = make_uint4(0, 0, 0, 0);
+        for (uint32_t h = 0; h < (uint32_t)NH; ++h) {
+            const int hc = __builtin_popcount(h);
+            // interval A(h): passes 0/1 of h (lanes < 192) beside pass L of h - 1 (lanes 192..)
+            uint32_t t = opaque_u32(tid);
+            {
+                constexpr int M2 = tiled_moff(L, 2), C2 = cbinom(L, 2);
+                ent = rowtab[M2 + (t < (uint32_t)C2 ? t : 0u)];
+            }
+            if (t < 192u)
+                sub_dispatch_first<V, N, L>(c, h, hc, t);
+            else if (h > 0)
+                sub_dispatch_last<V, N, L>(c, h - 1, __builtin_popcount(h - 1), t - 192u);
+            __syncthreads();
+            // middle passes j = 2..L-2, unrolled (every offset a compile-time
+            // constant); the next pass's row entry is loaded one pass ahead
+            static_for<L - 3>([&](auto jj) {
+                constexpr int j = 2 + decltype(jj)::value;
+                const uint4 cur = ent;
+                const uint32_t tj = opaque_u32(tid);
+                if constexpr (j + 1 <= L - 2) {
+                    constexpr int MN = tiled_moff(L, j + 1), CN = cbinom(L, j + 1);
+                    ent = rowtab[MN + (tj < (uint32_t)CN ? tj : 0u)];
+                }
+                sub_dispatch_mid_j<V, N, L, j>(c, h, hc, tj, cur);
+                lds_barrier();
+            });
+            // pass L - 1 (lanes < 128) beside the next sub-cube's high image rows/columns (lanes 128..)
+            t = opaque_u32(tid);
+            if (t < 128u)
+                sub_dispatch_penult<V, N, L>(c, h, hc, t);
+            else if (h + 1 < (uint32_t)NH)
+                sub_build_high<V, N, L>(c, h + 1, t - 128u);
+            __syncthreads();
+        }
+
+        // closing min (tsp.cpp:483-499): G[full][m] + d[m][0], first strict min
+        if (tid < 64) {
+            const int m = tid + 1;
+            const bool valid = m <= N;
+            V gl = V(0);
+            if (valid) {
+                if (m <= L)
+                    gl = c.layerL[m - 1];
+                else
+                    gl = c.push.load((NL - 1) * VB, ((uint32_t)((NH - 1) * H + (m - 1 - L)) * NL) * VB);
+            }
+            const V cand = valid ? gl + dc[m - 1] : ValT<V>::invalid;
+            const V best = ValT<V>::vmin(wave_min(cand), ValT<V>::inf);
+            const unsigned long long hit = __ballot(valid && cand == best && cand < ValT<V>::inf);
+            const int bestM = hit ? __ffsll(hit) : 0;
+            if (tid == 0) {
+                int32_t *tour = tour_out + (size_t)blk * (n + 1);
+                tour[0] = 0;
+                tour[n - 1] = bestM;
+                tour[n] = 0;
+                cost_out[blk] = bestM ? best : V(-1);
+            }
+        }
+        __syncthreads();
+    }
+}
+
+struct SubArgs {
+    const void *dist;
+    int n, blk0, blk1;
+    char *slots;
+    uint32_t slot_bytes;
+    const SubRow *rows;       // row table of L
+    const TiledInfo *info;    // (backtracking)
+    void *cost;
+    int32_t *tour;
+    int grid, bt_grid;
+    hipStream_t stream;
+    hipEvent_t ev_mid;
+};
+
+template <typename V, int N, int L, int THREADS, int WG>
+hipError_t launch_sub_n(const SubArgs &a)
+{
+    const size_t lds = sub_lds_bytes(N, L, sizeof(V));
+    static bool raised = false;
+    if (!raised) {
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&hk_sub_kernel<V, N, L, THREADS, WG>),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) return e;
+        raised = true;
+    }
+    hipLaunchKernelGGL((hk_sub_kernel<V, N, L, THREADS, WG>), dim3(a.grid), dim3(THREADS), lds, a.stream,
+                       static_cast<const V *>(a.dist), a.blk1, a.blk0, a.slots, a.slot_bytes, a.rows,
+                       static_cast<V *>(a.cost), a.tour);
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess && a.ev_mid) e = hipEventRecord(a.ev_mid, a.stream);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL((hk_tiled_backtrack<V, N, L>), dim3(a.bt_grid), dim3(64 * kTiledBtWaves), 0, a.stream, a.blk1,
+                       a.blk0, a.slots, a.slot_bytes, a.info, static_cast<const V *>(a.dist), static_cast<V *>(a.cost),
+                       a.tour);
+    return hipGetLastError();
+}
+
+}  // namespace tspgpu

@@ -1,4 +1,4 @@
-// K1 variant 5 instantiation 19 (table: hkt_cfg.h)
+// K1 variant 5 configuration 19 (k1_cfg.h, tools/gen_k1_cfgs.py)
 #include "hk_tiled.h"
 namespace tspgpu {
 template hipError_t launch_tiled_n<int32_t, 15, 10, 256, 1, 6>(const TiledArgs &);

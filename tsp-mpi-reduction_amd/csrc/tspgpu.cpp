@@ -23,7 +23,7 @@
 
 #include "ctx.h"
 #include "heldkarp.h"
-#include "hkt_cfg.h"
+#include "k1_cfg.h"
 
 namespace tspgpu {
 
@@ -163,6 +163,114 @@ int ensure_tiled_info(tspgpu_ctx *c, int L)
     return 0;
 }
 
+// Variant 6 row table of L (hk_sub.h SubRow): per L-bit mask, its members
+// then non-members as nibbles, and the colex rank of mask | (1 << k) for every
+// non-member k (the destination row of the next low layer).
+int ensure_sub_rows(tspgpu_ctx *c, int L)
+{
+    if (L > 10) return -EINVAL;  // 8-bit ranks: C(10, 5) = 252
+    if (c->d_subrows[L]) return 0;
+    int rc = ensure_tiled_info(c, L);
+    if (rc) return rc;
+    std::vector<int> rank(1 << L, 0);
+    std::vector<uint32_t> order;  // masks by (popcount, value) = TiledInfo::mask
+    for (int j = 0; j <= L; ++j) {
+        int r = 0;
+        for (uint32_t m = 0; m < (1u << L); ++m)
+            if (__builtin_popcount(m) == j) {
+                rank[m] = r++;
+                order.push_back(m);
+            }
+    }
+    std::vector<SubRow> rows(order.size());
+    for (size_t i = 0; i < order.size(); ++i) {
+        const uint32_t m = order[i];
+        uint8_t bytes[16] = {0};
+        int slot = 0, q = 0;
+        auto put_nib = [&](int idx, uint32_t v) { bytes[idx / 2] |= (uint8_t)(v << (4 * (idx & 1))); };
+        for (int b = 0; b < L; ++b)
+            if (m >> b & 1) put_nib(slot++, (uint32_t)b);
+        for (int b = 0; b < L; ++b)
+            if (!(m >> b & 1)) {
+                put_nib(slot++, (uint32_t)b);
+                bytes[5 + q++] = (uint8_t)rank[m | (1u << b)];
+            }
+        std::memcpy(rows[i].w, bytes, 16);
+    }
+    void *d = nullptr;
+    hipError_t e = hipMalloc(&d, rows.size() * sizeof(SubRow));
+    if (e == hipSuccess) e = hipMemcpy(d, rows.data(), rows.size() * sizeof(SubRow), hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+        if (d) (void)hipFree(d);
+        return hip_err(e);
+    }
+    c->d_subrows[L] = d;
+    return 0;
+}
+
+// K1 variant 6 (hk_sub.h) configuration for (N, value bytes): the one
+// TSPGPU_TILED_CFG names, else the first row of the table; null if none.
+const SubCfg *pick_sub(const tspgpu_ctx *c, int N, int vbytes)
+{
+    int cnt = 0;
+    const SubCfg *t = sub_cfgs(&cnt);
+    if (c->tiled_cfg >= 0) {
+        for (int i = 0; i < cnt; ++i)
+            if (t[i].id == c->tiled_cfg && t[i].N == N && t[i].vbytes == vbytes) return &t[i];
+        return nullptr;
+    }
+    for (int i = 0; i < cnt; ++i)
+        if (t[i].N == N && t[i].vbytes == vbytes) return &t[i];
+    return nullptr;
+}
+
+int solve_sub(tspgpu_ctx *c, const SubCfg *cfg, const void *d_dist, int n, int nblocks, void *d_cost,
+              int32_t *d_tour, hipStream_t stream)
+{
+    const int N = n - 1, L = cfg->L;
+    int rc = ensure_sub_rows(c, L);
+    if (rc) return rc;
+    const int grid = std::min(nblocks, c->cu_count * cfg->wg);
+    // the same per-block slot as variant 5 (push area, parent words,
+    // recompute area), kept until the backtracking kernel has run
+    const size_t slot = tiled_slot_bytes(N, L, cfg->vbytes);
+    const int chunk = std::min(nblocks, 16384);
+    if ((rc = ensure(&c->d_tslots, &c->tslots_bytes, (size_t)chunk * slot))) return rc;
+    const bool split = c->split_timing && nblocks <= chunk;
+    c->split_valid = 0;
+    if (split) {
+        for (auto &ev : c->ev_split)
+            if (!ev && hipEventCreate(&ev) != hipSuccess) return -EIO;
+        if (hipEventRecord(c->ev_split[0], stream) != hipSuccess) return -EIO;
+    }
+    for (int b0 = 0; b0 < nblocks; b0 += chunk) {
+        SubArgs a{};
+        a.ev_mid = split ? c->ev_split[1] : nullptr;
+        a.dist = d_dist;
+        a.n = n;
+        a.blk0 = b0;
+        a.blk1 = std::min(nblocks, b0 + chunk);
+        a.slots = c->d_tslots;
+        a.slot_bytes = (uint32_t)slot;
+        a.rows = static_cast<const SubRow *>(c->d_subrows[L]);
+        a.info = static_cast<const TiledInfo *>(c->d_tinfo[L]);
+        a.cost = d_cost;
+        a.tour = d_tour;
+        a.grid = std::min(grid, a.blk1 - a.blk0);
+        a.bt_grid = std::min((a.blk1 - a.blk0 + kTiledBtWaves - 1) / kTiledBtWaves, c->cu_count * TSPGPU_TILED_BTWG);
+        a.stream = stream;
+        hipError_t e = cfg->launch(a);
+        if (e != hipSuccess) return hip_err(e);
+    }
+    if (split) {
+        if (hipEventRecord(c->ev_split[2], stream) != hipSuccess) return -EIO;
+        c->split_valid = 1;
+    }
+    c->last_grid = grid;
+    c->last_variant = 6;
+    return 0;
+}
+
 // K1 variant 5 (sub-cube tiled, hk_tiled.h) configuration for (N, value
 // bytes): TSPGPU_TILED_CFG / c->tiled_cfg, else the measured default; null if
 // none exists for this size.
@@ -191,8 +299,7 @@ int solve_tiled(tspgpu_ctx *c, const TiledCfg *cfg, const void *d_dist, int n, i
     // backtracking recompute area: 1.65 MB at n = 16, hk_tiled.h), kept until
     // the backtracking kernel of the launch has run: blocks go in launches of
     // at most 16384 (27 GB of the 288 GB at n = 16)
-    size_t slot = tiled_slot_bytes(N, L, cfg->vbytes);
-    if (const char *e = std::getenv("TSPGPU_SLOT_PAD")) slot += (size_t)std::atol(e);  // (layout experiments)
+    const size_t slot = tiled_slot_bytes(N, L, cfg->vbytes);
     const int chunk = std::min(nblocks, 16384);
     if ((rc = ensure(&c->d_tslots, &c->tslots_bytes, (size_t)chunk * slot))) return rc;
     const bool split = c->split_timing && nblocks <= chunk;  // one launch pair: one split
@@ -302,15 +409,20 @@ int solve_device_unordered(tspgpu_ctx *c, const void *d_dist, int n, int nblocks
         // all 256 resident blocks then stay in the Infinity Cache), not below
         // (with a full wave of blocks: one block alone is latency-bound and the
         // argmin's extra VALU only costs there)
-        // a full wave of blocks: the sub-cube tiled kernel (variant 5,
-        // hk_tiled.h) at 13-16 cities f64 and 16 cities i32; per 16384 blocks
-        // (profiles/r02/k1_tiled_v17_cfgs.log, k1_tiled_v19_small.log): n = 16
-        // f64 7.6 vs 12.0 ms (variant 4), n = 15 3.75 vs 4.59, n = 14 1.80 vs
-        // 2.20, n = 13 0.88 vs 1.06, n = 16 i32 5.72 vs 7.63 (variant 2); the
-        // compact layer pass (variant 2) stays ahead below 13 cities and for
-        // i32 at 14-15 (1.34 vs 1.38, 2.78 vs 2.74 ms)
+        // a full wave of blocks: the sub-cube kernels — variant 6 (hk_sub.h)
+        // where it has a configuration, else variant 5 (hk_tiled.h) — at
+        // 13-16 cities f64 and 16 cities i32 (round 2, per 16384 blocks:
+        // variant 5 n = 16 f64 7.6 vs 12.0 ms for variant 4, n = 15 3.75 vs
+        // 4.59, n = 14 1.80 vs 2.20, n = 13 0.88 vs 1.06, n = 16 i32 5.72 vs
+        // 7.63 for variant 2, profiles/r02/k1_tiled_v17_cfgs.log); the compact
+        // layer pass (variant 2) elsewhere
         const bool tiled = vbytes == 8 ? (N >= 12 && N <= 15) : N == 15;
-        a.variant = c->variant >= 0 ? c->variant : (tiled && nblocks >= c->cu_count ? 5 : 2);
+        a.variant = c->variant >= 0 ? c->variant : (tiled && nblocks >= c->cu_count ? 6 : 2);
+        if (a.variant == 6) {
+            if (const SubCfg *cfg = pick_sub(c, N, vbytes))
+                return solve_sub(c, cfg, d_dist, n, nblocks, d_cost, d_tour, stream);
+            a.variant = 5;  // no variant-6 configuration for this size
+        }
         if (a.variant == 5) {
             if (const TiledCfg *cfg = pick_tiled(c, N, vbytes))
                 return solve_tiled(c, cfg, d_dist, n, nblocks, d_cost, d_tour, stream);
@@ -482,7 +594,7 @@ int tspgpu_ctx_create(const tspgpu_opts *opts, tspgpu_ctx **out)
     }
     if (const char *e = std::getenv("TSPGPU_K1")) {
         const int v = std::atoi(e);
-        c->variant = v < 0 ? 1 : (v >= 5 ? 5 : (v >= 4 ? 4 : (v > 2 ? 2 : v)));
+        c->variant = v < 0 ? 1 : (v >= 6 ? 6 : (v >= 4 ? v : (v > 2 ? 2 : v)));
     }
     if (const char *e = std::getenv("TSPGPU_TILED_CFG")) c->tiled_cfg = std::atoi(e);
     if (const char *e = std::getenv("TSPGPU_WG_PER_CU")) c->wg_per_cu = std::atoi(e) > 0 ? std::atoi(e) : 0;
@@ -507,6 +619,8 @@ int tspgpu_ctx_destroy(tspgpu_ctx *c)
     if (c->search_pool_free) c->search_pool_free(c->search_pool);
     if (c->d_slots) (void)hipFree(c->d_slots);
     for (void *p : c->d_tinfo)
+        if (p) (void)hipFree(p);
+    for (void *p : c->d_subrows)
         if (p) (void)hipFree(p);
     if (c->d_tslots) (void)hipFree(c->d_tslots);
     if (c->d_dist) (void)hipFree(c->d_dist);
@@ -648,7 +762,7 @@ int tspgpu_k1_split_timing(tspgpu_ctx *c, int enable)
 int tspgpu_k1_last_split_ms(tspgpu_ctx *c, float *forward_ms, float *backtrack_ms)
 {
     if (!c || !forward_ms || !backtrack_ms) return -EINVAL;
-    if (!c->split_valid || c->last_variant != 5) return -ENOENT;
+    if (!c->split_valid || (c->last_variant != 5 && c->last_variant != 6)) return -ENOENT;
     if (hipSetDevice(c->device) != hipSuccess) return -ENODEV;
     hipError_t e = hipEventSynchronize(c->ev_split[2]);
     if (e == hipSuccess) e = hipEventElapsedTime(forward_ms, c->ev_split[0], c->ev_split[1]);

@@ -12,9 +12,14 @@
 // reference's share (cnt[r] contiguous blocks, tsp.cpp:167-192), on GPU
 // r mod (visible devices) (TSP_GPU overrides), and hands its costs and tours
 // to rank 0 through a file in a per-job directory (no MPI library is linked:
-// TSP_GATHER_DIR, else /tmp/tspgpu-<uid>-<parent pid>-<args>, the parent
-// being mpirun's proxy, shared by the ranks of one node); rank 0 waits for all
-// of them, replays the reduction and prints.  One node only.
+// TSP_GATHER_DIR, else /tmp/tspgpu-<uid>-<job key>); rank 0 waits for all of
+// them, replays the reduction and prints.  One node only.  The job key hashes
+// the launcher's job id (PMIX_NAMESPACE, OMPI_MCA_ess_base_jobid,
+// SLURM_JOB_ID.SLURM_STEP_ID) or, under MPICH's hydra (which exports none),
+// the parent process — the node's proxy, shared by its ranks — with its start
+// time, plus the four arguments; every rank file carries it, so a file left by
+// an earlier run is recognised as stale and ignored.  A worker that fails
+// publishes a failure record, so rank 0 stops waiting at once.
 // Without mpirun, physical GPUs (TSP_GPUS, default 1; device g mod visible
 // devices for g < TSP_GPUS) only change speed: the blocks are split into
 // contiguous ranges, one host thread per GPU.  The merges (local folds +
@@ -101,25 +106,78 @@ int solve_range(const std::vector<tspgpu_city> &cities, int n, int lo, int count
 // ---- rank-per-GPU mode: every rank's block results to rank 0 through files ----
 struct RankFileHeader {
     uint32_t magic, rank, count, n;
+    int32_t B, X, Y, status;  // status 0: results follow; < 0: the rank failed with this code
+    uint64_t job;             // job key (job_key): equal in every rank of one run
 };
-constexpr uint32_t kMagic = 0x54535047;  // "TSPG"
+constexpr uint32_t kMagic = 0x32505354;  // "TSP2"
 
-std::string gather_dir(int n, int B, int X, int Y)
+uint64_t fnv1a(const std::string &s)
+{
+    uint64_t h = 1469598103934665603ull;
+    for (unsigned char c : s) h = (h ^ c) * 1099511628211ull;
+    return h;
+}
+
+// Start time (clock ticks since boot) of process `pid`, 0 if unknown: with the
+// pid it names one process, even after the pid is reused.
+unsigned long long proc_start_ticks(int pid)
+{
+    char path[64], buf[1024];
+    std::snprintf(path, sizeof path, "/proc/%d/stat", pid);
+    FILE *f = std::fopen(path, "r");
+    if (!f) return 0;
+    const size_t len = std::fread(buf, 1, sizeof buf - 1, f);
+    std::fclose(f);
+    buf[len] = 0;
+    const char *p = std::strrchr(buf, ')');  // the command name may contain spaces
+    if (!p) return 0;
+    unsigned long long v = 0;
+    int field = 2;
+    for (const char *q = p + 1; *q; ++q)
+        if (*q == ' ' && ++field == 22) {
+            v = std::strtoull(q + 1, nullptr, 10);
+            break;
+        }
+    return v;
+}
+
+// One key per job and arguments, the same in every rank of that job.
+uint64_t job_key(int n, int B, int X, int Y)
+{
+    std::string id;
+    const char *slurm = std::getenv("SLURM_JOB_ID");
+    if (const char *v = std::getenv("PMIX_NAMESPACE"))
+        id = std::string("pmix:") + v;
+    else if (const char *v2 = std::getenv("OMPI_MCA_ess_base_jobid"))
+        id = std::string("ompi:") + v2;
+    else if (slurm)
+        id = std::string("slurm:") + slurm + "." + (std::getenv("SLURM_STEP_ID") ? std::getenv("SLURM_STEP_ID") : "");
+    else
+        id = "ppid:" + std::to_string((int)getppid()) + "@" + std::to_string(proc_start_ticks((int)getppid()));
+    char args[96];
+    std::snprintf(args, sizeof args, "|%d %d %d %d|%u", n, B, X, Y, (unsigned)getuid());
+    return fnv1a(id + args);
+}
+
+std::string gather_dir(uint64_t key)
 {
     if (const char *d = std::getenv("TSP_GATHER_DIR")) return d;
     char buf[256];
-    std::snprintf(buf, sizeof buf, "/tmp/tspgpu-%u-%d-%d-%d-%d-%d", (unsigned)getuid(), (int)getppid(), n, B, X, Y);
+    std::snprintf(buf, sizeof buf, "/tmp/tspgpu-%u-%016llx", (unsigned)getuid(), (unsigned long long)key);
     return buf;
 }
 
-int write_rank_file(const std::string &dir, int rank, int n, int count, const double *cost, const int32_t *tour)
+// status 0: this rank's results; status < 0: it failed (no payload)
+int write_rank_file(const std::string &dir, uint64_t key, int rank, int n, int B, int X, int Y, int count,
+                    const double *cost, const int32_t *tour, int status = 0)
 {
     mkdir(dir.c_str(), 0700);  // may exist already
     const std::string tmp = dir + "/rank" + std::to_string(rank) + ".tmp";
     const std::string fin = dir + "/rank" + std::to_string(rank) + ".bin";
     FILE *f = std::fopen(tmp.c_str(), "wb");
     if (!f) return -errno;
-    RankFileHeader h{kMagic, (uint32_t)rank, (uint32_t)count, (uint32_t)n};
+    RankFileHeader h{kMagic, (uint32_t)rank, (uint32_t)count, (uint32_t)n, B, X, Y, status, key};
+    if (status) count = 0;
     bool ok = std::fwrite(&h, sizeof h, 1, f) == 1;
     ok = ok && (count == 0 || std::fwrite(cost, sizeof(double), (size_t)count, f) == (size_t)count);
     ok = ok && (count == 0 || std::fwrite(tour, sizeof(int32_t), (size_t)count * (n + 1), f) == (size_t)count * (n + 1));
@@ -129,30 +187,48 @@ int write_rank_file(const std::string &dir, int rank, int n, int count, const do
 }
 
 // Rank 0: wait (up to TSP_GATHER_TIMEOUT_S, default 600 s) for every other
-// rank's file and place its blocks at their offsets.
-int read_rank_files(const std::string &dir, int P, int n, const std::vector<int> &cnt, const std::vector<int> &off,
-                    double *cost, int32_t *tour)
+// rank's file and place its blocks at their offsets.  A file of another job
+// (key or arguments differ: left by an earlier run) is removed and waited past;
+// a failure record of this job ends the wait with that rank's error.
+int read_rank_files(const std::string &dir, uint64_t key, int P, int n, int B, int X, int Y,
+                    const std::vector<int> &cnt, const std::vector<int> &off, double *cost, int32_t *tour,
+                    int *failed_rank)
 {
     const double limit = env_int("TSP_GATHER_TIMEOUT_S", 600);
     struct timespec t0, t;
     clock_gettime(CLOCK_MONOTONIC, &t0);
     for (int r = 1; r < P; ++r) {
         const std::string fin = dir + "/rank" + std::to_string(r) + ".bin";
-        FILE *f = nullptr;
-        while (!(f = std::fopen(fin.c_str(), "rb"))) {
-            clock_gettime(CLOCK_MONOTONIC, &t);
-            if ((t.tv_sec - t0.tv_sec) + 1e-9 * (t.tv_nsec - t0.tv_nsec) > limit) return -ETIMEDOUT;
-            usleep(1000);
+        for (;;) {
+            FILE *f = std::fopen(fin.c_str(), "rb");
+            if (!f) {
+                clock_gettime(CLOCK_MONOTONIC, &t);
+                if ((t.tv_sec - t0.tv_sec) + 1e-9 * (t.tv_nsec - t0.tv_nsec) > limit) return -ETIMEDOUT;
+                usleep(1000);
+                continue;
+            }
+            RankFileHeader h{};
+            const bool hdr = std::fread(&h, sizeof h, 1, f) == 1 && h.magic == kMagic;
+            if (!hdr || h.job != key || h.B != B || h.X != X || h.Y != Y || (int)h.n != n || (int)h.rank != r) {
+                std::fclose(f);  // stale (an earlier run's) or foreign: drop it, keep waiting for this job's
+                std::remove(fin.c_str());
+                continue;
+            }
+            if (h.status != 0) {
+                std::fclose(f);
+                std::remove(fin.c_str());
+                *failed_rank = r;
+                return h.status;
+            }
+            bool ok = (int)h.count == cnt[r];
+            ok = ok && (cnt[r] == 0 || std::fread(cost + off[r], sizeof(double), cnt[r], f) == (size_t)cnt[r]);
+            ok = ok && (cnt[r] == 0 || std::fread(tour + (size_t)off[r] * (n + 1), sizeof(int32_t),
+                                                  (size_t)cnt[r] * (n + 1), f) == (size_t)cnt[r] * (n + 1));
+            std::fclose(f);
+            std::remove(fin.c_str());
+            if (!ok) return -EIO;
+            break;
         }
-        RankFileHeader h{};
-        bool ok = std::fread(&h, sizeof h, 1, f) == 1 && h.magic == kMagic && (int)h.rank == r &&
-                  (int)h.count == cnt[r] && (int)h.n == n;
-        ok = ok && (cnt[r] == 0 || std::fread(cost + off[r], sizeof(double), cnt[r], f) == (size_t)cnt[r]);
-        ok = ok && (cnt[r] == 0 || std::fread(tour + (size_t)off[r] * (n + 1), sizeof(int32_t), (size_t)cnt[r] * (n + 1),
-                                              f) == (size_t)cnt[r] * (n + 1));
-        std::fclose(f);
-        std::remove(fin.c_str());
-        if (!ok) return -EIO;
     }
     if (!std::getenv("TSP_GATHER_DIR")) rmdir(dir.c_str());  // the per-job default directory
     return 0;
@@ -199,9 +275,19 @@ int main(int argc, char **argv)
         std::vector<int32_t> tour((size_t)cnt[my_rank] * (n + 1), -1);
         const int ndev = visible_devices();
         const int dev = env_int("TSP_GPU", my_rank % ndev);
-        int rc = solve_range(cities, n, off[my_rank], cnt[my_rank], env_int("TSP_GPUS", 1), dev, cost.data(),
-                             tour.data());
-        if (!rc) rc = write_rank_file(gather_dir(n, B, X, Y), my_rank, n, cnt[my_rank], cost.data(), tour.data());
+        const uint64_t key = job_key(n, B, X, Y);
+        const std::string dir = gather_dir(key);
+        // TSP_INJECT_FAIL_RANK (fault injection for the tests): that rank fails
+        int rc = env_int("TSP_INJECT_FAIL_RANK", -1) == my_rank
+                     ? -EIO
+                     : solve_range(cities, n, off[my_rank], cnt[my_rank], env_int("TSP_GPUS", 1), dev, cost.data(),
+                                   tour.data());
+        if (rc) {
+            // tell rank 0 at once instead of leaving it waiting for this file
+            (void)write_rank_file(dir, key, my_rank, n, B, X, Y, 0, nullptr, nullptr, rc);
+        } else {
+            rc = write_rank_file(dir, key, my_rank, n, B, X, Y, cnt[my_rank], cost.data(), tour.data());
+        }
         if (rc) {
             std::fprintf(stderr, "tsp: rank %d failed: %s (%d)\n", my_rank, tspgpu_strerror(rc), rc);
             return 3;
@@ -230,8 +316,15 @@ int main(int argc, char **argv)
         std::vector<int> cnt(P), off(P, 0);
         tsphost_distribution_counts(B, P, cnt.data());
         for (int r = 1; r < P; ++r) off[r] = off[r - 1] + cnt[r - 1];
+        const uint64_t key = job_key(n, B, X, Y);
+        int failed = 0;
         rc = solve_range(cities, n, 0, cnt[0], env_int("TSP_GPUS", 1), env_int("TSP_GPU", 0), cost.data(), tour.data());
-        if (!rc) rc = read_rank_files(gather_dir(n, B, X, Y), P, n, cnt, off, cost.data(), tour.data());
+        if (!rc) rc = read_rank_files(gather_dir(key), key, P, n, B, X, Y, cnt, off, cost.data(), tour.data(), &failed);
+        if (rc && failed) {
+            std::fflush(stdout);
+            std::fprintf(stderr, "tsp: rank %d failed: %s (%d)\n", failed, tspgpu_strerror(rc), rc);
+            return 3;
+        }
     } else {
         rc = solve_range(cities, n, 0, B, env_int("TSP_GPUS", 1), env_int("TSP_GPU", 0), cost.data(), tour.data());
     }

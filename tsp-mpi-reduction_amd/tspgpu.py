@@ -303,7 +303,7 @@ class Context:
         return lib().tspgpu_last_grid(self.handle)
 
     def last_variant(self) -> int:
-        """K1 variant of the last batched launch (5: hk_tiled_kernel, else heldkarp_kernel)."""
+        """K1 variant of the last batched launch (6: hk_sub_kernel, 5: hk_tiled_kernel, else heldkarp_kernel)."""
         return lib().tspgpu_last_variant(self.handle)
 
     def k1_split_timing(self, enable: bool = True):
