@@ -1,14 +1,20 @@
 #!/usr/bin/env python3
 """Benchmark of the hot path: exact 16-city block search on MI355X.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--n 16] [--blocks-per-gpu B]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--n 16]
+                    [--scaling strong|weak] [--global-blocks G] [--blocks-per-gpu B]
 
-One STEP = one launch of the K1 Held-Karp kernel over this rank's shard of B
-blocks (inputs already resident in HBM).  Ranks (one process per GPU) each
-own a contiguous shard of the instance `./tsp n B*N 1000 1000` (the
-reference's own generator, srand(0)); there is no data-path collective, so
-scaling is weak.  A gloo process group provides the barriers and the
-max-over-ranks of the timed region (measurement only).
+One STEP = one pass of K1 (the batched Held-Karp forward kernel + its
+backtracking kernel, in launches of at most 16384 blocks) over this rank's
+shard of blocks, inputs already resident in HBM.  The default is STRONG
+scaling along the reference's own axis (tsp.cpp:159-195, 318-345): one fixed
+instance `./tsp n G 1000 1000` (the reference's generator, srand(0);
+G = 65536 by default) whose blocks the N ranks split with the reference's
+per-rank counts, contiguously; `--scaling weak` gives every rank a fixed
+`--blocks-per-gpu` shard instead, and the line carries the other form as
+`other_scaling`.  There is no data-path collective: a gloo process group
+provides the barriers and the max-over-ranks of the timed region
+(measurement only).
 
 `python bench.py --gpus N` without a launcher starts the N ranks itself (a
 torch.distributed.run child; this parent never touches the GPU); under
@@ -88,6 +94,24 @@ class Shard:
 def shard_bounds(rank, world, per_rank):
     """Contiguous shard of the global instance owned by `rank` (weak scaling)."""
     return rank * per_rank, (rank + 1) * per_rank
+
+
+def reference_counts(blocks, world):
+    """Blocks per rank as the reference deals them (tsp.cpp:167-171: block
+    b = B..1 goes to rank b mod P), in rank order."""
+    cnt = [0] * world
+    for b in range(blocks, 0, -1):
+        cnt[b % world] += 1
+    return cnt
+
+
+def strong_bounds(rank, world, blocks):
+    """Contiguous shard [lo, hi) of a FIXED global instance of `blocks` blocks
+    owned by `rank` (strong scaling): the reference's per-rank counts, ranks
+    in order (tsp.cpp:173-191 sends consecutive blocks to rank 0, 1, ...)."""
+    cnt = reference_counts(blocks, world)
+    lo = sum(cnt[:rank])
+    return lo, lo + cnt[rank]
 
 
 class Group:
@@ -327,6 +351,76 @@ def cli_wall(n, reps=3):
             best = {"command": f"./tsp {n} 1 1000 1000", "process_wall_ms": wall, "program_ms": int(m.group(1)),
                     "cost": m.group(3)}
     return best
+
+
+def reference_multiblock(n=16, blocks=8, procs=(1, 2, 4, 8)):
+    """The reference's own multi-block runs beside the drop-in, on this box:
+    `mpirun -np P ./tsp n B 1000 1000` (the reference, oracle/_ref/tsp, one
+    core per rank) against `bin/tsp n B 1000 1000` for the same logical P —
+    once as one process (TSP_NPROCS=P, every block in one batched launch) and
+    once under the same `mpirun -np P` (a process per rank, each solving its
+    share on the GPU).  Each time is the program's own clock, process start to
+    the final line (tsp.cpp:275-276, 360-363), next to the launcher's wall; the
+    final cost lines must agree.  BASELINE.md quotes the reference's 8-core
+    Xeon times for `./tsp 16 8` at P = 1/2/4/8: 33.5 / 17.1 / 8.4 / 5.0 s."""
+    ref = os.path.join(ROOT, "oracle", "_ref", "tsp")
+    mpirun = find_mpirun()
+    if not (mpirun and os.path.exists(ref) and os.path.exists(TSP_BIN)):
+        return {"error": "needs mpirun, oracle/_ref/tsp and bin/tsp"}
+    pat = re.compile(r"TSP ran in (\d+) ms for (\d+) cities and the trip cost ([0-9.]+)")
+
+    def run(cmd, env):
+        t0 = time.perf_counter()
+        p = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env, cwd="/tmp")
+        wall = time.perf_counter() - t0
+        m = pat.search(p.stdout)
+        if p.returncode != 0 or not m:
+            return {"error": f"rc={p.returncode} {p.stderr[-200:]}"}
+        return {"program_ms": int(m.group(1)), "process_wall_ms": wall * 1e3, "cost": m.group(3)}
+
+    base_env = dict(os.environ, OMP_NUM_THREADS="1")
+    base_env.pop("TSP_NPROCS", None)
+    out = {"command": f"./tsp {n} {blocks} 1000 1000", "cpu_model": cpu_model(), "runs": {}}
+    for P in procs:
+        if P > host_cpus():
+            continue
+        args = [str(n), str(blocks), "1000", "1000"]
+        r = {"reference_mpirun": run([mpirun, "-np", str(P), ref, *args], base_env),
+             "dropin_one_process": run([TSP_BIN, *args], dict(base_env, TSP_NPROCS=str(P))),
+             "dropin_mpirun": run([mpirun, "-np", str(P), TSP_BIN, *args], base_env)}
+        costs = {v.get("cost") for v in r.values()}
+        r["same_cost"] = len(costs) == 1 and None not in costs
+        if "program_ms" in r["reference_mpirun"] and "program_ms" in r["dropin_one_process"]:
+            r["speedup_program_clock"] = (r["reference_mpirun"]["program_ms"] /
+                                          max(r["dropin_one_process"]["program_ms"], 1))
+        out["runs"][f"P{P}"] = r
+    return out
+
+
+def scaling_probe(ctx, args, world, rank, group, n, relax):
+    """The scaling form the headline does not use, on the same ranks: with
+    --scaling strong every rank also solves its own fixed --blocks-per-gpu
+    shard of `./tsp n blocks_per_gpu*N` (weak), with --scaling weak the ranks
+    split one fixed --global-blocks instance (strong).  Same step, barriers
+    and max-over-ranks as the headline; fewer steps."""
+    if args.scaling == "strong":
+        form, total = "weak", args.blocks_per_gpu * world
+        lo, hi = shard_bounds(rank, world, args.blocks_per_gpu)
+    else:
+        form, total = "strong", args.global_blocks
+        lo, hi = strong_bounds(rank, world, total)
+    B = hi - lo
+    d = Shard(n, total, lo, hi).distances()
+    dd, dc, dt = ctx.upload(d), ctx.alloc(max(B, 1) * 8), ctx.alloc(max(B, 1) * (n + 1) * 4)
+    steps = max(3, args.steps // 2)
+    try:
+        wall_max, _ = timed_steps(lambda: ctx.solve_device(dd, n, B, dc, dt, ctx.stream), ctx.synchronize,
+                                  group, 1, steps)
+    finally:
+        for p_ in (dd, dc, dt):
+            ctx.free(p_)
+    return {"scaling": form, "value": total * steps * relax / wall_max, "unit": UNIT, "global_blocks": total,
+            "blocks_this_rank": B, "steps": steps, "ms_per_step": wall_max / steps * 1e3}
 
 
 # --------------------------------------------------------------------------
@@ -596,13 +690,18 @@ def plumbing(args, world, rank):
     bounds of every rank, the barrier-bracketed region and the max over
     ranks — printed by rank 0 (tests/test_bench_cli.py)."""
     group = Group(world)
-    lo, hi = shard_bounds(rank, world, args.blocks_per_gpu)
+    if args.scaling == "strong":
+        lo, hi = strong_bounds(rank, world, args.global_blocks)
+        global_blocks = args.global_blocks
+    else:
+        lo, hi = shard_bounds(rank, world, args.blocks_per_gpu)
+        global_blocks = args.blocks_per_gpu * world
     wall_max, wall = timed_steps(lambda: None, lambda: None, group, args.warmup, args.steps)
     shards = group.gather([lo, hi])
     if rank == 0:
         print(json.dumps({"plumbing": True, "metric": METRIC, "n_gpus": world, "steps": args.steps,
-                          "warmup": args.warmup, "shards": shards, "wall_max_s": wall_max,
-                          "global_blocks": args.blocks_per_gpu * world}), flush=True)
+                          "warmup": args.warmup, "scaling": args.scaling, "shards": shards,
+                          "wall_max_s": wall_max, "global_blocks": global_blocks}), flush=True)
     if group.dist is not None:
         group.dist.destroy_process_group()
 
@@ -613,13 +712,19 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--n", type=int, default=16, help="cities per block (config 3: 16)")
-    ap.add_argument("--blocks-per-gpu", type=int, default=16384)
+    ap.add_argument("--scaling", choices=("strong", "weak"), default="strong",
+                    help="strong: one fixed instance of --global-blocks blocks split over the ranks (the "
+                         "reference's axis); weak: --blocks-per-gpu blocks per rank")
+    ap.add_argument("--global-blocks", type=int, default=65536, help="strong scaling: ./tsp n G instance")
+    ap.add_argument("--blocks-per-gpu", type=int, default=16384, help="weak scaling (and the weak probe)")
     ap.add_argument("--k2-n", type=int, default=32, help="cities of the K2 strong-scaling instance")
     ap.add_argument("--k2-seed", type=int, default=35)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pmc", action="store_true")
     ap.add_argument("--no-tto", action="store_true", help="skip the time-to-optimal probes")
     ap.add_argument("--no-k2", action="store_true", help="skip the K2 search probes")
+    ap.add_argument("--no-ref-multiblock", action="store_true",
+                    help="skip the reference-vs-drop-in `./tsp 16 8` runs at P = 1/2/4/8")
     ap.add_argument("--plumbing", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
@@ -635,15 +740,21 @@ def main():
         return plumbing(args, world, rank)
     group = Group(world)
 
-    n, Bp = args.n, args.blocks_per_gpu
+    n = args.n
     ndev = max(1, tspgpu.device_count())
     device = local_rank % ndev
     ctx = tspgpu.Context(device=device, strict=False)
     cu, devname = ctx.device_info()
-    lo, hi = shard_bounds(rank, world, Bp)
-    shard = Shard(n, Bp * world, lo, hi)
+    if args.scaling == "strong":
+        global_blocks = args.global_blocks
+        lo, hi = strong_bounds(rank, world, global_blocks)
+    else:
+        global_blocks = args.blocks_per_gpu * world
+        lo, hi = shard_bounds(rank, world, args.blocks_per_gpu)
+    Bp = hi - lo  # this rank's blocks
+    shard = Shard(n, global_blocks, lo, hi)
     d = shard.distances()
-    dd, dc, dt = ctx.upload(d), ctx.alloc(Bp * 8), ctx.alloc(Bp * (n + 1) * 4)
+    dd, dc, dt = ctx.upload(d), ctx.alloc(max(Bp, 1) * 8), ctx.alloc(max(Bp, 1) * (n + 1) * 4)
     stream = ctx.stream
 
     ev = {}
@@ -651,14 +762,29 @@ def main():
     def step():
         ctx.solve_device(dd, n, Bp, dc, dt, stream)
 
+    # the forward / backtracking kernels' own times come from the timed
+    # launches themselves: HIP events before, between and after the two
+    # kernels of every chunk (variants 5/6; summed by libtspgpu, read after)
+    def begin():
+        ctx.k1_split_timing(True)
+        ctx.timer_start()
+
     def stop_events():
         ev["ms"] = ctx.timer_stop()  # HIP events on the kernel's stream
 
-    wall_max, _ = timed_steps(step, ctx.synchronize, group, args.warmup, args.steps, begin=ctx.timer_start,
+    wall_max, _ = timed_steps(step, ctx.synchronize, group, args.warmup, args.steps, begin=begin,
                               end=stop_events)
     kernel_ms = ev["ms"] / args.steps
     variant = ctx.last_variant()
     kname = kernel_name(variant)
+    split = None
+    if variant in (5, 6):
+        f_ms, b_ms = ctx.k1_last_split_ms()
+        split = {"forward_kernel_ms": f_ms / args.steps, "backtrack_kernel_ms": b_ms / args.steps,
+                 "forward_kernel": kname, "backtrack_kernel": "hk_tiled_backtrack",
+                 "source": f"HIP events around both kernels of every chunk of the {args.steps} timed steps "
+                           f"(per-step sums)"}
+    ctx.k1_split_timing(False)
 
     # correctness of what was timed: every tour is a permutation whose left fold equals its cost
     cost = ctx.download(dc, (Bp,), np.float64)
@@ -671,23 +797,17 @@ def main():
         assert acc == cost[b], "timed result failed the left-fold check"
 
     relax = tspgpu.relaxations_per_block(n)
-    total_blocks = Bp * world * args.steps
+    total_blocks = global_blocks * args.steps
     value = total_blocks * relax / wall_max
 
-    # variants 5/6 run two kernels per launch: time each on its stream (HIP
-    # events between them), outside the timed region
-    split = None
-    if variant in (5, 6):
-        ctx.k1_split_timing(True)
-        fw, bt = [], []
-        for _ in range(5):
-            ctx.solve_device(dd, n, Bp, dc, dt, stream)
-            f_ms, b_ms = ctx.k1_last_split_ms()
-            fw.append(f_ms)
-            bt.append(b_ms)
-        ctx.k1_split_timing(False)
-        split = {"forward_kernel_ms": statistics.mean(fw), "backtrack_kernel_ms": statistics.mean(bt),
-                 "forward_kernel": kname, "backtrack_kernel": "hk_tiled_backtrack", "launches": 5}
+    # the other scaling form beside the headline: with strong scaling, every
+    # rank also solves a fixed --blocks-per-gpu shard (weak), and vice versa
+    other_scaling = None
+    if os.environ.get("BENCH_OTHER_SCALING", "1") != "0":
+        try:
+            other_scaling = scaling_probe(ctx, args, world, rank, group, n, relax)
+        except Exception as e:  # noqa: BLE001 - the probe must never cost the headline line
+            other_scaling = {"error": f"{type(e).__name__}: {e}"}
 
     # time to optimal: one block through the ABI (in process), and the whole
     # program as a child process (the reference's definition)
@@ -782,7 +902,12 @@ def main():
     dom_ms = split["forward_kernel_ms"] if split else kernel_ms  # the dominant kernel's own time
     relax_s_kernel = Bp * relax / (dom_ms * 1e-3)
     roof = roofline(variant, kname, n, Bp, dom_ms, relax_s_kernel, alg_bytes_per_block, prof, peaks)
-    cpu = cpu_opt = None
+    cpu = cpu_opt = refmb = None
+    if world == 1 and not args.no_ref_multiblock:
+        try:
+            refmb = reference_multiblock(n)
+        except Exception as e:  # noqa: BLE001
+            refmb = {"error": f"{type(e).__name__}: {e}"}
     if world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(n)
         try:
@@ -798,18 +923,21 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": wall_max / args.steps * 1e3,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": args.scaling,
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic: the reference's own generator (srand(0), ./tsp n B 1000 1000), no dataset",
         "config": {"workload": f"{n}-city blocks, exact Held-Karp per block (config 3 cities/block; "
-                               f"./tsp {n} {Bp * world} 1000 1000 instance)",
-                   "n": n, "blocks_per_gpu": Bp, "global_blocks": Bp * world,
-                   "parallelism": f"blocks sharded over {world} rank(s) (one per GPU), no data-path collective",
+                               f"./tsp {n} {global_blocks} 1000 1000 instance)",
+                   "n": n, "blocks_rank0": Bp, "global_blocks": global_blocks,
+                   "parallelism": f"{args.scaling} scaling: blocks sharded contiguously over {world} rank(s) "
+                                  f"(one per GPU; the reference's per-rank counts), no data-path collective",
                    "k1_variant": variant, "kernel": kname},
         "blocks_per_s": total_blocks / wall_max,
         "kernel_ms_per_launch": kernel_ms,
         "k1_kernel_split": split,
+        "other_scaling": other_scaling,
+        "reference_multiblock": refmb,
         "time_to_optimal": tto,
         "roofline": roof,
         "counters": prof,

@@ -136,14 +136,18 @@ int tspgpu_device_info(const tspgpu_ctx *ctx, int *cu_count, char *name, int nam
  * the last launch used and the DP relaxations per block for n cities,
  * N(N-1)2^(N-2) with N = n-1 (tsp.cpp:442-471). */
 int tspgpu_last_grid(const tspgpu_ctx *ctx);
-/* K1 variant the last batched launch used: 5 = sub-cube tiled (hk_tiled_kernel),
- * 4 = ping-pong + parent words, 2 = compact + prefetch, ... (heldkarp_kernel). */
+/* K1 variant the last batched launch used: 6 = sub-cube restructured
+ * (hk_sub_kernel), 5 = sub-cube tiled (hk_tiled_kernel), 4 = ping-pong +
+ * parent words, 2 = compact + prefetch, ... (heldkarp_kernel). */
 int tspgpu_last_variant(const tspgpu_ctx *ctx);
-/* Measurement aid for variant 5, which runs two kernels per launch (the
- * forward pass hk_tiled_kernel, then hk_tiled_backtrack): with split timing
- * enabled every variant-5 launch also records a HIP event between the two, and
- * tspgpu_k1_last_split_ms waits for the last such launch and returns both
- * kernels' durations (-ENOENT if the last launch recorded no split). */
+/* Measurement aid for variants 5 and 6, which run two kernels per chunk of at
+ * most 16384 blocks (the forward pass, then hk_tiled_backtrack): with split
+ * timing enabled every chunk also records HIP events before, between and
+ * after the two kernels, on the launch's stream.  tspgpu_k1_last_split_ms
+ * waits for the last of them and returns both kernels' durations SUMMED over
+ * every chunk of every launch since the previous read (or since enabling),
+ * then starts a new sum: -ENOENT if nothing was recorded, -ENOSPC if more
+ * than 4096 chunks were (recording stopped).  Enabling resets the sum. */
 int tspgpu_k1_split_timing(tspgpu_ctx *ctx, int enable);
 int tspgpu_k1_last_split_ms(tspgpu_ctx *ctx, float *forward_ms, float *backtrack_ms);
 /* Number of visible HIP devices (0 when none). */

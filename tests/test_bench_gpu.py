@@ -2,7 +2,8 @@
 ranks itself (torch.distributed.run child); on a one-GPU box both ranks share
 device 0 and the K2 incumbent exchange runs over gloo (RCCL wants one rank
 per device), on an 8-GPU node the same code takes the RCCL group.  Checks
-the line the driver reads: n_gpus, the global block count, both ranks' K2
+the line the driver reads: n_gpus, the fixed global block count (strong
+scaling) and the weak probe beside it, both ranks' K2
 shards and the strong-scaling instance's optimum (= K1-wide on one GPU)."""
 import json
 import os
@@ -21,13 +22,19 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def test_bench_two_ranks_end_to_end(gpu_ctx):
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1",
-           "--blocks-per-gpu", "512", "--no-pmc", "--no-cpu-baseline", "--no-tto", "--k2-n", "18", "--k2-seed", "1"]
+           "--global-blocks", "1000", "--blocks-per-gpu", "512", "--no-pmc", "--no-cpu-baseline", "--no-tto",
+           "--no-ref-multiblock", "--k2-n", "18", "--k2-seed", "1"]
     env = dict(os.environ, BENCH_I32="0")
     p = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
     assert p.returncode == 0, p.stderr[-2000:]
     line = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
-    assert line["n_gpus"] == 2 and line["config"]["global_blocks"] == 1024
-    assert line["value"] > 0 and line["scaling"] == "weak"
+    assert line["n_gpus"] == 2 and line["config"]["global_blocks"] == 1000
+    assert line["config"]["blocks_rank0"] == 500  # the reference's deal of 1000 blocks over 2 ranks
+    assert line["value"] > 0 and line["scaling"] == "strong"
+    other = line["other_scaling"]
+    assert other["scaling"] == "weak" and other["global_blocks"] == 1024 and other["value"] > 0
+    split = line["k1_kernel_split"]  # forward + backtracking kernels of the timed launches fit in the step
+    assert split is None or split["forward_kernel_ms"] + split["backtrack_kernel_ms"] <= line["ms_per_step"] * 1.001
     k2s = line["k2_strong_scaling"]
     assert "error" not in k2s, k2s
     assert k2s["ranks"] == 2 and len(k2s["rank_walls_ms"]) == 2

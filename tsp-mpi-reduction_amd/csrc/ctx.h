@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <mutex>
+#include <vector>
 
 #include "heldkarp.h"
 #include "tspgpu.h"
@@ -44,10 +45,14 @@ struct tspgpu_ctx {
     // per context, so a launch on a stream other than the previous one waits
     // for the previous launch (event recorded after every K1 launch)
     hipEvent_t ev_k1_done = nullptr;
-    // variant-5 split timing (tspgpu_k1_split_timing): events around the
-    // forward and the backtracking kernel of the last launch
-    int split_timing = 0, split_valid = 0;
-    hipEvent_t ev_split[3] = {nullptr, nullptr, nullptr};
+    // variant-5/6 split timing (tspgpu_k1_split_timing): per chunk launched
+    // since the last read, three events (before the forward kernel, between
+    // it and the backtracking kernel, after that); read and reset by
+    // tspgpu_k1_last_split_ms
+    int split_timing = 0;
+    std::vector<hipEvent_t> ev_split;
+    size_t split_used = 0;
+    bool split_overflow = false;
     hipStream_t k1_last_stream = nullptr;
     bool k1_launched = false;
     char name[256] = {0};

@@ -163,6 +163,29 @@ int ensure_tiled_info(tspgpu_ctx *c, int L)
     return 0;
 }
 
+// Split timing (tspgpu_k1_split_timing): three events per chunk, kept until
+// tspgpu_k1_last_split_ms reads them; the first is recorded here.  *ev0 = the
+// chunk's first event index (unused when split timing is off).
+int split_begin(tspgpu_ctx *c, hipStream_t stream, size_t *ev0)
+{
+    *ev0 = 0;
+    if (!c->split_timing) return 0;
+    constexpr size_t kMaxEvents = 3 * 4096;
+    if (c->split_used + 3 > kMaxEvents) {  // more chunks than the pool: stop recording
+        c->split_overflow = true;
+        c->split_timing = 0;
+        return 0;
+    }
+    while (c->ev_split.size() < c->split_used + 3) {
+        hipEvent_t ev = nullptr;
+        if (hipEventCreate(&ev) != hipSuccess) return -EIO;
+        c->ev_split.push_back(ev);
+    }
+    *ev0 = c->split_used;
+    c->split_used += 3;
+    return hipEventRecord(c->ev_split[*ev0], stream) == hipSuccess ? 0 : -EIO;
+}
+
 // Variant 6 row table of L (hk_sub.h SubRow): per L-bit mask, its members
 // then non-members as nibbles, and the colex rank of mask | (1 << k) for every
 // non-member k (the destination row of the next low layer).
@@ -236,16 +259,11 @@ int solve_sub(tspgpu_ctx *c, const SubCfg *cfg, const void *d_dist, int n, int n
     const size_t slot = tiled_slot_bytes(N, L, cfg->vbytes);
     const int chunk = std::min(nblocks, 16384);
     if ((rc = ensure(&c->d_tslots, &c->tslots_bytes, (size_t)chunk * slot))) return rc;
-    const bool split = c->split_timing && nblocks <= chunk;
-    c->split_valid = 0;
-    if (split) {
-        for (auto &ev : c->ev_split)
-            if (!ev && hipEventCreate(&ev) != hipSuccess) return -EIO;
-        if (hipEventRecord(c->ev_split[0], stream) != hipSuccess) return -EIO;
-    }
     for (int b0 = 0; b0 < nblocks; b0 += chunk) {
         SubArgs a{};
-        a.ev_mid = split ? c->ev_split[1] : nullptr;
+        size_t ev0 = 0;
+        if ((rc = split_begin(c, stream, &ev0))) return rc;
+        a.ev_mid = c->split_timing ? c->ev_split[ev0 + 1] : nullptr;
         a.dist = d_dist;
         a.n = n;
         a.blk0 = b0;
@@ -261,10 +279,7 @@ int solve_sub(tspgpu_ctx *c, const SubCfg *cfg, const void *d_dist, int n, int n
         a.stream = stream;
         hipError_t e = cfg->launch(a);
         if (e != hipSuccess) return hip_err(e);
-    }
-    if (split) {
-        if (hipEventRecord(c->ev_split[2], stream) != hipSuccess) return -EIO;
-        c->split_valid = 1;
+        if (c->split_timing && hipEventRecord(c->ev_split[ev0 + 2], stream) != hipSuccess) return -EIO;
     }
     c->last_grid = grid;
     c->last_variant = 6;
@@ -302,16 +317,11 @@ int solve_tiled(tspgpu_ctx *c, const TiledCfg *cfg, const void *d_dist, int n, i
     const size_t slot = tiled_slot_bytes(N, L, cfg->vbytes);
     const int chunk = std::min(nblocks, 16384);
     if ((rc = ensure(&c->d_tslots, &c->tslots_bytes, (size_t)chunk * slot))) return rc;
-    const bool split = c->split_timing && nblocks <= chunk;  // one launch pair: one split
-    c->split_valid = 0;
-    if (split) {
-        for (auto &ev : c->ev_split)
-            if (!ev && hipEventCreate(&ev) != hipSuccess) return -EIO;
-        if (hipEventRecord(c->ev_split[0], stream) != hipSuccess) return -EIO;
-    }
     for (int b0 = 0; b0 < nblocks; b0 += chunk) {
         TiledArgs a{};
-        a.ev_mid = split ? c->ev_split[1] : nullptr;
+        size_t ev0 = 0;
+        if ((rc = split_begin(c, stream, &ev0))) return rc;
+        a.ev_mid = c->split_timing ? c->ev_split[ev0 + 1] : nullptr;
         a.dist = d_dist;
         a.n = n;
         a.blk0 = b0;
@@ -326,10 +336,7 @@ int solve_tiled(tspgpu_ctx *c, const TiledCfg *cfg, const void *d_dist, int n, i
         a.stream = stream;
         hipError_t e = cfg->launch(a);
         if (e != hipSuccess) return hip_err(e);
-    }
-    if (split) {
-        if (hipEventRecord(c->ev_split[2], stream) != hipSuccess) return -EIO;
-        c->split_valid = 1;
+        if (c->split_timing && hipEventRecord(c->ev_split[ev0 + 2], stream) != hipSuccess) return -EIO;
     }
     c->last_grid = grid;
     c->last_variant = 5;
@@ -629,8 +636,7 @@ int tspgpu_ctx_destroy(tspgpu_ctx *c)
     if (c->ev_start) (void)hipEventDestroy(c->ev_start);
     if (c->ev_stop) (void)hipEventDestroy(c->ev_stop);
     if (c->ev_k1_done) (void)hipEventDestroy(c->ev_k1_done);
-    for (auto ev : c->ev_split)
-        if (ev) (void)hipEventDestroy(ev);
+    for (auto ev : c->ev_split) (void)hipEventDestroy(ev);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
     return 0;
@@ -755,18 +761,32 @@ int tspgpu_last_variant(const tspgpu_ctx *c) { return c ? c->last_variant : -1; 
 int tspgpu_k1_split_timing(tspgpu_ctx *c, int enable)
 {
     if (!c) return -EINVAL;
+    std::lock_guard<std::mutex> g(c->mu);
     c->split_timing = enable ? 1 : 0;
+    c->split_used = 0;
+    c->split_overflow = false;
     return 0;
 }
 
 int tspgpu_k1_last_split_ms(tspgpu_ctx *c, float *forward_ms, float *backtrack_ms)
 {
     if (!c || !forward_ms || !backtrack_ms) return -EINVAL;
-    if (!c->split_valid || (c->last_variant != 5 && c->last_variant != 6)) return -ENOENT;
+    std::lock_guard<std::mutex> g(c->mu);
+    if (c->split_overflow) return -ENOSPC;
+    if (!c->split_used) return -ENOENT;
     if (hipSetDevice(c->device) != hipSuccess) return -ENODEV;
-    hipError_t e = hipEventSynchronize(c->ev_split[2]);
-    if (e == hipSuccess) e = hipEventElapsedTime(forward_ms, c->ev_split[0], c->ev_split[1]);
-    if (e == hipSuccess) e = hipEventElapsedTime(backtrack_ms, c->ev_split[1], c->ev_split[2]);
+    hipError_t e = hipEventSynchronize(c->ev_split[c->split_used - 1]);
+    double fw = 0.0, bt = 0.0;
+    for (size_t i = 0; e == hipSuccess && i < c->split_used; i += 3) {
+        float f = 0.f, b = 0.f;
+        e = hipEventElapsedTime(&f, c->ev_split[i], c->ev_split[i + 1]);
+        if (e == hipSuccess) e = hipEventElapsedTime(&b, c->ev_split[i + 1], c->ev_split[i + 2]);
+        fw += f;
+        bt += b;
+    }
+    c->split_used = 0;
+    *forward_ms = (float)fw;
+    *backtrack_ms = (float)bt;
     return hip_err(e);
 }
 
