@@ -1,0 +1,105 @@
+"""The RCCL incumbent exchange actually runs on a one-GPU box.
+
+K2's only collective is the MIN of the 64-bit incumbent word (IEEE bits of
+the f64 cost), the step that replaces the reference's hand-rolled
+MPI_Send/MPI_Recv reduction tree for picking the global best tour
+(tsp.cpp:52-134).  Two drivers carry it:
+
+  * bin/tsp_search (one host thread per shard): `--rccl` makes even one shard
+    build a one-rank communicator (ncclCommInitAll) and all-reduce its device
+    word in place (ncclAllReduce uint64 MIN); `--gpus 2` on one device maps
+    both shards to it and combines the words through the host (RCCL takes one
+    rank per device), on a multi-GPU node the same flag is the RCCL path;
+  * search_dist.solve_sharded over a world-1 `nccl` process group: every
+    collective (bound, incumbent/busy exchange, optimum, record all-gather)
+    runs through RCCL on the device.
+
+Both must return the reference's golden answer for `./tsp 16 1 1000 1000`
+(cost 3871.1947567096445, tour 0 14 2 13 10 12 6 4 9
+11 3 5 15 8 1 7 0)."""
+import os
+import subprocess
+import sys
+
+import pytest
+
+import tspgpu
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BIN = os.path.join(os.path.dirname(tspgpu.TSP_BIN), "tsp_search")
+GOLD_COST = 3871.1947567096445
+GOLD_TOUR = [0, 14, 2, 13, 10, 12, 6, 4, 9, 11, 3, 5, 15, 8, 1, 7, 0]
+
+
+def _cities_file(tmp_path):
+    sys.path.insert(0, ROOT)
+    from bench import Shard
+
+    blk = Shard(16, 1, 0, 1).block(0)
+    f = tmp_path / "tsp16_1.txt"
+    f.write_text("".join(f"{i} {x!r} {y!r}\n" for i, x, y in blk))
+    return f
+
+
+def _parse(out):
+    cost = tour = exch = None
+    for ln in out.splitlines():
+        if ln.startswith("optimal cost "):
+            cost = float(ln.split()[2])
+        if ln.startswith("tour "):
+            tour = [int(x) for x in ln.split()[1:]]
+        if " exchange " in ln:
+            exch = ln.rsplit(" exchange ", 1)[1].strip()
+    return cost, tour, exch
+
+
+def _run(*args):
+    p = subprocess.run([BIN, *map(str, args)], capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0, p.stderr[-2000:]
+    return _parse(p.stdout)
+
+
+def test_tsp_search_one_rank_rccl_communicator(tmp_path):
+    cost, tour, exch = _run("--cities", _cities_file(tmp_path), "--solver", "k2", "--rccl")
+    assert exch == "rccl"
+    assert cost == GOLD_COST and tour == GOLD_TOUR
+
+
+def test_tsp_search_two_shards_any_box(tmp_path):
+    """Two shards: RCCL when the box has two GPUs, the host MIN when they share one."""
+    cost, tour, exch = _run("--cities", _cities_file(tmp_path), "--solver", "k2", "--gpus", 2)
+    assert exch == ("rccl" if tspgpu.device_count() >= 2 else "host")
+    assert cost == GOLD_COST and tour == GOLD_TOUR
+
+
+WORLD1_NCCL = r"""
+import json, os, socket, sys
+sys.path.insert(0, os.path.join(sys.argv[1], "tsp-mpi-reduction_amd"))
+sys.path.insert(0, sys.argv[1])
+import torch, torch.distributed as dist
+s = socket.socket(); s.bind(("127.0.0.1", 0)); port = s.getsockname()[1]; s.close()
+torch.cuda.set_device(0)
+dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+import tspgpu, search_dist
+from bench import Shard
+ctx = tspgpu.Context(device=0)
+d = Shard(16, 1, 0, 1).distances()[0]
+cost, tour, st = search_dist.solve_sharded(ctx, d, group=dist.group.WORLD)
+print(json.dumps({"cost": cost, "tour": [int(x) for x in tour], "backend": st["backend"],
+                  "exchanges": st["exchanges"], "world": st["world"]}))
+dist.destroy_process_group()
+"""
+
+
+def test_search_dist_world1_nccl_group():
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+    p = subprocess.run([sys.executable, "-c", WORLD1_NCCL, ROOT], capture_output=True, text=True, timeout=180,
+                       env=env)
+    assert p.returncode == 0, p.stderr[-3000:]
+    import json
+
+    r = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
+    assert r["backend"] == "nccl" and r["world"] == 1 and r["exchanges"] >= 1
+    assert r["cost"] == GOLD_COST and r["tour"] == GOLD_TOUR

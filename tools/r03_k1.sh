@@ -26,6 +26,10 @@ for s in ${STEPS:-time16 tests}; do
     tests) step k1_tests 400 python -u -m pytest tests/test_k1_variants_gpu.py tests/test_gpu_parity.py -x -q --timeout 200 --timeout-method thread ;;
     trace) rm -rf $OUT/trace_timed
            BENCH_I32=0 BENCH_OTHER_SCALING=0 step trace_timed 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace_timed -o run -- python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-pmc --no-tto --no-k2 --no-ref-multiblock ;;
+    pmc6) step pmc6 300 bash tools/k1_pmc.sh v6_n16 16 4096 8 6 ;;
+    rccl) step rccl_tests 300 python -u -m pytest tests/test_rccl_gpu.py tests/test_bench_gpu.py -x -v --timeout 200 --timeout-method thread ;;
+    k2phases) step k2_phases 120 python -u tools/k2_phases.py 5 ;;
+    ab) step ab_time 600 bash tools/ab_time.sh ;;
     gputests) step gpu_tests 900 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread ;;
     bench) step bench 600 python3 -u bench.py --steps 20 --warmup 3 ;;
     bench2) step bench_2ranks 300 python3 -u bench.py --gpus 2 --steps 10 --warmup 2 --no-k2 ;;

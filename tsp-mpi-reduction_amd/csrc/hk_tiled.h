@@ -12,12 +12,13 @@
 // So the DP can run sub-cube by sub-cube (h = 0, 1, ..., 2^H-1: every h\k is
 // done before h), and inside a sub-cube layer by layer over |l| = j.  The
 // entries G[S][m] with m LOW never leave the workgroup's LDS (only the two
-// live low layers of the current sub-cube are kept: 41 KB at L = 11); only
+// live low layers of the current sub-cube are kept: 20 KB at L = 10); only
 // the entries with m HIGH go through memory, written once by sub-cube h\m
 // ("push", coalesced: same row index l on both sides) and read once by
-// sub-cube h.  At n = 16 (N = 15, L = 11, H = 4) that is 65,536 of the
-// block's 245,760 entries: 1.05 MB of table traffic per block instead of
-// 3.93 MB (SURVEY.md §8(d)'s compulsory bytes of the layer-by-layer form).
+// sub-cube h.  At n = 16 with the default L = 10 (N = 15, H = 5) that is
+// 81,920 of the block's 245,760 entries: 1.31 MB of table traffic per block
+// instead of 3.93 MB (SURVEY.md §8(d)'s compulsory bytes of the
+// layer-by-layer form).
 //
 // Row-owner pass (h, j): a thread owns a source row T = h<<L | l, |l| = j,
 // t = |h|+j members, Q = N-t non-members; for every non-member k it computes
@@ -36,11 +37,11 @@
 // backtracking per 16384 blocks, against 9.6 ms with the argmin everywhere
 // (profiles/r02/k1_argmin_threshold.txt).
 //
-// Distances: the N x N inner matrix is replicated R times in LDS, element e of
-// copy c at 8*(e*R + c), lane uses copy lane % R: with R = 32 the per-lane
-// gather d[m][k] of a half-wave hits 32 distinct bank pairs (conflict-free),
-// the d[m][k] gathers of the compact pass cost +48% LDS cycles in bank
-// conflicts (round-1 counters) without it.
+// Distances: the N x N inner matrix in LDS with an odd row stride
+// (kTiledDS = 19 entries), optionally replicated R times (element e of copy c
+// at 8*(e*R + c), lane uses copy lane % R).  The product configurations use
+// R = 1: replication R = 2..32 measured within +-1% (k1_cfg.h,
+// profiles/r02/k1_tiled_v*.log).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -72,6 +73,9 @@ constexpr int kTiledDS = TSPGPU_TILED_DS;
 //   2048 / 4096 skip the passes with j <= 1 or >= L-1 / j <= 2 or >= L-2
 #ifndef TSPGPU_TILED_ABL
 #define TSPGPU_TILED_ABL 0
+#endif
+#if TSPGPU_TILED_ABL != 0 && !defined(TSPGPU_K1_SWEEP)
+#error "TSPGPU_TILED_ABL gives wrong results: measurement builds only (make K1_SWEEP=1)"
 #endif
 // Rows with at least N - TSPGPU_TILED_TA_OFF members keep the argmin (a
 // 64-bit parent word each); every smaller row is relaxed without it and the

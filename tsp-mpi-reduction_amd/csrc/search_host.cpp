@@ -1,0 +1,448 @@
+// Host-only parts of K2 (search_host.h): bound tour, city weights, input
+// check and the tie rule over the optimal set (tsp.cpp:457-470, 483-499).
+#include "search_host.h"
+
+#include <algorithm>
+#include <cerrno>
+#include <climits>
+#include <cmath>
+#include <cstdlib>
+#include <cstring>
+#include <thread>
+#include <vector>
+
+#include "tspgpu.h"
+
+namespace tspgpu {
+namespace host {
+
+// Left fold of the closed tour 0 -> t1 -> ... -> tN -> 0 (tsp.cpp's cost).
+template <typename V>
+V fold_tour(const V *d, int n, const int32_t *t)
+{
+    V c = 0;
+    int prev = 0;
+    for (int i = 0; i < n - 1; ++i) {
+        c = c + d[prev * n + t[i]];
+        prev = t[i];
+    }
+    return c + d[prev * n];
+}
+
+// Local search on a closed tour (cyclic, real-valued sums): 2-opt and Or-opt
+// (a segment of 1..3 cities moved elsewhere, either direction) until neither
+// improves.
+template <typename V>
+void local_search(const V *d, int n, std::vector<int> &t)
+{
+    auto D = [&](int a, int b) { return (double)d[a * n + b]; };
+    auto len_of = [&](const std::vector<int> &u) {
+        double c = 0;
+        for (int i = 0; i < n; ++i) c += D(u[i], u[(i + 1) % n]);
+        return c;
+    };
+    // a move is kept only if the whole cyclic length drops by more than the
+    // tolerance (asymmetric matrices: the local deltas assume symmetry), and
+    // the number of moves is capped: the loop always ends
+    double cur = len_of(t);
+    auto accept = [&](std::vector<int> &cand) {
+        const double c = len_of(cand);
+        if (c < cur - 1e-9 * (1.0 + std::fabs(cur))) {
+            t.swap(cand);
+            cur = c;
+            return true;
+        }
+        return false;
+    };
+    for (int moves = 0, improved = 1; improved && moves < 64 * n; ++moves) {
+        improved = 0;
+        for (int i = 1; i < n - 1 && !improved; ++i)
+            for (int j = i + 1; j < n && !improved; ++j) {
+                const int a = t[i - 1], b = t[i], c = t[j], e = t[(j + 1) % n];
+                if ((D(a, c) + D(b, e)) - (D(a, b) + D(c, e)) < 0) {
+                    std::vector<int> cand(t);
+                    std::reverse(cand.begin() + i, cand.begin() + j + 1);
+                    improved = accept(cand);
+                }
+            }
+        for (int len = 1; len <= 3 && !improved && n > len + 2; ++len)
+            for (int i = 0; i < n && !improved; ++i) {
+                // segment t[i..i+len-1] (cyclic), between p = t[i-1] and q = t[i+len]
+                const int p = t[(i - 1 + n) % n], q = t[(i + len) % n];
+                const int s0 = t[i], s1 = t[(i + len - 1) % n];
+                const double gain = D(p, s0) + D(s1, q) - D(p, q);
+                for (int k = 0; k < n && !improved; ++k) {
+                    bool touch = false;  // edge (t[k], t[k+1]) must not touch the segment
+                    for (int z = -1; z < len; ++z)
+                        if ((i + z + n) % n == k) touch = true;
+                    if (touch) continue;
+                    const int u = t[k], v = t[(k + 1) % n];
+                    const double fwd = D(u, s0) + D(s1, v) - D(u, v);
+                    const double rev = D(u, s1) + D(s0, v) - D(u, v);
+                    const bool r = rev < fwd;
+                    if ((r ? rev : fwd) - gain >= 0) continue;
+                    std::vector<int> seg, cand;
+                    for (int z = 0; z < len; ++z) seg.push_back(t[(i + z) % n]);
+                    if (r) std::reverse(seg.begin(), seg.end());
+                    for (int z = 0; z < n - len; ++z) {
+                        const int c = t[(i + len + z) % n];
+                        cand.push_back(c);
+                        if (c == u) cand.insert(cand.end(), seg.begin(), seg.end());
+                    }
+                    improved = accept(cand);
+                }
+            }
+    }
+}
+
+// Lagrangian city weights for the two-edge bound (symmetric matrices): with
+// d'[x][y] = d[x][y] + pi_x + pi_y, every path j -> R -> 0 has d'-cost =
+// d-cost + pi_j + pi_0 + 2 sum_{x in R} pi_x, so the bound "interior cities
+// pay half their two cheapest d' edges, the two ends half their cheapest"
+// minus those pi terms is again a lower bound on the d-cost, for ANY pi.
+// pi is chosen to maximise the whole-tour version, sum_x (two cheapest d'
+// edges)/2 - 2 sum pi (the degree relaxation), by subgradient ascent: a city
+// picked by more than two neighbours gets dearer (Polyak steps towards a
+// nearest-neighbour tour's cost, 200 iterations, O(n^2) each).  On 30 random
+// cities the root bound rises from 0.81 to 0.90 of the optimum, on ulysses22
+// from 0.66 to 0.87 (tools/k2_lagrange_proto.py).
+void lagrange_pi(const std::vector<double> &D, int n, std::vector<double> &best_pi)
+{
+    double ub = 0.0;  // nearest-neighbour tour from city 0: the step target
+    {
+        std::vector<char> used(n, 0);
+        int k = 0;
+        used[0] = 1;
+        for (int i = 1; i < n; ++i) {
+            int b = -1;
+            for (int j = 0; j < n; ++j)
+                if (!used[j] && (b < 0 || D[(size_t)k * n + j] < D[(size_t)k * n + b])) b = j;
+            ub += D[(size_t)k * n + b];
+            used[b] = 1;
+            k = b;
+        }
+        ub += D[(size_t)k * n];
+    }
+    std::vector<double> pi(n, 0.0);
+    std::vector<int> cnt(n);
+    double best = -INFINITY, lam = 2.0;
+    int stall = 0;
+    best_pi.assign(n, 0.0);
+    for (int it = 0; it < 200; ++it) {
+        double lb = 0.0;
+        std::fill(cnt.begin(), cnt.end(), 0);
+        for (int x = 0; x < n; ++x) {
+            double m1 = INFINITY, m2 = INFINITY;
+            int y1 = -1, y2 = -1;
+            for (int y = 0; y < n; ++y) {
+                if (y == x) continue;
+                const double v = D[(size_t)x * n + y] + pi[x] + pi[y];
+                if (v < m1) {
+                    m2 = m1, y2 = y1;
+                    m1 = v, y1 = y;
+                } else if (v < m2) {
+                    m2 = v, y2 = y;
+                }
+            }
+            lb += (m1 + m2) * 0.5 - 2.0 * pi[x];
+            ++cnt[y1];
+            ++cnt[y2];
+        }
+        if (lb > best) {
+            best = lb;
+            best_pi = pi;
+            stall = 0;
+        } else if (++stall >= 10) {
+            lam *= 0.7;
+            stall = 0;
+        }
+        double nn = 0.0;
+        for (int x = 0; x < n; ++x) nn += (cnt[x] * 0.5 - 1.0) * (cnt[x] * 0.5 - 1.0);
+        if (nn == 0.0 || !(ub > lb)) break;
+        const double t = lam * (ub - lb) / nn;
+        for (int x = 0; x < n; ++x) pi[x] += t * (cnt[x] * 0.5 - 1.0);
+    }
+}
+
+// Held-Karp city weights: subgradient ascent on the 1-tree bound (a minimum
+// spanning tree of cities 1..n-1 plus the two cheapest edges at city 0, on
+// d' = d + pi_x + pi_y, minus 2 sum pi), the same Polyak steps towards a
+// nearest-neighbour tour's cost as lagrange_pi, 300 iterations of an O(n^2)
+// Prim.  On the hardest 32-city seeds (bench.py's k2_instance 14, 30, 35) the
+// bound reaches the optimum to 5 digits, where the two-edge bound stops at
+// 0.83-0.88 (tools/k2_tree_bound_proto.py).  These weights serve the tree
+// bound of the expand kernel (SearchArgs::mst); the bound is valid for any pi.
+void held_karp_pi(const std::vector<double> &D, int n, std::vector<double> &best_pi)
+{
+    double ub = 0.0;
+    {
+        std::vector<char> used(n, 0);
+        int k = 0;
+        used[0] = 1;
+        for (int i = 1; i < n; ++i) {
+            int b = -1;
+            for (int j = 0; j < n; ++j)
+                if (!used[j] && (b < 0 || D[(size_t)k * n + j] < D[(size_t)k * n + b])) b = j;
+            ub += D[(size_t)k * n + b];
+            used[b] = 1;
+            k = b;
+        }
+        ub += D[(size_t)k * n];
+    }
+    std::vector<double> pi(n, 0.0), key(n);
+    std::vector<int> deg(n), par(n);
+    std::vector<char> in(n);
+    double best = -INFINITY, lam = 2.0;
+    int stall = 0;
+    best_pi.assign(n, 0.0);
+    auto dp = [&](int x, int y) { return D[(size_t)x * n + y] + pi[x] + pi[y]; };
+    for (int it = 0; it < 300 && n >= 3; ++it) {
+        std::fill(deg.begin(), deg.end(), 0);
+        std::fill(in.begin(), in.end(), 0);
+        double lb = 0.0;
+        for (int v = 1; v < n; ++v) key[v] = dp(1, v), par[v] = 1;
+        in[1] = 1;
+        for (int step = 2; step < n; ++step) {
+            int u = -1;
+            for (int v = 2; v < n; ++v)
+                if (!in[v] && (u < 0 || key[v] < key[u])) u = v;
+            in[u] = 1;
+            lb += key[u];
+            ++deg[u];
+            ++deg[par[u]];
+            for (int v = 2; v < n; ++v)
+                if (!in[v] && dp(u, v) < key[v]) key[v] = dp(u, v), par[v] = u;
+        }
+        int a = -1, b = -1;
+        for (int v = 1; v < n; ++v) {
+            if (a < 0 || dp(0, v) < dp(0, a))
+                b = a, a = v;
+            else if (b < 0 || dp(0, v) < dp(0, b))
+                b = v;
+        }
+        lb += dp(0, a) + dp(0, b);
+        deg[0] = 2;
+        ++deg[a];
+        ++deg[b];
+        for (int x = 0; x < n; ++x) lb -= 2.0 * pi[x];
+        if (lb > best) {
+            best = lb;
+            best_pi = pi;
+            stall = 0;
+        } else if (++stall >= 10) {
+            lam *= 0.7;
+            stall = 0;
+        }
+        double nn = 0.0;
+        for (int x = 0; x < n; ++x) nn += (double)(deg[x] - 2) * (deg[x] - 2);
+        if (nn == 0.0 || !(ub > lb)) break;
+        const double t = lam * (ub - lb) / nn;
+        for (int x = 0; x < n; ++x) pi[x] += t * (deg[x] - 2);
+    }
+}
+
+// Multi-start upper bound: a nearest-neighbour tour from every city, each
+// improved by 2-opt + Or-opt, rotated to start at city 0; the best exact fold
+// (tsp.cpp's cost, either direction) is a valid bound >= OPT.  A tight start
+// matters: every node the search prunes is pruned against it.
+// Starts first, first + step, ... (several ranks split the starts and take the
+// MIN of their costs: the same bound as all starts in one process).  From 20
+// cities the starts run on up to 8 host threads (32 cities: ~2.2 ms serial,
+// more than the search's kernels); the results are combined in start order by
+// the same rule, so the tour is the serial one.
+template <typename V>
+bool heuristic(const V *d, int n, std::vector<int32_t> &best, V &cost, int first = 0, int step = 1)
+{
+    std::vector<int> starts;
+    for (int s0 = first; s0 < n; s0 += step) starts.push_back(s0);
+    const int ns = (int)starts.size();
+    std::vector<std::vector<int32_t>> tours(ns);
+    std::vector<V> costs(ns);
+    auto one = [&](int i) {
+        const int s0 = starts[i];
+        std::vector<int> t(n);
+        std::vector<char> used(n, 0);
+        t[0] = s0;
+        used[s0] = 1;
+        for (int a = 1; a < n; ++a) {
+            int b = -1;
+            for (int j = 0; j < n; ++j)
+                if (!used[j] && (b < 0 || d[t[a - 1] * n + j] < d[t[a - 1] * n + b])) b = j;
+            t[a] = b;
+            used[b] = 1;
+        }
+        local_search(d, n, t);
+        std::rotate(t.begin(), std::find(t.begin(), t.end(), 0), t.end());
+        std::vector<int32_t> fw(t.begin() + 1, t.end()), bw(fw.rbegin(), fw.rend());
+        const V cf = fold_tour(d, n, fw.data()), cb = fold_tour(d, n, bw.data());
+        costs[i] = cb < cf ? cb : cf;
+        tours[i] = cb < cf ? std::move(bw) : std::move(fw);
+    };
+    int nt = n >= 20 ? std::min(ns, 8) : 1;
+    if (const char *e = std::getenv("TSPGPU_HEURISTIC_THREADS")) nt = std::max(1, std::min(ns, std::atoi(e)));
+    bool done = false;
+    if (nt > 1) {
+        std::vector<std::thread> th;
+        try {
+            th.reserve(nt);
+            for (int w = 0; w < nt; ++w)
+                th.emplace_back([&, w] {
+                    for (int i = w; i < ns; i += nt) one(i);
+                });
+            done = true;
+        } catch (...) {  // no thread: the serial loop below (every start again)
+        }
+        for (auto &x : th) x.join();
+    }
+    if (!done)
+        for (int i = 0; i < ns; ++i) one(i);
+    bool have = false;
+    for (int i = 0; i < ns; ++i)
+        if (!have || costs[i] < cost) {
+            best = tours[i];
+            cost = costs[i];
+            have = true;
+        }
+    return have;
+}
+
+template <typename V>
+int select_tour(const V *d, int n, const tspgpu_tour_record *rec, int count, V opt, int32_t *tour_out)
+{
+    const int N = n - 1;
+    // keep the optimal records; fold[c * N + j-1] = left fold up to the j-th inner city
+    std::vector<const uint8_t *> city;
+    std::vector<V> fold;
+    city.reserve(count);
+    fold.reserve((size_t)count * N);
+    for (int r = 0; r < count; ++r) {
+        const uint8_t *t = rec[r].city;
+        V acc = 0;
+        int prev = 0;
+        const size_t base = fold.size();
+        for (int j = 1; j <= N; ++j) {
+            acc = acc + d[prev * n + t[j - 1]];
+            fold.push_back(acc);
+            prev = t[j - 1];
+        }
+        if (!(acc + d[prev * n] == opt)) {  // recorded against an older incumbent
+            fold.resize(base);
+            continue;
+        }
+        city.push_back(t);
+    }
+    if (city.empty()) return -EIO;
+    std::vector<int> alive(city.size());
+    for (size_t i = 0; i < city.size(); ++i) alive[i] = (int)i;
+    std::vector<int32_t> tour(N + 2, 0);
+    std::vector<char> seen(n);
+    std::vector<V> best(n);
+    V target = opt;
+    int next = 0;
+    for (int j = N; j >= 1; --j) {
+        // t_j candidates among the tours sharing the chosen suffix: best prefix fold per city
+        std::fill(seen.begin(), seen.end(), 0);
+        for (int idx : alive) {
+            const int m = city[idx][j - 1];
+            const V f = fold[(size_t)idx * N + (j - 1)];
+            if (!seen[m] || f < best[m]) best[m] = f;
+            seen[m] = 1;
+        }
+        int pick = -1;
+        for (int m = 1; m <= N; ++m)
+            if (seen[m] && best[m] + d[m * n + next] == target) {
+                pick = m;
+                break;
+            }
+        if (pick < 0) return -EIO;
+        std::vector<int> keep;
+        for (int idx : alive)
+            if (city[idx][j - 1] == pick) keep.push_back(idx);
+        alive.swap(keep);
+        tour[j] = pick;
+        target = best[pick];
+        next = pick;
+    }
+    std::memcpy(tour_out, tour.data(), sizeof(int32_t) * (N + 2));
+    return 0;
+}
+
+int validate_search(const void *dist, int dtype, int n)
+{
+    if (!dist || n < 3 || n > TSPGPU_SEARCH_MAX_CITIES) return -EINVAL;
+    if (dtype == TSPGPU_F64) {
+        const double *d = static_cast<const double *>(dist);
+        double mx = 0.0;
+        for (int i = 0; i < n * n; ++i) {
+            if (!(d[i] >= 0.0) || !std::isfinite(d[i])) return -EINVAL;
+            mx = std::max(mx, d[i]);
+        }
+        if ((double)n * mx >= (double)INT_MAX) return -ERANGE;  // tsp.cpp:411,453 sentinel
+        return 0;
+    }
+    if (dtype == TSPGPU_I32) {
+        const int32_t *d = static_cast<const int32_t *>(dist);
+        long long mx = 0;
+        for (int i = 0; i < n * n; ++i) {
+            if (d[i] < 0) return -EINVAL;
+            mx = std::max<long long>(mx, d[i]);
+        }
+        if ((long long)n * mx >= (1ll << 30)) return -ERANGE;
+        return 0;
+    }
+    return -EINVAL;
+}
+
+}  // namespace host
+}  // namespace tspgpu
+
+using namespace tspgpu::host;
+
+extern "C" {
+
+int tspgpu_heuristic_tour(const void *dist, int dtype, int n, double *cost_out, int32_t *tour_out)
+{
+    return tspgpu_heuristic_tour_starts(dist, dtype, n, 0, 1, cost_out, tour_out);
+}
+
+int tspgpu_heuristic_tour_starts(const void *dist, int dtype, int n, int first, int step, double *cost_out,
+                                 int32_t *tour_out)
+{
+    int rc = validate_search(dist, dtype, n);
+    if (rc) return rc;
+    if (first < 0 || step < 1) return -EINVAL;
+    if (first >= n) return -ENOENT;  // no start city in this range
+    std::vector<int32_t> t;
+    if (dtype == TSPGPU_F64) {
+        double c;
+        heuristic(static_cast<const double *>(dist), n, t, c, first, step);
+        if (cost_out) *cost_out = c;
+    } else {
+        int32_t c;
+        heuristic(static_cast<const int32_t *>(dist), n, t, c, first, step);
+        if (cost_out) *cost_out = c;
+    }
+    if (tour_out) {
+        tour_out[0] = 0;
+        for (int i = 0; i < n - 1; ++i) tour_out[i + 1] = t[i];
+        tour_out[n] = 0;
+    }
+    return 0;
+}
+
+int tspgpu_select_tour(const void *dist, int dtype, int n, const tspgpu_tour_record *records, int count,
+                       uint64_t cost_bits, int32_t *tour_out)
+{
+    int rc = validate_search(dist, dtype, n);
+    if (rc) return rc;
+    if (count <= 0 || !records || !tour_out) return -EINVAL;
+    if (dtype == TSPGPU_F64) {
+        double opt;
+        std::memcpy(&opt, &cost_bits, 8);
+        return select_tour(static_cast<const double *>(dist), n, records, count, opt, tour_out);
+    }
+    return select_tour(static_cast<const int32_t *>(dist), n, records, count, (int32_t)(uint32_t)cost_bits,
+                       tour_out);
+}
+
+}  // extern "C"

@@ -1,0 +1,22 @@
+// Host-only parts of K2 (no HIP): the initial bound (multi-start 2-opt /
+// Or-opt tour), the Lagrangian and Held-Karp (1-tree) city weights of the
+// search bounds, the input check, and the selection of tsp()'s own tour from
+// the optimal set O (why that selection is exact: search_abi.cpp's header).
+// Split from search_abi.cpp so the host ASan/UBSan check (make check-asan)
+// builds it with plain g++.
+#pragma once
+#include <stdint.h>
+
+#include <vector>
+
+namespace tspgpu {
+namespace host {
+// 0, -EINVAL (null, n outside 3..32, negative / non-finite entries, dtype) or
+// -ERANGE (a tour could reach the reference's INT_MAX sentinel, tsp.cpp:411,453)
+int validate_search(const void *dist, int dtype, int n);
+// subgradient ascent on the degree relaxation: city weights for the two-edge bound
+void lagrange_pi(const std::vector<double> &D, int n, std::vector<double> &best_pi);
+// Held-Karp 1-tree weights (the tree bound of the expand kernel)
+void held_karp_pi(const std::vector<double> &D, int n, std::vector<double> &best_pi);
+}  // namespace host
+}  // namespace tspgpu

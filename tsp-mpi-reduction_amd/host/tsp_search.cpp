@@ -12,7 +12,8 @@
 //                                                         CEIL_2D, ATT, GEO or EXPLICIT
 //                                                         weights: integer mode), e.g.
 //                                                         tests/golden/tsplib/gr17.tsp
-//   options: --gpus G (devices 0..G-1)  --solver auto|wide|k1|k2|enum  --verify (n <= 20: K1 too)
+//   options: --gpus G (shard g on device g mod visible devices)  --rccl (the RCCL
+//            exchange even for G = 1)  --solver auto|wide|k1|k2|enum  --verify (n <= 20: K1 too)
 //   (enum: every tour enumerated on one GPU, BASELINE config 2)
 //   auto = K1-wide (the DP with every CU on each layer) up to 25 cities on one
 //   GPU, else K2 over the GPUs.
@@ -22,11 +23,12 @@
 // instead (integer mode).  The answer is the reference's: the optimal
 // left-fold cost and the DP's tie-broken tour.
 //
-// Multi-GPU: one host thread and one context per device; shard g of G seeds
-// the prefixes p = g mod G; after every round the incumbent word is combined
-// in place with an RCCL all-reduce MIN (uint64, over xGMI), and the final
-// optimum is that all-reduce's result; the optimal records of all shards then
-// go through tspgpu_select_tour.
+// Multi-GPU: one host thread and one context per shard; shard g of G seeds
+// the prefixes p = g mod G; after every few steps the incumbent word is
+// combined in place with an RCCL all-reduce MIN (uint64, over xGMI; through
+// the host when shards share a device), and the final optimum is that
+// all-reduce's result; the optimal records of all shards then go through
+// tspgpu_select_tour.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
@@ -268,17 +270,28 @@ struct Result {
     uint64_t nodes = 0;
     double kernel_ms = 0.0;
     int rounds = 0;
+    const char *exchange = "none";  // how the shards' incumbents were combined (K2)
 };
 
-// K2 over G GPUs of this process, RCCL all-reduce MIN of the incumbent every
-// `every` frontier steps.
-int search_multi(const Instance &in, int G, Result &res)
+// K2 over G shards of this process, shard g on device g mod (visible
+// devices), with an all-reduce MIN of the incumbent every `every` frontier
+// steps: RCCL (uint64 MIN in place on the device words, over xGMI) when every
+// shard has its own device — also for G = 1 with force_rccl, a one-rank
+// communicator — else (shards sharing a device: a rehearsal on a smaller box;
+// RCCL takes one rank per device) the same MIN through the host.
+int search_multi(const Instance &in, int G, bool force_rccl, Result &res)
 {
-    // one RCCL communicator per GPU (a single GPU needs none)
-    std::vector<ncclComm_t> comms(G > 1 ? G : 0);
+    int ndev = tspgpu_device_count();
+    if (ndev < 1) ndev = 1;
+    const bool shared = G > ndev;
+    const bool rccl = (G > 1 || force_rccl) && !shared;
+    if (force_rccl && shared) die("--rccl needs one GPU per shard (RCCL takes one rank per device)");
+    std::vector<ncclComm_t> comms(rccl ? G : 0);
     std::vector<int> devs(G);
-    for (int g = 0; g < G; ++g) devs[g] = g;
-    if (G > 1 && ncclCommInitAll(comms.data(), G, devs.data()) != ncclSuccess) die("RCCL initialisation failed");
+    for (int g = 0; g < G; ++g) devs[g] = g % ndev;
+    if (rccl && ncclCommInitAll(comms.data(), G, devs.data()) != ncclSuccess) die("RCCL initialisation failed");
+    std::atomic<uint64_t> host_min{~0ull};
+    res.exchange = rccl ? "rccl" : (G > 1 ? "host" : "none");
     double ub = 0.0;
     if (int rc = tspgpu_heuristic_tour(dist_ptr(in), in.dtype, in.n, &ub, nullptr)) return rc;
     std::vector<int> rcs(G, 0);
@@ -296,7 +309,7 @@ int search_multi(const Instance &in, int G, Result &res)
         th.emplace_back([&, g] {
             tspgpu_opts o;
             std::memset(&o, 0, sizeof o);
-            o.device = g;
+            o.device = devs[g];
             tspgpu_ctx *ctx = nullptr;
             tspgpu_search *s = nullptr;
             int rc = tspgpu_ctx_create(&o, &ctx);
@@ -315,8 +328,22 @@ int search_multi(const Instance &in, int G, Result &res)
                 busy.fetch_add(!rc && pending ? 1 : 0);
                 // incumbent exchange: in-place RCCL all-reduce MIN on the device word
                 void *w = s ? tspgpu_search_incumbent_device(s) : nullptr;
-                if (G > 1 && w && ncclAllReduce(w, w, 1, ncclUint64, ncclMin, comms[g], st) != ncclSuccess) rc = -EIO;
+                if (rccl && w && ncclAllReduce(w, w, 1, ncclUint64, ncclMin, comms[g], st) != ncclSuccess) rc = -EIO;
                 if (st) (void)hipStreamSynchronize(st);
+                if (!rccl && G > 1) {
+                    // shared devices: MIN of the words through the host (the
+                    // word only ever decreases, and no search kernel is running)
+                    uint64_t inc = ~0ull, nd = 0, nr = 0;
+                    if (s && !tspgpu_search_counters(s, &inc, &nd, &nr)) {
+                        uint64_t cur = host_min.load();
+                        while (inc < cur && !host_min.compare_exchange_weak(cur, inc)) {
+                        }
+                    }
+                    sync.arrive_and_wait();
+                    const uint64_t m = host_min.load();
+                    if (w && m < inc && hipMemcpyAsync(w, &m, 8, hipMemcpyHostToDevice, st) != hipSuccess) rc = -EIO;
+                    if (st) (void)hipStreamSynchronize(st);
+                }
                 sync.arrive_and_wait();
                 const bool more = busy.load() > 0;
                 sync.arrive_and_wait();
@@ -415,6 +442,7 @@ int main(int argc, char **argv)
     Instance in;
     bool have = false, verify = false, tsplib_round = false, dump = false;
     int gpus = 1, random_n = 0, clusters = 0;
+    bool force_rccl = false;
     uint64_t seed = 1;
     std::string solver = "auto", cities_file, matrix_file, tsplib_file;
     for (int i = 1; i < argc; ++i) {
@@ -431,12 +459,13 @@ int main(int argc, char **argv)
         else if (a == "--tsplib") tsplib_file = next();
         else if (a == "--tsplib-round") tsplib_round = true;
         else if (a == "--gpus") gpus = std::atoi(next());
+        else if (a == "--rccl") force_rccl = true;  // the RCCL exchange even on one GPU (one-rank communicator)
         else if (a == "--solver") solver = next();
         else if (a == "--verify") verify = true;
         else if (a == "--dump-matrix") dump = true;  // print the instance's matrix and exit (no GPU)
         else {
             std::fprintf(stderr, "usage: tsp_search (--random N [--seed S] [--clustered K] | --cities FILE "
-                                 "[--tsplib-round] | --matrix FILE | --tsplib FILE) [--gpus G] [--solver auto|wide|k1|k2|enum] [--verify]\n");
+                                 "[--tsplib-round] | --matrix FILE | --tsplib FILE) [--gpus G] [--rccl] [--solver auto|wide|k1|k2|enum] [--verify]\n");
             return 1;
         }
     }
@@ -474,7 +503,7 @@ int main(int argc, char **argv)
     // (with the Lagrangian two-edge bound K2 overtakes the DP from ~25 cities:
     // n = 28 2.0-2.5 ms vs ~10 ms, n = 30 2.3-5.8 ms vs ~40 ms;
     // profiles/r02/k2_lagrange.log)
-    if (solver == "auto") solver = (in.n <= 25 && gpus == 1) ? "wide" : "k2";
+    if (solver == "auto") solver = (in.n <= 25 && gpus == 1 && !force_rccl) ? "wide" : "k2";
     if (solver != "k1" && solver != "k2" && solver != "wide" && solver != "enum")
         die("--solver must be auto, wide, k1, k2 or enum");
 
@@ -483,7 +512,7 @@ int main(int argc, char **argv)
     int rc = solver == "k1"     ? solve_k1(in, res)
              : solver == "wide" ? solve_wide(in, res)
              : solver == "enum" ? solve_enum(in, res)
-                                : search_multi(in, gpus, res);
+                                : search_multi(in, gpus, force_rccl, res);
     if (rc == -EOVERFLOW && in.n <= TSPGPU_WIDE_MAX_CITIES) {
         // more tied optima than the record buffers hold (e.g. coincident cities):
         // the DP returns the same tour directly
@@ -503,9 +532,9 @@ int main(int argc, char **argv)
     for (int t : res.tour) std::printf(" %d", t);
     std::printf("\n");
     if (solver == "k2" || solver == "enum")
-        std::printf("search nodes %llu  rounds %d  kernel %.3f ms  %.3f Gnodes/s  wall %.3f ms\n",
+        std::printf("search nodes %llu  rounds %d  kernel %.3f ms  %.3f Gnodes/s  wall %.3f ms  exchange %s\n",
                     (unsigned long long)res.nodes, res.rounds, res.kernel_ms,
-                    res.kernel_ms > 0 ? res.nodes / res.kernel_ms / 1e6 : 0.0, wall);
+                    res.kernel_ms > 0 ? res.nodes / res.kernel_ms / 1e6 : 0.0, wall, res.exchange);
     else if (solver == "wide")
         std::printf("kernel %.3f ms  wall %.3f ms\n", res.kernel_ms, wall);
     else

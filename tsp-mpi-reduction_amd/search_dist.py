@@ -57,15 +57,19 @@ def solve_sharded(ctx, dist, group=None, depth: int = 0, device=None, exchange_e
     if device is None:
         device = torch.device("cuda", torch.cuda.current_device()) if backend == "nccl" else torch.device("cpu")
 
+    # an nccl group runs every collective, even with one rank (a one-rank RCCL
+    # communicator: the device all-reduce path exercised on a one-GPU box)
+    collective = world > 1 or backend == "nccl"
+
     def allmin(word: int) -> int:
-        if world == 1:
+        if not collective:
             return word
         t = _word_tensor(word, device)
         tdist.all_reduce(t, op=tdist.ReduceOp.MIN, group=group)
         return int(t.item())
 
     def allmin2(a: int, b: int):
-        if world == 1:
+        if not collective:
             return a, b
         import torch
 
@@ -97,7 +101,7 @@ def solve_sharded(ctx, dist, group=None, depth: int = 0, device=None, exchange_e
     if "v" not in heur:
         _heuristic()  # (no thread, or it raised: here, so an error surfaces)
     try:
-        if world > 1:
+        if collective:
             # then the MIN of the ranks' costs: all starts' bound at 1/W of the host time
             ub_r, _ = heur["v"]
             word = tspgpu.cost_bits(ub_r, S.dtype) if ub_r is not None else (1 << 63) - 1
@@ -161,7 +165,7 @@ def solve_sharded(ctx, dist, group=None, depth: int = 0, device=None, exchange_e
                          "backend": backend}
                 return cost, t, stats
         blob = np.frombuffer(b"".join(bytes(r) for r in mine), dtype=np.uint8) if mine else np.zeros(0, np.uint8)
-        if world > 1:
+        if collective:
             parts = [None] * world
             tdist.all_gather_object(parts, blob, group=group)
             node_t = _word_tensor(int(nodes), device)
