@@ -37,7 +37,7 @@ struct tspgpu_ctx {
                          // 2 = compact + next-row prefetch, 1 = compact, 0 = member sweep
     int tiled_cfg = -1;  // K1 variant 5/6 configuration id (k1_cfg.h); -1 = per-(n, type) default
     void *d_tinfo[16] = {};        // TiledInfo per L (variants 5, 6)
-    void *d_subrows[16][2] = {};   // SubRow table per L and value size (f64, i32) (variant 6)
+    void *d_subrows[16] = {};      // SubRow table per L (variant 6)
     char *d_tslots = nullptr;      // variant 5/6 slots (one per block of a launch)
     size_t tslots_bytes = 0;
     hipEvent_t ev_start = nullptr, ev_stop = nullptr;

@@ -40,56 +40,13 @@ namespace tspgpu {
 #endif
 constexpr int kSubDS = TSPGPU_SUB_DS;
 
-// one 32-byte entry per L-bit mask l (indexed like TiledInfo::mask, L <= 10)
-// and value size, everything a middle pass needs pre-scaled (tspgpu.cpp
-// ensure_sub_rows builds it), so decoding a field is one bit-field extract:
-//   u16 f[0..9] (bytes 0..19):  f[p] = m_p * row stride in bytes (the p-th
-//     member's image row), p < |l|; f[|l| + q] = the byte offset, inside the
-//     next low layer, of destination k_q (the q-th non-member):
-//     ((k_q - q) * C(L, |l|+1) + colex rank of l | 1 << k_q) * value bytes
-//   u8 g[0..9] (bytes 20..29):   g[p] = m_p; g[|l| + q] = k_q * value bytes
+// one entry per L-bit mask (indexed like TiledInfo::mask, L <= 10): nibbles
+// 0..L-1 = the members ascending, then the non-members ascending; bytes
+// 5..14 = colex rank of mask | (1 << k_q) among the masks of one more member,
+// for the q-th non-member k_q
 struct SubRow {
-    uint32_t w[8];
+    uint32_t w[4];
 };
-// field i (compile-time) of a row entry held as two uint4 (a = bytes 0..15)
-__device__ __forceinline__ uint32_t sub_f16(const uint4 &a, const uint4 &b, int i)
-{
-    const int wi = i / 2;
-    const uint32_t w = wi == 0 ? a.x : wi == 1 ? a.y : wi == 2 ? a.z : wi == 3 ? a.w : b.x;
-    return (i & 1) ? (w >> 16) : (w & 0xffffu);
-}
-__device__ __forceinline__ uint32_t sub_g8(const uint4 &b, int i)
-{
-    const int byte = 20 + i;
-    const uint32_t w = byte < 24 ? b.y : byte < 28 ? b.z : b.w;
-    return (w >> (8 * (byte & 3))) & 0xffu;
-}
-// one entry of the pre-scaled row table of (L, value bytes), host side
-// (tspgpu.cpp); colex_rank[m] = rank of mask m among the masks of its popcount
-inline void sub_row_entry(uint32_t mask, int L, int vb, const int *colex_rank, SubRow *out)
-{
-    const uint32_t ds = (uint32_t)kSubDS * (uint32_t)vb;
-    const int j = __builtin_popcount(mask);
-    int rows_next = 1;  // C(L, j + 1)
-    for (int i = 0; i < j + 1; ++i) rows_next = rows_next * (L - i) / (i + 1);
-    uint16_t f[10] = {0};
-    uint8_t g[10] = {0};
-    int p = 0, q = 0;
-    for (int b = 0; b < L; ++b)
-        if (mask >> b & 1) {
-            f[p] = (uint16_t)(b * ds);
-            g[p++] = (uint8_t)b;
-        }
-    for (int b = 0; b < L; ++b)
-        if (!(mask >> b & 1)) {
-            f[j + q] = (uint16_t)(((b - q) * rows_next + colex_rank[mask | (1u << b)]) * vb);
-            g[j + q] = (uint8_t)(b * vb);
-            ++q;
-        }
-    for (int i = 0; i < 8; ++i) out->w[i] = 0;
-    for (int i = 0; i < 10; ++i) out->w[i / 2] |= (uint32_t)f[i] << (16 * (i & 1));
-    for (int i = 0; i < 10; ++i) out->w[(20 + i) / 4] |= (uint32_t)g[i] << (8 * ((20 + i) & 3));
-}
 
 __host__ __device__ constexpr size_t sub_img_bytes(int N, int L, int vb)
 {
@@ -212,6 +169,16 @@ __device__ __forceinline__ uint64_t group_or(uint64_t w)
     return w;
 }
 
+__device__ __forceinline__ uint32_t sub_nib(const uint4 &e, int i)
+{
+    return i < 8 ? (e.x >> (4 * i)) & 15u : (e.y >> (4 * (i - 8))) & 15u;
+}
+__device__ __forceinline__ uint32_t sub_rank(const uint4 &e, int q)
+{
+    const int b = 5 + q;  // byte index
+    const uint32_t w = b < 4 ? e.x : (b < 8 ? e.y : (b < 12 ? e.z : e.w));
+    return (w >> (8 * (b & 3))) & 255u;
+}
 
 // ---------------------------------------------------------------------------
 // Middle pass (h, J), 2 <= J <= L-2: a thread owns row r = tid (colex rank of
@@ -245,12 +212,6 @@ __host__ __device__ constexpr int sub_lds_pair(int k)
     return -1;
 }
 
-#ifndef TSPGPU_SUB_STATIC_LDS
-#define TSPGPU_SUB_STATIC_LDS 1  // the kernel's LDS as a static array (offsets fold into immediates)
-#endif
-#ifndef TSPGPU_SUB_HOIST_HH
-#define TSPGPU_SUB_HOIST_HH 1  // high-high distances read once per sub-cube (else once per pass)
-#endif
 #ifndef TSPGPU_SUB_QC
 #define TSPGPU_SUB_QC 7  // destinations relaxed together (register budget)
 #endif
@@ -259,8 +220,7 @@ __host__ __device__ constexpr int sub_lds_pair(int k)
 #endif
 
 template <typename V, int N, int L, int T, int J>
-__device__ __forceinline__ void sub_mid(const SubCtx<V, N, L> &c, uint32_t h, uint32_t tid, const uint4 &e0,
-                                        const uint4 &e1, const V (&hh)[6])
+__device__ __forceinline__ void sub_mid(const SubCtx<V, N, L> &c, uint32_t h, uint32_t tid, const uint4 &ent)
 {
     constexpr int H = N - L;
     constexpr int Q = N - T;
@@ -295,18 +255,12 @@ __device__ __forceinline__ void sub_mid(const SubCtx<V, N, L> &c, uint32_t h, ui
             nb &= nb - 1u;
         }
     }
-    // hh: the high-high distances d[hm_i][hn_u] of this sub-cube at i * QH + u
-    // (wave-uniform, loaded once per sub-cube by the kernel)
-    static_assert(HC * QH <= 6, "high-high block of a sub-cube");
-#if !TSPGPU_SUB_HOIST_HH
-    V hhp[6];
+    // high-high distances of this sub-cube: wave-uniform
+    V hh[HC * QH > 0 ? HC * QH : 1];
 #pragma unroll
     for (int i = 0; i < HC; ++i)
 #pragma unroll
-        for (int u = 0; u < QH; ++u) hhp[i * QH + u] = uniform_val<V>(c.img, HR0 + i * DSB + HC0 + u * VB);
-#else
-    const V(&hhp)[6] = hh;
-#endif
+        for (int u = 0; u < QH; ++u) hh[i * QH + u] = uniform_val<V>(c.img, HR0 + i * DSB + HC0 + u * VB);
     if (tid >= (uint32_t)ROWS) return;
     const uint32_t r = tid;
     const uint32_t voff = (BASE + r) * VB;  // the row's offset in a push column
@@ -317,9 +271,9 @@ __device__ __forceinline__ void sub_mid(const SubCtx<V, N, L> &c, uint32_t h, ui
     for (int i = 0; i < HC; ++i) g[J + i] = c.push.load(voff, (h * H + hm[i]) * (uint32_t)(NL * VB));
     uint32_t mrow[J], kof[QL];
 #pragma unroll
-    for (int p = 0; p < J; ++p) mrow[p] = sub_f16(e0, e1, p);
+    for (int p = 0; p < J; ++p) mrow[p] = sub_nib(ent, p) * DSB;
 #pragma unroll
-    for (int q = 0; q < QL; ++q) kof[q] = sub_g8(e1, J + q);
+    for (int q = 0; q < QL; ++q) kof[q] = sub_nib(ent, J + q) * VB;
     // argmin operand: the member's image row offset (low: mrow, high: L + hm)
     uint32_t hrow[HC > 0 ? HC : 1];
 #pragma unroll
@@ -371,9 +325,9 @@ __device__ __forceinline__ void sub_mid(const SubCtx<V, N, L> &c, uint32_t h, ui
                 const int q = C0 + qq;
                 if (q >= QL) {
                     if constexpr (ARG)
-                        relax_argmin_s(acc[qq], arg[qq], g[J + i], hhp[i * QH + (q - QL)], hrow[i]);
+                        relax_argmin_s(acc[qq], arg[qq], g[J + i], hh[i * QH + (q - QL)], hrow[i]);
                     else
-                        relax_min_s(acc[qq], g[J + i], hhp[i * QH + (q - QL)]);
+                        relax_min_s(acc[qq], g[J + i], hh[i * QH + (q - QL)]);
                 }
             }
 #pragma unroll
@@ -381,8 +335,9 @@ __device__ __forceinline__ void sub_mid(const SubCtx<V, N, L> &c, uint32_t h, ui
             const int q = C0 + qq;
             if (q < QL) {
                 // low k -> next LDS layer: position k - q, colex rank of l + k
-                // (the byte offset comes pre-scaled from the row entry)
-                *reinterpret_cast<V *>(reinterpret_cast<char *>(c.region + NXT) + sub_f16(e0, e1, J + q)) = acc[qq];
+                const uint32_t k = kof[q] / VB;
+                const uint32_t slot = (k - (uint32_t)q) * (uint32_t)ROWS_N + sub_rank(ent, q);
+                c.region[NXT + slot] = acc[qq];
             } else {
                 // high k -> push column (h | k, k) of sub-cube h | k, same row index
                 const uint32_t cb = hn[q - QL];
@@ -595,12 +550,12 @@ __device__ __forceinline__ void sub_build_high(const SubCtx<V, N, L> &c, uint32_
 
 template <typename V, int N, int L, int J>
 __device__ __forceinline__ void sub_dispatch_mid_j(const SubCtx<V, N, L> &c, uint32_t h, int hc, uint32_t tid,
-                                                   const uint4 &e0, const uint4 &e1, const V (&hh)[6])
+                                                   const uint4 &ent)
 {
     constexpr int H = N - L;
-#define TSPGPU_SM(HC)                                                                                \
-    case HC:                                                                                         \
-        if constexpr (HC <= H) sub_mid<V, N, L, J + (HC <= H ? HC : 0), J>(c, h, tid, e0, e1, hh);  \
+#define TSPGPU_SM(HC)                                                                       \
+    case HC:                                                                                \
+        if constexpr (HC <= H) sub_mid<V, N, L, J + (HC <= H ? HC : 0), J>(c, h, tid, ent);  \
         break;
     switch (hc) {
         TSPGPU_SM(0) TSPGPU_SM(1) TSPGPU_SM(2) TSPGPU_SM(3) TSPGPU_SM(4) TSPGPU_SM(5) TSPGPU_SM(6) TSPGPU_SM(7)
@@ -652,8 +607,14 @@ __device__ __forceinline__ void sub_dispatch_last(const SubCtx<V, N, L> &c, uint
 // Forward pass + closing min of blocks blk0 + blockIdx.x, +gridDim.x, ...;
 // writes cost_out[blk] and the tour's last inner city (tour[n-1]) like
 // hk_tiled_kernel; hk_tiled_backtrack completes the tour from the slot.
+// (TSPGPU_SUB_WG_OVERRIDE: a measurement build's occupancy for every
+// configuration; the host then sizes the grid from TSPGPU_WG_PER_CU)
+#ifndef TSPGPU_SUB_WG_OVERRIDE
+#define TSPGPU_SUB_WG_OVERRIDE 0
+#endif
+__host__ __device__ constexpr int sub_wg(int wg) { return TSPGPU_SUB_WG_OVERRIDE > 0 ? TSPGPU_SUB_WG_OVERRIDE : wg; }
 template <typename V, int N, int L, int THREADS, int WG>
-__global__ __launch_bounds__(THREADS, tiled_waves(THREADS, WG)) void hk_sub_kernel(
+__global__ __launch_bounds__(THREADS, tiled_waves(THREADS, sub_wg(WG))) void hk_sub_kernel(
     const V *__restrict__ dist, int nblocks, int blk0, char *__restrict__ slots, uint32_t slot_bytes,
     const SubRow *__restrict__ rows, V *__restrict__ cost_out, int32_t *__restrict__ tour_out)
 {
@@ -666,13 +627,9 @@ __global__ __launch_bounds__(THREADS, tiled_waves(THREADS, WG)) void hk_sub_kern
     static_assert(H >= 1 && H <= 6 && L >= 5 && L <= 10, "variant 6 sizes");
     static_assert(kSubDS >= N + H, "image stride");
     static_assert(THREADS >= 256 && L * (N - 1) + H <= 192, "edge passes: lanes 0..191, pass L at 192..");
-#if TSPGPU_SUB_STATIC_LDS
-    // static LDS: every image/region offset folds into the instructions'
-    // immediate offsets (a dynamic-LDS base costs an add per address)
+    // static LDS: image/region offsets fold into immediates (A/B against
+    // dynamic LDS: equal within noise, profiles/r03/k1_ab_table.log)
     __shared__ __attribute__((aligned(16))) char smem[sub_lds_bytes(N, L, VB)];
-#else
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-#endif
     SubCtx<V, N, L> c;
     c.img = smem;
     V *d0 = reinterpret_cast<V *>(smem + sub_img_bytes(N, L, VB));
@@ -704,46 +661,31 @@ __global__ __launch_bounds__(THREADS, tiled_waves(THREADS, WG)) void hk_sub_kern
         if (tid < H) c.push.store(0, (((1u << tid) * H + tid) * NL) * VB, dsrc[L + tid + 1]);
         __syncthreads();
 
-        uint4 e0 = make_uint4(0, 0, 0, 0), e1 = e0;
+        uint4 ent = make_uint4(0, 0, 0, 0);
         for (uint32_t h = 0; h < (uint32_t)NH; ++h) {
             const int hc = __builtin_popcount(h);
             // interval A(h): passes 0/1 of h (lanes < 192) beside pass L of h - 1 (lanes 192..)
             uint32_t t = opaque_u32(tid);
             {
                 constexpr int M2 = tiled_moff(L, 2), C2 = cbinom(L, 2);
-                const uint32_t idx = 2u * (M2 + (t < (uint32_t)C2 ? t : 0u));
-                e0 = rowtab[idx];
-                e1 = rowtab[idx + 1];
+                ent = rowtab[M2 + (t < (uint32_t)C2 ? t : 0u)];
             }
             if (t < 192u)
                 sub_dispatch_first<V, N, L>(c, h, hc, t);
             else if (h > 0)
                 sub_dispatch_last<V, N, L>(c, h - 1, __builtin_popcount(h - 1), t - 192u);
             __syncthreads();
-            // the sub-cube's high-high distances d[hm_i][hn_u] (image rows and
-            // columns N.., sub-cube order), wave-uniform, for all its passes
-            V hh[6] = {};
-            if (TSPGPU_SUB_HOIST_HH) {
-                const int qh = H - hc > 0 ? H - hc : 1;
-#pragma unroll
-                for (int i = 0; i < 6; ++i) {
-                    const int ii = i < hc * (H - hc) ? i : 0;
-                    hh[i] = uniform_val<V>(c.img, (uint32_t)(N + ii / qh) * DSB + (uint32_t)(N + ii % qh) * VB);
-                }
-            }
             // middle passes j = 2..L-2, unrolled (every offset a compile-time
             // constant); the next pass's row entry is loaded one pass ahead
             static_for<L - 3>([&](auto jj) {
                 constexpr int j = 2 + decltype(jj)::value;
-                const uint4 c0 = e0, c1 = e1;
+                const uint4 cur = ent;
                 const uint32_t tj = opaque_u32(tid);
                 if constexpr (j + 1 <= L - 2) {
                     constexpr int MN = tiled_moff(L, j + 1), CN = cbinom(L, j + 1);
-                    const uint32_t idx = 2u * (MN + (tj < (uint32_t)CN ? tj : 0u));
-                    e0 = rowtab[idx];
-                    e1 = rowtab[idx + 1];
+                    ent = rowtab[MN + (tj < (uint32_t)CN ? tj : 0u)];
                 }
-                sub_dispatch_mid_j<V, N, L, j>(c, h, hc, tj, c0, c1, hh);
+                sub_dispatch_mid_j<V, N, L, j>(c, h, hc, tj, cur);
                 lds_barrier();
             });
             // pass L - 1 (lanes < 128) beside the next sub-cube's high image rows/columns (lanes 128..)
@@ -799,19 +741,7 @@ struct SubArgs {
 template <typename V, int N, int L, int THREADS, int WG>
 hipError_t launch_sub_n(const SubArgs &a)
 {
-#if TSPGPU_SUB_STATIC_LDS
-    const size_t lds = 0;
-#else
-    const size_t lds = sub_lds_bytes(N, L, sizeof(V));
-    static bool raised = false;
-    if (!raised) {
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&hk_sub_kernel<V, N, L, THREADS, WG>),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        if (e != hipSuccess) return e;
-        raised = true;
-    }
-#endif
-    hipLaunchKernelGGL((hk_sub_kernel<V, N, L, THREADS, WG>), dim3(a.grid), dim3(THREADS), lds, a.stream,
+    hipLaunchKernelGGL((hk_sub_kernel<V, N, L, THREADS, WG>), dim3(a.grid), dim3(THREADS), 0, a.stream,
                        static_cast<const V *>(a.dist), a.blk1, a.blk0, a.slots, a.slot_bytes, a.rows,
                        static_cast<V *>(a.cost), a.tour);
     hipError_t e = hipGetLastError();

@@ -186,14 +186,13 @@ int split_begin(tspgpu_ctx *c, hipStream_t stream, size_t *ev0)
     return hipEventRecord(c->ev_split[*ev0], stream) == hipSuccess ? 0 : -EIO;
 }
 
-// Variant 6 row table of (L, value bytes) (hk_sub.h SubRow): per L-bit mask,
-// in TiledInfo::mask order, its members' image row offsets and cities, its
-// non-members' column offsets and next-layer store offsets, pre-scaled.
-int ensure_sub_rows(tspgpu_ctx *c, int L, int vb)
+// Variant 6 row table of L (hk_sub.h SubRow): per L-bit mask, its members
+// then non-members as nibbles, and the colex rank of mask | (1 << k) for every
+// non-member k (the destination row of the next low layer).
+int ensure_sub_rows(tspgpu_ctx *c, int L)
 {
-    if (L > 10) return -EINVAL;  // 16-bit offsets, ten fields
-    const int vi = vb == 4 ? 1 : 0;
-    if (c->d_subrows[L][vi]) return 0;
+    if (L > 10) return -EINVAL;  // 8-bit ranks: C(10, 5) = 252
+    if (c->d_subrows[L]) return 0;
     int rc = ensure_tiled_info(c, L);
     if (rc) return rc;
     std::vector<int> rank(1 << L, 0);
@@ -207,7 +206,20 @@ int ensure_sub_rows(tspgpu_ctx *c, int L, int vb)
             }
     }
     std::vector<SubRow> rows(order.size());
-    for (size_t i = 0; i < order.size(); ++i) sub_row_entry(order[i], L, vb, rank.data(), &rows[i]);
+    for (size_t i = 0; i < order.size(); ++i) {
+        const uint32_t m = order[i];
+        uint8_t bytes[16] = {0};
+        int slot = 0, q = 0;
+        auto put_nib = [&](int idx, uint32_t v) { bytes[idx / 2] |= (uint8_t)(v << (4 * (idx & 1))); };
+        for (int b = 0; b < L; ++b)
+            if (m >> b & 1) put_nib(slot++, (uint32_t)b);
+        for (int b = 0; b < L; ++b)
+            if (!(m >> b & 1)) {
+                put_nib(slot++, (uint32_t)b);
+                bytes[5 + q++] = (uint8_t)rank[m | (1u << b)];
+            }
+        std::memcpy(rows[i].w, bytes, 16);
+    }
     void *d = nullptr;
     hipError_t e = hipMalloc(&d, rows.size() * sizeof(SubRow));
     if (e == hipSuccess) e = hipMemcpy(d, rows.data(), rows.size() * sizeof(SubRow), hipMemcpyHostToDevice);
@@ -215,7 +227,7 @@ int ensure_sub_rows(tspgpu_ctx *c, int L, int vb)
         if (d) (void)hipFree(d);
         return hip_err(e);
     }
-    c->d_subrows[L][vi] = d;
+    c->d_subrows[L] = d;
     return 0;
 }
 
@@ -239,9 +251,10 @@ int solve_sub(tspgpu_ctx *c, const SubCfg *cfg, const void *d_dist, int n, int n
               int32_t *d_tour, hipStream_t stream)
 {
     const int N = n - 1, L = cfg->L;
-    int rc = ensure_sub_rows(c, L, cfg->vbytes);
+    int rc = ensure_sub_rows(c, L);
     if (rc) return rc;
-    const int grid = std::min(nblocks, c->cu_count * cfg->wg);
+    // (TSPGPU_WG_PER_CU: measurement builds with another occupancy, hk_sub.h)
+    const int grid = std::min(nblocks, c->cu_count * (c->wg_per_cu > 0 ? c->wg_per_cu : cfg->wg));
     // the same per-block slot as variant 5 (push area, parent words,
     // recompute area), kept until the backtracking kernel has run
     const size_t slot = tiled_slot_bytes(N, L, cfg->vbytes);
@@ -258,7 +271,7 @@ int solve_sub(tspgpu_ctx *c, const SubCfg *cfg, const void *d_dist, int n, int n
         a.blk1 = std::min(nblocks, b0 + chunk);
         a.slots = c->d_tslots;
         a.slot_bytes = (uint32_t)slot;
-        a.rows = static_cast<const SubRow *>(c->d_subrows[L][cfg->vbytes == 4 ? 1 : 0]);
+        a.rows = static_cast<const SubRow *>(c->d_subrows[L]);
         a.info = static_cast<const TiledInfo *>(c->d_tinfo[L]);
         a.cost = d_cost;
         a.tour = d_tour;
@@ -615,9 +628,8 @@ int tspgpu_ctx_destroy(tspgpu_ctx *c)
     if (c->d_slots) (void)hipFree(c->d_slots);
     for (void *p : c->d_tinfo)
         if (p) (void)hipFree(p);
-    for (auto &pr : c->d_subrows)
-        for (void *p : pr)
-            if (p) (void)hipFree(p);
+    for (void *p : c->d_subrows)
+        if (p) (void)hipFree(p);
     if (c->d_tslots) (void)hipFree(c->d_tslots);
     if (c->d_dist) (void)hipFree(c->d_dist);
     if (c->d_cost) (void)hipFree(c->d_cost);
