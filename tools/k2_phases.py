@@ -54,7 +54,23 @@ def phases(ctx, d):
     return t
 
 
+VARIANTS = [{}, {"TSPGPU_SEARCH_LAGRANGE": "0"}, {"TSPGPU_SEARCH_MST": "0"},
+            {"TSPGPU_SEARCH_LAGRANGE": "0", "TSPGPU_SEARCH_MST": "0"}]
+
+
 def main():
+    if len(sys.argv) > 1 and sys.argv[1] == "--variants":
+        import subprocess
+        for v in VARIANTS:
+            out = subprocess.run([sys.executable, __file__, "5"], env=dict(os.environ, **v), capture_output=True,
+                                 text=True, timeout=120).stdout
+            for ln in out.splitlines():
+                if ln.startswith("{"):
+                    d = json.loads(ln)
+                    d.pop("tour", None)
+                    d.pop("step_ms", None)
+                    print(json.dumps(dict(env=v, **d)), flush=True)
+        return
     reps = int(sys.argv[1]) if len(sys.argv) > 1 else 5
     ctx = tspgpu.Context(device=0)
     cases = {"tsp16_1": Shard(16, 1, 0, 1).distances()[0], "rand32_s35": np.asarray(k2_instance(32, 35))}

@@ -29,7 +29,9 @@ for s in ${STEPS:-time16 tests}; do
     pmc6) step pmc6 300 bash tools/k1_pmc.sh v6_n16 16 4096 8 6 ;;
     rccl) step rccl_tests 300 python -u -m pytest tests/test_rccl_gpu.py tests/test_bench_gpu.py -x -v --timeout 200 --timeout-method thread ;;
     k2phases) step k2_phases 120 python -u tools/k2_phases.py 5 ;;
+    k2var) step k2_variants 300 python -u tools/k2_phases.py --variants ;;
     ab) step ab_time 600 bash tools/ab_time.sh ;;
+    k2tests) step k2_tests 600 python -u -m pytest tests/test_search_gpu.py tests/test_rccl_gpu.py tests/test_search_cli.py tests/test_tsplib.py -x -q -m gpu --timeout 200 --timeout-method thread ;;
     gputests) step gpu_tests 900 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread ;;
     bench) step bench 600 python3 -u bench.py --steps 20 --warmup 3 ;;
     bench2) step bench_2ranks 300 python3 -u bench.py --gpus 2 --steps 10 --warmup 2 --no-k2 ;;

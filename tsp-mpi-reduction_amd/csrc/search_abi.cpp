@@ -132,6 +132,9 @@ struct tspgpu_search {
     double ms = 0.0;             // device time of all seed/round launches
     hipEvent_t e0 = nullptr, e1 = nullptr;
     unsigned long long *h_cnt = nullptr;  // pinned host words: the frontier step's counter readback
+    // pinned host copy of the statistics lines + 8 counter words (one DMA
+    // pair and one synchronisation per counters read)
+    unsigned long long *h_stats = nullptr;
 };
 
 namespace {
@@ -169,6 +172,7 @@ struct SearchPool {
     unsigned int tail_alloc = 0;
     hipEvent_t e0 = nullptr, e1 = nullptr;
     unsigned long long *h_cnt = nullptr;
+    unsigned long long *h_stats = nullptr;
     void *d_bnd2 = nullptr;
     double *d_mst = nullptr;
     double *d_hsuf = nullptr;
@@ -199,6 +203,7 @@ void move_buffers(A &to, B &from)
     to.e0 = from.e0, from.e0 = nullptr;
     to.e1 = from.e1, from.e1 = nullptr;
     to.h_cnt = from.h_cnt, from.h_cnt = nullptr;
+    to.h_stats = from.h_stats, from.h_stats = nullptr;
     to.d_bnd2 = from.d_bnd2, from.d_bnd2 = nullptr;
     to.d_mst = from.d_mst, from.d_mst = nullptr;
     to.d_hsuf = from.d_hsuf, from.d_hsuf = nullptr;
@@ -224,6 +229,7 @@ void free_buffers(A &b)
     if (b.e0) (void)hipEventDestroy(b.e0);
     if (b.e1) (void)hipEventDestroy(b.e1);
     if (b.h_cnt) (void)hipHostFree(b.h_cnt);
+    if (b.h_stats) (void)hipHostFree(b.h_stats);
     if (b.d_bnd2) (void)hipFree(b.d_bnd2);
     if (b.d_mst) (void)hipFree(b.d_mst);
     if (b.d_hsuf) (void)hipFree(b.d_hsuf);
@@ -412,7 +418,11 @@ int tspgpu_search_create(tspgpu_ctx *c, const void *dist, int dtype, int n, int 
             std::vector<double> pi(n, 0.0);
             // the tree bound's weights on a second thread meanwhile (host time
             // at n = 32: 1.3 ms beside lagrange_pi's 0.45 ms)
-            const bool want_tree = s->use_mst && n >= 4;
+            // (only if some path can reach it: the expand kernel applies the
+            // tree bound to paths with >= mst_min_rem cities left, and the
+            // frontier starts at the seed depth — at n = 16 none does, and
+            // the weights cost 0.22 ms of host time, profiles/r03/k2_variants.log)
+            const bool want_tree = s->use_mst && n >= 4 && s->frontier && N - depth >= s->mst_min_rem;
             std::thread ht;
             bool threaded = false;
             if (want_tree && n >= 20) {  // (smaller: a thread costs more than it saves)
@@ -521,6 +531,8 @@ int tspgpu_search_create(tspgpu_ctx *c, const void *dist, int dtype, int n, int 
     if (e == hipSuccess && !s->e1) e = hipEventCreate(&s->e1);
     if (e == hipSuccess && !s->h_cnt && !std::getenv("TSPGPU_SEARCH_PAGEABLE"))
         e = hipHostMalloc((void **)&s->h_cnt, 8 * sizeof(unsigned long long), hipHostMallocDefault);
+    if (e == hipSuccess && !s->h_stats && !std::getenv("TSPGPU_SEARCH_PAGEABLE"))
+        e = hipHostMalloc((void **)&s->h_stats, kStatBytes + 8 * sizeof(unsigned long long), hipHostMallocDefault);
     if (e != hipSuccess) {
         tspgpu_search_destroy(s);
         return herr(e);
@@ -624,16 +636,26 @@ static int ensure_items(tspgpu_search *s, int which, size_t count)
 }
 
 // the statistics lines, summed: [0] nodes, [1] lane slots, [2] active lane steps, [3] item loads
-static int read_stats(tspgpu_search *s, uint64_t (&out)[4])
+// The counter words [0..4] and the summed statistics lines in one
+// synchronisation (both copies into the pinned h_stats when it exists).
+static int read_words_stats(tspgpu_search *s, unsigned long long (&w)[5], uint64_t (&out)[4])
 {
-    std::vector<unsigned long long> h(kStatLines * kStatStride);
-    hipError_t e = hipMemcpyAsync(h.data(), s->d_stats, kStatBytes, hipMemcpyDeviceToHost, s->ctx->stream);
+    std::vector<unsigned long long> tmp;
+    unsigned long long *h = s->h_stats;
+    if (!h) {
+        tmp.resize(kStatLines * kStatStride + 8);
+        h = tmp.data();
+    }
+    unsigned long long *hw = h + kStatLines * kStatStride;
+    hipError_t e = hipMemcpyAsync(h, s->d_stats, kStatBytes, hipMemcpyDeviceToHost, s->ctx->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(hw, s->d_words, 5 * sizeof(unsigned long long), hipMemcpyDeviceToHost, s->ctx->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(s->ctx->stream);
     if (e != hipSuccess) return herr(e);
     for (int i = 0; i < 4; ++i) {
         out[i] = 0;
         for (int l = 0; l < kStatLines; ++l) out[i] += h[l * kStatStride + i];
     }
+    for (int i = 0; i < 5; ++i) w[i] = hw[i];
     return 0;
 }
 
@@ -1021,16 +1043,11 @@ int tspgpu_search_counters(tspgpu_search *s, uint64_t *incumbent_bits, uint64_t 
     if (!s) return -EINVAL;
     (void)hipSetDevice(s->ctx->device);
     unsigned long long w[5];
-    hipError_t e = hipMemcpyAsync(w, s->d_words, sizeof w, hipMemcpyDeviceToHost, s->ctx->stream);
-    if (e == hipSuccess) e = hipStreamSynchronize(s->ctx->stream);
-    if (e != hipSuccess) return herr(e);
+    uint64_t st[4];
+    if (int rc = read_words_stats(s, w, st)) return rc;
     if (incumbent_bits) *incumbent_bits = w[1];
     if (records) *records = (uint32_t)w[3];
-    if (nodes) {
-        uint64_t st[4];
-        if (int rc = read_stats(s, st)) return rc;
-        *nodes = st[0];
-    }
+    if (nodes) *nodes = st[0];
     return 0;
 }
 
@@ -1053,12 +1070,10 @@ int tspgpu_search_reset_records(tspgpu_search *s, unsigned int capacity)
     return herr(e);
 }
 
-int tspgpu_search_records(tspgpu_search *s, uint64_t cost_bits, tspgpu_tour_record *out, int cap, int *count)
+// the records of cost cost_bits among the `claimed` the kernels wrote
+static int records_of(tspgpu_search *s, uint64_t claimed, uint64_t cost_bits, tspgpu_tour_record *out, int cap,
+                      int *count)
 {
-    if (!s || !count || (cap > 0 && !out)) return -EINVAL;
-    uint64_t claimed = 0;
-    int rc = tspgpu_search_counters(s, nullptr, nullptr, &claimed);
-    if (rc) return rc;
     if (claimed > s->rec_cap) return -EOVERFLOW;
     std::vector<SearchRecord> h(claimed);
     if (claimed) {
@@ -1073,6 +1088,15 @@ int tspgpu_search_records(tspgpu_search *s, uint64_t cost_bits, tspgpu_tour_reco
     }
     *count = k;
     return k > cap ? -ENOSPC : 0;
+}
+
+int tspgpu_search_records(tspgpu_search *s, uint64_t cost_bits, tspgpu_tour_record *out, int cap, int *count)
+{
+    if (!s || !count || (cap > 0 && !out)) return -EINVAL;
+    uint64_t claimed = 0;
+    int rc = tspgpu_search_counters(s, nullptr, nullptr, &claimed);
+    if (rc) return rc;
+    return records_of(s, claimed, cost_bits, out, cap, count);
 }
 
 static int search_solve(tspgpu_ctx *c, const void *dist, int dtype, int n, double *cost_out, int32_t *tour_out,
@@ -1117,8 +1141,18 @@ static int search_solve(tspgpu_ctx *c, const void *dist, int dtype, int n, doubl
     if (!rc) rc = tspgpu_search_set_bound(s, ub);
     int phases = 1, fallback = 0;
     uint64_t inc = 0, nodes = 0, nodes_total = 0, recs = 0;
+    uint64_t u[4] = {0, 0, 0, 0};  // statistics of the last read (lane-step counters)
+    unsigned long long w[5] = {};
+    // counter words and statistics in one readback
+    auto counters = [&]() {
+        int r = read_words_stats(s, w, u);
+        inc = w[1];
+        recs = (uint32_t)w[3];
+        nodes = u[0];
+        return r;
+    };
     if (!rc) rc = tspgpu_search_run_all(s);
-    if (!rc) rc = tspgpu_search_counters(s, &inc, &nodes, &recs);
+    if (!rc) rc = counters();
     nodes_total = nodes;
     // the record buffer overflowed: search again with the optimum as the bound,
     // so only optimal tours are recorded, into a buffer of the size now known
@@ -1130,7 +1164,7 @@ static int search_solve(tspgpu_ctx *c, const void *dist, int dtype, int n, doubl
         if (!rc) rc = herr(hipMemcpy(s->d_words + 1, &w, 8, hipMemcpyHostToDevice));
         if (!rc) rc = herr(hipMemset(s->d_stats, 0, kStatBytes));
         if (!rc) rc = tspgpu_search_run_all(s);
-        if (!rc) rc = tspgpu_search_counters(s, &inc, &nodes, &recs);
+        if (!rc) rc = counters();
         nodes_total += nodes;
     }
     std::vector<tspgpu_tour_record> opt;
@@ -1151,7 +1185,7 @@ static int search_solve(tspgpu_ctx *c, const void *dist, int dtype, int n, doubl
         }
     } else if (!rc) {
         opt.resize(recs);
-        rc = tspgpu_search_records(s, inc, opt.data(), (int)recs, &count);
+        rc = records_of(s, recs, inc, opt.data(), (int)recs, &count);
         if (!rc) rc = tspgpu_select_tour(dist, dtype, n, opt.data(), count, inc, tour_out);
         if (!rc) {
             if (dtype == TSPGPU_F64)
@@ -1171,12 +1205,9 @@ static int search_solve(tspgpu_ctx *c, const void *dist, int dtype, int n, doubl
         stats->kernel_ms = s->ms;
         stats->items = s->items;
         stats->rounds = s->rounds;
-        uint64_t u[4];
-        if (read_stats(s, u) == 0) {
-            stats->lane_steps = u[1];
-            stats->active_steps = u[2];
-            stats->item_loads = u[3];
-        }
+        stats->lane_steps = u[1];
+        stats->active_steps = u[2];
+        stats->item_loads = u[3];
     }
     tspgpu_search_destroy(s);
     return rc;
