@@ -851,9 +851,18 @@ __global__ __launch_bounds__(256) void expand_kernel(SearchArgs a)
     if (a.out_next && blockIdx.x == 0 && threadIdx.x == 0) *a.out_next = 0u;
     const uint32_t full = (uint32_t)((1ull << n) - 1ull) & ~1u;
     const V thr = EThr<V>::of(ENum<V>::val(__hip_atomic_load(a.inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)));
-    const uint32_t b0 = blockIdx.x * a.fin_per_block;
-    const uint32_t b1 = b0 + a.fin_per_block < a.fin_count ? b0 + a.fin_per_block : a.fin_count;
+    uint32_t fin_count = a.fin_count;
+    if (a.fin_count_dev) {  // chained level: the previous level's child count, at most its buffer
+        const uint32_t c = __hip_atomic_load(a.fin_count_dev, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        fin_count = c < a.fout_cap ? c : a.fout_cap;
+    }
     const int lane = __lane_id(), wv = threadIdx.x >> 6;
+    __shared__ uint32_t bskip;
+    // every run of fin_per_block input paths (one per block, or a fixed grid looping)
+    for (uint32_t runi = blockIdx.x; runi * a.fin_per_block < fin_count; runi += gridDim.x) {
+    __syncthreads();  // the previous run's wtot / bbase reads are done
+    const uint32_t b0 = runi * a.fin_per_block;
+    const uint32_t b1 = b0 + a.fin_per_block < fin_count ? b0 + a.fin_per_block : fin_count;
 
     // ---- pass 1: this block's live children per output, nodes evaluated; the
     // live masks stay in registers for pass 2 (at most kExpandTiles tiles of
@@ -890,8 +899,14 @@ __global__ __launch_bounds__(256) void expand_kernel(SearchArgs a)
         const uint32_t tf = wtot[1][0] + wtot[1][1] + wtot[1][2] + wtot[1][3];
         bbase[0] = tt ? atomicAdd(a.tail_count, tt) : 0u;
         bbase[1] = tf ? atomicAdd(a.out_count, tf) : 0u;
+        bskip = 0u;
+        if (a.overflow && ((tt && (uint64_t)bbase[0] + tt > a.tail_cap) || (tf && (uint64_t)bbase[1] + tf > a.fout_cap))) {
+            *a.overflow = 1u;  // the chained search is abandoned (the host reruns it step by step)
+            bskip = 1u;
+        }
     }
     __syncthreads();
+    if (bskip) continue;  // (block-uniform)
     uint32_t run[2] = {bbase[0], bbase[1]};
 
     // ---- pass 2: the children, at block-scanned offsets
@@ -948,6 +963,7 @@ __global__ __launch_bounds__(256) void expand_kernel(SearchArgs a)
             dst[1] = make_uint4(o[4], o[5], o[6], o[7]);
         }
     }
+    }  // runs
 }
 
 // Seeds (SearchItem, from seed_kernel) -> frontier paths.
@@ -997,7 +1013,8 @@ hipError_t launch_expand(const SearchArgs &a, bool f64)
     if (a.n > kSearchMaxN || a.fin_count == 0) return a.fin_count ? hipErrorInvalidValue : hipSuccess;
     if (a.fin_per_block == 0 || a.fin_per_block % 256u || a.fin_per_block > 256u * kExpandTiles)
         return hipErrorInvalidValue;
-    const int grid = (int)((a.fin_count + a.fin_per_block - 1u) / a.fin_per_block);
+    int grid = (int)((a.fin_count + a.fin_per_block - 1u) / a.fin_per_block);
+    if (a.max_grid > 0 && grid > a.max_grid) grid = a.max_grid;  // chained: the blocks loop over the runs
     if (a.tail_len == 5) {
         if (f64)
             hipLaunchKernelGGL((expand_kernel<double, 5>), dim3(grid), dim3(256), 0, a.stream, a);

@@ -127,6 +127,34 @@ __device__ __forceinline__ void relax_argmin_s(int32_t &acc, uint32_t &arg, int3
         : "vcc");
 }
 
+// two / four independent min-only relaxations in one block: every add is
+// issued before the first min, so no min waits on the add just before it
+__device__ __forceinline__ void relax_min2(double &a0, double g0, double d0, double &a1, double g1, double d1)
+{
+    double t0, t1;
+    asm volatile(
+        "v_add_f64 %[t0], %[g0], %[d0]\n\t"
+        "v_add_f64 %[t1], %[g1], %[d1]\n\t"
+        "v_min_f64 %[a0], %[a0], %[t0]\n\t"
+        "v_min_f64 %[a1], %[a1], %[t1]"
+        : [a0] "+v"(a0), [a1] "+v"(a1), [t0] "=&v"(t0), [t1] "=&v"(t1)
+        : [g0] "v"(g0), [d0] "v"(d0), [g1] "v"(g1), [d1] "v"(d1));
+}
+__device__ __forceinline__ void relax_min2(int32_t &a0, int32_t g0, int32_t d0, int32_t &a1, int32_t g1, int32_t d1)
+{
+    int32_t t0, t1;
+    asm volatile(
+        "v_add_u32 %[t0], %[g0], %[d0]\n\t"
+        "v_add_u32 %[t1], %[g1], %[d1]\n\t"
+        "v_min_i32 %[a0], %[a0], %[t0]\n\t"
+        "v_min_i32 %[a1], %[a1], %[t1]"
+        : [a0] "+v"(a0), [a1] "+v"(a1), [t0] "=&v"(t0), [t1] "=&v"(t1)
+        : [g0] "v"(g0), [d0] "v"(d0), [g1] "v"(g1), [d1] "v"(d1));
+}
+#ifndef TSPGPU_SUB_PAIR
+#define TSPGPU_SUB_PAIR 1  // middle passes: min-only relaxations two at a time (relax_min2)
+#endif
+
 // generic relaxation with a first-member initialisation (edge passes)
 template <bool ARG, typename V>
 __device__ __forceinline__ void relax_any(bool first, V &acc, uint32_t &arg, V g, V d, uint32_t m)
@@ -300,7 +328,8 @@ __device__ __forceinline__ void sub_mid(const SubCtx<V, N, L> &c, uint32_t h, ui
         };
         V dv[AH > 0 ? AH : 1];
         static_for<AH>([&](auto kk) { dv[decltype(kk)::value] = dload(kk); });
-        static_for<CNT>([&](auto kk) {
+        // relaxation k of the chunk (its distance from the load pipeline)
+        auto relax_one = [&](auto kk) {
             constexpr int k = decltype(kk)::value;
             constexpr int pq = sub_lds_pair<T, J, QL, C0, QN>(k);
             constexpr int p = pq / 64, qq = pq % 64;
@@ -315,8 +344,31 @@ __device__ __forceinline__ void sub_mid(const SubCtx<V, N, L> &c, uint32_t h, ui
             } else {
                 relax_min(acc[qq], g[p], d);
             }
-            __builtin_amdgcn_sched_barrier(0);
-        });
+        };
+        if constexpr (TSPGPU_SUB_PAIR && !ARG) {
+            static_for<(CNT + 1) / 2>([&](auto kk2) {
+                constexpr int k0 = 2 * decltype(kk2)::value, k1 = k0 + 1;
+                constexpr int pq0 = sub_lds_pair<T, J, QL, C0, QN>(k0);
+                constexpr int pq1 = k1 < CNT ? sub_lds_pair<T, J, QL, C0, QN>(k1) : 0;
+                constexpr int p0 = pq0 / 64, q0 = pq0 % 64, p1 = pq1 / 64, q1 = pq1 % 64;
+                if constexpr (k1 < CNT && p0 > 0 && p1 > 0 && q0 != q1) {
+                    const V d0 = dv[k0 % AH];
+                    if constexpr (k0 + AH < CNT) dv[k0 % AH] = dload(std::integral_constant<int, k0 + AH>{});
+                    const V d1 = dv[k1 % AH];
+                    if constexpr (k1 + AH < CNT) dv[k1 % AH] = dload(std::integral_constant<int, k1 + AH>{});
+                    relax_min2(acc[q0], g[p0], d0, acc[q1], g[p1], d1);
+                } else {
+                    relax_one(std::integral_constant<int, k0>{});
+                    if constexpr (k1 < CNT) relax_one(std::integral_constant<int, k1>{});
+                }
+                __builtin_amdgcn_sched_barrier(0);
+            });
+        } else {
+            static_for<CNT>([&](auto kk) {
+                relax_one(kk);
+                __builtin_amdgcn_sched_barrier(0);
+            });
+        }
         // high members x high destinations: SGPR distances
 #pragma unroll
         for (int i = 0; i < HC; ++i)

@@ -106,6 +106,15 @@ struct SearchArgs {
     unsigned int *tail_count;  // items in ftail (tail_kernel reads it on the device)
     unsigned int *out_next;    // expand_kernel: zeroes the next step's out_count (double-buffered counters)
     unsigned int tail_cap;
+    // chained frontier levels (search_abi.cpp run_chain): the step's input
+    // count read on the device (fin_count is then only the grid's bound),
+    // a fixed grid of at most max_grid blocks looping over the input runs,
+    // and outputs checked against fout_cap / tail_cap (*overflow = 1, the
+    // block's children dropped) instead of sized on the host
+    const unsigned int *fin_count_dev;
+    unsigned int fout_cap;
+    unsigned int *overflow;
+    int max_grid;
     // stronger bounds of the frontier search (expand_kernel):
     //  * bnd2 (sym != 0, symmetric matrices only): per city x the pair
     //    {b[x], e[x]} = half the sum of its two cheapest incident edges and

@@ -90,6 +90,7 @@ struct tspgpu_search {
     // frontier is empty.
     int tail_len = 6;
     bool frontier = false;
+    bool chain = true;  // run_all: small searches as chained levels (TSPGPU_SEARCH_CHAIN=0: step by step)
     // stronger frontier bounds (SearchArgs::bnd2 / ::hsuf): the two-edge bound
     // for symmetric matrices and the suffix table for the last tail_len cities
     int sym = 0;
@@ -130,7 +131,7 @@ struct tspgpu_search {
     uint64_t tails = 0;          // items waiting in d_tail
     int rounds = 0;
     double ms = 0.0;             // device time of all seed/round launches
-    hipEvent_t e0 = nullptr, e1 = nullptr;
+    hipEvent_t e0 = nullptr, e1 = nullptr, e2 = nullptr;
     unsigned long long *h_cnt = nullptr;  // pinned host words: the frontier step's counter readback
     // pinned host copy of the statistics lines + 8 counter words (one DMA
     // pair and one synchronisation per counters read)
@@ -170,7 +171,7 @@ struct SearchPool {
     std::vector<size_t> fb_cap;
     PathItem *d_tail = nullptr;
     unsigned int tail_alloc = 0;
-    hipEvent_t e0 = nullptr, e1 = nullptr;
+    hipEvent_t e0 = nullptr, e1 = nullptr, e2 = nullptr;
     unsigned long long *h_cnt = nullptr;
     unsigned long long *h_stats = nullptr;
     void *d_bnd2 = nullptr;
@@ -202,6 +203,7 @@ void move_buffers(A &to, B &from)
     to.tail_alloc = from.tail_alloc, from.tail_alloc = 0;
     to.e0 = from.e0, from.e0 = nullptr;
     to.e1 = from.e1, from.e1 = nullptr;
+    to.e2 = from.e2, from.e2 = nullptr;
     to.h_cnt = from.h_cnt, from.h_cnt = nullptr;
     to.h_stats = from.h_stats, from.h_stats = nullptr;
     to.d_bnd2 = from.d_bnd2, from.d_bnd2 = nullptr;
@@ -228,6 +230,7 @@ void free_buffers(A &b)
     if (b.d_tail) (void)hipFree(b.d_tail);
     if (b.e0) (void)hipEventDestroy(b.e0);
     if (b.e1) (void)hipEventDestroy(b.e1);
+    if (b.e2) (void)hipEventDestroy(b.e2);
     if (b.h_cnt) (void)hipHostFree(b.h_cnt);
     if (b.h_stats) (void)hipHostFree(b.h_stats);
     if (b.d_bnd2) (void)hipFree(b.d_bnd2);
@@ -319,6 +322,7 @@ int tspgpu_search_create(tspgpu_ctx *c, const void *dist, int dtype, int n, int 
         s->suffix_len = (v == 5 || v == 6) ? v : 0;
     }
     if (const char *e = std::getenv("TSPGPU_SEARCH_TWO_EDGE")) s->use_two_edge = std::atoi(e) != 0;
+    if (const char *e = std::getenv("TSPGPU_SEARCH_CHAIN")) s->chain = std::atoi(e) != 0;
     if (const char *e = std::getenv("TSPGPU_SEARCH_LAGRANGE")) s->use_lagrange = std::atoi(e) != 0;
     if (const char *e = std::getenv("TSPGPU_SEARCH_MST")) s->use_mst = std::atoi(e) != 0;
     if (const char *e = std::getenv("TSPGPU_SEARCH_MST_MINREM")) s->mst_min_rem = std::atoi(e);
@@ -529,6 +533,7 @@ int tspgpu_search_create(tspgpu_ctx *c, const void *dist, int dtype, int n, int 
     if (e == hipSuccess) e = hipStreamSynchronize(st);
     if (e == hipSuccess && !s->e0) e = hipEventCreate(&s->e0);
     if (e == hipSuccess && !s->e1) e = hipEventCreate(&s->e1);
+    if (e == hipSuccess && !s->e2) e = hipEventCreate(&s->e2);
     if (e == hipSuccess && !s->h_cnt && !std::getenv("TSPGPU_SEARCH_PAGEABLE"))
         e = hipHostMalloc((void **)&s->h_cnt, 8 * sizeof(unsigned long long), hipHostMallocDefault);
     if (e == hipSuccess && !s->h_stats && !std::getenv("TSPGPU_SEARCH_PAGEABLE"))
@@ -693,8 +698,11 @@ static void front_release(tspgpu_search *s)
     s->seg_n.clear();
 }
 
-// launch + wait + read the item count the launch produced
-static int launch_and_count(tspgpu_search *s, bool seed, int grid, SearchArgs &a, uint32_t suffix_sets = 0)
+// launch + wait + read the item count the launch produced (sync = false: the
+// count stays in word 4 for a chained search to read on the device; the
+// launch's time is then the chain's)
+static int launch_and_count(tspgpu_search *s, bool seed, int grid, SearchArgs &a, uint32_t suffix_sets = 0,
+                            bool sync = true)
 {
     hipStream_t st = s->ctx->stream;
     hipError_t e = hipMemsetAsync(s->d_words, 0, 8, st);  // queue
@@ -707,6 +715,7 @@ static int launch_and_count(tspgpu_search *s, bool seed, int grid, SearchArgs &a
         e = seed ? launch_seed(a, s->dtype == TSPGPU_F64, grid) : launch_round(a, s->dtype == TSPGPU_F64, grid);
     (void)hipEventRecord(s->e1, st);
     if (e != hipSuccess) return herr(e);
+    if (!sync) return 0;
     unsigned long long out = 0;
     e = hipMemcpyAsync(&out, s->d_words + 4, 8, hipMemcpyDeviceToHost, st);
     if (e == hipSuccess) e = hipStreamSynchronize(st);
@@ -754,9 +763,14 @@ static int build_suffix(tspgpu_search *s, bool launch, uint32_t *sets_out)
     return 0;
 }
 
-int tspgpu_search_start(tspgpu_search *s)
+static int search_start(tspgpu_search *s, bool sync);
+int tspgpu_search_start(tspgpu_search *s) { return s ? search_start(s, true) : -EINVAL; }
+
+// sync = false (chained searches): the seeds' launch is only enqueued, their
+// count stays on the device (word 4), s->pending is the upper bound
+// local_items and the seed segment is left to the caller
+static int search_start(tspgpu_search *s, bool sync)
 {
-    if (!s) return -EINVAL;
     (void)hipSetDevice(s->ctx->device);
     if (int rc = ensure_items(s, 0, s->local_items + 1)) return rc;
     SearchArgs a = args_of(s);
@@ -784,7 +798,13 @@ int tspgpu_search_start(tspgpu_search *s)
     }
     const uint64_t blocks = (s->local_items + kSearchThreads - 1) / kSearchThreads;
     const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>(blocks, (uint64_t)s->ctx->cu_count * 8));
-    int rc = launch_and_count(s, true, grid, a, s->frontier ? sets : 0u);
+    int rc = launch_and_count(s, true, grid, a, s->frontier ? sets : 0u, sync);
+    if (!rc && !sync) {
+        s->pending = s->local_items;
+        s->seg_buf.push_back(seed_buf);
+        s->seg_n.push_back(0);
+        return 0;
+    }
     if (!rc && s->frontier && s->pending) {
         s->seg_buf.push_back(seed_buf);
         s->seg_n.push_back(s->pending);
@@ -927,6 +947,87 @@ int tspgpu_search_step(tspgpu_search *s, uint64_t *pending)
     return 0;
 }
 
+// Small searches, chained (one shard, n <= kChainMaxN): after the seeds, every
+// frontier level is enqueued back to back — each expand launch reads its input
+// count from the counter the previous level wrote (three counter words in
+// rotation: read one, write the next, zero the third), loops a fixed grid
+// over its input runs and writes its children into one of two ping-pong
+// buffers of kChainCap paths — then the tail fold, and ONE synchronisation.
+// No host round trip per level (the stepwise search pays ~30 us each: 0.2 of
+// the 16-city search's 0.45 ms, profiles/r03/k2_variants.log).  A level whose
+// children or tails would not fit sets an overflow word; the search is then
+// rerun step by step (records and tails reset; the incumbent, a real tour's
+// cost, is kept).  Breadth first instead of the stepwise LIFO: the same
+// bounds, the same optimal set, a different node count.
+constexpr int kChainMaxN = 18;
+constexpr uint64_t kChainCap = (uint64_t)1 << 22;
+static int run_chain(tspgpu_search *s, bool *done)
+{
+    *done = false;
+    SearchArgs a0 = args_of(s);
+    const int levels = a0.tail_level - s->depth;
+    if (levels < 1 || s->local_items + 1 > kChainCap) return 0;
+    hipStream_t st = s->ctx->stream;
+    const bool f64 = s->dtype == TSPGPU_F64;
+    // words 10..13 zeroed before the seeds (10..12: level counters, 13: overflow)
+    hipError_t e = hipMemsetAsync(s->d_words + 10, 0, 4 * sizeof(unsigned long long), st);
+    if (e != hipSuccess) return herr(e);
+    (void)hipEventRecord(s->e2, st);
+    int rc = search_start(s, false);  // the seeds, enqueued: their count stays in word 4
+    if (rc) return rc;
+    int ob[2];
+    for (int k = 0; k < 2; ++k) {
+        ob[k] = front_spare(s, (size_t)kChainCap, &rc);
+        if (ob[k] < 0) return rc;
+        s->seg_buf.push_back(ob[k]);  // (marked used so the second front_spare picks another)
+        s->seg_n.push_back(0);
+    }
+    // level l reads its input count from word 4 (the seeds, l = 0) or
+    // 10 + l%3, writes 10 + (l+1)%3 and zeroes 10 + (l+2)%3
+    for (int l = 0; l < levels && e == hipSuccess; ++l) {
+        SearchArgs a = args_of(s);
+        a.fseg[0] = l == 0 ? s->fb[s->seg_buf[0]] : s->fb[ob[(l - 1) & 1]];
+        a.fseg_start[0] = 0;
+        a.nseg = 1;
+        a.fin = a.fseg[0];
+        a.fin_count = l == 0 ? (uint32_t)s->local_items : (uint32_t)kChainCap;  // (the grid's bound)
+        a.fin_count_dev = reinterpret_cast<const unsigned int *>(s->d_words + (l == 0 ? 4 : 10 + l % 3));
+        a.out_count = reinterpret_cast<unsigned int *>(s->d_words + 10 + (l + 1) % 3);
+        a.out_next = reinterpret_cast<unsigned int *>(s->d_words + 10 + (l + 2) % 3);
+        a.fout = s->fb[ob[l & 1]];
+        a.fout_cap = (uint32_t)kChainCap;
+        a.overflow = reinterpret_cast<unsigned int *>(s->d_words + 13);
+        a.fin_per_block = 1024;
+        a.max_grid = s->ctx->cu_count;  // (blocks beyond the level's runs only stage tables and leave)
+        e = launch_expand(a, f64);
+    }
+    if (e == hipSuccess) {
+        SearchArgs a = args_of(s);
+        e = launch_tail(a, f64, s->ctx->cu_count * 8);
+    }
+    (void)hipEventRecord(s->e1, st);
+    unsigned long long local[8] = {};
+    unsigned long long *h = s->h_cnt ? s->h_cnt : local;
+    if (e == hipSuccess) e = hipMemcpyAsync(h, s->d_words + 8, 6 * sizeof(unsigned long long), hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (e != hipSuccess) return herr(e);
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, s->e2, s->e1) == hipSuccess) s->ms += ms;  // seeds through the tail fold
+    s->rounds += levels + 1;
+    front_release(s);
+    s->pending = 0;
+    s->tails = 0;
+    if ((uint32_t)h[5] == 0) {  // word 13: no overflow
+        *done = true;
+        return 0;
+    }
+    // overflow: records and tails reset, the search reruns step by step
+    e = hipMemsetAsync(s->d_words + 3, 0, 8, st);
+    if (e == hipSuccess) e = hipMemsetAsync(s->d_words + 8, 0, 8, st);
+    if (e == hipSuccess) e = hipMemsetAsync(s->d_words + 13, 0, 8, st);
+    return herr(e);
+}
+
 // The whole search in ONE persistent launch (kernel 3): seeds decoded on the
 // fly, work handed between lanes through a device ring, no rounds.
 static int run_persist(tspgpu_search *s)
@@ -1022,6 +1123,11 @@ int tspgpu_search_run_all(tspgpu_search *s)
     if (!s) return -EINVAL;
     if (s->noprune && s->enum_kernel) return run_enum(s);
     if (s->kernel == 3 && !s->noprune) return run_persist(s);
+    if (s->frontier && !s->noprune && s->nshards == 1 && s->n <= kChainMaxN && s->chain) {
+        bool done = false;
+        int rc = run_chain(s, &done);
+        if (rc || done) return rc;
+    }
     int rc = tspgpu_search_start(s);
     uint64_t pending = 1;
     while (!rc && pending) rc = tspgpu_search_step(s, &pending);
@@ -1151,8 +1257,21 @@ static int search_solve(tspgpu_ctx *c, const void *dist, int dtype, int n, doubl
         nodes = u[0];
         return r;
     };
+    // counters, statistics and (speculatively) the first kSpecRecs records in
+    // one synchronisation
+    constexpr unsigned kSpecRecs = 2048;
+    std::vector<SearchRecord> spec;
+    bool spec_ok = false;
     if (!rc) rc = tspgpu_search_run_all(s);
-    if (!rc) rc = counters();
+    if (!rc) {
+        const unsigned k = std::min<unsigned>(kSpecRecs, s->rec_cap);
+        spec.resize(k);
+        hipError_t e = hipMemcpyAsync(spec.data(), s->d_rec, sizeof(SearchRecord) * k, hipMemcpyDeviceToHost,
+                                      s->ctx->stream);
+        rc = herr(e);
+        if (!rc) rc = counters();  // (its synchronisation covers the record copy)
+        spec_ok = !rc && recs <= k;
+    }
     nodes_total = nodes;
     // the record buffer overflowed: search again with the optimum as the bound,
     // so only optimal tours are recorded, into a buffer of the size now known
@@ -1165,6 +1284,7 @@ static int search_solve(tspgpu_ctx *c, const void *dist, int dtype, int n, doubl
         if (!rc) rc = herr(hipMemset(s->d_stats, 0, kStatBytes));
         if (!rc) rc = tspgpu_search_run_all(s);
         if (!rc) rc = counters();
+        spec_ok = false;
         nodes_total += nodes;
     }
     std::vector<tspgpu_tour_record> opt;
@@ -1185,7 +1305,12 @@ static int search_solve(tspgpu_ctx *c, const void *dist, int dtype, int n, doubl
         }
     } else if (!rc) {
         opt.resize(recs);
-        rc = records_of(s, recs, inc, opt.data(), (int)recs, &count);
+        if (spec_ok) {
+            for (uint64_t i = 0; i < recs; ++i)
+                if (spec[i].cost == inc) std::memcpy(&opt[count++], &spec[i], sizeof(SearchRecord));
+        } else {
+            rc = records_of(s, recs, inc, opt.data(), (int)recs, &count);
+        }
         if (!rc) rc = tspgpu_select_tour(dist, dtype, n, opt.data(), count, inc, tour_out);
         if (!rc) {
             if (dtype == TSPGPU_F64)

@@ -255,6 +255,15 @@ bool heuristic(const V *d, int n, std::vector<int32_t> &best, V &cost, int first
 {
     std::vector<int> starts;
     for (int s0 = first; s0 < n; s0 += step) starts.push_back(s0);
+    // below 20 cities (one thread) four spread-out starts: each start costs
+    // ~7 us at 16 cities, all sixteen were a quarter of the whole in-process
+    // search, and the device's suffix tests tighten the bound within the
+    // first expansion anyway (profiles/r03/k2_variants.log)
+    if (n < 20 && (int)starts.size() > 4 && !std::getenv("TSPGPU_HEURISTIC_ALL_STARTS")) {
+        std::vector<int> few;
+        for (int i = 0; i < 4; ++i) few.push_back(starts[(size_t)i * starts.size() / 4]);
+        starts.swap(few);
+    }
     const int ns = (int)starts.size();
     std::vector<std::vector<int32_t>> tours(ns);
     std::vector<V> costs(ns);
@@ -414,11 +423,11 @@ int tspgpu_heuristic_tour_starts(const void *dist, int dtype, int n, int first, 
     if (first >= n) return -ENOENT;  // no start city in this range
     std::vector<int32_t> t;
     if (dtype == TSPGPU_F64) {
-        double c;
+        double c = 0.0;
         heuristic(static_cast<const double *>(dist), n, t, c, first, step);
         if (cost_out) *cost_out = c;
     } else {
-        int32_t c;
+        int32_t c = 0;
         heuristic(static_cast<const int32_t *>(dist), n, t, c, first, step);
         if (cost_out) *cost_out = c;
     }
