@@ -187,6 +187,31 @@ def test_frontier_16_golden(gpu_ctx, monkeypatch):
         assert [blk[t][0] for t in tour] == case["solutions"][0]["ids"], st
 
 
+@pytest.mark.parametrize("mode", ["chain", "steps", "chain_overflow"])
+def test_chained_small_search(gpu_ctx, monkeypatch, mode):
+    """Small single-shard searches run as chained frontier levels (one
+    synchronisation); a level that overflows the ping-pong buffers falls back
+    to the stepwise search.  All three give the reference's golden 16-city
+    answer, and random / tie-heavy instances equal the oracle."""
+    if mode == "steps":
+        monkeypatch.setenv("TSPGPU_SEARCH_CHAIN", "0")
+    if mode == "chain_overflow":
+        monkeypatch.setenv("TSPGPU_SEARCH_CHAIN_CAP_LOG2", "8")
+    case = next(c for c in O.load_golden("seed0_blocks.json") if c["n"] == 16 and c["B"] == 1 and c["X"] == 1000)
+    blk = _cities(case["cities"][0])
+    d = tspgpu.distance_matrix([blk])[0]
+    cost, tour, st = tspgpu.search_solve(gpu_ctx, d)
+    assert cost == O.hexf(case["solutions"][0]["cost_hex"]), st
+    assert [blk[t][0] for t in tour] == case["solutions"][0]["ids"], st
+    rng = np.random.default_rng(11)
+    for n in (9, 12, 14, 17, 18):
+        for kind in ("random", "lattice"):
+            xy = rng.uniform(0, 1000, size=(n, 2)) if kind == "random" else rng.integers(0, 4, size=(n, 2)) * 1.0
+            dd = O.distance_matrix([(i, xy[i, 0], xy[i, 1]) for i in range(n)])
+            c2, t2, s2 = tspgpu.search_solve(gpu_ctx, dd)
+            assert (c2, t2.tolist()) == O.solve_block(dd), (mode, n, kind, s2)
+
+
 @pytest.mark.parametrize("nshards", [2, 3, 5])
 def test_sharded_on_one_gpu(gpu_ctx, nshards):
     """The multi-GPU decomposition, run shard by shard on one device: min of

@@ -32,6 +32,7 @@ for s in ${STEPS:-time16 tests}; do
     k2var) step k2_variants 300 python -u tools/k2_phases.py --variants ;;
     ab) step ab_time 600 bash tools/ab_time.sh ;;
     k2tests) step k2_tests 600 python -u -m pytest tests/test_search_gpu.py tests/test_rccl_gpu.py tests/test_search_cli.py tests/test_tsplib.py -x -q -m gpu --timeout 200 --timeout-method thread ;;
+    chaintest) step chain_test 300 python -u -m pytest tests/test_search_gpu.py -k "chained" -x -q --timeout 200 --timeout-method thread ;;
     gputests) step gpu_tests 900 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread ;;
     bench) step bench 600 python3 -u bench.py --steps 20 --warmup 3 ;;
     bench2) step bench_2ranks 300 python3 -u bench.py --gpus 2 --steps 10 --warmup 2 --no-k2 ;;

@@ -34,9 +34,10 @@ namespace tspgpu {
 
 // row stride (entries) of the LDS distance image: N natural columns + H
 // sub-cube-ordered high columns, odd so that the low-low gathers of a
-// half-wave spread over the banks
+// half-wave spread over the banks (25: 1% faster than 21 and 23 at n = 16,
+// profiles/r03/k1_ab_table.log run 6)
 #ifndef TSPGPU_SUB_DS
-#define TSPGPU_SUB_DS 21
+#define TSPGPU_SUB_DS 25
 #endif
 constexpr int kSubDS = TSPGPU_SUB_DS;
 

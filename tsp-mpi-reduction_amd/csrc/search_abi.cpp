@@ -960,10 +960,15 @@ int tspgpu_search_step(tspgpu_search *s, uint64_t *pending)
 // cost, is kept).  Breadth first instead of the stepwise LIFO: the same
 // bounds, the same optimal set, a different node count.
 constexpr int kChainMaxN = 18;
-constexpr uint64_t kChainCap = (uint64_t)1 << 22;
 static int run_chain(tspgpu_search *s, bool *done)
 {
     *done = false;
+    // ping-pong buffer capacity (TSPGPU_SEARCH_CHAIN_CAP_LOG2: tests force the overflow fallback)
+    uint64_t kChainCap = (uint64_t)1 << 22;
+    if (const char *ev = std::getenv("TSPGPU_SEARCH_CHAIN_CAP_LOG2")) {
+        const int v = std::atoi(ev);
+        if (v >= 8 && v <= 24) kChainCap = (uint64_t)1 << v;
+    }
     SearchArgs a0 = args_of(s);
     const int levels = a0.tail_level - s->depth;
     if (levels < 1 || s->local_items + 1 > kChainCap) return 0;

@@ -163,6 +163,25 @@ int ensure_tiled_info(tspgpu_ctx *c, int L)
     return 0;
 }
 
+// Variants 5/6 keep one global slot per block of a launch (1.65 MB at
+// n = 16) until its backtracking kernel has run, so a launch takes blocks in
+// chunks: up to 65536 (108 GB of the 288 GB at n = 16 — a persistent grid of
+// 1536 workgroups then idles a third of the chip for 0.67 of 42.7 rounds
+// instead of 0.67 of 10.7 at 16384), halved while the allocation fails.
+int ensure_slots(tspgpu_ctx *c, int nblocks, size_t slot, int *chunk)
+{
+    int ch = std::min(nblocks, 65536);
+    for (;;) {
+        const int rc = ensure(&c->d_tslots, &c->tslots_bytes, (size_t)ch * slot);
+        if (rc == 0 || rc != -ENOMEM || ch <= 1024) {
+            *chunk = ch;
+            return rc;
+        }
+        (void)hipGetLastError();  // (clear the failed allocation's error)
+        ch /= 2;
+    }
+}
+
 // Split timing (tspgpu_k1_split_timing): three events per chunk, kept until
 // tspgpu_k1_last_split_ms reads them; the first is recorded here.  *ev0 = the
 // chunk's first event index (unused when split timing is off).
@@ -258,8 +277,8 @@ int solve_sub(tspgpu_ctx *c, const SubCfg *cfg, const void *d_dist, int n, int n
     // the same per-block slot as variant 5 (push area, parent words,
     // recompute area), kept until the backtracking kernel has run
     const size_t slot = tiled_slot_bytes(N, L, cfg->vbytes);
-    const int chunk = std::min(nblocks, 16384);
-    if ((rc = ensure(&c->d_tslots, &c->tslots_bytes, (size_t)chunk * slot))) return rc;
+    int chunk = 0;
+    if ((rc = ensure_slots(c, nblocks, slot, &chunk))) return rc;
     for (int b0 = 0; b0 < nblocks; b0 += chunk) {
         SubArgs a{};
         size_t ev0 = 0;
@@ -313,11 +332,10 @@ int solve_tiled(tspgpu_ctx *c, const TiledCfg *cfg, const void *d_dist, int n, i
     const int grid = std::min(nblocks, c->cu_count * cfg->wg);
     // one global slot per block (push area, parent words of the top rows,
     // backtracking recompute area: 1.65 MB at n = 16, hk_tiled.h), kept until
-    // the backtracking kernel of the launch has run: blocks go in launches of
-    // at most 16384 (27 GB of the 288 GB at n = 16)
+    // the backtracking kernel of the launch has run (ensure_slots: chunks)
     const size_t slot = tiled_slot_bytes(N, L, cfg->vbytes);
-    const int chunk = std::min(nblocks, 16384);
-    if ((rc = ensure(&c->d_tslots, &c->tslots_bytes, (size_t)chunk * slot))) return rc;
+    int chunk = 0;
+    if ((rc = ensure_slots(c, nblocks, slot, &chunk))) return rc;
     for (int b0 = 0; b0 < nblocks; b0 += chunk) {
         TiledArgs a{};
         size_t ev0 = 0;
