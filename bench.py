@@ -602,30 +602,72 @@ def valu_peaks():
     return out
 
 
-def _rocprof_pass(counters, n, blocks, kernel, tag, timeout=90):
+def _rocprof_pass(counters, n, blocks, kernel, tag, timeout=90, child=None, reduce="median"):
+    """One rocprofv3 --pmc pass over a child run of this file: the K1 launch
+    (--pmc-child) or, with child = [...], other child arguments.  `kernel`: a
+    substring or a tuple of them; reduce "median" over the matching
+    dispatches, or "sum"."""
     rocprof = shutil.which("rocprofv3")
     if not rocprof:
         return None, "rocprofv3 not found"
     d = os.path.join(ROOT, "gpurun_out", f"pmc_{tag}")
     shutil.rmtree(d, ignore_errors=True)
+    child = child or ["--pmc-child", "--n", str(n), "--blocks-per-gpu", str(blocks)]
     cmd = ["timeout", "-s", "KILL", str(timeout), rocprof, "--pmc", *counters, "--output-format", "csv",
-           "-d", d, "-o", "pmc", "--", sys.executable, os.path.abspath(__file__), "--pmc-child",
-           "--n", str(n), "--blocks-per-gpu", str(blocks)]
+           "-d", d, "-o", "pmc", "--", sys.executable, os.path.abspath(__file__), *child]
     p = subprocess.run(cmd, capture_output=True, text=True, cwd="/tmp")
     import collections
     import csv
 
+    names = (kernel,) if isinstance(kernel, str) else tuple(kernel)
     vals = collections.defaultdict(list)
     for root, _, files in os.walk(d):
         for f in files:
             if f.endswith("counter_collection.csv"):
                 with open(os.path.join(root, f)) as fh:
                     for row in csv.DictReader(fh):
-                        if kernel in row.get("Kernel_Name", ""):
+                        if any(k in row.get("Kernel_Name", "") for k in names):
                             vals[row["Counter_Name"]].append(float(row["Counter_Value"]))
     if p.returncode != 0 or not vals:
         return None, f"rc={p.returncode} {p.stderr[-300:]}"
-    return {k: statistics.median(v) for k, v in vals.items()}, None
+    agg = sum if reduce == "sum" else statistics.median
+    return {k: agg(v) for k, v in vals.items()}, None
+
+
+K2_KERNELS = ("prologue_kernel", "expand_kernel", "tail_kernel")
+K2_PMC_SEARCHES = 4  # searches the K2 PMC child runs (counters are summed over them)
+
+
+def k2_pmc(cus, peaks, nodes_per_search, kernel_ms):
+    """SQ counters of the K2 search kernels (the reference's 16-city
+    instance, K2_PMC_SEARCHES searches, counters summed and divided back per
+    search): VALU instructions per B&B node, VALU active, and the VALU issue
+    rate those kernels reach against the f64 add rate measured on this GPU."""
+    sq, err = _rocprof_pass(SQ_PASS, 16, 1, K2_KERNELS, "k2_sq", child=["--pmc-child-k2"], reduce="sum")
+    if not sq:
+        return {"error": err}
+    per = {k: v / K2_PMC_SEARCHES for k, v in sq.items()}
+    lane_instr = per["SQ_INSTS_VALU"] * 64.0
+    out = {"kernels": list(K2_KERNELS), "valu_wave_instructions_per_search": per["SQ_INSTS_VALU"],
+           "valu_lane_instructions_per_node": lane_instr / max(nodes_per_search, 1),
+           "waves_per_search": per["SQ_WAVES"], "sq_raw_per_search": per}
+    peak = (peaks or {}).get("v_add_f64")
+    if peak and kernel_ms:
+        ach = lane_instr / (kernel_ms * 1e-3)
+        out["roofline"] = {"bound": "valu (issue)", "achieved": ach / 1e12, "peak": peak / 1e12,
+                           "unit": "T VALU lane-instructions/s", "frac": ach / peak,
+                           "note": "VALU lane-instructions of the search kernels (PMC SQ_INSTS_VALU x 64) per search / "
+                                   "the search's device time (the chained launches' event span, gaps included), "
+                                   "against the f64 add issue rate (bin/ubench); "
+                                   "a node costs valu_lane_instructions_per_node of them"}
+    return out
+
+
+def pmc_child_k2():
+    ctx = tspgpu.Context(device=0)
+    d = Shard(16, 1, 0, 1).distances()[0]
+    for _ in range(K2_PMC_SEARCHES):
+        tspgpu.search_solve(ctx, d)
 
 
 SQ_PASS = ("SQ_WAVES", "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES", "SQ_ACTIVE_INST_VALU", "SQ_INSTS_VALU",
@@ -727,9 +769,12 @@ def main():
                     help="skip the reference-vs-drop-in `./tsp 16 8` runs at P = 1/2/4/8")
     ap.add_argument("--plumbing", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--pmc-child-k2", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
     if args.pmc_child:
         return pmc_child(args)
+    if args.pmc_child_k2:
+        return pmc_child_k2()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(spawn_ranks(sys.argv[1:], args.gpus))
 
@@ -912,6 +957,11 @@ def main():
     dom_ms = split["forward_kernel_ms"] if split else kernel_ms  # the dominant kernel's own time
     relax_s_kernel = Bp * relax / (dom_ms * 1e-3)
     roof = roofline(variant, kname, n, Bp, dom_ms, relax_s_kernel, alg_bytes_per_block, prof, peaks)
+    if world == 1 and not args.no_pmc and k2 and "bb_nodes_expanded" in k2:
+        try:
+            k2["pmc"] = k2_pmc(cu, peaks, k2["bb_nodes_expanded"], k2["kernel_ms"])
+        except Exception as e:  # noqa: BLE001
+            k2["pmc"] = {"error": f"{type(e).__name__}: {e}"}
     cpu = cpu_opt = refmb = None
     if world == 1 and not args.no_ref_multiblock:
         try:

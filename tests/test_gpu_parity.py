@@ -185,16 +185,24 @@ def test_torch_tensors_and_stream_interop():
     assert p.returncode == 0 and "OK" in p.stdout, p.stderr[-2000:]
 
 
+@pytest.mark.parametrize("variant", ["default", "5"])
 @pytest.mark.parametrize("case", O.load_golden("k1_batches.json"), ids=lambda c: f"n{c['n']}")
-def test_k1_batches_reference_goldens_default_kernel(gpu_ctx, case):
+def test_k1_batches_reference_goldens_default_kernel(gpu_ctx, monkeypatch, case, variant):
     """The reference's own tsp() outputs for 522 blocks per n = 13..16 (tie-heavy
-    lattices and uniform cities), solved in ONE batch through the default path:
-    a batch of more than one block per CU runs the large-batch kernel (variant
-    5 or later), the configuration ./tsp 16 16384 times."""
+    lattices and uniform cities), solved in ONE batch: a batch of more than
+    one block per CU runs the large-batch kernel — variant 6 (hk_sub_kernel,
+    the default: the configuration ./tsp 16 65536 times) and variant 5
+    (hk_tiled_kernel, TSPGPU_K1=5) — both against the reference itself."""
     blocks = O.k1_batch_blocks(case)
     n = case["n"]
-    _, cost, tour = _solve_blocks_of_cities(gpu_ctx, blocks)
-    assert gpu_ctx.last_variant() >= 5, gpu_ctx.last_variant()
+    ctx = gpu_ctx
+    if variant != "default":
+        monkeypatch.setenv("TSPGPU_K1", variant)
+        ctx = tspgpu.Context(device=0)
+    _, cost, tour = _solve_blocks_of_cities(ctx, blocks)
+    assert ctx.last_variant() == (6 if variant == "default" else int(variant)), ctx.last_variant()
+    if ctx is not gpu_ctx:
+        ctx.close()
     bad = [b for b, ref in enumerate(case["blocks"])
            if cost[b] != O.hexf(ref["cost_hex"]) or _ids(blocks[b], tour[b], n) != ref["ids"]]
     assert not bad, f"n={n}: mismatching blocks {bad[:10]}"

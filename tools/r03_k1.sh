@@ -33,8 +33,10 @@ for s in ${STEPS:-time16 tests}; do
     ab) step ab_time 600 bash tools/ab_time.sh ;;
     k2tests) step k2_tests 600 python -u -m pytest tests/test_search_gpu.py tests/test_rccl_gpu.py tests/test_search_cli.py tests/test_tsplib.py -x -q -m gpu --timeout 200 --timeout-method thread ;;
     chaintest) step chain_test 300 python -u -m pytest tests/test_search_gpu.py -k "chained" -x -q --timeout 200 --timeout-method thread ;;
+    pyk) step pyk 600 python -u -m pytest tests -m gpu -k "$PYK" -x -q --timeout 200 --timeout-method thread ;;
     gputests) step gpu_tests 900 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread ;;
     bench) step bench 600 python3 -u bench.py --steps 20 --warmup 3 ;;
+    benchk2) step bench_k2 300 python3 -u bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-ref-multiblock --no-tto ;;
     bench2) step bench_2ranks 300 python3 -u bench.py --gpus 2 --steps 10 --warmup 2 --no-k2 ;;
     esac
 done
