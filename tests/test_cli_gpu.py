@@ -45,3 +45,21 @@ def test_cli_matches_reference(case):
     rc, lines, err = run_tsp(case["args"], case["P"])
     assert rc == case["rc"], err
     assert split(lines) == split(case["lines"])
+
+
+@pytest.mark.gpu
+def test_cli_stats_line_is_opt_in_and_on_stderr():
+    """TSP_STATS=1 adds one statistics line on stderr; stdout stays the
+    reference's (SURVEY.md §5 "Metrics")."""
+    case = next(c for c in CASES if not c.get("error_case") and list(c["args"][:2]) == [16, 8] and c["P"] == 1)
+    env = dict(os.environ, TSP_NPROCS=str(case["P"]), TSP_STATS="1")
+    for k in ("PMI_SIZE", "PMI_RANK", "OMPI_COMM_WORLD_SIZE", "OMPI_COMM_WORLD_RANK"):
+        env.pop(k, None)
+    p = subprocess.run([tspgpu.TSP_BIN, *map(str, case["args"])], capture_output=True, text=True, env=env, timeout=300)
+    assert p.returncode == case["rc"], p.stderr
+    lines = [MS.sub("TSP ran in <ms> ms ", ln) for ln in p.stdout.splitlines()]
+    assert split(lines) == split(case["lines"])
+    stats = [ln for ln in p.stderr.splitlines() if ln.startswith("tsp stats: ")]
+    assert len(stats) == 1 and "DP relaxations/s" in stats[0] and "block search" in stats[0]
+    _, _, plain_err = run_tsp(case["args"], case["P"])
+    assert "tsp stats" not in plain_err

@@ -26,6 +26,8 @@
 // reduction tree) run on the GPU too (K3, tspgpu_reduce); TSP_HOST_MERGE=1
 // replays them on the host instead.
 //
+// TSP_STATS=1 adds one statistics line on stderr (phase times, relaxations/s).
+//
 // Deviations (documented in DESIGN.md), all where the reference is undefined:
 // n < 2, numBlocks < 1 or numBlocks < P exit 2 with a message on stderr
 // instead of crashing or hanging (tsp.cpp:326-330, 355).
@@ -311,6 +313,8 @@ int main(int argc, char **argv)
     std::vector<double> cost(B, 0.0);
     std::vector<int32_t> tour((size_t)B * (n + 1), -1);
     int rc;
+    timespec ts_solve0, ts_solve1, ts_merge1;
+    clock_gettime(CLOCK_MONOTONIC_RAW, &ts_solve0);
     if (multi) {
         // rank 0's own share here, the other ranks' shares from their files
         std::vector<int> cnt(P), off(P, 0);
@@ -334,6 +338,7 @@ int main(int argc, char **argv)
         return 3;
     }
 
+    clock_gettime(CLOCK_MONOTONIC_RAW, &ts_solve1);
     // convPathToCityPath (assignment2.h:76-84) for every block
     const int L = tspgpu_tour_length(n);
     std::vector<tspgpu_city> paths((size_t)B * L);
@@ -366,10 +371,27 @@ int main(int argc, char **argv)
         return 2;
     }
     std::fputs(log.data(), stdout);
+    clock_gettime(CLOCK_MONOTONIC_RAW, &ts_merge1);
 
     clock_gettime(CLOCK_MONOTONIC_RAW, &end);
     const uint64_t ms = (uint64_t)((1000000000L * (end.tv_sec - start.tv_sec) + end.tv_nsec - start.tv_nsec) / 1e6);
     std::printf("TSP ran in %llu ms for %lu cities and the trip cost %f\n", (unsigned long long)ms,
                 (unsigned long)(unsigned int)(B * n), final_cost);
+    // opt-in statistics on stderr (SURVEY.md §5 "Metrics": stdout stays the
+    // reference's byte for byte): phase times and the block search's rate
+    if (env_int("TSP_STATS", 0)) {
+        auto sec = [](const timespec &a, const timespec &b) {
+            return (double)(b.tv_sec - a.tv_sec) + 1e-9 * (double)(b.tv_nsec - a.tv_nsec);
+        };
+        const double solve_s = sec(ts_solve0, ts_solve1);
+        const double relax = tspgpu_relaxations_per_block(n) * (multi ? 0.0 : (double)B);
+        std::fprintf(stderr,
+                     "tsp stats: n %d blocks %d ranks %d | setup %.3f ms, block search %.3f ms (%s), merge %.3f ms, "
+                     "total %.3f ms | %.4g DP relaxations/s\n",
+                     n, B, P, 1e3 * sec(start, ts_solve0), 1e3 * solve_s,
+                     multi ? "rank 0's share + the rank files" : "all blocks, one process",
+                     1e3 * sec(ts_solve1, ts_merge1), 1e3 * sec(start, end),
+                     solve_s > 0 && relax > 0 ? relax / solve_s : 0.0);
+    }
     return 0;
 }
