@@ -53,9 +53,30 @@ __host__ __device__ constexpr size_t sub_img_bytes(int N, int L, int vb)
 {
     return (size_t)(N + (N - L)) * kSubDS * vb;
 }
+// One low layer in LDS at a time (TSPGPU_SUB_ONE_LAYER): a middle pass loads
+// its rows' values into registers, the workgroup passes a barrier, and the
+// next layer is written over the one just read — the region is the largest
+// layer, C(10,5) x 5 = 1260 values (10 KB), instead of two adjacent layers
+// (20 KB), so the block's LDS drops from 24.5 to 14.5 KB and occupancy is set
+// by registers alone.
+#ifndef TSPGPU_SUB_ONE_LAYER
+#define TSPGPU_SUB_ONE_LAYER 0  // measured 5% slower (the extra barrier), profiles/r03/k1_ab_table.log run 8
+#endif
+__host__ __device__ constexpr int sub_region_vals(int L)
+{
+    if (!TSPGPU_SUB_ONE_LAYER) return tiled_region_vals(L);
+    int m = 0;
+    for (int j = 0; j <= L; ++j) m = tiled_layer_vals(L, j) > m ? tiled_layer_vals(L, j) : m;
+    return m;
+}
+// where layer j starts in the region
+__host__ __device__ constexpr int sub_layer_off(int L, int j)
+{
+    return (!TSPGPU_SUB_ONE_LAYER && (j & 1)) ? tiled_region_vals(L) - tiled_layer_vals(L, j) : 0;
+}
 __host__ __device__ constexpr size_t sub_lds_bytes(int N, int L, int vb)
 {
-    return sub_img_bytes(N, L, vb) + (size_t)2 * 16 * vb + (size_t)tiled_region_vals(L) * vb + (size_t)16 * vb;
+    return sub_img_bytes(N, L, vb) + (size_t)2 * 16 * vb + (size_t)sub_region_vals(L) * vb + (size_t)16 * vb;
 }
 
 template <typename V, int N, int L>
@@ -262,9 +283,8 @@ __device__ __forceinline__ void sub_mid(const SubCtx<V, N, L> &c, uint32_t h, ui
     constexpr int ROWS = cbinom(L, J);
     constexpr int BASE = tiled_moff(L, J);
     constexpr int ROWS_N = cbinom(L, J + 1);
-    constexpr int REGV = tiled_region_vals(L);
-    constexpr int CUR = (J & 1) ? REGV - ROWS * J : 0;
-    constexpr int NXT = ((J + 1) & 1) ? REGV - ROWS_N * (J + 1) : 0;
+    constexpr int CUR = sub_layer_off(L, J);
+    constexpr int NXT = sub_layer_off(L, J + 1);
     constexpr bool ARG = T >= N - TSPGPU_TILED_TA_OFF;
     constexpr uint32_t DSB = (uint32_t)(kSubDS * VB);
     constexpr uint32_t HR0 = (uint32_t)N * DSB;  // image row N: the first sub-cube-ordered high row
@@ -290,12 +310,16 @@ __device__ __forceinline__ void sub_mid(const SubCtx<V, N, L> &c, uint32_t h, ui
     for (int i = 0; i < HC; ++i)
 #pragma unroll
         for (int u = 0; u < QH; ++u) hh[i * QH + u] = uniform_val<V>(c.img, HR0 + i * DSB + HC0 + u * VB);
-    if (tid >= (uint32_t)ROWS) return;
     const uint32_t r = tid;
-    const uint32_t voff = (BASE + r) * VB;  // the row's offset in a push column
+    const bool act = r < (uint32_t)ROWS;
     V g[T];
 #pragma unroll
-    for (int p = 0; p < J; ++p) g[p] = c.region[CUR + p * ROWS + r];
+    for (int p = 0; p < J; ++p) g[p] = act ? c.region[CUR + p * ROWS + r] : V(0);
+    // (one layer in LDS: every wave has its row's values before any of the
+    // next layer overwrites them)
+    if (TSPGPU_SUB_ONE_LAYER) lds_barrier();
+    if (!act) return;
+    const uint32_t voff = (BASE + r) * VB;  // the row's offset in a push column
 #pragma unroll
     for (int i = 0; i < HC; ++i) g[J + i] = c.push.load(voff, (h * H + hm[i]) * (uint32_t)(NL * VB));
     uint32_t mrow[J], kof[QL];
@@ -530,8 +554,8 @@ __device__ __forceinline__ void sub_penult(const SubCtx<V, N, L> &c, uint32_t h,
     constexpr int QP = pow2_at_least(Q);
     constexpr int NL = 1 << L, VB = sizeof(V);
     constexpr uint32_t DSB = (uint32_t)(kSubDS * VB);
-    constexpr int ROWS = L, BASE = tiled_moff(L, J), REGV = tiled_region_vals(L);
-    constexpr int CUR = (J & 1) ? REGV - ROWS * J : 0;
+    constexpr int ROWS = L, BASE = tiled_moff(L, J);
+    constexpr int CUR = sub_layer_off(L, J);
     if (tid >= (uint32_t)(L * QP)) return;
     uint32_t hm[C > 0 ? C : 1];
     {
@@ -689,7 +713,7 @@ __global__ __launch_bounds__(THREADS, tiled_waves(THREADS, sub_wg(WG))) void hk_
     V *dc = d0 + 16;
     c.d0 = d0;
     c.region = dc + 16;
-    c.layerL = c.region + tiled_region_vals(L);
+    c.layerL = c.region + sub_region_vals(L);
     const uint32_t tid = threadIdx.x;
     const uint4 *rowtab = reinterpret_cast<const uint4 *>(rows);
 
