@@ -38,5 +38,6 @@ for s in ${STEPS:-time16 tests}; do
     bench) step bench 600 python3 -u bench.py --steps 20 --warmup 3 ;;
     benchk2) step bench_k2 300 python3 -u bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-ref-multiblock --no-tto ;;
     bench2) step bench_2ranks 300 python3 -u bench.py --gpus 2 --steps 10 --warmup 2 --no-k2 ;;
+    bench4) step bench_4ranks 400 python3 -u bench.py --gpus 4 --steps 5 --warmup 1 --no-k2 --no-tto ;;
     esac
 done
