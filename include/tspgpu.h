@@ -203,7 +203,24 @@ typedef struct
     uint64_t lane_steps;    /* lane slots of the search loop (64 per wave step) */
     uint64_t active_steps;  /* ... of which a lane worked on an item (lane utilisation = active/lane) */
     uint64_t item_loads;    /* items loaded by lanes (seeds and hand-backs) */
+    int tie;                /* 1: the tour is the device tie rule's (tspgpu_tie_tour certified it) */
+    int tie_checked;        /* 1: the records were also read and their host rule gave the same tour */
 } tspgpu_search_stats;
+
+/* Device tie rule (K2): the kernels keep, per recorded cost, the least
+ * reverse-lexicographic key (t_N most significant) of the tours offered at
+ * that cost; digit p = rank of t_(N-p) among the cities not placed yet, radix
+ * N-p, in w0 for N <= 20, else digits 0..12 in w0 and the rest in w1.  This
+ * decodes the key of the optimum's slot into tour_out (n+1 entries) and
+ * certifies it as tsp()'s tour (tsp.cpp:457-470, 484-499): its fold must equal
+ * cost_bits and, for f64, no fold one ulp below any of its prefixes may round
+ * to the same next prefix (then every prefix fold is minimal and the DP's
+ * backward argmin chain picks exactly this tour).  0: certified; -EAGAIN:
+ * valid but not certified (use the records); -EINVAL: not a tour of that cost. */
+int tspgpu_tie_tour(const void *dist, int dtype, int n, uint64_t w0, uint64_t w1, uint64_t cost_bits,
+                    int32_t *tour_out);
+/* the key of a tour (tour[0] = 0, tour[1..n-1] = t1..tN): test helper */
+int tspgpu_tie_key(int n, const int32_t *tour, uint64_t *w0, uint64_t *w1);
 
 typedef struct tspgpu_search tspgpu_search; /* one instance (or one shard of it) on one context */
 

@@ -250,10 +250,17 @@ def test_solve_sharded_single_process(gpu_ctx):
     assert st4["exchange_every"] == 4 and 1 <= st4["exchanges"] <= st4["rounds"] // 4 + 1
 
 
-def test_overflow_falls_back_to_second_phase(gpu_ctx):
+def test_overflow_falls_back_to_second_phase(gpu_ctx, monkeypatch):
     """All-equal distances: every tour is optimal.  7! = 5040 fit the record
-    buffer; 9! = 362880 at n = 10 do not, so the search runs a second phase
-    with the optimum as the bound and a buffer of the needed size."""
+    buffer; 9! = 362880 at n = 10 do not, so (device tie rule off) the search
+    runs a second phase with the optimum as the bound and a buffer of the
+    needed size.  With the device tie rule on, one phase answers it."""
+    d = np.full((10, 10), 7, dtype=np.int32)
+    np.fill_diagonal(d, 0)
+    cost, tour, st = tspgpu.search_solve(gpu_ctx, d)
+    oc, ot = O.solve_block(d.astype(np.float64))
+    assert cost == int(oc) and tour.tolist() == ot and st["phases"] == 1 and st["tie"] == 1, st
+    monkeypatch.setenv("TSPGPU_SEARCH_TIE", "0")
     d = np.full((8, 8), 7, dtype=np.int32)
     np.fill_diagonal(d, 0)
     cost, tour, st = tspgpu.search_solve(gpu_ctx, d)  # 7! = 5040 optimal tours: fits
@@ -273,14 +280,73 @@ def test_forced_second_phase_and_k1_fallback(gpu_ctx, monkeypatch):
     xy = rng.integers(0, 3, size=(11, 2)).astype(np.float64)
     d = O.distance_matrix([(i, xy[i, 0], xy[i, 1]) for i in range(11)])
     monkeypatch.setenv("TSPGPU_SEARCH_RECORD_CAP", "2")
+    cost, tour, st = tspgpu.search_solve(gpu_ctx, d)  # device tie rule: one phase
+    oc, ot = O.solve_block(d)
+    assert (cost, tour.tolist()) == (oc, ot) and st["phases"] == 1 and st["tie"] == 1, st
+    monkeypatch.setenv("TSPGPU_SEARCH_TIE", "0")
     cost, tour, st = tspgpu.search_solve(gpu_ctx, d)
     monkeypatch.delenv("TSPGPU_SEARCH_RECORD_CAP")
-    oc, ot = O.solve_block(d)
     assert (cost, tour.tolist()) == (oc, ot) and st["phases"] == 2, st
     d = np.zeros((13, 13))
     cost, tour, st = tspgpu.search_solve(gpu_ctx, d)
     oc, ot = O.solve_block(d)
     assert (cost, tour.tolist()) == (oc, ot) and st["fallback"] == 1, st
+
+
+def test_coincident_cities_device_tie_rule(gpu_ctx):
+    """12! optimal tours (13 coincident cities): the device tie rule answers in
+    one phase, with neither a second search nor the K1-wide fallback."""
+    d = np.zeros((13, 13))
+    cost, tour, st = tspgpu.search_solve(gpu_ctx, d)
+    oc, ot = O.solve_block(d)
+    assert (cost, tour.tolist()) == (oc, ot), st
+    assert st["phases"] == 1 and st["fallback"] == 0 and st["tie"] == 1, st
+
+
+@pytest.mark.parametrize("n", [9, 12, 14, 17])
+def test_device_tie_rule_agrees_with_records(gpu_ctx, monkeypatch, n):
+    """Tie-heavy lattices and uniform cities.  Default: the records decide and
+    the device answer, when certified cheaply, must agree (tie_checked != -1).
+    With a 2-record buffer (as in a tie storm) the device tie rule decides in
+    one phase (certified with the prefix DP) and gives the same tour — tsp()'s
+    (oracle) up to 16 cities, the records' rule at 17."""
+    rng = np.random.default_rng(77 + n)
+    used = 0
+    for k in range(6):
+        if k % 3 == 2:
+            xy = rng.uniform(0, 1000, size=(n, 2))
+        else:
+            xy = rng.integers(0, 3 + k, size=(n, 2)).astype(np.float64)
+        d = O.distance_matrix([(i, xy[i, 0], xy[i, 1]) for i in range(n)])
+        cost, tour, st = tspgpu.search_solve(gpu_ctx, d)
+        assert st["tie_checked"] != -1, st
+        if n <= 16:
+            oc, ot = O.solve_block(d)
+            assert (cost, tour.tolist()) == (oc, ot), (k, st)
+        monkeypatch.setenv("TSPGPU_SEARCH_RECORD_CAP", "2")
+        c2, t2, s2 = tspgpu.search_solve(gpu_ctx, d)
+        monkeypatch.delenv("TSPGPU_SEARCH_RECORD_CAP")
+        assert (c2, t2.tolist()) == (cost, tour.tolist()), (k, s2)
+        if s2["tie"]:
+            assert s2["phases"] == 1 and s2["fallback"] == 0, s2
+        used += s2["tie"]
+    assert used >= 5
+
+
+@pytest.mark.parametrize("n", [22, 26])
+def test_device_tie_rule_two_word_keys(gpu_ctx, monkeypatch, n):
+    """Above 21 cities the key takes two words (the slot's locked pair): the
+    device answer equals the records' rule on symmetric instances (two optimal
+    orientations at least) and on a small lattice (many ties)."""
+    rng = np.random.default_rng(5 * n)
+    for k in range(3):
+        xy = rng.uniform(0, 1000, size=(n, 2)) if k == 0 else rng.integers(0, 6, size=(n, 2)).astype(np.float64)
+        d = O.distance_matrix([(i, xy[i, 0], xy[i, 1]) for i in range(n)])
+        monkeypatch.delenv("TSPGPU_SEARCH_TIE", raising=False)
+        c1, t1, s1 = tspgpu.search_solve(gpu_ctx, d)
+        monkeypatch.setenv("TSPGPU_SEARCH_TIE", "0")
+        c0, t0, s0 = tspgpu.search_solve(gpu_ctx, d)
+        assert c1 == c0 and t1.tolist() == t0.tolist() and s1["tie_checked"] != -1, (k, s1, s0)
 
 
 @pytest.mark.parametrize("n", [3, 4, 6, 8, 10, 11])

@@ -157,3 +157,83 @@ def test_search_validation():
     big = np.full((5, 5), 1 << 28, dtype=np.int32)
     with pytest.raises(tspgpu.TspGpuError):
         tspgpu.heuristic_tour(big)                       # n * max(d) >= 2^30
+
+
+# --- device tie rule, host half (tspgpu_tie_key / tspgpu_tie_tour) ----------
+
+def rev_lex(t):
+    """tsp()'s tie order among DP-consistent optimal tours: t_N first."""
+    return tuple(reversed(t))
+
+
+@pytest.mark.parametrize("n", [3, 5, 8, 13, 21, 22, 27, 32])
+def test_tie_key_orders_reverse_lex_and_round_trips(n):
+    """The key is order-isomorphic to reverse-lex order (one u64 up to 20 inner
+    cities, a (w0, w1) pair above) and decodes back to the tour."""
+    rng = np.random.default_rng(40 + n)
+    d = np.ones((n, n))
+    np.fill_diagonal(d, 0)
+    tours = [rng.permutation(np.arange(1, n)).tolist() for _ in range(60)]
+    if n > 3:  # neighbours in reverse-lex order: one swap near the front
+        tours += [t[:1] + t[1:2][::-1] + t[2:] for t in tours[:10]]
+        tours += [[t[1], t[0]] + t[2:] for t in tours[:10]]
+    keys = {}
+    for t in tours:
+        full = [0] + t + [0]
+        k = tspgpu.tie_key(full)
+        keys[tuple(t)] = k
+        if n - 1 <= 20:
+            assert k[1] == 0
+        rc, back = tspgpu.tie_tour(d, k[0], k[1], float(n))
+        assert rc == 0 and back.tolist() == full  # all-ones: every fold exact
+    order_key = sorted(keys, key=lambda t: keys[t])
+    order_rl = sorted(keys, key=rev_lex)
+    assert order_key == order_rl
+
+
+@pytest.mark.parametrize("n", [4, 5, 6, 7, 8])
+def test_tie_rule_least_key_is_tsp_tour(n):
+    """The least key among the optimal tours, once certified, is exactly the
+    tour tsp() returns (random, lattice and collinear instances: heavy ties);
+    the certificate must hold on most of them."""
+    rng = np.random.default_rng(700 + n)
+    certified = total = 0
+    for d in instances(rng, n, 24 if n <= 7 else 8):
+        opt, oset = optimal_set(d)
+        best = min(oset, key=lambda p: tspgpu.tie_key([0, *p, 0]))
+        assert best == min(oset, key=rev_lex)
+        w0, w1 = tspgpu.tie_key([0, *best, 0])
+        rc, tour = tspgpu.tie_tour(d, w0, w1, opt)
+        total += 1
+        if rc == 0:
+            certified += 1
+            assert tour.tolist() == O.solve_block(d)[1], (n, len(oset))
+        else:
+            assert rc == -11  # -EAGAIN: the records decide
+    assert certified == total  # (the prefix DP proves the cases the one-ulp test cannot)
+
+
+@pytest.mark.parametrize("n", [4, 6, 8])
+def test_tie_rule_integer_costs_always_certified(n):
+    rng = np.random.default_rng(990 + n)
+    for k in range(12 if n < 8 else 4):
+        m = rng.integers(1, 6, size=(n, n)).astype(np.int32)
+        if k % 2 == 0:
+            m = np.minimum(m, m.T)
+        np.fill_diagonal(m, 0)
+        opt, oset = optimal_set(m)
+        best = min(oset, key=rev_lex)
+        w0, w1 = tspgpu.tie_key([0, *best, 0])
+        rc, tour = tspgpu.tie_tour(m, w0, w1, int(opt))
+        assert rc == 0 and tour.tolist() == O.solve_block(m.astype(np.float64))[1]
+
+
+def test_tie_tour_rejects_wrong_cost_and_bad_keys():
+    rng = np.random.default_rng(8)
+    d = next(instances(rng, 7, 1))
+    opt, oset = optimal_set(d)
+    w0, w1 = tspgpu.tie_key([0, *oset[0], 0])
+    assert tspgpu.tie_tour(d, w0, w1, opt * 2)[0] == -22      # -EINVAL: not that cost
+    assert tspgpu.tie_tour(d, 10 ** 9, 0, opt)[0] == -22      # digits out of range
+    with pytest.raises(tspgpu.TspGpuError):
+        tspgpu.tie_key([0, 1, 1, 2, 0])                       # not a permutation

@@ -94,6 +94,7 @@ __global__ __launch_bounds__(256) void enum_kernel(SearchArgs a)
     __syncthreads();
 
     unsigned long long lanes = 0;  // wave-uniform
+    TieCache tcache;
     const uint32_t stride = gridDim.x * blockDim.x;
     for (uint32_t base = blockIdx.x * blockDim.x; base < a.items; base += stride) {
         const uint32_t idx = base + threadIdx.x;
@@ -182,6 +183,14 @@ __global__ __launch_bounds__(256) void enum_kernel(SearchArgs a)
 #pragma unroll
                             for (int l = 0; l < kTail; ++l) R->city[G + l] = (uint8_t)ord[l];
                         }
+                        tie_offer(a, tcache, tb, [&](int q) {
+                            int v = 0;  // (static indices: the arrays stay in registers)
+#pragma unroll
+                            for (int l = 0; l < G; ++l) v = q == l + 1 ? pc[l] : v;
+#pragma unroll
+                            for (int l = 0; l < kTail; ++l) v = q == G + 1 + l ? ord[l] : v;
+                            return v;
+                        });
                     }
                     const V o = ENum<V>::val(old);
                     inc = o < total ? o : total;
@@ -298,7 +307,7 @@ __device__ __forceinline__ void fold_path(const V *dl, const uint32_t (&w)[8], i
 // TL! completions; `act` false = a lane with nothing to do (wave-uniform code).
 template <typename V, int TL>
 __device__ __forceinline__ void tail_one(const SearchArgs &a, const V *dl, const V *am, uint32_t full, uint32_t idx,
-                                         bool act, unsigned long long &lanes)
+                                         bool act, unsigned long long &lanes, TieCache &tcache)
 {
     uint32_t w[8];
     load_path(a.ftail + idx, act, w);
@@ -408,6 +417,13 @@ __device__ __forceinline__ void tail_one(const SearchArgs &a, const V *dl, const
 #pragma unroll
                             for (int l = 0; l < TL; ++l) R->city[olen - 1 + l] = (uint8_t)ord[l];
                         }
+                        const uint8_t *pb = a.ftail[oidx].b;
+                        tie_offer(a, tcache, tb, [&](int q) {
+                            int v = 0;
+#pragma unroll
+                            for (int l = 0; l < TL; ++l) v = q == olen + l ? ord[l] : v;
+                            return q < olen ? (int)pb[q] : v;
+                        });
                     }
                 }
             }
@@ -438,6 +454,7 @@ __global__ __launch_bounds__(256) void tail_kernel(SearchArgs a)
     uint32_t *q = wq[threadIdx.x >> 6];
     uint32_t qn = 0;               // wave-uniform: live slots queued
     unsigned long long lanes = 0;  // wave-uniform
+    TieCache tcache;
     const uint32_t wave = blockIdx.x * 4 + (threadIdx.x >> 6), waves = gridDim.x * 4;
     for (uint32_t base = wave * 64u;; base += waves * 64u) {
         const bool more = base < count;
@@ -457,7 +474,7 @@ __global__ __launch_bounds__(256) void tail_kernel(SearchArgs a)
             const uint32_t idx = act ? q[qn - take + lane] : 0u;
             __builtin_amdgcn_wave_barrier();
             qn -= take;
-            tail_one<V, TL>(a, dl, am, full, idx, act, lanes);
+            tail_one<V, TL>(a, dl, am, full, idx, act, lanes, tcache);
         }
         if (!more) break;
     }

@@ -138,8 +138,113 @@ struct SearchArgs {
     const double *hsuf;
     int hs_len;
     uint32_t hs_off[8];
+    // device tie rule (TieSlot below; null: records only)
+    struct TieSlot *tie;
+    uint32_t tie_mask;         // slots - 1 (power of two)
+    unsigned int *tie_overflow;
     hipStream_t stream;
 };
+
+// ---------------------------------------------------------------------------
+// Device tie rule.  tsp() returns, among the optimal tours, the one its
+// backward argmin chain picks (tsp.cpp:457-470 first strict minimum over the
+// members ascending, tsp.cpp:484-499 the same at the closing step).  Every
+// tour that chain can pick has all its prefix folds minimal ("DP-consistent"),
+// and among those it is the least in reverse-lexicographic order (t_N first,
+// then t_(N-1), ...).  The kernels therefore keep, per recorded cost, the
+// reverse-lex least tour offered at that cost — a two-level MIN: the slot of
+// the cost (claimed by CAS), then the key (atomicMin).  The host certifies the
+// winner of the optimum's slot as DP-consistent (exact for integer costs; for
+// f64 a per-step rounding test, search_host.cpp tie_certify) and otherwise
+// falls back to the record set.
+//
+// Key: digit p (p = 0..N-1) = rank of t_(N-p) among the cities not placed
+// yet, radix N - p; for N <= 20 all digits fit one word (N! < 2^64), else
+// digits 0..12 go to w0 and 13..N-1 to w1 (31!/18! and 18! < 2^64).
+struct TieSlot {
+    unsigned long long cost;  // kTieEmpty: free
+    unsigned long long w0;    // least first word offered at this cost
+    unsigned long long lw0;   // (two-word keys) least (w0, w1) pair, under `lock`
+    unsigned long long lw1;
+    unsigned int lock;        // kTieFree: unlocked
+    unsigned int pad[3];
+};
+constexpr unsigned long long kTieEmpty = ~0ull;  // (never a cost: f64 NaN bits / > any u32 cost)
+constexpr unsigned int kTieFree = ~0u;
+constexpr int kTieSplit = 13;  // digits in w0 when N > 20
+constexpr uint32_t kTieSlots = 1024;
+constexpr int kTieProbe = 32;
+
+__host__ __device__ constexpr int tie_split(int N) { return N <= 20 ? N : kTieSplit; }
+
+// the key of the tour t_1..t_N, city(i) = t_i
+template <typename F>
+__device__ __forceinline__ void tie_key(int N, F city, unsigned long long &w0, unsigned long long &w1)
+{
+    const int split = tie_split(N);
+    uint32_t unused = (uint32_t)(((1ull << N) - 1ull) << 1);  // cities 1..N
+    w0 = 0;
+    w1 = 0;
+    for (int p = 0; p < N; ++p) {
+        const int c = city(N - p);
+        const unsigned long long dig = (unsigned long long)__builtin_popcount(unused & ((1u << c) - 1u));
+        unused &= ~(1u << c);
+        if (p < split)
+            w0 = w0 * (unsigned long long)(N - p) + dig;
+        else
+            w1 = w1 * (unsigned long long)(N - p) + dig;
+    }
+}
+
+// Per-lane filter of repeated offers at one cost: the last slot minimum seen.
+struct TieCache {
+    unsigned long long cost = kTieEmpty, w0 = kTieEmpty;
+};
+
+// Offer a recorded tour (cost bits tb, tb <= the incumbent when it was found).
+template <typename F>
+__device__ __forceinline__ void tie_offer(const SearchArgs &a, TieCache &tc, unsigned long long tb, F city)
+{
+    if (!a.tie) return;
+    const int N = a.n - 1;
+    unsigned long long w0, w1;
+    tie_key(N, city, w0, w1);
+    const bool two = N > 20;
+    if (tb == tc.cost && (two ? w0 > tc.w0 : w0 >= tc.w0)) return;  // a better key holds this slot already
+    const uint32_t h = (uint32_t)((tb ^ (tb >> 31)) * 0x9E3779B97F4A7C15ull >> 40);
+    TieSlot *e = nullptr;
+    for (int i = 0; i < kTieProbe; ++i) {
+        TieSlot *s = a.tie + ((h + (uint32_t)i) & a.tie_mask);
+        const unsigned long long old = atomicCAS(&s->cost, kTieEmpty, tb);
+        if (old == kTieEmpty || old == tb) {
+            e = s;
+            break;
+        }
+    }
+    if (!e) {
+        atomicOr(a.tie_overflow, 1u);
+        return;
+    }
+    const unsigned long long o0 = atomicMin(&e->w0, w0);
+    tc.cost = tb;
+    tc.w0 = o0 < w0 ? o0 : w0;
+    if (!two || w0 > o0) return;
+    // second word: the (w0, w1) pair under the slot's lock; the lanes of a
+    // wave take it in turn (each releases it in the iteration that took it)
+    bool pending = true;
+    while (pending) {
+        if (atomicCAS(&e->lock, kTieFree, 0u) == kTieFree) {
+            const unsigned long long c0 = __hip_atomic_load(&e->lw0, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+            const unsigned long long c1 = __hip_atomic_load(&e->lw1, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+            if (w0 < c0 || (w0 == c0 && w1 < c1)) {
+                __hip_atomic_store(&e->lw0, w0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(&e->lw1, w1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            __hip_atomic_store(&e->lock, kTieFree, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+            pending = false;
+        }
+    }
+}
 
 constexpr int kStatLines = 64, kStatStride = 16;
 __device__ __forceinline__ unsigned long long *stat_line(const SearchArgs &a)
@@ -158,6 +263,8 @@ hipError_t launch_to_paths(const SearchArgs &a);  // a.in (seeds) -> a.fout
 hipError_t launch_expand(const SearchArgs &a, bool f64);
 hipError_t launch_tail(const SearchArgs &a, bool f64, int grid);
 hipError_t launch_persist(const SearchArgs &a, bool f64, int grid);
+// the optimum's tie slot -> out[0..4] (search.hip tie_lookup_kernel)
+hipError_t launch_tie_lookup(const SearchArgs &a, unsigned long long *out);
 // suffix table (enum.hip): size a.hs_len of a.hsuf, one thread per set
 hipError_t launch_suffix(const SearchArgs &a, bool f64, uint32_t sets);
 // seeds (seed_grid blocks) and the suffix table in one launch (enum.hip)

@@ -103,6 +103,7 @@ __global__ __launch_bounds__(kSearchThreads) void round_kernel_v1(SearchArgs a)
     for (int x = 0; x < n; ++x) aall += (W)al[x];                // exact: grid values
     V inc = Num<V>::val(__hip_atomic_load(a.inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
     unsigned long long nodes = 0;
+    TieCache tcache;
     int L = -1;          // current depth; < root: the lane needs an item
     int root = 0;        // depth of the item's last fixed city
     int k = 0;           // city at depth L
@@ -262,6 +263,7 @@ __global__ __launch_bounds__(kSearchThreads) void round_kernel_v1(SearchArgs a)
                         for (int l = 1; l <= L; ++l) R->city[l - 1] = CITY(l);
                         R->city[L] = (uint8_t)j;
                     }
+                    tie_offer(a, tcache, tb, [&](int i) { return i <= L ? (int)CITY(i) : j; });
                 }
                 const V o = Num<V>::val(old);
                 inc = o < total ? o : total;
@@ -363,7 +365,8 @@ __host__ __device__ constexpr size_t v2_lds(int n)
 // Returns the mask of first-city slots evaluated (16 nodes each).
 template <typename V>
 __device__ __forceinline__ uint32_t tail4(const V *dl, const APair<V> *ad, const uint8_t *myk, int T, int krow, V ck,
-                                          uint32_t rem, uint32_t fm, int L, V &inc, V &thr, const SearchArgs &a)
+                                          uint32_t rem, uint32_t fm, int L, V &inc, V &thr, const SearchArgs &a,
+                                          TieCache &tcache)
 {
     int c[4];
     uint32_t x = rem;
@@ -432,6 +435,9 @@ __device__ __forceinline__ uint32_t tail4(const V *dl, const APair<V> *ad, const
                                 R->city[L + 2] = (uint8_t)c[l];
                                 R->city[L + 3] = (uint8_t)c[m];
                             }
+                            tie_offer(a, tcache, tb, [&](int q) {
+                                return q <= L ? (int)myk[q * T] : (q == L + 1 ? c[i] : q == L + 2 ? c[j] : q == L + 3 ? c[l] : c[m]);
+                            });
                         }
                         const V o = Num<V>::val(old);
                         inc = o < total ? o : total;
@@ -476,6 +482,7 @@ __global__ __launch_bounds__(kSearchThreads) void round_kernel(SearchArgs a)
     V inc = Num<V>::val(__hip_atomic_load(a.inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
     V thr = Thr<V>::of(inc);
     unsigned long long nodes = 0;  // wave-uniform counts
+    TieCache tcache;
     unsigned long long wsteps = 0, wactive = 0, wloads = 0;
     int L = -1, root = 1;          // L < root: the lane needs an item
     int k = 0, krow = 0;           // path end and its row offset in d
@@ -529,7 +536,7 @@ __global__ __launch_bounds__(kSearchThreads) void round_kernel(SearchArgs a)
         const bool tail = a.tails && act && __builtin_popcount(rem) == 4;
         if (__ballot(tail)) {
             uint32_t valid = 0;
-            if (tail) valid = tail4<V>(dl, ad, myk, T, krow, ck, rem, fm, L, inc, thr, a);
+            if (tail) valid = tail4<V>(dl, ad, myk, T, krow, ck, rem, fm, L, inc, thr, a, tcache);
             nodes += 16ull * (unsigned long long)(__popcll(__ballot(valid & 1u)) + __popcll(__ballot(valid & 2u)) +
                                                   __popcll(__ballot(valid & 4u)) + __popcll(__ballot(valid & 8u)));
         }
@@ -565,6 +572,7 @@ __global__ __launch_bounds__(kSearchThreads) void round_kernel(SearchArgs a)
                     R->city[L] = (uint8_t)j;
                     if (sc) R->city[L + 1] = (uint8_t)r;
                 }
+                tie_offer(a, tcache, tb, [&](int q) { return q <= L ? (int)myk[q * T] : (q == L + 1 ? j : r); });
             }
             const V o = Num<V>::val(old);
             inc = o < total ? o : total;
@@ -795,6 +803,7 @@ __global__ __launch_bounds__(kSearchThreads) void persist_kernel(SearchArgs a)
     uint32_t tick = 0, idle = 0;
     bool seeds_left = true, hungry = false;
     unsigned long long nodes = 0, wsteps = 0, wactive = 0, wloads = 0, wfin = 0;
+    TieCache tcache;
 
     auto start = [&](int len, int prev, V c, uint32_t rr, V ra, uint32_t from) {
         root = len - 1;
@@ -892,6 +901,7 @@ __global__ __launch_bounds__(kSearchThreads) void persist_kernel(SearchArgs a)
                     R->city[L] = (uint8_t)j;
                     if (sc) R->city[L + 1] = (uint8_t)r;
                 }
+                tie_offer(a, tcache, tb, [&](int q) { return q <= L ? (int)myk[q * T] : (q == L + 1 ? j : r); });
             }
             const V o = Num<V>::val(old);
             inc = o < total ? o : total;
@@ -1097,7 +1107,35 @@ __global__ __launch_bounds__(kSearchThreads) void persist_kernel(SearchArgs a)
     }
 }
 
+// The optimum's tie slot: out[0] = 1 if a slot holds cost *a.inc, out[1] =
+// its w0, out[2..3] = its (lw0, lw1), out[4] = the overflow flag.  One wave.
+__global__ __launch_bounds__(64) void tie_lookup_kernel(SearchArgs a, unsigned long long *out)
+{
+    const unsigned long long opt = __hip_atomic_load(a.inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int lane = (int)threadIdx.x;
+    if (lane == 0) {
+        out[0] = 0;
+        out[4] = *a.tie_overflow;
+    }
+    __syncthreads();
+    for (uint32_t i = (uint32_t)lane; i <= a.tie_mask; i += 64) {
+        const TieSlot &e = a.tie[i];
+        if (e.cost == opt) {
+            out[0] = 1;
+            out[1] = e.w0;
+            out[2] = e.lw0;
+            out[3] = e.lw1;
+        }
+    }
+}
+
 }  // namespace
+
+hipError_t launch_tie_lookup(const SearchArgs &a, unsigned long long *out)
+{
+    hipLaunchKernelGGL(tie_lookup_kernel, dim3(1), dim3(64), 0, a.stream, a, out);
+    return hipGetLastError();
+}
 
 size_t search_lds_bytes(int n, bool f64, int kernel)
 {

@@ -136,6 +136,10 @@ struct tspgpu_search {
     // pinned host copy of the statistics lines + 8 counter words (one DMA
     // pair and one synchronisation per counters read)
     unsigned long long *h_stats = nullptr;
+    // device tie rule (search.h): kTieSlots slots, then 8 words: [0..4] the
+    // optimum's slot (tie_lookup_kernel), [5] the overflow flag
+    TieSlot *d_tie = nullptr;
+    bool tie_on = true;  // TSPGPU_SEARCH_TIE=0: records and the host rule only
 };
 
 namespace {
@@ -178,6 +182,7 @@ struct SearchPool {
     double *d_mst = nullptr;
     double *d_hsuf = nullptr;
     size_t hsuf_alloc = 0;
+    TieSlot *d_tie = nullptr;
 };
 
 template <typename A, typename B>
@@ -210,6 +215,7 @@ void move_buffers(A &to, B &from)
     to.d_mst = from.d_mst, from.d_mst = nullptr;
     to.d_hsuf = from.d_hsuf, from.d_hsuf = nullptr;
     to.hsuf_alloc = from.hsuf_alloc, from.hsuf_alloc = 0;
+    to.d_tie = from.d_tie, from.d_tie = nullptr;
 }
 
 template <typename A>
@@ -236,6 +242,7 @@ void free_buffers(A &b)
     if (b.d_bnd2) (void)hipFree(b.d_bnd2);
     if (b.d_mst) (void)hipFree(b.d_mst);
     if (b.d_hsuf) (void)hipFree(b.d_hsuf);
+    if (b.d_tie) (void)hipFree(b.d_tie);
     SearchPool z;
     move_buffers(b, z);
 }
@@ -512,6 +519,12 @@ int tspgpu_search_create(tspgpu_ctx *c, const void *dist, int dtype, int n, int 
         e = hipMalloc((void **)&s->d_rec, sizeof(SearchRecord) * s->rec_cap);
         if (e == hipSuccess) s->rec_alloc = s->rec_cap;
     }
+    if (const char *ev = std::getenv("TSPGPU_SEARCH_TIE")) s->tie_on = std::atoi(ev) != 0;
+    constexpr size_t kTieBytes = sizeof(TieSlot) * kTieSlots;
+    if (e == hipSuccess && !s->d_tie) e = hipMalloc((void **)&s->d_tie, kTieBytes + 8 * sizeof(unsigned long long));
+    if (e == hipSuccess) e = hipMemsetAsync(s->d_tie, 0xFF, kTieBytes, st);
+    if (e == hipSuccess)
+        e = hipMemsetAsync(reinterpret_cast<char *>(s->d_tie) + kTieBytes, 0, 8 * sizeof(unsigned long long), st);
     if (e == hipSuccess) e = hipMemsetAsync(s->d_stats, 0, kStatBytes, st);
     if (e == hipSuccess) e = hipMemcpyAsync(s->d_dist, dist, vb * n * n, hipMemcpyHostToDevice, st);
     if (e == hipSuccess)
@@ -535,7 +548,7 @@ int tspgpu_search_create(tspgpu_ctx *c, const void *dist, int dtype, int n, int 
     if (e == hipSuccess && !s->e1) e = hipEventCreate(&s->e1);
     if (e == hipSuccess && !s->e2) e = hipEventCreate(&s->e2);
     if (e == hipSuccess && !s->h_cnt && !std::getenv("TSPGPU_SEARCH_PAGEABLE"))
-        e = hipHostMalloc((void **)&s->h_cnt, 8 * sizeof(unsigned long long), hipHostMallocDefault);
+        e = hipHostMalloc((void **)&s->h_cnt, 16 * sizeof(unsigned long long), hipHostMallocDefault);
     if (e == hipSuccess && !s->h_stats && !std::getenv("TSPGPU_SEARCH_PAGEABLE"))
         e = hipHostMalloc((void **)&s->h_stats, kStatBytes + 8 * sizeof(unsigned long long), hipHostMallocDefault);
     if (e != hipSuccess) {
@@ -584,6 +597,11 @@ int tspgpu_search_set_bound(tspgpu_search *s, double bound)
     return herr(hipMemcpy(s->d_words + 1, &w, 8, hipMemcpyHostToDevice));
 }
 
+static unsigned long long *tie_words(tspgpu_search *s)
+{
+    return reinterpret_cast<unsigned long long *>(reinterpret_cast<char *>(s->d_tie) + sizeof(TieSlot) * kTieSlots);
+}
+
 static SearchArgs args_of(tspgpu_search *s)
 {
     SearchArgs a{};
@@ -621,6 +639,11 @@ static SearchArgs args_of(tspgpu_search *s)
     a.hsuf = s->d_hsuf;
     a.hs_len = s->hs_len;
     for (int i = 0; i < 8; ++i) a.hs_off[i] = s->hs_off[i];
+    if (s->tie_on) {
+        a.tie = s->d_tie;
+        a.tie_mask = kTieSlots - 1;
+        a.tie_overflow = reinterpret_cast<unsigned int *>(tie_words(s) + 5);
+    }
     a.stream = s->ctx->stream;
     return a;
 }
@@ -1268,6 +1291,17 @@ static int search_solve(tspgpu_ctx *c, const void *dist, int dtype, int n, doubl
     std::vector<SearchRecord> spec;
     bool spec_ok = false;
     if (!rc) rc = tspgpu_search_run_all(s);
+    // the device tie rule's answer: the optimum's slot, read with the counters
+    unsigned long long tie_local[5] = {};
+    unsigned long long *tie_h = s->h_cnt ? s->h_cnt + 8 : tie_local;
+    if (!rc && s->tie_on) {
+        SearchArgs a = args_of(s);
+        hipError_t e = launch_tie_lookup(a, tie_words(s));
+        if (e == hipSuccess)
+            e = hipMemcpyAsync(tie_h, tie_words(s), 5 * sizeof(unsigned long long), hipMemcpyDeviceToHost,
+                               s->ctx->stream);
+        rc = herr(e);
+    }
     if (!rc) {
         const unsigned k = std::min<unsigned>(kSpecRecs, s->rec_cap);
         spec.resize(k);
@@ -1278,10 +1312,21 @@ static int search_solve(tspgpu_ctx *c, const void *dist, int dtype, int n, doubl
         spec_ok = !rc && recs <= k;
     }
     nodes_total = nodes;
+    // device tie rule: the optimum's slot decoded and certified on the host
+    // (tspgpu_tie_tour); then neither the records nor a second search are needed
+    bool tie_done = false;
+    int tie_checked = 0;
+    std::vector<int32_t> tie_tour(n + 1, 0);
+    if (!rc && s->tie_on && tie_h[0] == 1 && tie_h[4] == 0) {
+        const bool two = n - 1 > 20;
+        if (!two || tie_h[2] == tie_h[1])
+            tie_done = tspgpu::host::tie_tour(dist, dtype, n, two ? tie_h[2] : tie_h[1], two ? tie_h[3] : 0ull, inc,
+                                              tie_tour.data(), recs > s->rec_cap) == 0;
+    }
     // the record buffer overflowed: search again with the optimum as the bound,
     // so only optimal tours are recorded, into a buffer of the size now known
     constexpr uint64_t kPhase2Cap = 1u << 22;
-    if (!rc && recs > s->rec_cap && recs <= kPhase2Cap) {
+    if (!rc && !tie_done && recs > s->rec_cap && recs <= kPhase2Cap) {
         phases = 2;
         unsigned long long w = inc;
         rc = tspgpu_search_reset_records(s, (unsigned int)recs);
@@ -1294,7 +1339,25 @@ static int search_solve(tspgpu_ctx *c, const void *dist, int dtype, int n, doubl
     }
     std::vector<tspgpu_tour_record> opt;
     int count = 0;
-    if (!rc && recs > s->rec_cap) {
+    if (!rc && tie_done) {
+        std::memcpy(tour_out, tie_tour.data(), sizeof(int32_t) * (n + 1));
+        if (dtype == TSPGPU_F64)
+            std::memcpy(cost_out, &inc, 8);
+        else
+            *cost_out = (double)(int32_t)(uint32_t)inc;
+        // the records came back with the counters: the host rule over them
+        // must give the same tour (a self-check; the records then decide)
+        if (spec_ok) {
+            for (uint64_t i = 0; i < recs; ++i)
+                if (spec[i].cost == inc) opt.push_back(reinterpret_cast<const tspgpu_tour_record &>(spec[i]));
+            count = (int)opt.size();
+            std::vector<int32_t> ht(n + 1, 0);
+            if (count > 0 && tspgpu_select_tour(dist, dtype, n, opt.data(), count, inc, ht.data()) == 0) {
+                tie_checked = ht == tie_tour ? 1 : -1;
+                if (tie_checked < 0) std::memcpy(tour_out, ht.data(), sizeof(int32_t) * (n + 1));
+            }
+        }
+    } else if (!rc && recs > s->rec_cap) {
         // |O| too large to enumerate (e.g. coincident cities): the DP itself
         // (K1-wide, also on the GPU) gives tsp()'s tour directly for n <= 31
         if (n <= TSPGPU_WIDE_MAX_CITIES) {
@@ -1338,6 +1401,8 @@ static int search_solve(tspgpu_ctx *c, const void *dist, int dtype, int n, doubl
         stats->lane_steps = u[1];
         stats->active_steps = u[2];
         stats->item_loads = u[3];
+        stats->tie = tie_done && tie_checked >= 0 ? 1 : 0;
+        stats->tie_checked = tie_checked;
     }
     tspgpu_search_destroy(s);
     return rc;

@@ -9,6 +9,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <thread>
+#include <type_traits>
 #include <vector>
 
 #include "tspgpu.h"
@@ -376,6 +377,120 @@ int select_tour(const V *d, int n, const tspgpu_tour_record *rec, int count, V o
     return 0;
 }
 
+// Device tie rule, host side (search.h "Device tie rule"): key <-> tour and
+// the certificate that the decoded tour is the one tsp()'s argmin chain picks.
+int tie_split(int N) { return N <= 20 ? N : 13; }
+
+void tie_key(int N, const int32_t *t /* t[1..N] */, uint64_t &w0, uint64_t &w1)
+{
+    const int split = tie_split(N);
+    uint32_t unused = (uint32_t)(((1ull << N) - 1ull) << 1);
+    w0 = w1 = 0;
+    for (int p = 0; p < N; ++p) {
+        const int c = t[N - p];
+        const uint64_t dig = (uint64_t)__builtin_popcount(unused & ((1u << c) - 1u));
+        unused &= ~(1u << c);
+        if (p < split)
+            w0 = w0 * (uint64_t)(N - p) + dig;
+        else
+            w1 = w1 * (uint64_t)(N - p) + dig;
+    }
+}
+
+// digits of the key -> t[1..N]; false if a digit is out of range
+bool tie_decode(int N, uint64_t w0, uint64_t w1, int32_t *t)
+{
+    const int split = tie_split(N);
+    std::vector<uint64_t> dig(N);
+    for (int p = N - 1; p >= 0; --p) {
+        uint64_t &w = p < split ? w0 : w1;
+        const uint64_t r = (uint64_t)(N - p);
+        dig[p] = w % r;
+        w /= r;
+    }
+    if (w0 != 0 || w1 != 0) return false;
+    std::vector<int> left;
+    for (int c = 1; c <= N; ++c) left.push_back(c);
+    for (int p = 0; p < N; ++p) {
+        t[N - p] = left[dig[p]];
+        left.erase(left.begin() + (long)dig[p]);
+    }
+    return true;
+}
+
+// G[{t1..tj}][tj] of the reference's DP (the minimum left fold of a path from
+// city 0 over t1..tj ending at tj), by Held-Karp over those j cities
+constexpr int kTieDpMax = 16;
+double prefix_min(const double *d, int n, const int32_t *t, int j)
+{
+    const int J = j;
+    const uint32_t full = (1u << J) - 1u;
+    std::vector<double> G((size_t)J << J, INFINITY);
+    for (int a = 0; a < J; ++a) G[((size_t)1u << a) * J + a] = d[t[a + 1]];
+    for (uint32_t S = 1; S <= full; ++S)
+        for (int k = 0; k < J; ++k) {
+            if (!((S >> k) & 1u) || S == (1u << k)) continue;
+            const uint32_t P = S & ~(1u << k);
+            double best = INFINITY;
+            for (int m = 0; m < J; ++m)
+                if ((P >> m) & 1u) {
+                    const double v = G[(size_t)P * J + m] + d[t[m + 1] * n + t[k + 1]];
+                    best = v < best ? v : best;
+                }
+            G[(size_t)S * J + k] = best;
+        }
+    return G[(size_t)full * J + (J - 1)];
+}
+
+// 0: t (t[0] = 0, t[1..N]) folds to opt and every prefix fold is minimal
+// (no value one ulp lower could round to the same next fold); -EAGAIN: the
+// fold matches but that is not proven; -EINVAL: not a tour of cost opt
+template <typename V>
+int tie_certify(const V *d, int n, const int32_t *t, V opt, bool allow_dp)
+{
+    const int N = n - 1;
+    std::vector<V> F(N + 2);
+    V acc = 0;
+    int prev = 0;
+    for (int j = 1; j <= N; ++j) {
+        acc = acc + d[prev * n + t[j]];
+        F[j] = acc;
+        prev = t[j];
+    }
+    F[N + 1] = acc + d[prev * n];
+    if (!(F[N + 1] == opt)) return -EINVAL;
+    if constexpr (std::is_same<V, double>::value) {
+        // every fold exact (all distances multiples of one power of two 2^e
+        // and n * max below 2^(e+53), e.g. integer-valued or coincident
+        // cities): the arithmetic is the integers', nothing to prove
+        int emin = INT_MAX;
+        double mx = 0.0;
+        for (int i = 0; i < n * n; ++i) {
+            const double v = d[i];
+            if (v == 0.0) continue;
+            uint64_t b;
+            std::memcpy(&b, &v, 8);
+            const int be = (int)((b >> 52) & 0x7FF);
+            uint64_t m = b & ((1ull << 52) - 1ull);
+            if (be) m |= 1ull << 52;
+            const int low = (be ? be - 1075 : -1074) + __builtin_ctzll(m);
+            emin = std::min(emin, low);
+            mx = std::max(mx, v);
+        }
+        if (emin == INT_MAX || (double)n * mx < std::ldexp(1.0, emin + 53)) return 0;
+        for (int j = 2; j <= N; ++j) {
+            const double dj = j < N ? d[t[j] * n + t[j + 1]] : d[t[N] * n];
+            const volatile double below = std::nextafter(F[j], -INFINITY);
+            const volatile double next = below + dj;
+            if (next < F[j + 1]) continue;
+            // a fold just below F[j] would round to the same next fold: the
+            // prefix is proven minimal only by the DP over its own cities
+            if (!allow_dp || j > kTieDpMax || !(prefix_min(d, n, t, j) == F[j])) return -EAGAIN;
+        }
+    }
+    return 0;
+}
+
 int validate_search(const void *dist, int dtype, int n)
 {
     if (!dist || n < 3 || n > TSPGPU_SEARCH_MAX_CITIES) return -EINVAL;
@@ -400,6 +515,25 @@ int validate_search(const void *dist, int dtype, int n)
         return 0;
     }
     return -EINVAL;
+}
+
+int tie_tour(const void *dist, int dtype, int n, uint64_t w0, uint64_t w1, uint64_t cost_bits, int32_t *tour_out,
+             bool allow_dp)
+{
+    int rc = validate_search(dist, dtype, n);
+    if (rc) return rc;
+    if (!tour_out) return -EINVAL;
+    std::vector<int32_t> t(n + 1, 0);
+    if (!tie_decode(n - 1, w0, w1, t.data())) return -EINVAL;
+    if (dtype == TSPGPU_F64) {
+        double opt;
+        std::memcpy(&opt, &cost_bits, 8);
+        rc = tie_certify(static_cast<const double *>(dist), n, t.data(), opt, allow_dp);
+    } else {
+        rc = tie_certify(static_cast<const int32_t *>(dist), n, t.data(), (int32_t)(uint32_t)cost_bits, allow_dp);
+    }
+    if (rc != -EINVAL) std::memcpy(tour_out, t.data(), sizeof(int32_t) * (n + 1));
+    return rc;
 }
 
 }  // namespace host
@@ -452,6 +586,27 @@ int tspgpu_select_tour(const void *dist, int dtype, int n, const tspgpu_tour_rec
     }
     return select_tour(static_cast<const int32_t *>(dist), n, records, count, (int32_t)(uint32_t)cost_bits,
                        tour_out);
+}
+
+int tspgpu_tie_key(int n, const int32_t *tour, uint64_t *w0, uint64_t *w1)
+{
+    if (!tour || !w0 || !w1 || n < 3 || n > TSPGPU_SEARCH_MAX_CITIES) return -EINVAL;
+    uint32_t seen = 0;
+    for (int j = 1; j < n; ++j) {
+        if (tour[j] < 1 || tour[j] >= n || ((seen >> tour[j]) & 1u)) return -EINVAL;
+        seen |= 1u << tour[j];
+    }
+    uint64_t a, b;
+    tie_key(n - 1, tour, a, b);
+    *w0 = a;
+    *w1 = b;
+    return 0;
+}
+
+int tspgpu_tie_tour(const void *dist, int dtype, int n, uint64_t w0, uint64_t w1, uint64_t cost_bits,
+                    int32_t *tour_out)
+{
+    return tie_tour(dist, dtype, n, w0, w1, cost_bits, tour_out, true);
 }
 
 }  // extern "C"

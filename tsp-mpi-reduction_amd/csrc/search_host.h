@@ -18,5 +18,9 @@ int validate_search(const void *dist, int dtype, int n);
 void lagrange_pi(const std::vector<double> &D, int n, std::vector<double> &best_pi);
 // Held-Karp 1-tree weights (the tree bound of the expand kernel)
 void held_karp_pi(const std::vector<double> &D, int n, std::vector<double> &best_pi);
+// tspgpu_tie_tour; allow_dp = false skips the prefix DP of the certificate
+// (a cheap check when the records can decide anyway)
+int tie_tour(const void *dist, int dtype, int n, uint64_t w0, uint64_t w1, uint64_t cost_bits, int32_t *tour_out,
+             bool allow_dp);
 }  // namespace host
 }  // namespace tspgpu

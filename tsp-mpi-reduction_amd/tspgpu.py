@@ -32,7 +32,7 @@ EXPORTED_SYMBOLS = (
     "tspgpu_search_timing", "tspgpu_search_incumbent_device",
     "tspgpu_search_counters", "tspgpu_search_reset_records", "tspgpu_search_records", "tspgpu_heuristic_tour",
     "tspgpu_heuristic_tour_starts",
-    "tspgpu_select_tour",
+    "tspgpu_select_tour", "tspgpu_tie_tour", "tspgpu_tie_key",
     # K3
     "tspgpu_merge", "tspgpu_reduce",
     # K1-wide
@@ -55,7 +55,8 @@ class SearchStats(ctypes.Structure):
     _fields_ = [("nodes", ctypes.c_uint64), ("records", ctypes.c_uint64), ("optimal_tours", ctypes.c_uint64),
                 ("items", ctypes.c_uint64), ("depth", ctypes.c_int), ("phases", ctypes.c_int),
                 ("fallback", ctypes.c_int), ("rounds", ctypes.c_int), ("kernel_ms", ctypes.c_double),
-                ("lane_steps", ctypes.c_uint64), ("active_steps", ctypes.c_uint64), ("item_loads", ctypes.c_uint64)]
+                ("lane_steps", ctypes.c_uint64), ("active_steps", ctypes.c_uint64), ("item_loads", ctypes.c_uint64),
+                ("tie", ctypes.c_int), ("tie_checked", ctypes.c_int)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -148,6 +149,9 @@ def lib():
         L.tspgpu_heuristic_tour_starts.argtypes = [vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, dp, ip]
         L.tspgpu_select_tour.argtypes = [vp, ctypes.c_int, ctypes.c_int, ctypes.POINTER(TourRecord), ctypes.c_int,
                                          ctypes.c_uint64, ip]
+        L.tspgpu_tie_tour.argtypes = [vp, ctypes.c_int, ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
+                                      ip]
+        L.tspgpu_tie_key.argtypes = [ctypes.c_int, ip, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]
         cp = ctypes.POINTER(City)
         L.tspgpu_solve_instance.argtypes = [vp, dp, ctypes.c_int, dp, ip, dp]
         L.tspgpu_merge.argtypes = [vp, cp, ctypes.c_int, ctypes.c_double, cp, ctypes.c_int, ctypes.c_double, cp, dp]
@@ -540,6 +544,26 @@ def select_tour(dist, records, cost):
     if rc:
         raise TspGpuError(rc, "tspgpu_select_tour")
     return tour
+
+
+def tie_key(tour):
+    """The device tie rule's key (w0, w1) of a tour 0, t1..tN, 0 (tspgpu_tie_key)."""
+    t = np.ascontiguousarray(tour, dtype=np.int32)
+    w0, w1 = ctypes.c_uint64(), ctypes.c_uint64()
+    rc = lib().tspgpu_tie_key(len(t) - 1, _ip(t), ctypes.byref(w0), ctypes.byref(w1))
+    if rc:
+        raise TspGpuError(rc, "tspgpu_tie_key")
+    return w0.value, w1.value
+
+
+def tie_tour(dist, w0: int, w1: int, cost):
+    """Decode + certify a tie key (tspgpu_tie_tour): (rc, tour); rc 0 = tsp()'s
+    tour, -EAGAIN = a tour of that cost the DP may not pick."""
+    d, dt = _search_dist(dist)
+    n = d.shape[0]
+    tour = np.zeros(n + 1, dtype=np.int32)
+    rc = lib().tspgpu_tie_tour(d.ctypes.data, dt, n, w0, w1, cost_bits(cost, dt), _ip(tour))
+    return rc, tour
 
 
 class Search:
