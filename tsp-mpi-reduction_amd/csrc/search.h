@@ -153,7 +153,8 @@ struct SearchArgs {
 // and among those it is the least in reverse-lexicographic order (t_N first,
 // then t_(N-1), ...).  The kernels therefore keep, per recorded cost, the
 // reverse-lex least tour offered at that cost — a two-level MIN: the slot of
-// the cost (claimed by CAS), then the key (atomicMin).  The host certifies the
+// the cost (claimed by CAS), then the key (atomicMin); a two-word key's second
+// word goes to a sub-slot of its first word (CAS, then atomicMin).  The host certifies the
 // winner of the optimum's slot as DP-consistent (exact for integer costs; for
 // f64 a per-step rounding test, search_host.cpp tie_certify) and otherwise
 // falls back to the record set.
@@ -161,16 +162,15 @@ struct SearchArgs {
 // Key: digit p (p = 0..N-1) = rank of t_(N-p) among the cities not placed
 // yet, radix N - p; for N <= 20 all digits fit one word (N! < 2^64), else
 // digits 0..12 go to w0 and 13..N-1 to w1 (31!/18! and 18! < 2^64).
+constexpr int kTieSub = 8;  // second-word sub-slots per cost slot
 struct TieSlot {
     unsigned long long cost;  // kTieEmpty: free
     unsigned long long w0;    // least first word offered at this cost
-    unsigned long long lw0;   // (two-word keys) least (w0, w1) pair, under `lock`
-    unsigned long long lw1;
-    unsigned int lock;        // kTieFree: unlocked
-    unsigned int pad[3];
+    // (two-word keys) per first word that was ever the least at this cost:
+    // sub[i][0] = that w0 (claimed by CAS), sub[i][1] = the least w1 offered with it
+    unsigned long long sub[kTieSub][2];
 };
 constexpr unsigned long long kTieEmpty = ~0ull;  // (never a cost: f64 NaN bits / > any u32 cost)
-constexpr unsigned int kTieFree = ~0u;
 constexpr int kTieSplit = 13;  // digits in w0 when N > 20
 constexpr uint32_t kTieSlots = 1024;
 constexpr int kTieProbe = 32;
@@ -229,21 +229,15 @@ __device__ __forceinline__ void tie_offer(const SearchArgs &a, TieCache &tc, uns
     tc.cost = tb;
     tc.w0 = o0 < w0 ? o0 : w0;
     if (!two || w0 > o0) return;
-    // second word: the (w0, w1) pair under the slot's lock; the lanes of a
-    // wave take it in turn (each releases it in the iteration that took it)
-    bool pending = true;
-    while (pending) {
-        if (atomicCAS(&e->lock, kTieFree, 0u) == kTieFree) {
-            const unsigned long long c0 = __hip_atomic_load(&e->lw0, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-            const unsigned long long c1 = __hip_atomic_load(&e->lw1, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-            if (w0 < c0 || (w0 == c0 && w1 < c1)) {
-                __hip_atomic_store(&e->lw0, w0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                __hip_atomic_store(&e->lw1, w1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-            __hip_atomic_store(&e->lock, kTieFree, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-            pending = false;
+    // second word: the sub-slot of this w0 (lock-free: CAS claim, atomicMin)
+    for (int i = 0; i < kTieSub; ++i) {
+        const unsigned long long old = atomicCAS(&e->sub[i][0], kTieEmpty, w0);
+        if (old == kTieEmpty || old == w0) {
+            atomicMin(&e->sub[i][1], w1);
+            return;
         }
     }
+    atomicOr(a.tie_overflow, 1u);
 }
 
 constexpr int kStatLines = 64, kStatStride = 16;
@@ -265,6 +259,11 @@ hipError_t launch_tail(const SearchArgs &a, bool f64, int grid);
 hipError_t launch_persist(const SearchArgs &a, bool f64, int grid);
 // the optimum's tie slot -> out[0..4] (search.hip tie_lookup_kernel)
 hipError_t launch_tie_lookup(const SearchArgs &a, unsigned long long *out);
+// statistics sums, counter words, tie slot and the first records -> pinned
+// host memory in one launch (search.hip fetch_kernel; layout there)
+hipError_t launch_fetch(const SearchArgs &a, const unsigned long long *words, unsigned long long *out,
+                        uint32_t spec_cap);
+constexpr int kFetchWords = 32;  // fetch_kernel's words before the records
 // suffix table (enum.hip): size a.hs_len of a.hsuf, one thread per set
 hipError_t launch_suffix(const SearchArgs &a, bool f64, uint32_t sets);
 // seeds (seed_grid blocks) and the suffix table in one launch (enum.hip)

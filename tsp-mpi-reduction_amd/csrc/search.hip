@@ -1108,7 +1108,8 @@ __global__ __launch_bounds__(kSearchThreads) void persist_kernel(SearchArgs a)
 }
 
 // The optimum's tie slot: out[0] = 1 if a slot holds cost *a.inc, out[1] =
-// its w0, out[2..3] = its (lw0, lw1), out[4] = the overflow flag.  One wave.
+// its least w0, out[2..3] = (w0, least w1) of that w0's sub-slot (two-word
+// keys), out[4] = the overflow flag.  One wave.
 __global__ __launch_bounds__(64) void tie_lookup_kernel(SearchArgs a, unsigned long long *out)
 {
     const unsigned long long opt = __hip_atomic_load(a.inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1123,13 +1124,71 @@ __global__ __launch_bounds__(64) void tie_lookup_kernel(SearchArgs a, unsigned l
         if (e.cost == opt) {
             out[0] = 1;
             out[1] = e.w0;
-            out[2] = e.lw0;
-            out[3] = e.lw1;
+            out[2] = kTieEmpty;
+            out[3] = kTieEmpty;
+            for (int k = 0; k < kTieSub; ++k)
+                if (e.sub[k][0] == e.w0) {
+                    out[2] = e.sub[k][0];
+                    out[3] = e.sub[k][1];
+                }
         }
     }
 }
 
+// search_solve's readbacks in ONE launch, written straight into pinned host
+// memory (no copy commands): out[0..3] the summed statistics lines, out[4..19]
+// the 16 counter words, out[20..24] the optimum's tie slot (as
+// tie_lookup_kernel), out[32..] the first min(records, spec_cap) records.
+__global__ __launch_bounds__(256) void fetch_kernel(SearchArgs a, const unsigned long long *words,
+                                                    unsigned long long *out, uint32_t spec_cap)
+{
+    const int t = (int)threadIdx.x;
+    __shared__ unsigned long long part[4][kStatLines];
+    __shared__ unsigned long long tie[4];
+    part[t & 3][t >> 2] = a.nodes[(t >> 2) * kStatStride + (t & 3)];  // 256 threads = 64 lines x 4
+    if (t == 0) tie[0] = 0;
+    __syncthreads();
+    const unsigned long long opt = __hip_atomic_load(a.inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (a.tie)
+        for (uint32_t i = (uint32_t)t; i <= a.tie_mask; i += 256) {
+            const TieSlot &e = a.tie[i];
+            if (e.cost == opt) {  // (at most one slot holds a cost)
+                tie[0] = 1;
+                tie[1] = e.w0;
+                tie[2] = kTieEmpty;
+                tie[3] = kTieEmpty;
+                for (int k = 0; k < kTieSub; ++k)
+                    if (e.sub[k][0] == e.w0) {
+                        tie[2] = e.sub[k][0];
+                        tie[3] = e.sub[k][1];
+                    }
+            }
+        }
+    __syncthreads();
+    if (t < 4) {
+        unsigned long long sum = 0;
+        for (int l = 0; l < kStatLines; ++l) sum += part[t][l];
+        out[t] = sum;
+    }
+    if (t < 16) out[4 + t] = words[t];
+    if (t < 4) out[20 + t] = tie[t];
+    if (t == 0) out[24] = a.tie_overflow ? *a.tie_overflow : 0u;
+    const uint32_t claimed = *a.rec_count;
+    const uint32_t cnt = claimed < spec_cap ? claimed : spec_cap;
+    const unsigned long long *src = reinterpret_cast<const unsigned long long *>(a.rec);
+    constexpr uint32_t kW = sizeof(SearchRecord) / 8;
+    for (uint32_t i = (uint32_t)t; i < cnt * kW; i += 256) out[32 + i] = src[i];
+}
+
 }  // namespace
+
+hipError_t launch_fetch(const SearchArgs &a, const unsigned long long *words, unsigned long long *out,
+                        uint32_t spec_cap)
+{
+    static_assert(sizeof(SearchRecord) % 8 == 0 && kStatLines * 4 == 256, "fetch layout");
+    hipLaunchKernelGGL(fetch_kernel, dim3(1), dim3(256), 0, a.stream, a, words, out, spec_cap);
+    return hipGetLastError();
+}
 
 hipError_t launch_tie_lookup(const SearchArgs &a, unsigned long long *out)
 {

@@ -19,6 +19,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cerrno>
 #include <climits>
 #include <cmath>
@@ -42,6 +43,9 @@ using tspgpu::host::validate_search;
 static_assert(sizeof(SearchRecord) == sizeof(tspgpu_tour_record), "record layout");
 constexpr int kWords = 16;  // device counter words of a search (see tspgpu_search::d_words)
 constexpr size_t kStatBytes = sizeof(unsigned long long) * kStatLines * kStatStride;
+constexpr size_t kStageSpec = 24 * 1024;  // h_stage: tables below, speculative records above
+constexpr unsigned kSpecRecs = 512;
+constexpr size_t kStageBytes = kStageSpec + 8 * kFetchWords + sizeof(SearchRecord) * kSpecRecs;
 
 struct tspgpu_search {
     tspgpu_ctx *ctx = nullptr;
@@ -140,6 +144,12 @@ struct tspgpu_search {
     // optimum's slot (tie_lookup_kernel), [5] the overflow flag
     TieSlot *d_tie = nullptr;
     bool tie_on = true;  // TSPGPU_SEARCH_TIE=0: records and the host rule only
+    // pinned staging: the host tables of create (so their copies need no
+    // synchronisation) and, at kStageSpec, the speculative records readback
+    char *h_stage = nullptr;
+    // search_solve: the chained run enqueues the solve's readbacks (counters,
+    // statistics, records, tie slot) before its one synchronisation
+    bool fetch = false, fetched = false;
 };
 
 namespace {
@@ -183,6 +193,7 @@ struct SearchPool {
     double *d_hsuf = nullptr;
     size_t hsuf_alloc = 0;
     TieSlot *d_tie = nullptr;
+    char *h_stage = nullptr;
 };
 
 template <typename A, typename B>
@@ -216,6 +227,7 @@ void move_buffers(A &to, B &from)
     to.d_hsuf = from.d_hsuf, from.d_hsuf = nullptr;
     to.hsuf_alloc = from.hsuf_alloc, from.hsuf_alloc = 0;
     to.d_tie = from.d_tie, from.d_tie = nullptr;
+    to.h_stage = from.h_stage, from.h_stage = nullptr;
 }
 
 template <typename A>
@@ -243,6 +255,7 @@ void free_buffers(A &b)
     if (b.d_mst) (void)hipFree(b.d_mst);
     if (b.d_hsuf) (void)hipFree(b.d_hsuf);
     if (b.d_tie) (void)hipFree(b.d_tie);
+    if (b.h_stage) (void)hipHostFree(b.h_stage);
     SearchPool z;
     move_buffers(b, z);
 }
@@ -287,8 +300,9 @@ static void front_release(tspgpu_search *s);
 
 extern "C" {
 
-int tspgpu_search_create(tspgpu_ctx *c, const void *dist, int dtype, int n, int shard, int nshards, int depth,
-                         tspgpu_search **out)
+// (bound: the initial incumbent, written with the counter words; null: none)
+static int search_create(tspgpu_ctx *c, const void *dist, int dtype, int n, int shard, int nshards, int depth,
+                         const double *bound, tspgpu_search **out)
 {
     if (!c || !out) return -EINVAL;
     *out = nullptr;
@@ -526,37 +540,55 @@ int tspgpu_search_create(tspgpu_ctx *c, const void *dist, int dtype, int n, int 
     if (e == hipSuccess)
         e = hipMemsetAsync(reinterpret_cast<char *>(s->d_tie) + kTieBytes, 0, 8 * sizeof(unsigned long long), st);
     if (e == hipSuccess) e = hipMemsetAsync(s->d_stats, 0, kStatBytes, st);
-    if (e == hipSuccess) e = hipMemcpyAsync(s->d_dist, dist, vb * n * n, hipMemcpyHostToDevice, st);
-    if (e == hipSuccess)
-        e = hipMemcpyAsync(s->d_amin, f64 ? (const void *)ad.data() : (const void *)ai.data(), vb * n,
-                           hipMemcpyHostToDevice, st);
-    if (e == hipSuccess && s->sym)
-        e = hipMemcpyAsync(s->d_bnd2, f64 ? (const void *)bd.data() : (const void *)bi.data(), vb * 2 * n,
-                           hipMemcpyHostToDevice, st);
-    if (e == hipSuccess && s->mst_on)
-        e = hipMemcpyAsync(s->d_mst, mt.data(), sizeof(double) * mt.size(), hipMemcpyHostToDevice, st);
+    const bool pinned = !std::getenv("TSPGPU_SEARCH_PAGEABLE");
+    if (e == hipSuccess && pinned && !s->h_cnt)
+        e = hipHostMalloc((void **)&s->h_cnt, 16 * sizeof(unsigned long long), hipHostMallocDefault);
+    if (e == hipSuccess && pinned && !s->h_stats)
+        e = hipHostMalloc((void **)&s->h_stats, kStatBytes + 8 * sizeof(unsigned long long), hipHostMallocDefault);
+    if (e == hipSuccess && pinned && !s->h_stage) e = hipHostMalloc((void **)&s->h_stage, kStageBytes, hipHostMallocDefault);
+    // the tables go through the pinned staging area, so the copies are
+    // asynchronous and create returns without a synchronisation (pageable:
+    // synchronised below)
+    size_t soff = 0;
+    auto put = [&](void *dst, const void *src, size_t bytes) {
+        const void *from = src;
+        if (s->h_stage && soff + bytes <= kStageSpec) {
+            std::memcpy(s->h_stage + soff, src, bytes);
+            from = s->h_stage + soff;
+            soff += (bytes + 15) & ~(size_t)15;
+        } else if (s->h_stage) {
+            soff = kStageSpec + 1;  // (does not fit: synchronise below)
+        }
+        return hipMemcpyAsync(dst, from, bytes, hipMemcpyHostToDevice, st);
+    };
+    if (e == hipSuccess) e = put(s->d_dist, dist, vb * n * n);
+    if (e == hipSuccess) e = put(s->d_amin, f64 ? (const void *)ad.data() : (const void *)ai.data(), vb * n);
+    if (e == hipSuccess && s->sym) e = put(s->d_bnd2, f64 ? (const void *)bd.data() : (const void *)bi.data(), vb * 2 * n);
+    if (e == hipSuccess && s->mst_on) e = put(s->d_mst, mt.data(), sizeof(double) * mt.size());
     unsigned long long w[kWords] = {};
     if (f64) {
         const double inf = INFINITY;
-        std::memcpy(&w[1], &inf, 8);
+        std::memcpy(&w[1], bound ? bound : &inf, 8);
     } else {
-        w[1] = (unsigned long long)INT32_MAX;
+        w[1] = bound ? (unsigned long long)std::min<double>(*bound, (double)INT32_MAX) : (unsigned long long)INT32_MAX;
     }
-    if (e == hipSuccess) e = hipMemcpyAsync(s->d_words, w, sizeof w, hipMemcpyHostToDevice, st);
-    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (e == hipSuccess) e = put(s->d_words, w, sizeof w);
+    if (e == hipSuccess && (!s->h_stage || soff > kStageSpec)) e = hipStreamSynchronize(st);
     if (e == hipSuccess && !s->e0) e = hipEventCreate(&s->e0);
     if (e == hipSuccess && !s->e1) e = hipEventCreate(&s->e1);
     if (e == hipSuccess && !s->e2) e = hipEventCreate(&s->e2);
-    if (e == hipSuccess && !s->h_cnt && !std::getenv("TSPGPU_SEARCH_PAGEABLE"))
-        e = hipHostMalloc((void **)&s->h_cnt, 16 * sizeof(unsigned long long), hipHostMallocDefault);
-    if (e == hipSuccess && !s->h_stats && !std::getenv("TSPGPU_SEARCH_PAGEABLE"))
-        e = hipHostMalloc((void **)&s->h_stats, kStatBytes + 8 * sizeof(unsigned long long), hipHostMallocDefault);
     if (e != hipSuccess) {
         tspgpu_search_destroy(s);
         return herr(e);
     }
     *out = s;
     return 0;
+}
+
+int tspgpu_search_create(tspgpu_ctx *c, const void *dist, int dtype, int n, int shard, int nshards, int depth,
+                         tspgpu_search **out)
+{
+    return search_create(c, dist, dtype, n, shard, nshards, depth, nullptr, out);
 }
 
 int tspgpu_search_destroy(tspgpu_search *s)
@@ -594,7 +626,10 @@ int tspgpu_search_set_bound(tspgpu_search *s, double bound)
         w = (unsigned long long)std::min<double>(bound, (double)INT32_MAX);
     }
     (void)hipSetDevice(s->ctx->device);
-    return herr(hipMemcpy(s->d_words + 1, &w, 8, hipMemcpyHostToDevice));
+    // on the search's stream: ordered after create's (asynchronous) counter words
+    hipError_t e = hipMemcpyAsync(s->d_words + 1, &w, 8, hipMemcpyHostToDevice, s->ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(s->ctx->stream);
+    return herr(e);
 }
 
 static unsigned long long *tie_words(tspgpu_search *s)
@@ -982,6 +1017,19 @@ int tspgpu_search_step(tspgpu_search *s, uint64_t *pending)
 // rerun step by step (records and tails reset; the incumbent, a real tour's
 // cost, is kept).  Breadth first instead of the stepwise LIFO: the same
 // bounds, the same optimal set, a different node count.
+// search_solve's readbacks, enqueued behind the search: one kernel writes
+// the statistics, counter words, tie slot and first records straight into
+// the pinned h_stage + kStageSpec (fetch_kernel's layout)
+static unsigned long long *fetch_buf(tspgpu_search *s)
+{
+    return reinterpret_cast<unsigned long long *>(s->h_stage + kStageSpec);
+}
+static hipError_t enqueue_fetch(tspgpu_search *s)
+{
+    SearchArgs a = args_of(s);
+    return launch_fetch(a, s->d_words, fetch_buf(s), std::min(kSpecRecs, s->rec_cap));
+}
+
 constexpr int kChainMaxN = 18;
 static int run_chain(tspgpu_search *s, bool *done)
 {
@@ -994,6 +1042,13 @@ static int run_chain(tspgpu_search *s, bool *done)
     }
     SearchArgs a0 = args_of(s);
     const int levels = a0.tail_level - s->depth;
+    // a run of 256 paths per block (one per lane) and two blocks per CU:
+    // the reference's 16-city instance 0.30 -> 0.22 ms in process against
+    // 1024-path runs on one block per CU (profiles/r03/k2_chain_sweep.log)
+    uint32_t chain_fpb = 256;
+    int chain_grid = 2;
+    if (const char *ev = std::getenv("TSPGPU_CHAIN_FPB")) chain_fpb = (uint32_t)std::atoi(ev);  // (sweeps)
+    if (const char *ev = std::getenv("TSPGPU_CHAIN_GRID")) chain_grid = std::max(1, std::atoi(ev));
     if (levels < 1 || s->local_items + 1 > kChainCap) return 0;
     hipStream_t st = s->ctx->stream;
     const bool f64 = s->dtype == TSPGPU_F64;
@@ -1025,8 +1080,8 @@ static int run_chain(tspgpu_search *s, bool *done)
         a.fout = s->fb[ob[l & 1]];
         a.fout_cap = (uint32_t)kChainCap;
         a.overflow = reinterpret_cast<unsigned int *>(s->d_words + 13);
-        a.fin_per_block = 1024;
-        a.max_grid = s->ctx->cu_count;  // (blocks beyond the level's runs only stage tables and leave)
+        a.fin_per_block = chain_fpb;
+        a.max_grid = s->ctx->cu_count * chain_grid;  // (blocks beyond the level's runs only stage tables and leave)
         e = launch_expand(a, f64);
     }
     if (e == hipSuccess) {
@@ -1036,7 +1091,14 @@ static int run_chain(tspgpu_search *s, bool *done)
     (void)hipEventRecord(s->e1, st);
     unsigned long long local[8] = {};
     unsigned long long *h = s->h_cnt ? s->h_cnt : local;
-    if (e == hipSuccess) e = hipMemcpyAsync(h, s->d_words + 8, 6 * sizeof(unsigned long long), hipMemcpyDeviceToHost, st);
+    // (search_solve: its readbacks ride on this synchronisation, words 8..13 among them)
+    const bool fetch = s->fetch && s->h_stage;
+    if (e == hipSuccess && fetch) {
+        e = enqueue_fetch(s);
+        h = fetch_buf(s) + 4 + 8;
+    } else if (e == hipSuccess) {
+        e = hipMemcpyAsync(h, s->d_words + 8, 6 * sizeof(unsigned long long), hipMemcpyDeviceToHost, st);
+    }
     if (e == hipSuccess) e = hipStreamSynchronize(st);
     if (e != hipSuccess) return herr(e);
     float ms = 0.f;
@@ -1047,6 +1109,7 @@ static int run_chain(tspgpu_search *s, bool *done)
     s->tails = 0;
     if ((uint32_t)h[5] == 0) {  // word 13: no overflow
         *done = true;
+        s->fetched = fetch;
         return 0;
     }
     // overflow: records and tails reset, the search reruns step by step
@@ -1158,7 +1221,14 @@ int tspgpu_search_run_all(tspgpu_search *s)
     }
     int rc = tspgpu_search_start(s);
     uint64_t pending = 1;
-    while (!rc && pending) rc = tspgpu_search_step(s, &pending);
+    const char *dbg = std::getenv("TSPGPU_SEARCH_DEBUG");
+    const bool trace = dbg && std::atoi(dbg) >= 2;
+    while (!rc && pending) {
+        rc = tspgpu_search_step(s, &pending);
+        if (trace)
+            std::fprintf(stderr, "step %d: pending %llu tails %llu kernel %.3f ms\n", s->rounds,
+                         (unsigned long long)pending, (unsigned long long)s->tails, s->ms);
+    }
     return rc;
 }
 
@@ -1237,6 +1307,12 @@ static int search_solve(tspgpu_ctx *c, const void *dist, int dtype, int n, doubl
                         tspgpu_search_stats *stats, int noprune)
 {
     if (!c || !cost_out || !tour_out) return -EINVAL;
+    // TSPGPU_SEARCH_DEBUG: host phase times on stderr (development aid)
+    const bool dbg = std::getenv("TSPGPU_SEARCH_DEBUG") != nullptr;
+    using clk = std::chrono::steady_clock;
+    const clk::time_point T0 = clk::now();
+    clk::time_point T1 = T0, T2 = T0, T3 = T0, T4 = T0;
+    auto ms_of = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
     tspgpu_search *s = nullptr;
     int depth = 0;  // automatic; TSPGPU_SEARCH_DEPTH (tests): a shallow seed, a deep frontier
     if (const char *e = std::getenv("TSPGPU_SEARCH_DEPTH")) depth = std::max(0, std::atoi(e));
@@ -1253,11 +1329,10 @@ static int search_solve(tspgpu_ctx *c, const void *dist, int dtype, int n, doubl
         } catch (...) {
         }
     }
-    int rc = tspgpu_search_create(c, dist, dtype, n, 0, 1, depth, &s);
-    if (threaded)
-        ht.join();
-    else
-        hrc = tspgpu_heuristic_tour(dist, dtype, n, &ub, nullptr);
+    // (n < 20: the bound first, then written with the counter words at create)
+    if (!threaded) hrc = tspgpu_heuristic_tour(dist, dtype, n, &ub, nullptr);
+    int rc = search_create(c, dist, dtype, n, 0, 1, depth, threaded || hrc ? nullptr : &ub, &s);
+    if (threaded) ht.join();
     if (rc) return rc;
     s->noprune = noprune;
     // enumeration work is uniform and every lane reaches the register tails:
@@ -1272,7 +1347,8 @@ static int search_solve(tspgpu_ctx *c, const void *dist, int dtype, int n, doubl
         if (v > 0) s->rec_cap = (unsigned int)std::min<long>(v, s->rec_cap);
     }
     rc = hrc;
-    if (!rc) rc = tspgpu_search_set_bound(s, ub);
+    if (dbg) T1 = clk::now();
+    if (!rc && threaded) rc = tspgpu_search_set_bound(s, ub);
     int phases = 1, fallback = 0;
     uint64_t inc = 0, nodes = 0, nodes_total = 0, recs = 0;
     uint64_t u[4] = {0, 0, 0, 0};  // statistics of the last read (lane-step counters)
@@ -1287,14 +1363,27 @@ static int search_solve(tspgpu_ctx *c, const void *dist, int dtype, int n, doubl
     };
     // counters, statistics and (speculatively) the first kSpecRecs records in
     // one synchronisation
-    constexpr unsigned kSpecRecs = 2048;
     std::vector<SearchRecord> spec;
+    const SearchRecord *specp = nullptr;
     bool spec_ok = false;
+    if (dbg) T2 = clk::now();
+    s->fetch = true;  // (the chained search reads everything below in its one synchronisation)
     if (!rc) rc = tspgpu_search_run_all(s);
+    if (dbg) T3 = clk::now();
     // the device tie rule's answer: the optimum's slot, read with the counters
     unsigned long long tie_local[5] = {};
     unsigned long long *tie_h = s->h_cnt ? s->h_cnt + 8 : tie_local;
-    if (!rc && s->tie_on) {
+    if (!rc && s->fetched) {
+        const unsigned long long *f = fetch_buf(s);
+        for (int i = 0; i < 4; ++i) u[i] = f[i];
+        for (int i = 0; i < 5; ++i) w[i] = f[4 + i];
+        tie_h = const_cast<unsigned long long *>(f + 20);
+        inc = w[1];
+        recs = (uint32_t)w[3];
+        nodes = u[0];
+        specp = reinterpret_cast<const SearchRecord *>(f + kFetchWords);
+        spec_ok = recs <= std::min(kSpecRecs, s->rec_cap);
+    } else if (!rc && s->tie_on) {
         SearchArgs a = args_of(s);
         hipError_t e = launch_tie_lookup(a, tie_words(s));
         if (e == hipSuccess)
@@ -1302,7 +1391,7 @@ static int search_solve(tspgpu_ctx *c, const void *dist, int dtype, int n, doubl
                                s->ctx->stream);
         rc = herr(e);
     }
-    if (!rc) {
+    if (!rc && !s->fetched) {
         const unsigned k = std::min<unsigned>(kSpecRecs, s->rec_cap);
         spec.resize(k);
         hipError_t e = hipMemcpyAsync(spec.data(), s->d_rec, sizeof(SearchRecord) * k, hipMemcpyDeviceToHost,
@@ -1310,8 +1399,10 @@ static int search_solve(tspgpu_ctx *c, const void *dist, int dtype, int n, doubl
         rc = herr(e);
         if (!rc) rc = counters();  // (its synchronisation covers the record copy)
         spec_ok = !rc && recs <= k;
+        specp = spec.data();
     }
     nodes_total = nodes;
+    if (dbg) T4 = clk::now();
     // device tie rule: the optimum's slot decoded and certified on the host
     // (tspgpu_tie_tour); then neither the records nor a second search are needed
     bool tie_done = false;
@@ -1349,7 +1440,7 @@ static int search_solve(tspgpu_ctx *c, const void *dist, int dtype, int n, doubl
         // must give the same tour (a self-check; the records then decide)
         if (spec_ok) {
             for (uint64_t i = 0; i < recs; ++i)
-                if (spec[i].cost == inc) opt.push_back(reinterpret_cast<const tspgpu_tour_record &>(spec[i]));
+                if (specp[i].cost == inc) opt.push_back(reinterpret_cast<const tspgpu_tour_record &>(specp[i]));
             count = (int)opt.size();
             std::vector<int32_t> ht(n + 1, 0);
             if (count > 0 && tspgpu_select_tour(dist, dtype, n, opt.data(), count, inc, ht.data()) == 0) {
@@ -1375,7 +1466,7 @@ static int search_solve(tspgpu_ctx *c, const void *dist, int dtype, int n, doubl
         opt.resize(recs);
         if (spec_ok) {
             for (uint64_t i = 0; i < recs; ++i)
-                if (spec[i].cost == inc) std::memcpy(&opt[count++], &spec[i], sizeof(SearchRecord));
+                if (specp[i].cost == inc) std::memcpy(&opt[count++], &specp[i], sizeof(SearchRecord));
         } else {
             rc = records_of(s, recs, inc, opt.data(), (int)recs, &count);
         }
@@ -1404,7 +1495,14 @@ static int search_solve(tspgpu_ctx *c, const void *dist, int dtype, int n, doubl
         stats->tie = tie_done && tie_checked >= 0 ? 1 : 0;
         stats->tie_checked = tie_checked;
     }
+    const double dev_ms = s->ms;
     tspgpu_search_destroy(s);
+    if (dbg)
+        std::fprintf(stderr,
+                     "search_solve n=%d: create+bound %.3f ms, set_bound %.3f, run %.3f (device %.3f), read %.3f, "
+                     "select+destroy %.3f, total %.3f; tie %d checked %d phases %d\n",
+                     n, ms_of(T0, T1), ms_of(T1, T2), ms_of(T2, T3), dev_ms, ms_of(T3, T4), ms_of(T4, clk::now()),
+                     ms_of(T0, clk::now()), stats ? stats->tie : -1, stats ? stats->tie_checked : -1, phases);
     return rc;
 }
 
