@@ -549,9 +549,12 @@ def k2_single_instance(ctx, n, group, backend, world, reps=3):
             "kernel_ms": st["kernel_ms"], "bb_nodes_expanded": st["nodes"],
             "bb_nodes_per_s": st["nodes"] / max(st["kernel_ms"] * 1e-3, 1e-12), "rounds": st["rounds"],
             "exchanges": st["exchanges"], "ranks": world, "exchange_backend": backend,
-            "path": "tspgpu_search_solve (native rounds)" if world == 1 else "search_dist.solve_sharded",
+            "path": "tspgpu_search_solve (chained levels, one synchronisation)" if world == 1
+            else "search_dist.solve_sharded",
             "python_exchange_loop_ms": sharded[0],
-            "optimal_tours": st["optimal_tours"], "tour": [int(x) for x in tour]}
+            "optimal_tours": st["optimal_tours"], "tour": [int(x) for x in tour],
+            "device_tie_rule": {"used": int(st.get("tie", 0)), "records_agree": int(st.get("tie_checked", 0)),
+                                "phases": int(st.get("phases", 1)), "fallback": int(st.get("fallback", 0))}}
 
 
 def k2_strong_scaling(ctx, n, seed, group, backend, world, rank, reps=2):

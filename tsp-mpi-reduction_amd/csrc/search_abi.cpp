@@ -1030,7 +1030,10 @@ static hipError_t enqueue_fetch(tspgpu_search *s)
     return launch_fetch(a, s->d_words, fetch_buf(s), std::min(kSpecRecs, s->rec_cap));
 }
 
-constexpr int kChainMaxN = 18;
+// (up to 32 cities: at 20-32 cities the chained search takes 0.70-1.73 ms in
+// process against 0.95-2.8 ms step by step, same nodes and answers,
+// profiles/r03/k2_chain_maxn.log)
+constexpr int kChainMaxN = 32;
 static int run_chain(tspgpu_search *s, bool *done)
 {
     *done = false;
@@ -1214,7 +1217,11 @@ int tspgpu_search_run_all(tspgpu_search *s)
     if (!s) return -EINVAL;
     if (s->noprune && s->enum_kernel) return run_enum(s);
     if (s->kernel == 3 && !s->noprune) return run_persist(s);
-    if (s->frontier && !s->noprune && s->nshards == 1 && s->n <= kChainMaxN && s->chain) {
+    // above 18 cities only with the tree bound (its frontiers are small; without
+    // it a 32-city chain overflows its level buffers and reruns step by step)
+    int chain_max = s->mst_on ? kChainMaxN : 18;
+    if (const char *ev = std::getenv("TSPGPU_CHAIN_MAXN")) chain_max = std::atoi(ev);  // (sweeps)
+    if (s->frontier && !s->noprune && s->nshards == 1 && s->n <= chain_max && s->chain) {
         bool done = false;
         int rc = run_chain(s, &done);
         if (rc || done) return rc;
