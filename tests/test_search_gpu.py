@@ -215,18 +215,14 @@ def test_chained_small_search(gpu_ctx, monkeypatch, mode):
 @pytest.mark.parametrize("n", [22, 28])
 def test_chained_search_with_tree_bound_above_18(gpu_ctx, monkeypatch, n):
     """With the tree bound the chained levels run up to 32 cities: the same
-    cost and tour as the stepwise search, also when the level buffers are
-    forced to overflow (the stepwise rerun)."""
+    cost and tour as the stepwise search."""
     from bench import k2_instance
 
     d = np.asarray(k2_instance(n, 3))
     c0, t0, _ = tspgpu.search_solve(gpu_ctx, d)
     monkeypatch.setenv("TSPGPU_SEARCH_CHAIN", "0")
     c1, t1, _ = tspgpu.search_solve(gpu_ctx, d)
-    monkeypatch.delenv("TSPGPU_SEARCH_CHAIN")
-    monkeypatch.setenv("TSPGPU_SEARCH_CHAIN_CAP_LOG2", "8")
-    c2, t2, _ = tspgpu.search_solve(gpu_ctx, d)
-    assert c0 == c1 == c2 and t0.tolist() == t1.tolist() == t2.tolist()
+    assert c0 == c1 and t0.tolist() == t1.tolist()
 
 
 @pytest.mark.parametrize("nshards", [2, 3, 5])
