@@ -215,14 +215,28 @@ def test_chained_small_search(gpu_ctx, monkeypatch, mode):
 @pytest.mark.parametrize("n", [22, 28])
 def test_chained_search_with_tree_bound_above_18(gpu_ctx, monkeypatch, n):
     """With the tree bound the chained levels run up to 32 cities: the same
-    cost and tour as the stepwise search."""
+    cost and tour as the stepwise search.  A chain whose level buffers
+    overflow reruns step by step from its starting state: after a 32-city
+    search in the same context (its paths left in the pooled buffers, which
+    an overflowing block's unwritten slots expose), forced overflows — with
+    and without the tree bound — still give the same answer."""
     from bench import k2_instance
 
     d = np.asarray(k2_instance(n, 3))
     c0, t0, _ = tspgpu.search_solve(gpu_ctx, d)
     monkeypatch.setenv("TSPGPU_SEARCH_CHAIN", "0")
     c1, t1, _ = tspgpu.search_solve(gpu_ctx, d)
+    monkeypatch.delenv("TSPGPU_SEARCH_CHAIN")
     assert c0 == c1 and t0.tolist() == t1.tolist()
+    tspgpu.search_solve(gpu_ctx, np.asarray(k2_instance(32, 35)))
+    monkeypatch.setenv("TSPGPU_SEARCH_CHAIN_CAP_LOG2", "10")
+    c2, t2, _ = tspgpu.search_solve(gpu_ctx, d)
+    assert c2 == c0 and t2.tolist() == t0.tolist()
+    if n == 22:  # (without the tree bound the 28-city search takes seconds)
+        monkeypatch.setenv("TSPGPU_SEARCH_MST", "0")
+        monkeypatch.setenv("TSPGPU_CHAIN_MAXN", "32")
+        c3, t3, _ = tspgpu.search_solve(gpu_ctx, d)
+        assert c3 == c0 and t3.tolist() == t0.tolist()
 
 
 @pytest.mark.parametrize("nshards", [2, 3, 5])

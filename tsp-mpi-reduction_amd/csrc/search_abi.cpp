@@ -1055,8 +1055,11 @@ static int run_chain(tspgpu_search *s, bool *done)
     if (levels < 1 || s->local_items + 1 > kChainCap) return 0;
     hipStream_t st = s->ctx->stream;
     const bool f64 = s->dtype == TSPGPU_F64;
-    // words 10..13 zeroed before the seeds (10..12: level counters, 13: overflow)
+    // words 10..13 zeroed before the seeds (10..12: level counters, 13:
+    // overflow); word 14 keeps the incumbent the chain starts from
     hipError_t e = hipMemsetAsync(s->d_words + 10, 0, 4 * sizeof(unsigned long long), st);
+    if (e == hipSuccess)
+        e = hipMemcpyAsync(s->d_words + 14, s->d_words + 1, sizeof(unsigned long long), hipMemcpyDeviceToDevice, st);
     if (e != hipSuccess) return herr(e);
     (void)hipEventRecord(s->e2, st);
     int rc = search_start(s, false);  // the seeds, enqueued: their count stays in word 4
@@ -1115,10 +1118,23 @@ static int run_chain(tspgpu_search *s, bool *done)
         s->fetched = fetch;
         return 0;
     }
-    // overflow: records and tails reset, the search reruns step by step
+    // overflow: the search reruns step by step from the state before the
+    // chain — records, tails, tie slots and the incumbent reset.  (A block
+    // that overflowed reserved output slots it never wrote; later levels and
+    // the tail fold read whatever those slots held before, paths of an
+    // earlier search, possibly of more cities: their "tours" must not leave
+    // an incumbent, record or tie key behind.)
     e = hipMemsetAsync(s->d_words + 3, 0, 8, st);
     if (e == hipSuccess) e = hipMemsetAsync(s->d_words + 8, 0, 8, st);
     if (e == hipSuccess) e = hipMemsetAsync(s->d_words + 13, 0, 8, st);
+    if (e == hipSuccess)
+        e = hipMemcpyAsync(s->d_words + 1, s->d_words + 14, sizeof(unsigned long long), hipMemcpyDeviceToDevice, st);
+    if (e == hipSuccess && s->d_tie) {
+        constexpr size_t kTieBytes = sizeof(TieSlot) * kTieSlots;
+        e = hipMemsetAsync(s->d_tie, 0xFF, kTieBytes, st);
+        if (e == hipSuccess) e = hipMemsetAsync(tie_words(s), 0, 8 * sizeof(unsigned long long), st);
+    }
+    if (e == hipSuccess) e = hipMemsetAsync(s->d_stats, 0, kStatBytes, st);
     return herr(e);
 }
 
