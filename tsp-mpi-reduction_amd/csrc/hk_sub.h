@@ -176,6 +176,9 @@ __device__ __forceinline__ void relax_min2(int32_t &a0, int32_t g0, int32_t d0, 
 #ifndef TSPGPU_SUB_PAIR
 #define TSPGPU_SUB_PAIR 1  // middle passes: min-only relaxations two at a time (relax_min2)
 #endif
+#ifndef TSPGPU_SUB_SB
+#define TSPGPU_SUB_SB 1  // middle passes: a scheduling barrier after every SB relaxation pairs
+#endif
 
 // generic relaxation with a first-member initialisation (edge passes)
 template <bool ARG, typename V>
@@ -386,7 +389,7 @@ __device__ __forceinline__ void sub_mid(const SubCtx<V, N, L> &c, uint32_t h, ui
                     relax_one(std::integral_constant<int, k0>{});
                     if constexpr (k1 < CNT) relax_one(std::integral_constant<int, k1>{});
                 }
-                __builtin_amdgcn_sched_barrier(0);
+                if constexpr ((decltype(kk2)::value + 1) % TSPGPU_SUB_SB == 0) __builtin_amdgcn_sched_barrier(0);
             });
         } else {
             static_for<CNT>([&](auto kk) {
