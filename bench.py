@@ -554,7 +554,10 @@ def k2_single_instance(ctx, n, group, backend, world, reps=3):
             "python_exchange_loop_ms": sharded[0],
             "optimal_tours": st["optimal_tours"], "tour": [int(x) for x in tour],
             "device_tie_rule": {"used": int(st.get("tie", 0)), "records_agree": int(st.get("tie_checked", 0)),
-                                "phases": int(st.get("phases", 1)), "fallback": int(st.get("fallback", 0))}}
+                                "phases": int(st.get("phases", 1)), "fallback": int(st.get("fallback", 0)),
+                                "record_gather": int(st.get("record_gather", 0)),
+                                "chained": int(st.get("chained", 1)),
+                                "collectives": int(st.get("collectives", 0))}}
 
 
 def k2_strong_scaling(ctx, n, seed, group, backend, world, rank, reps=2):
@@ -981,7 +984,11 @@ def main():
         "metric": METRIC,
         "value": value,
         "unit": UNIT,
-        "n_gpus": world,
+        # GPUs actually used: ranks sharing a device (a rehearsal on a smaller
+        # box) do not add GPUs, and the line says so
+        "n_gpus": min(world, ndev),
+        "ranks": world,
+        "ranks_per_gpu": -(-world // ndev),
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": wall_max / args.steps * 1e3,

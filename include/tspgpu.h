@@ -219,6 +219,11 @@ typedef struct
  * valid but not certified (use the records); -EINVAL: not a tour of that cost. */
 int tspgpu_tie_tour(const void *dist, int dtype, int n, uint64_t w0, uint64_t w1, uint64_t cost_bits,
                     int32_t *tour_out);
+/* The same certificate with the prefix DPs it may need run on the context's
+ * GPU (K1-wide over the prefix's cities, up to 26; the host DP stops at 16),
+ * so binade crossings late in long tours are proven too. */
+int tspgpu_tie_tour_gpu(tspgpu_ctx *ctx, const void *dist, int dtype, int n, uint64_t w0, uint64_t w1,
+                        uint64_t cost_bits, int32_t *tour_out);
 /* the key of a tour (tour[0] = 0, tour[1..n-1] = t1..tN): test helper */
 int tspgpu_tie_key(int n, const int32_t *tour, uint64_t *w0, uint64_t *w1);
 
@@ -273,6 +278,36 @@ int tspgpu_search_reset_records(tspgpu_search *s, unsigned int capacity);
 /* the recorded tours whose cost bits equal cost_bits; -EOVERFLOW if records
  * were lost (rerun with the optimum as the bound), -ENOSPC if cap is short */
 int tspgpu_search_records(tspgpu_search *s, uint64_t cost_bits, tspgpu_tour_record *out, int cap, int *count);
+
+/* Chained run of this shard (any shard count): the seeds,
+ * every frontier level and the tail fold enqueued back to back on the
+ * context's stream, ONE synchronisation, and the counters, this shard's tie
+ * slot at its incumbent and its first records read back with it.  Between
+ * levels, every `exchange_every` levels (0: never), hook(user, stream,
+ * incumbent word) is called to enqueue an exchange of the device incumbent on
+ * that stream — e.g. ncclAllReduce(word, word, 1, ncclUint64, ncclMin, comm,
+ * stream): the same number of calls on every shard, chained or not.
+ * *done = 1: the shard's search is complete.  *done = 0: the search is too
+ * large to chain (a level overflowed, or n is above the chain's limit) and is
+ * back at its starting state (incumbent restored, no records): continue with
+ * tspgpu_search_start / tspgpu_search_step. */
+typedef void (*tspgpu_level_hook)(void *user, void *stream, void *incumbent_word);
+int tspgpu_search_chain(tspgpu_search *s, int exchange_every, tspgpu_level_hook hook, void *user, int *done);
+
+/* The device tie rule's least key among the tours this shard recorded at
+ * cost cost_bits (tspgpu_tie_tour's w0/w1).  A driver of S shards takes the
+ * all-reduce MIN of the incumbents (the optimum), then the MIN of w0 over the
+ * shards (~0 where !found), then of w1 over the holders of that w0, and
+ * certifies the winner once with tspgpu_tie_tour — the DP's tour without
+ * gathering any record; overflow != 0 on any shard: the
+ * records decide instead (tspgpu_search_records, tspgpu_select_tour). */
+typedef struct
+{
+    uint64_t w0, w1; /* the key (w1 = 0 when n - 1 <= 20) */
+    int found;       /* 1: a recorded tour of this shard has that cost */
+    int overflow;    /* 1: the tie table lost an offer, the key may not be least */
+} tspgpu_tie_slot;
+int tspgpu_search_tie_slot(tspgpu_search *s, uint64_t cost_bits, tspgpu_tie_slot *out);
 
 /* Host helpers.  A nearest-neighbour + 2-opt tour and its left-fold cost (an
  * upper bound); and the DP's tie rule applied to the optimal set O: walking

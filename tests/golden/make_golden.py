@@ -240,9 +240,23 @@ def gen_cli():
     return cases
 
 
+def gen_cli_large():
+    """SURVEY Appendix B's merge-dominated runs (mergeBlocks, tsp.cpp:202-269, is
+    O(L1*L2^2) there): minutes of reference CPU time each, so they live in their
+    own fixture (cli_large.json) and are regenerated only on request."""
+    cases = []
+    for (n, B, X, Y), Ps in {(4, 1024, 1000, 1000): (1, 8), (8, 1024, 1000, 1000): (8,)}.items():
+        for P in Ps:
+            r = run_cli([str(n), str(B), str(X), str(Y)], P)
+            cases.append({"args": [n, B, X, Y], "P": P, **r})
+            print(f"cli {n} {B} {X} {Y} P={P}: {r['lines'][-1] if r['lines'] else r}", flush=True)
+    return cases
+
+
 def main():
     if not os.path.exists(HARNESS):
         sys.exit("build the reference first: make -C oracle (needs /root/reference)")
+    # cli_large (~10 min of reference time) runs only when named
     which = set(sys.argv[1:]) or {"seed0", "dist", "ties", "random", "fold", "cli", "k1batch"}
     jobs = {
         "seed0": ("seed0_blocks.json", gen_seed0_blocks),
@@ -252,6 +266,7 @@ def main():
         "fold": ("fold.json", gen_fold),
         "cli": ("cli.json", gen_cli),
         "k1batch": ("k1_batches.json", gen_k1_batches),
+        "cli_large": ("cli_large.json", gen_cli_large),
     }
     for key in sorted(which):
         fname, fn = jobs[key]

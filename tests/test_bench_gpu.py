@@ -28,7 +28,9 @@ def test_bench_two_ranks_end_to_end(gpu_ctx):
     p = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
     assert p.returncode == 0, p.stderr[-2000:]
     line = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
-    assert line["n_gpus"] == 2 and line["config"]["global_blocks"] == 1000
+    ndev = tspgpu.device_count()
+    assert line["ranks"] == 2 and line["n_gpus"] == min(2, ndev) and line["config"]["global_blocks"] == 1000
+    assert line["ranks_per_gpu"] == (1 if ndev >= 2 else 2)
     assert line["config"]["blocks_rank0"] == 500  # the reference's deal of 1000 blocks over 2 ranks
     assert line["value"] > 0 and line["scaling"] == "strong"
     other = line["other_scaling"]
@@ -46,3 +48,6 @@ def test_bench_two_ranks_end_to_end(gpu_ctx):
     assert k2s["cost"] == wide_cost and k2s["tour"] == [int(x) for x in wide_tour]
     k2 = line["k2_single_instance"]
     assert "error" not in k2 and k2["ranks"] == 2 and k2["cost"] == 3871.1947567096445
+    # every rank one device chain, the winner from the all-reduced device tie key
+    rule = k2["device_tie_rule"]
+    assert rule["used"] == 1 and rule["phases"] == 1 and rule["record_gather"] == 0 and rule["chained"] == 1, rule

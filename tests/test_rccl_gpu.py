@@ -45,13 +45,17 @@ def _cities_file(tmp_path):
 
 def _parse(out):
     cost = tour = exch = None
+    winner = None
     for ln in out.splitlines():
+        if ln.startswith("winner "):
+            winner = ln.split()[1:]
         if ln.startswith("optimal cost "):
             cost = float(ln.split()[2])
         if ln.startswith("tour "):
             tour = [int(x) for x in ln.split()[1:]]
         if " exchange " in ln:
             exch = ln.rsplit(" exchange ", 1)[1].strip()
+    assert winner == ["tie-key", "chained", "1"], out  # (the device tie key; every shard one chain)
     return cost, tour, exch
 
 
@@ -87,8 +91,16 @@ from bench import Shard
 ctx = tspgpu.Context(device=0)
 d = Shard(16, 1, 0, 1).distances()[0]
 cost, tour, st = search_dist.solve_sharded(ctx, d, group=dist.group.WORLD)
+import numpy as np
+rng = np.random.default_rng(4)
+xy = rng.integers(0, 4, size=(14, 2)) * 1.0
+dl = tspgpu.distance_matrix([[(i, xy[i, 0], xy[i, 1]) for i in range(14)]])[0]
+cl, tl, sl = search_dist.solve_sharded(ctx, dl, group=dist.group.WORLD)
+c1, t1, _ = tspgpu.search_solve(ctx, dl)
 print(json.dumps({"cost": cost, "tour": [int(x) for x in tour], "backend": st["backend"],
-                  "exchanges": st["exchanges"], "world": st["world"]}))
+                  "exchanges": st["exchanges"], "world": st["world"], "phases": st["phases"], "tie": st["tie"],
+                  "record_gather": st["record_gather"], "lattice_same": bool(cl == c1 and list(tl) == list(t1)),
+                  "lattice_tie": sl["tie"], "lattice_gather": sl["record_gather"]}))
 dist.destroy_process_group()
 """
 
@@ -103,3 +115,6 @@ def test_search_dist_world1_nccl_group():
     r = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
     assert r["backend"] == "nccl" and r["world"] == 1 and r["exchanges"] >= 1
     assert r["cost"] == GOLD_COST and r["tour"] == GOLD_TOUR
+    # the winner from the RCCL all-reduce of the device tie key: one phase, no record gather
+    assert r["phases"] == 1 and r["tie"] == 1 and r["record_gather"] == 0
+    assert r["lattice_same"] and r["lattice_tie"] == 1 and r["lattice_gather"] == 0

@@ -234,7 +234,6 @@ def test_chained_search_with_tree_bound_above_18(gpu_ctx, monkeypatch, n):
     assert c2 == c0 and t2.tolist() == t0.tolist()
     if n == 22:  # (without the tree bound the 28-city search takes seconds)
         monkeypatch.setenv("TSPGPU_SEARCH_MST", "0")
-        monkeypatch.setenv("TSPGPU_CHAIN_MAXN", "32")
         c3, t3, _ = tspgpu.search_solve(gpu_ctx, d)
         assert c3 == c0 and t3.tolist() == t0.tolist()
 
@@ -262,19 +261,67 @@ def test_sharded_on_one_gpu(gpu_ctx, nshards):
         S.close()
 
 
-def test_solve_sharded_single_process(gpu_ctx):
-    """search_dist's round driver with one rank (exchange is a no-op)."""
+def test_solve_sharded_single_process(gpu_ctx, monkeypatch):
+    """search_dist's driver with one rank (exchanges are no-ops): the shard as
+    one device chain and the winner from the device tie key (one phase, no
+    record read), also on tie-heavy lattices; step by step (chain off) with an
+    exchange every step or every 4 steps."""
     rng = np.random.default_rng(5)
-    xy = rng.uniform(0, 1000, size=(15, 2))
-    d = O.distance_matrix([(i, xy[i, 0], xy[i, 1]) for i in range(15)])
-    oc, ot = O.solve_block(d)
+    for kind in ("random", "lattice", "lattice"):
+        xy = rng.uniform(0, 1000, size=(15, 2)) if kind == "random" else rng.integers(0, 4, size=(15, 2)) * 1.0
+        d = O.distance_matrix([(i, xy[i, 0], xy[i, 1]) for i in range(15)])
+        oc, ot = O.solve_block(d)
+        cost, tour, st = search_dist.solve_sharded(gpu_ctx, d)
+        assert cost == oc and tour.tolist() == ot, st
+        assert st["chained"] == 1 and st["exchanges"] == 1, st
+        assert st["phases"] == 1 and st["tie"] == 1 and st["record_gather"] == 0, st
+    monkeypatch.setenv("TSPGPU_SEARCH_CHAIN", "0")
     cost, tour, st = search_dist.solve_sharded(gpu_ctx, d, exchange_every=1)
     assert cost == oc and tour.tolist() == ot, st
-    assert st["exchanges"] == st["rounds"] >= 1
-    # the default batches 4 steps per exchange: same answer, fewer exchanges
+    assert st["chained"] == 0 and st["exchanges"] == st["rounds"] >= 1 and st["tie"] == 1
+    # 4 steps per exchange: same answer, fewer exchanges
     cost, tour, st4 = search_dist.solve_sharded(gpu_ctx, d)
     assert cost == oc and tour.tolist() == ot, st4
     assert st4["exchange_every"] == 4 and 1 <= st4["exchanges"] <= st4["rounds"] // 4 + 1
+
+
+@pytest.mark.parametrize("n", [22, 26])
+def test_solve_sharded_two_word_keys(gpu_ctx, n):
+    """n - 1 > 20 inner cities: the tie key spans two words (w0, then w1 among
+    the holders of the least w0); the sharded driver's answer equals the
+    one-GPU search's."""
+    from bench import k2_instance
+
+    d = np.asarray(k2_instance(n, 7))
+    c0, t0, _ = tspgpu.search_solve(gpu_ctx, d)
+    cost, tour, st = search_dist.solve_sharded(gpu_ctx, d)
+    assert cost == c0 and tour.tolist() == t0.tolist(), st
+    assert st["tie"] == 1 and st["record_gather"] == 0 and st["chained"] == 1, st
+
+
+def test_chain_tie_slot_abi(gpu_ctx):
+    """tspgpu_search_chain + tspgpu_search_tie_slot on shards run one after
+    another: the MIN of the shards' keys at the MIN of their incumbents is
+    tsp()'s tour (tspgpu_tie_tour certifies it)."""
+    rng = np.random.default_rng(3)
+    xy = rng.integers(0, 4, size=(13, 2)).astype(np.float64)
+    d = O.distance_matrix([(i, xy[i, 0], xy[i, 1]) for i in range(13)])
+    ub, _ = tspgpu.heuristic_tour(d)
+    shards = [tspgpu.Search(gpu_ctx, d, shard=s, nshards=3) for s in range(3)]
+    for S in shards:
+        S.set_bound(ub)
+        assert S.chain()
+    opt = min(S.counters()[0] for S in shards)
+    slots = [S.tie_slot(opt) for S in shards]
+    assert not any(ovf for _, _, _, ovf in slots)
+    w0 = min(w for f, w, _, _ in slots if f)
+    rc, tour = tspgpu.tie_tour(d, w0, 0, tspgpu.bits_cost(opt, tspgpu.F64))
+    oc, ot = O.solve_block(d)
+    assert rc == 0 and tspgpu.bits_cost(opt, tspgpu.F64) == oc and tour.tolist() == ot
+    # the slot of a cost no shard recorded
+    assert all(not S.tie_slot(opt + 1)[0] for S in shards)
+    for S in shards:
+        S.close()
 
 
 def test_overflow_falls_back_to_second_phase(gpu_ctx, monkeypatch):

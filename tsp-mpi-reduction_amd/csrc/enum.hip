@@ -445,7 +445,12 @@ __global__ __launch_bounds__(256) void tail_kernel(SearchArgs a)
     const V *ga = static_cast<const V *>(a.amin);
     for (int i = threadIdx.x; i < n * n; i += blockDim.x) dl[(i / n) * kTRow + i % n] = gd[i];
     for (int i = threadIdx.x; i < n; i += blockDim.x) am[i] = ga[i];
+    // a chained search whose level overflowed is abandoned: its tail slots may
+    // hold paths nobody wrote (stale or uninitialised memory), so none is read
+    __shared__ uint32_t dead;
+    if (threadIdx.x == 0) dead = a.overflow ? __hip_atomic_load(a.overflow, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
     __syncthreads();
+    if (dead) return;  // (block-uniform)
 
     const unsigned int claimed = __hip_atomic_load(a.tail_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const uint32_t count = claimed < a.tail_cap ? claimed : a.tail_cap;
@@ -862,7 +867,13 @@ __global__ __launch_bounds__(256) void expand_kernel(SearchArgs a)
         for (int i = threadIdx.x; i < n; i += blockDim.x) dm[kSearchMaxN * kTRow + i] = a.mst[n * n + i];
         if (threadIdx.x == 0) dm[kSearchMaxN * kTRow + kSearchMaxN] = a.mst[n * n + n];
     }
+    // chained levels: once a level has overflowed, the later ones return at
+    // once — the input slots an overflowing block reserved were never written
+    // (they hold stale or uninitialised paths) and must not be read
+    __shared__ uint32_t dead;
+    if (threadIdx.x == 0) dead = a.overflow ? __hip_atomic_load(a.overflow, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
     __syncthreads();
+    if (dead) return;  // (block-uniform)
 
     // the next step counts its children into the other counter word (no host memset per step)
     if (a.out_next && blockIdx.x == 0 && threadIdx.x == 0) *a.out_next = 0u;

@@ -257,8 +257,9 @@ hipError_t launch_to_paths(const SearchArgs &a);  // a.in (seeds) -> a.fout
 hipError_t launch_expand(const SearchArgs &a, bool f64);
 hipError_t launch_tail(const SearchArgs &a, bool f64, int grid);
 hipError_t launch_persist(const SearchArgs &a, bool f64, int grid);
-// the optimum's tie slot -> out[0..4] (search.hip tie_lookup_kernel)
-hipError_t launch_tie_lookup(const SearchArgs &a, unsigned long long *out);
+// the tie slot of *cost (null: of the incumbent) -> out[0..4] (search.hip
+// tie_lookup_kernel): found, w0, the sub-slot's (w0, w1), overflow
+hipError_t launch_tie_lookup(const SearchArgs &a, unsigned long long *out, const unsigned long long *cost = nullptr);
 // statistics sums, counter words, tie slot and the first records -> pinned
 // host memory in one launch (search.hip fetch_kernel; layout there)
 hipError_t launch_fetch(const SearchArgs &a, const unsigned long long *words, unsigned long long *out,

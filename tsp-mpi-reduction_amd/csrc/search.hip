@@ -1110,9 +1110,11 @@ __global__ __launch_bounds__(kSearchThreads) void persist_kernel(SearchArgs a)
 // The optimum's tie slot: out[0] = 1 if a slot holds cost *a.inc, out[1] =
 // its least w0, out[2..3] = (w0, least w1) of that w0's sub-slot (two-word
 // keys), out[4] = the overflow flag.  One wave.
-__global__ __launch_bounds__(64) void tie_lookup_kernel(SearchArgs a, unsigned long long *out)
+__global__ __launch_bounds__(64) void tie_lookup_kernel(SearchArgs a, unsigned long long *out, int at_inc,
+                                                        unsigned long long cost)
 {
-    const unsigned long long opt = __hip_atomic_load(a.inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned long long opt =
+        at_inc ? __hip_atomic_load(a.inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : cost;
     const int lane = (int)threadIdx.x;
     if (lane == 0) {
         out[0] = 0;
@@ -1190,9 +1192,9 @@ hipError_t launch_fetch(const SearchArgs &a, const unsigned long long *words, un
     return hipGetLastError();
 }
 
-hipError_t launch_tie_lookup(const SearchArgs &a, unsigned long long *out)
+hipError_t launch_tie_lookup(const SearchArgs &a, unsigned long long *out, const unsigned long long *cost)
 {
-    hipLaunchKernelGGL(tie_lookup_kernel, dim3(1), dim3(64), 0, a.stream, a, out);
+    hipLaunchKernelGGL(tie_lookup_kernel, dim3(1), dim3(64), 0, a.stream, a, out, cost ? 0 : 1, cost ? *cost : 0ull);
     return hipGetLastError();
 }
 

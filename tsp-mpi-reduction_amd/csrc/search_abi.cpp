@@ -150,6 +150,9 @@ struct tspgpu_search {
     // search_solve: the chained run enqueues the solve's readbacks (counters,
     // statistics, records, tie slot) before its one synchronisation
     bool fetch = false, fetched = false;
+    // the fetch buffer still reflects the device state (a finished chain and
+    // nothing run or written since): counters, tie slot and records read from it
+    bool fresh = false;
 };
 
 namespace {
@@ -617,6 +620,7 @@ int tspgpu_search_info(const tspgpu_search *s, int *depth, uint64_t *items, uint
 int tspgpu_search_set_bound(tspgpu_search *s, double bound)
 {
     if (!s) return -EINVAL;
+    s->fresh = false;
     unsigned long long w;
     if (s->dtype == TSPGPU_F64) {
         if (!(bound >= 0.0)) return -EINVAL;
@@ -830,6 +834,7 @@ int tspgpu_search_start(tspgpu_search *s) { return s ? search_start(s, true) : -
 static int search_start(tspgpu_search *s, bool sync)
 {
     (void)hipSetDevice(s->ctx->device);
+    s->fresh = false;
     if (int rc = ensure_items(s, 0, s->local_items + 1)) return rc;
     SearchArgs a = args_of(s);
     a.out = s->d_items[0];
@@ -969,6 +974,7 @@ static int frontier_step(tspgpu_search *s, uint64_t *pending)
 int tspgpu_search_step(tspgpu_search *s, uint64_t *pending)
 {
     if (!s) return -EINVAL;
+    s->fresh = false;
     if (s->frontier) return frontier_step(s, pending);
     if (s->pending == 0) {
         if (pending) *pending = 0;
@@ -1034,7 +1040,49 @@ static hipError_t enqueue_fetch(tspgpu_search *s)
 // process against 0.95-2.8 ms step by step, same nodes and answers,
 // profiles/r03/k2_chain_maxn.log)
 constexpr int kChainMaxN = 32;
-static int run_chain(tspgpu_search *s, bool *done)
+// The tie certificate's prefix DP on the GPU (K1-wide): G[{t1..tj}][tj] is
+// the closing min of the sub-instance over the cities 0, t1..tj whose closing
+// edges are 0 from tj and BIG from every other city (BIG above any path:
+// the min is G + 0, exact).  Up to kTieGpuMax cities (K1-wide's table: 1 GB
+// at 26 cities, 2.4 ms); host Held-Karp below kTieHostMax (it grows as
+// j^2 2^j: 0.6 M steps at 12 cities, 17 M at 16).
+constexpr int kTieGpuMax = 26, kTieHostMax = 12;
+static int gpu_prefix(void *user, const double *d, int n, const int32_t *t, int j, double *g)
+{
+    const int m = j + 1;
+    if (m < 3 || m > kTieGpuMax) return -ERANGE;
+    double mx = 0.0;
+    for (int i = 0; i < n * n; ++i) mx = std::max(mx, d[i]);
+    const double big = mx * (m + 1) + 1.0;
+    if ((double)m * big >= (double)INT_MAX) return -ERANGE;
+    std::vector<double> sub((size_t)m * m);
+    auto city = [&](int a) { return a == 0 ? 0 : t[a]; };
+    for (int a = 0; a < m; ++a)
+        for (int b = 0; b < m; ++b)
+            sub[(size_t)a * m + b] = a == b ? 0.0 : (b == 0 ? (a == j ? 0.0 : big) : d[city(a) * n + city(b)]);
+    std::vector<int32_t> tour(m + 1);
+    return tspgpu_solve_instance(static_cast<tspgpu_ctx *>(user), sub.data(), m, g, tour.data(), nullptr);
+}
+
+int tspgpu_tie_tour_gpu(tspgpu_ctx *ctx, const void *dist, int dtype, int n, uint64_t w0, uint64_t w1,
+                        uint64_t cost_bits, int32_t *tour_out)
+{
+    if (!ctx) return -EINVAL;
+    return tspgpu::host::tie_tour(dist, dtype, n, w0, w1, cost_bits, tour_out, true, gpu_prefix, ctx, kTieHostMax);
+}
+
+static bool chainable(const tspgpu_search *s)
+{
+    // above 18 cities only with the tree bound (its frontiers are small; without
+    // it a 32-city chain overflows its level buffers and reruns step by step)
+    return s->frontier && !s->noprune && s->chain && s->kernel != 3 && s->n <= (s->mst_on ? kChainMaxN : 18);
+}
+
+// every `every` levels (0: never) hook(user, stream, incumbent word) enqueues
+// an exchange of the incumbent on the search's stream (e.g. an RCCL
+// all-reduce MIN): the same number of calls on every shard of one instance
+static int run_chain(tspgpu_search *s, bool *done, int every = 0, tspgpu_level_hook hook = nullptr,
+                     void *user = nullptr)
 {
     *done = false;
     // ping-pong buffer capacity (TSPGPU_SEARCH_CHAIN_CAP_LOG2: tests force the overflow fallback)
@@ -1052,8 +1100,13 @@ static int run_chain(tspgpu_search *s, bool *done)
     int chain_grid = 2;
     if (const char *ev = std::getenv("TSPGPU_CHAIN_FPB")) chain_fpb = (uint32_t)std::atoi(ev);  // (sweeps)
     if (const char *ev = std::getenv("TSPGPU_CHAIN_GRID")) chain_grid = std::max(1, std::atoi(ev));
-    if (levels < 1 || s->local_items + 1 > kChainCap) return 0;
     hipStream_t st = s->ctx->stream;
+    const int hooks = hook && every > 0 && levels > 1 ? (levels - 1) / every : 0;
+    if (levels < 1 || s->local_items + 1 > kChainCap) {
+        // (not chained: the exchanges still pair up with the other shards')
+        for (int k = 0; k < hooks; ++k) hook(user, st, s->d_words + 1);
+        return 0;
+    }
     const bool f64 = s->dtype == TSPGPU_F64;
     // words 10..13 zeroed before the seeds (10..12: level counters, 13:
     // overflow); word 14 keeps the incumbent the chain starts from
@@ -1089,9 +1142,12 @@ static int run_chain(tspgpu_search *s, bool *done)
         a.fin_per_block = chain_fpb;
         a.max_grid = s->ctx->cu_count * chain_grid;  // (blocks beyond the level's runs only stage tables and leave)
         e = launch_expand(a, f64);
+        if (e == hipSuccess && hooks && (l + 1) % every == 0 && (l + 1) / every <= hooks)
+            hook(user, st, s->d_words + 1);  // (enqueued between two levels)
     }
     if (e == hipSuccess) {
         SearchArgs a = args_of(s);
+        a.overflow = reinterpret_cast<unsigned int *>(s->d_words + 13);  // (an abandoned chain folds no tails)
         e = launch_tail(a, f64, s->ctx->cu_count * 8);
     }
     (void)hipEventRecord(s->e1, st);
@@ -1233,11 +1289,8 @@ int tspgpu_search_run_all(tspgpu_search *s)
     if (!s) return -EINVAL;
     if (s->noprune && s->enum_kernel) return run_enum(s);
     if (s->kernel == 3 && !s->noprune) return run_persist(s);
-    // above 18 cities only with the tree bound (its frontiers are small; without
-    // it a 32-city chain overflows its level buffers and reruns step by step)
-    int chain_max = s->mst_on ? kChainMaxN : 18;
-    if (const char *ev = std::getenv("TSPGPU_CHAIN_MAXN")) chain_max = std::atoi(ev);  // (sweeps)
-    if (s->frontier && !s->noprune && s->nshards == 1 && s->n <= chain_max && s->chain) {
+    s->fresh = false;
+    if (s->nshards == 1 && chainable(s)) {
         bool done = false;
         int rc = run_chain(s, &done);
         if (rc || done) return rc;
@@ -1253,6 +1306,63 @@ int tspgpu_search_run_all(tspgpu_search *s)
                          (unsigned long long)pending, (unsigned long long)s->tails, s->ms);
     }
     return rc;
+}
+
+int tspgpu_search_chain(tspgpu_search *s, int exchange_every, tspgpu_level_hook hook, void *user, int *done)
+{
+    if (!s || !done || exchange_every < 0) return -EINVAL;
+    *done = 0;
+    (void)hipSetDevice(s->ctx->device);
+    s->fresh = false;
+    if (!chainable(s)) {
+        // the same number of exchanges as a chained shard would enqueue
+        const int levels = s->frontier ? s->n - 1 - s->tail_len - s->depth : 0;
+        const int hooks = hook && exchange_every > 0 && levels > 1 ? (levels - 1) / exchange_every : 0;
+        for (int k = 0; k < hooks; ++k) hook(user, s->ctx->stream, s->d_words + 1);
+        return 0;
+    }
+    s->fetch = true;
+    bool ok = false;
+    const int rc = run_chain(s, &ok, exchange_every, hook, user);
+    s->fetch = false;
+    if (rc) return rc;
+    *done = ok ? 1 : 0;
+    s->fresh = ok && s->fetched;
+    return 0;
+}
+
+int tspgpu_search_tie_slot(tspgpu_search *s, uint64_t cost_bits, tspgpu_tie_slot *out)
+{
+    if (!s || !out) return -EINVAL;
+    std::memset(out, 0, sizeof *out);
+    if (!s->tie_on) {
+        out->overflow = 1;  // (no device tie rule: the records decide)
+        return 0;
+    }
+    (void)hipSetDevice(s->ctx->device);
+    unsigned long long local[5] = {};
+    const unsigned long long *t = local;
+    if (s->fresh && fetch_buf(s)[4 + 1] == cost_bits) {
+        t = fetch_buf(s) + 20;  // read with the chain's synchronisation
+    } else {
+        SearchArgs a = args_of(s);
+        const unsigned long long c = cost_bits;
+        unsigned long long *h = s->h_cnt ? s->h_cnt + 8 : local;
+        hipError_t e = launch_tie_lookup(a, tie_words(s), &c);
+        if (e == hipSuccess)
+            e = hipMemcpyAsync(h, tie_words(s), 5 * sizeof(unsigned long long), hipMemcpyDeviceToHost, s->ctx->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(s->ctx->stream);
+        if (e != hipSuccess) return herr(e);
+        t = h;
+    }
+    const bool two = s->n - 1 > 20;
+    out->found = t[0] == 1 ? 1 : 0;
+    out->overflow = t[4] != 0 ? 1 : 0;
+    out->w0 = out->found ? t[1] : ~0ull;
+    out->w1 = out->found && two ? t[3] : 0ull;
+    // two-word keys: the least w0's own sub-slot must hold its w1
+    if (out->found && two && t[2] != t[1]) out->overflow = 1;
+    return 0;
 }
 
 int tspgpu_search_timing(const tspgpu_search *s, double *kernel_ms, int *rounds)
@@ -1271,7 +1381,13 @@ int tspgpu_search_counters(tspgpu_search *s, uint64_t *incumbent_bits, uint64_t 
     (void)hipSetDevice(s->ctx->device);
     unsigned long long w[5];
     uint64_t st[4];
-    if (int rc = read_words_stats(s, w, st)) return rc;
+    if (s->fresh) {  // (the chain's readback)
+        const unsigned long long *f = fetch_buf(s);
+        for (int i = 0; i < 4; ++i) st[i] = f[i];
+        for (int i = 0; i < 5; ++i) w[i] = f[4 + i];
+    } else if (int rc = read_words_stats(s, w, st)) {
+        return rc;
+    }
     if (incumbent_bits) *incumbent_bits = w[1];
     if (records) *records = (uint32_t)w[3];
     if (nodes) *nodes = st[0];
@@ -1281,6 +1397,7 @@ int tspgpu_search_counters(tspgpu_search *s, uint64_t *incumbent_bits, uint64_t 
 int tspgpu_search_reset_records(tspgpu_search *s, unsigned int capacity)
 {
     if (!s) return -EINVAL;
+    s->fresh = false;
     (void)hipSetDevice(s->ctx->device);
     hipError_t e = hipStreamSynchronize(s->ctx->stream);
     if (e == hipSuccess && capacity > s->rec_cap) {
@@ -1303,7 +1420,9 @@ static int records_of(tspgpu_search *s, uint64_t claimed, uint64_t cost_bits, ts
 {
     if (claimed > s->rec_cap) return -EOVERFLOW;
     std::vector<SearchRecord> h(claimed);
-    if (claimed) {
+    if (claimed && s->fresh && claimed <= std::min(kSpecRecs, s->rec_cap)) {  // (the chain's readback)
+        std::memcpy(h.data(), fetch_buf(s) + kFetchWords, sizeof(SearchRecord) * claimed);
+    } else if (claimed) {
         hipError_t e = hipMemcpy(h.data(), s->d_rec, sizeof(SearchRecord) * claimed, hipMemcpyDeviceToHost);
         if (e != hipSuccess) return herr(e);
     }
@@ -1435,7 +1554,7 @@ static int search_solve(tspgpu_ctx *c, const void *dist, int dtype, int n, doubl
         const bool two = n - 1 > 20;
         if (!two || tie_h[2] == tie_h[1])
             tie_done = tspgpu::host::tie_tour(dist, dtype, n, two ? tie_h[2] : tie_h[1], two ? tie_h[3] : 0ull, inc,
-                                              tie_tour.data(), recs > s->rec_cap) == 0;
+                                              tie_tour.data(), recs > s->rec_cap, gpu_prefix, c, kTieHostMax) == 0;
     }
     // the record buffer overflowed: search again with the optimum as the bound,
     // so only optimal tours are recorded, into a buffer of the size now known

@@ -446,7 +446,7 @@ double prefix_min(const double *d, int n, const int32_t *t, int j)
 // (no value one ulp lower could round to the same next fold); -EAGAIN: the
 // fold matches but that is not proven; -EINVAL: not a tour of cost opt
 template <typename V>
-int tie_certify(const V *d, int n, const int32_t *t, V opt, bool allow_dp)
+int tie_certify(const V *d, int n, const int32_t *t, V opt, bool allow_dp, PrefixDp dp, void *user, int host_max)
 {
     const int N = n - 1;
     std::vector<V> F(N + 2);
@@ -485,7 +485,13 @@ int tie_certify(const V *d, int n, const int32_t *t, V opt, bool allow_dp)
             if (next < F[j + 1]) continue;
             // a fold just below F[j] would round to the same next fold: the
             // prefix is proven minimal only by the DP over its own cities
-            if (!allow_dp || j > kTieDpMax || !(prefix_min(d, n, t, j) == F[j])) return -EAGAIN;
+            if (!allow_dp) return -EAGAIN;
+            double g = 0.0;
+            if (j <= std::min(host_max, kTieDpMax))
+                g = prefix_min(d, n, t, j);
+            else if (!dp || dp(user, d, n, t, j, &g) != 0)
+                return -EAGAIN;
+            if (!(g == F[j])) return -EAGAIN;
         }
     }
     return 0;
@@ -518,7 +524,7 @@ int validate_search(const void *dist, int dtype, int n)
 }
 
 int tie_tour(const void *dist, int dtype, int n, uint64_t w0, uint64_t w1, uint64_t cost_bits, int32_t *tour_out,
-             bool allow_dp)
+             bool allow_dp, PrefixDp dp, void *user, int host_max)
 {
     int rc = validate_search(dist, dtype, n);
     if (rc) return rc;
@@ -528,9 +534,10 @@ int tie_tour(const void *dist, int dtype, int n, uint64_t w0, uint64_t w1, uint6
     if (dtype == TSPGPU_F64) {
         double opt;
         std::memcpy(&opt, &cost_bits, 8);
-        rc = tie_certify(static_cast<const double *>(dist), n, t.data(), opt, allow_dp);
+        rc = tie_certify(static_cast<const double *>(dist), n, t.data(), opt, allow_dp, dp, user, host_max);
     } else {
-        rc = tie_certify(static_cast<const int32_t *>(dist), n, t.data(), (int32_t)(uint32_t)cost_bits, allow_dp);
+        rc = tie_certify(static_cast<const int32_t *>(dist), n, t.data(), (int32_t)(uint32_t)cost_bits, allow_dp, dp,
+                         user, host_max);
     }
     if (rc != -EINVAL) std::memcpy(tour_out, t.data(), sizeof(int32_t) * (n + 1));
     return rc;

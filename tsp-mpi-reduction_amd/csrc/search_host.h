@@ -18,9 +18,14 @@ int validate_search(const void *dist, int dtype, int n);
 void lagrange_pi(const std::vector<double> &D, int n, std::vector<double> &best_pi);
 // Held-Karp 1-tree weights (the tree bound of the expand kernel)
 void held_karp_pi(const std::vector<double> &D, int n, std::vector<double> &best_pi);
+// G[{t1..tj}][tj] of the reference's DP for the certificate's prefix checks
+// above the host's own limit (e.g. K1-wide on the GPU): 0 and *g, or an error
+// (the certificate then stays unproven)
+typedef int (*PrefixDp)(void *user, const double *d, int n, const int32_t *t, int j, double *g);
 // tspgpu_tie_tour; allow_dp = false skips the prefix DP of the certificate
-// (a cheap check when the records can decide anyway)
+// (a cheap check when the records can decide anyway); prefixes of up to
+// host_max cities by Held-Karp on the host, longer ones through dp (if any)
 int tie_tour(const void *dist, int dtype, int n, uint64_t w0, uint64_t w1, uint64_t cost_bits, int32_t *tour_out,
-             bool allow_dp);
+             bool allow_dp, PrefixDp dp = nullptr, void *user = nullptr, int host_max = 16);
 }  // namespace host
 }  // namespace tspgpu

@@ -271,14 +271,38 @@ struct Result {
     double kernel_ms = 0.0;
     int rounds = 0;
     const char *exchange = "none";  // how the shards' incumbents were combined (K2)
+    int tie = 0;      // K2 over shards: the winner came from the device tie keys (no record read)
+    int chained = 0;  // K2 over shards: every shard ran as one device chain
 };
 
 // K2 over G shards of this process, shard g on device g mod (visible
-// devices), with an all-reduce MIN of the incumbent every `every` frontier
-// steps: RCCL (uint64 MIN in place on the device words, over xGMI) when every
-// shard has its own device — also for G = 1 with force_rccl, a one-rank
-// communicator — else (shards sharing a device: a rehearsal on a smaller box;
-// RCCL takes one rank per device) the same MIN through the host.
+// devices).  Each shard runs as ONE device chain (tspgpu_search_chain: every
+// frontier level enqueued back to back, one synchronisation) with the
+// incumbent exchanged between levels IN THE STREAM: an RCCL all-reduce MIN
+// (uint64, over xGMI) enqueued every kChainExchangeLevels levels, no host
+// round trip.  A shard too large to chain runs step by step, with the same
+// all-reduce every `every` steps.  RCCL needs every shard on its own device
+// (also G = 1 with force_rccl: a one-rank communicator); shards that share a
+// device (a rehearsal on a smaller box) exchange through the host between
+// steps instead.  The winner: after the last exchange the
+// incumbent is the optimum on every shard; each shard reads its device tie
+// slot at it, then an all-reduce MIN of w0 (and of w1 among the holders of
+// that w0) picks the least key, certified once (tspgpu_tie_tour).  Only when
+// that certificate cannot be given are the optimal records read and passed
+// to tspgpu_select_tour.
+constexpr int kChainExchangeLevels = 2;
+
+struct ChainHook {
+    ncclComm_t comm;
+    int rc;
+};
+
+void chain_exchange(void *user, void *stream, void *word)
+{
+    auto *h = static_cast<ChainHook *>(user);
+    if (ncclAllReduce(word, word, 1, ncclUint64, ncclMin, h->comm, (hipStream_t)stream) != ncclSuccess) h->rc = -EIO;
+}
+
 int search_multi(const Instance &in, int G, bool force_rccl, Result &res)
 {
     int ndev = tspgpu_device_count();
@@ -298,11 +322,17 @@ int search_multi(const Instance &in, int G, bool force_rccl, Result &res)
     std::vector<std::vector<tspgpu_tour_record>> recs(G);
     std::vector<uint64_t> nodes(G, 0), opt(G, 0);
     std::vector<double> ms(G, 0.0);
-    std::vector<int> rounds(G, 0);
+    std::vector<int> rounds(G, 0), chained(G, 0);
+    std::vector<tspgpu_tie_slot> slots(G);
     std::atomic<int> busy{0}, failed{0};
+    // the key exchange without RCCL: every shard's slot, combined by shard 0
+    uint64_t key[3] = {~0ull, ~0ull, 0};  // least w0, least w1 of its holders, any overflow
+    std::vector<int32_t> tie_tour(in.n + 1, 0);
+    std::atomic<int> tie_ok{0};
     // frontier steps between two incumbent exchanges (TSPGPU_EXCHANGE_EVERY, default 4)
     int every = 4;
     if (const char *e = std::getenv("TSPGPU_EXCHANGE_EVERY")) every = std::max(1, std::atoi(e));
+    const bool two = in.n - 1 > 20;
     std::barrier sync(G);
     std::vector<std::thread> th;
     for (int g = 0; g < G; ++g) {
@@ -315,12 +345,22 @@ int search_multi(const Instance &in, int G, bool force_rccl, Result &res)
             int rc = tspgpu_ctx_create(&o, &ctx);
             if (!rc) rc = tspgpu_search_create(ctx, dist_ptr(in), in.dtype, in.n, g, G, 0, &s);
             if (!rc) rc = tspgpu_search_set_bound(s, ub);
-            if (!rc) rc = tspgpu_search_start(s);
             hipStream_t st = ctx ? (hipStream_t)tspgpu_stream(ctx) : nullptr;
-            // every shard must join every all-reduce: if one could not start, none enters the loop
+            // every shard must join every all-reduce: if one could not start, none goes on
             if (rc) failed.store(1);
             sync.arrive_and_wait();
-            uint64_t pending = 1;
+            uint64_t pending = 0;
+            if (!failed.load()) {
+                ChainHook hk{rccl ? comms[g] : nullptr, 0};
+                int done = 0;
+                rc = tspgpu_search_chain(s, kChainExchangeLevels, rccl ? chain_exchange : nullptr, &hk, &done);
+                if (!rc) rc = hk.rc;
+                chained[g] = done;
+                if (!rc && !done) {
+                    rc = tspgpu_search_start(s);
+                    pending = 1;
+                }
+            }
             for (; !failed.load();) {
                 // up to `every` steps of this shard, then one exchange (the same
                 // count on every shard, so the all-reduces pair up)
@@ -341,8 +381,14 @@ int search_multi(const Instance &in, int G, bool force_rccl, Result &res)
                     }
                     sync.arrive_and_wait();
                     const uint64_t m = host_min.load();
-                    if (w && m < inc && hipMemcpyAsync(w, &m, 8, hipMemcpyHostToDevice, st) != hipSuccess) rc = -EIO;
-                    if (st) (void)hipStreamSynchronize(st);
+                    if (s && m < inc) {
+                        double b = 0.0;
+                        if (in.dtype == TSPGPU_F64)
+                            std::memcpy(&b, &m, 8);
+                        else
+                            b = (double)(int32_t)(uint32_t)m;
+                        if (int r = tspgpu_search_set_bound(s, b)) rc = r;
+                    }
                 }
                 sync.arrive_and_wait();
                 const bool more = busy.load() > 0;
@@ -355,7 +401,54 @@ int search_multi(const Instance &in, int G, bool force_rccl, Result &res)
             if (!rc && failed.load()) rc = -EIO;
             if (!rc) rc = tspgpu_search_counters(s, &inc, &nodes[g], &rec);
             opt[g] = inc;  // identical on every shard after the last all-reduce
-            if (!rc) {
+            // the winner: all-reduce MIN of the tie key (w0, then w1 among its holders)
+            tspgpu_tie_slot &ts = slots[g];
+            std::memset(&ts, 0, sizeof ts);
+            if (!rc) rc = tspgpu_search_tie_slot(s, inc, &ts);
+            if (rccl) {
+                unsigned long long *dk = nullptr;
+                unsigned long long hk[2] = {ts.found ? ts.w0 : ~0ull, ts.overflow ? 0ull : 1ull};
+                if (!rc && hipMalloc((void **)&dk, sizeof hk) != hipSuccess) rc = -ENOMEM;
+                // (a failed shard still joins the collectives, with neutral words)
+                if (dk) (void)hipMemcpyAsync(dk, hk, sizeof hk, hipMemcpyHostToDevice, st);
+                if (dk && ncclAllReduce(dk, dk, 2, ncclUint64, ncclMin, comms[g], st) != ncclSuccess) rc = -EIO;
+                if (dk) (void)hipMemcpyAsync(hk, dk, sizeof hk, hipMemcpyDeviceToHost, st);
+                if (st) (void)hipStreamSynchronize(st);
+                const uint64_t W0 = hk[0];
+                const bool clean = hk[1] == 1;
+                unsigned long long h1 = ts.found && ts.w0 == W0 ? ts.w1 : ~0ull;
+                if (two && dk) {
+                    (void)hipMemcpyAsync(dk, &h1, 8, hipMemcpyHostToDevice, st);
+                    if (ncclAllReduce(dk, dk, 1, ncclUint64, ncclMin, comms[g], st) != ncclSuccess) rc = -EIO;
+                    (void)hipMemcpyAsync(&h1, dk, 8, hipMemcpyDeviceToHost, st);
+                    (void)hipStreamSynchronize(st);
+                }
+                if (dk) (void)hipFree(dk);
+                if (g == 0) {
+                    key[0] = W0;
+                    key[1] = two ? h1 : 0;
+                    key[2] = clean ? 0 : 1;
+                }
+            } else {
+                sync.arrive_and_wait();
+                if (g == 0) {
+                    for (int q = 0; q < G; ++q) {
+                        if (slots[q].overflow) key[2] = 1;
+                        if (slots[q].found && slots[q].w0 < key[0]) key[0] = slots[q].w0;
+                    }
+                    for (int q = 0; q < G && two; ++q)
+                        if (slots[q].found && slots[q].w0 == key[0] && slots[q].w1 < key[1]) key[1] = slots[q].w1;
+                    if (!two) key[1] = 0;
+                }
+            }
+            sync.arrive_and_wait();
+            // certified once (shard 0, its prefix DPs on its GPU), then every
+            // shard knows whether its records are needed
+            if (g == 0 && !rc && !key[2] && key[0] != ~0ull &&
+                tspgpu_tie_tour_gpu(ctx, dist_ptr(in), in.dtype, in.n, key[0], key[1], opt[0], tie_tour.data()) == 0)
+                tie_ok.store(1);
+            sync.arrive_and_wait();
+            if (!rc && !tie_ok.load()) {
                 int cnt = 0;
                 recs[g].resize(rec);
                 rc = tspgpu_search_records(s, inc, recs[g].data(), (int)rec, &cnt);
@@ -371,12 +464,19 @@ int search_multi(const Instance &in, int G, bool force_rccl, Result &res)
     for (auto &c : comms) ncclCommDestroy(c);
     for (int rc : rcs)
         if (rc) return rc;  // incl. -EOVERFLOW (too many tied optima: use --solver k1)
-    std::vector<tspgpu_tour_record> all;
-    for (auto &r : recs) all.insert(all.end(), r.begin(), r.end());
     res.tour.assign(in.n + 1, 0);
-    if (int rc = tspgpu_select_tour(dist_ptr(in), in.dtype, in.n, all.data(), (int)all.size(), opt[0],
-                                    res.tour.data()))
-        return rc;
+    res.tie = tie_ok.load();
+    res.chained = 1;
+    for (int g = 0; g < G; ++g) res.chained &= chained[g];
+    if (res.tie) {
+        res.tour = tie_tour;
+    } else {
+        std::vector<tspgpu_tour_record> all;
+        for (auto &r : recs) all.insert(all.end(), r.begin(), r.end());
+        if (int rc = tspgpu_select_tour(dist_ptr(in), in.dtype, in.n, all.data(), (int)all.size(), opt[0],
+                                        res.tour.data()))
+            return rc;
+    }
     if (in.dtype == TSPGPU_F64)
         std::memcpy(&res.cost, &opt[0], 8);
     else
@@ -535,9 +635,11 @@ int main(int argc, char **argv)
         std::printf("search nodes %llu  rounds %d  kernel %.3f ms  %.3f Gnodes/s  wall %.3f ms  exchange %s\n",
                     (unsigned long long)res.nodes, res.rounds, res.kernel_ms,
                     res.kernel_ms > 0 ? res.nodes / res.kernel_ms / 1e6 : 0.0, wall, res.exchange);
-    else if (solver == "wide")
+    if (solver == "k2" && std::strcmp(res.exchange, "none") != 0)  // (the sharded driver)
+        std::printf("winner %s  chained %d\n", res.tie ? "tie-key" : "records", res.chained);
+    if (solver == "wide")
         std::printf("kernel %.3f ms  wall %.3f ms\n", res.kernel_ms, wall);
-    else
+    else if (solver != "k2" && solver != "enum")
         std::printf("wall %.3f ms\n", wall);
     if (verify && in.n <= TSPGPU_MAX_CITIES && solver != "k1") {
         Result k1;

@@ -1,22 +1,24 @@
 """Multi-GPU driver of K2 (one process per GPU, torch.distributed).
 
 One instance is split over the ranks of a process group: rank r searches the
-seed prefixes p with p mod W == r (libtspgpu's static shard); inside its GPU
-the work runs in rounds (a device queue hands items to lanes, items that
-exceed their budget are split and re-queued).  Between rounds the ranks
-all-reduce(MIN) the 64-bit incumbent word (IEEE bits of the
-f64 cost or the integer cost; both order like signed int64 for the
-non-negative costs the ABI accepts), so every GPU prunes with the best tour
-found anywhere.  At the end: all-reduce(MIN) of the incumbent = the optimum,
-all-gather of each rank's records at that cost (the optimal set O), and every
-rank applies the DP's tie rule (tspgpu_select_tour) to O — the same answer as
-tsp() / K1 on one GPU.
+seed prefixes p with p mod W == r (libtspgpu's static shard), as ONE chained
+device run (every frontier level enqueued back to back, one synchronisation)
+or, for searches too large to chain, step by step with an all-reduce(MIN) of
+the 64-bit incumbent word (IEEE bits of the f64 cost or the integer cost;
+both order like signed int64 for the non-negative costs the ABI accepts)
+every few steps, so every GPU prunes with the best tour found anywhere.  At
+the end: all-reduce(MIN) of the incumbent = the optimum, then all-reduce(MIN)
+of each rank's device tie key at that cost (the reverse-lex least optimal
+tour it found; w0, then w1 among its holders), certified once on every rank
+(tspgpu_tie_tour) — the same tour as tsp() / K1 on one GPU, SURVEY.md §8(e).
+Records are gathered only when the certificate cannot be given.
 
-With the "nccl" backend (RCCL on ROCm) the exchange is a device all-reduce
+With the "nccl" backend (RCCL on ROCm) the exchanges are device all-reduces
 over xGMI; "gloo" runs the same logic over host tensors (CPU tests, or several
 ranks sharing one GPU).  This replaces the reference's hand-rolled binary
 MPI_Send/MPI_Recv tree (tsp.cpp:52-134) for the one step of the search that
-needs a reduction: picking the global best tour.
+needs a reduction: picking the global best tour (tsp.cpp:483-499's closing
+min and its tie rule, across shards).
 """
 from __future__ import annotations
 
@@ -36,15 +38,40 @@ def _word_tensor(value: int, device):
     return torch.tensor([value], dtype=torch.int64, device=device)
 
 
+_I64_MAX = (1 << 63) - 1
+
+
+def _key_i64(u: int) -> int:
+    """u64 -> int64, order-preserving (torch all-reduce MIN is signed)."""
+    v = (u ^ (1 << 63)) & ((1 << 64) - 1)
+    return v - (1 << 64) if v >= (1 << 63) else v
+
+
+def _key_u64(v: int) -> int:
+    return ((v + (1 << 64)) % (1 << 64)) ^ (1 << 63)
+
+
 def solve_sharded(ctx, dist, group=None, depth: int = 0, device=None, exchange_every: int | None = None):
     """Search one instance over the ranks of `group` (None: the default group,
     or a single process when torch.distributed is not initialised).
 
-    Every rank runs `exchange_every` steps of its own shard (fewer once it runs
-    out of work), then all ranks exchange once: ONE all-reduce(MIN) of the pair
-    (incumbent word, -busy).  The count is the same on every rank, so the
-    collectives always pair up; a rank without work only joins the exchanges.
-    Default: TSPGPU_EXCHANGE_EVERY or 4.
+    1. The multi-start bound: each rank runs 1/W of the starts, all-reduce MIN.
+    2. Each rank runs its shard as ONE device chain (tspgpu_search_chain: the
+       seeds, every frontier level and the tail fold back to back, one
+       synchronisation).  A shard too large to chain runs step by step
+       instead, `exchange_every` steps between exchanges (default
+       TSPGPU_EXCHANGE_EVERY or 4).
+    3. Exchanges: ONE all-reduce(MIN) of the pair (incumbent word, -busy) —
+       the same count on every rank, so the collectives pair up; after the
+       last one (nobody busy) the MIN is the optimum.
+    4. The winner: each rank reads its device tie slot at the
+       optimum (the reverse-lex least optimal tour it found), all-reduce MIN
+       of w0 (ranks without one send the maximum), then of w1 among the
+       holders of that w0 (two-word keys, n > 21), and every rank certifies
+       the winning key once (tspgpu_tie_tour): tsp()'s tour with no record
+       leaving any rank.  Only when a tie table overflowed or the certificate
+       fails do the ranks fall back to gathering their optimal records for the
+       host tie rule (a second search first if records were lost).
 
     Returns (cost, tour (n+1,), stats dict); identical on every rank."""
     import torch
@@ -60,23 +87,15 @@ def solve_sharded(ctx, dist, group=None, depth: int = 0, device=None, exchange_e
     # an nccl group runs every collective, even with one rank (a one-rank RCCL
     # communicator: the device all-reduce path exercised on a one-GPU box)
     collective = world > 1 or backend == "nccl"
+    ncoll = [0]
 
-    def allmin(word: int) -> int:
+    def allmin(vals):
         if not collective:
-            return word
-        t = _word_tensor(word, device)
+            return [int(v) for v in vals]
+        t = torch.tensor(vals, dtype=torch.int64, device=device)
         tdist.all_reduce(t, op=tdist.ReduceOp.MIN, group=group)
-        return int(t.item())
-
-    def allmin2(a: int, b: int):
-        if not collective:
-            return a, b
-        import torch
-
-        t = torch.tensor([a, b], dtype=torch.int64, device=device)
-        tdist.all_reduce(t, op=tdist.ReduceOp.MIN, group=group)
-        v = t.tolist()
-        return int(v[0]), int(v[1])
+        ncoll[0] += 1
+        return [int(x) for x in t.tolist()]
 
     if exchange_every is None:
         exchange_every = int(os.environ.get("TSPGPU_EXCHANGE_EVERY", "4"))
@@ -104,15 +123,18 @@ def solve_sharded(ctx, dist, group=None, depth: int = 0, device=None, exchange_e
         if collective:
             # then the MIN of the ranks' costs: all starts' bound at 1/W of the host time
             ub_r, _ = heur["v"]
-            word = tspgpu.cost_bits(ub_r, S.dtype) if ub_r is not None else (1 << 63) - 1
-            ub = tspgpu.bits_cost(allmin2(word, 0)[0], S.dtype)
+            word = tspgpu.cost_bits(ub_r, S.dtype) if ub_r is not None else _I64_MAX
+            ub = tspgpu.bits_cost(allmin([word])[0], S.dtype)
         else:
             ub, _ = heur["v"]
         S.set_bound(ub)
         t0 = time.perf_counter()
         exchanges = 0
-        S.start()
-        busy = 1
+        chained = S.chain()
+        busy = 0
+        if not chained:
+            S.start()
+            busy = 1
         while True:
             # up to exchange_every steps on this rank (while it has work), then
             # the exchange: incumbent MIN and "anyone still busy" (MIN of the
@@ -122,73 +144,114 @@ def solve_sharded(ctx, dist, group=None, depth: int = 0, device=None, exchange_e
                     break
                 busy = 1 if S.step() else 0
             inc, _, _ = S.counters()
-            best, anybusy = allmin2(inc, -busy)
+            best, anybusy = allmin([inc, -busy])
             exchanges += 1
             if best < inc:
                 S.set_bound(tspgpu.bits_cost(best, S.dtype))
             if anybusy == 0:
                 break
-        inc, nodes, recs = S.counters()
-        opt = allmin(inc)
-        phases = 1
-
-        def local_records():
-            try:
-                return S.records(opt), 0
-            except tspgpu.TspGpuError as e:
-                if e.code != -errno.EOVERFLOW:
-                    raise
-                return [], 1
-
-        mine, lost = local_records()
-        if allmin(-lost) < 0:
-            # some rank lost records: search again with the optimum as the bound,
-            # so only optimal tours are recorded, in a buffer of the needed size
-            phases = 2
-            S.reset_records(int(min(max(recs, 1 << 16), 1 << 22)))
-            S.set_bound(tspgpu.bits_cost(opt, S.dtype))
-            S.run_all()
-            # the device node counter is cumulative over both phases (start does
-            # not reset it), so it already holds phase 1 + phase 2
-            _, nodes, recs = S.counters()
-            mine, lost = local_records()
-            if allmin(-lost) < 0:
-                # too many optimal tours to enumerate (coincident cities): the DP
-                # (K1-wide on this rank's GPU) gives tsp()'s tour directly for n <= 31
-                if S.n > 31:
-                    raise tspgpu.TspGpuError(-errno.EOVERFLOW, "solve_sharded")
-                c, t, _ = ctx.solve_instance(np.asarray(dist, dtype=np.float64))
-                cost = float(c) if S.dtype == tspgpu.F64 else int(c)
-                stats = {"nodes": int(nodes), "rank_nodes": int(nodes), "optimal_tours": 0, "depth": S.depth,
-                         "items": S.items, "phases": phases, "fallback": 1, "kernel_ms": S.timing()[0],
-                         "wall_s": time.perf_counter() - t0, "exchanges": exchanges, "world": world,
-                         "backend": backend}
-                return cost, t, stats
-        blob = np.frombuffer(b"".join(bytes(r) for r in mine), dtype=np.uint8) if mine else np.zeros(0, np.uint8)
-        if collective:
-            parts = [None] * world
-            tdist.all_gather_object(parts, blob, group=group)
-            node_t = _word_tensor(int(nodes), device)
-            tdist.all_reduce(node_t, op=tdist.ReduceOp.SUM, group=group)
-            total_nodes = int(node_t.item())
-        else:
-            parts, total_nodes = [blob], nodes
-        rsz = ctypes_sizeof_record()
-        allrec = []
-        for p in parts:
-            for i in range(0, len(p), rsz):
-                allrec.append(tspgpu.TourRecord.from_buffer_copy(bytes(p[i:i + rsz])))
+        opt = best  # (the last exchange: every rank finished, so the MIN is the optimum)
+        _, nodes, recs = S.counters()
+        node_t = None
+        if collective:  # (overlaps the tie exchange)
+            node_t = torch.tensor([int(nodes)], dtype=torch.int64, device=device)
+            node_w = tdist.all_reduce(node_t, op=tdist.ReduceOp.SUM, group=group, async_op=True)
         cost = tspgpu.bits_cost(opt, S.dtype)
-        tour = tspgpu.select_tour(dist, allrec, cost)
+
+        # the device tie rule across ranks: MIN of w0, then of w1 among its holders
+        found, w0, w1, ovf = S.tie_slot(opt) if inc <= opt else (False, 0, 0, False)
+        two = S.n - 1 > 20
+        k0 = _key_i64(w0) if found else _I64_MAX
+        K0, nov = allmin([k0, -int(ovf)])
+        K1 = 0
+        if two:
+            (K1,) = allmin([_key_i64(w1) if found and k0 == K0 else _I64_MAX])
+        tie, tour = 0, None
+        if nov == 0 and K0 != _I64_MAX:
+            w = (_key_u64(K0), _key_u64(K1) if two else 0, cost)
+            rc, t = tspgpu.tie_tour_gpu(ctx, dist, *w) if ctx is not None else tspgpu.tie_tour(dist, *w)
+            if rc == 0:
+                tie, tour = 1, t
+        phases, fallback, gathered, n_opt = 1, 0, 0, 0
+        if not tie:
+            tour, phases, fallback, nodes, n_opt = _records_winner(S, ctx, dist, opt, recs, nodes, allmin,
+                                                                  collective, group)
+            gathered = 1
+        total_nodes = int(nodes)
+        if node_t is not None:
+            node_w.wait()
+            if phases == 1:
+                total_nodes = int(node_t.item())
+            # (phases 2: _records_winner summed phase 1 + 2 over the ranks; the
+            # K1-wide fallback reports this rank's nodes)
         wall = time.perf_counter() - t0
         kernel_ms, rounds = S.timing()
-        stats = {"nodes": total_nodes, "rank_nodes": int(nodes), "optimal_tours": len(allrec), "depth": S.depth,
-                 "items": S.items, "phases": phases, "fallback": 0, "kernel_ms": kernel_ms, "rounds": rounds,
-                 "wall_s": wall,
-                 "exchanges": exchanges, "exchange_every": exchange_every, "world": world, "backend": backend}
+        stats = {"nodes": total_nodes, "rank_nodes": int(S.counters()[1]),
+                 "optimal_tours": n_opt, "depth": S.depth,
+                 "items": S.items, "phases": phases, "fallback": fallback, "kernel_ms": kernel_ms, "rounds": rounds,
+                 "wall_s": wall, "tie": tie, "record_gather": gathered, "chained": int(chained),
+                 "collectives": ncoll[0], "exchanges": exchanges, "exchange_every": exchange_every, "world": world,
+                 "backend": backend}
         return cost, tour, stats
     finally:
         S.close()
+
+
+def _records_winner(S, ctx, dist, opt, recs, nodes, allmin, collective, group):
+    """Fallback winner: every rank's records at the optimum gathered for the
+    host tie rule (a second search first when some rank lost records; K1-wide
+    when too many tours tie).  -> (tour, phases, fallback, nodes, |O|)."""
+    import torch
+    import torch.distributed as tdist
+
+    def local_records():
+        try:
+            return S.records(opt), 0
+        except tspgpu.TspGpuError as e:
+            if e.code != -errno.EOVERFLOW:
+                raise
+            return [], 1
+
+    phases = 1
+    mine, lost = local_records()
+    if allmin([-lost])[0] < 0:
+        # some rank lost records: search again with the optimum as the bound,
+        # so only optimal tours are recorded, in a buffer of the needed size
+        phases = 2
+        S.reset_records(int(min(max(recs, 1 << 16), 1 << 22)))
+        S.set_bound(tspgpu.bits_cost(opt, S.dtype))
+        S.run_all()
+        # the device node counter is cumulative over both phases (start does
+        # not reset it), so it already holds phase 1 + phase 2
+        _, nodes, recs = S.counters()
+        mine, lost = local_records()
+        if allmin([-lost])[0] < 0:
+            # too many optimal tours to enumerate (coincident cities): the DP
+            # (K1-wide on this rank's GPU) gives tsp()'s tour directly for n <= 31
+            if S.n > 31:
+                raise tspgpu.TspGpuError(-errno.EOVERFLOW, "solve_sharded")
+            _, t, _ = ctx.solve_instance(np.asarray(dist, dtype=np.float64))
+            return t, phases, 1, nodes, 0
+    blob = np.frombuffer(b"".join(bytes(r) for r in mine), dtype=np.uint8) if mine else np.zeros(0, np.uint8)
+    total_nodes = nodes
+    if collective:
+        parts = [None] * tdist.get_world_size(group)
+        tdist.all_gather_object(parts, blob, group=group)
+        if phases == 2:
+            dev = torch.device("cpu") if tdist.get_backend(group) != "nccl" else \
+                torch.device("cuda", torch.cuda.current_device())
+            t = torch.tensor([int(nodes)], dtype=torch.int64, device=dev)
+            tdist.all_reduce(t, op=tdist.ReduceOp.SUM, group=group)
+            total_nodes = int(t.item())
+    else:
+        parts = [blob]
+    rsz = ctypes_sizeof_record()
+    allrec = []
+    for p in parts:
+        for i in range(0, len(p), rsz):
+            allrec.append(tspgpu.TourRecord.from_buffer_copy(bytes(p[i:i + rsz])))
+    tour = tspgpu.select_tour(dist, allrec, tspgpu.bits_cost(opt, S.dtype))
+    return tour, phases, 0, total_nodes, len(allrec)
 
 
 def ctypes_sizeof_record() -> int:

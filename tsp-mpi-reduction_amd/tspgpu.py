@@ -29,10 +29,10 @@ EXPORTED_SYMBOLS = (
     # K2
     "tspgpu_search_solve", "tspgpu_search_enumerate", "tspgpu_search_create", "tspgpu_search_destroy", "tspgpu_search_info",
     "tspgpu_search_set_bound", "tspgpu_search_start", "tspgpu_search_step", "tspgpu_search_run_all",
-    "tspgpu_search_timing", "tspgpu_search_incumbent_device",
+    "tspgpu_search_timing", "tspgpu_search_incumbent_device", "tspgpu_search_chain", "tspgpu_search_tie_slot",
     "tspgpu_search_counters", "tspgpu_search_reset_records", "tspgpu_search_records", "tspgpu_heuristic_tour",
     "tspgpu_heuristic_tour_starts",
-    "tspgpu_select_tour", "tspgpu_tie_tour", "tspgpu_tie_key",
+    "tspgpu_select_tour", "tspgpu_tie_tour", "tspgpu_tie_tour_gpu", "tspgpu_tie_key",
     # K3
     "tspgpu_merge", "tspgpu_reduce",
     # K1-wide
@@ -60,6 +60,15 @@ class SearchStats(ctypes.Structure):
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+class TieSlot(ctypes.Structure):
+    """tspgpu_tie_slot: a shard's least tie key at one cost."""
+    _fields_ = [("w0", ctypes.c_uint64), ("w1", ctypes.c_uint64), ("found", ctypes.c_int),
+                ("overflow", ctypes.c_int)]
+
+
+LEVEL_HOOK = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p)
 
 
 class City(ctypes.Structure):
@@ -142,6 +151,8 @@ def lib():
         L.tspgpu_search_incumbent_device.argtypes = [vp]
         L.tspgpu_search_incumbent_device.restype = vp
         L.tspgpu_search_counters.argtypes = [vp, u64p, u64p, u64p]
+        L.tspgpu_search_chain.argtypes = [vp, ctypes.c_int, LEVEL_HOOK, vp, ctypes.POINTER(ctypes.c_int)]
+        L.tspgpu_search_tie_slot.argtypes = [vp, ctypes.c_uint64, ctypes.POINTER(TieSlot)]
         L.tspgpu_search_reset_records.argtypes = [vp, ctypes.c_uint]
         L.tspgpu_search_records.argtypes = [vp, ctypes.c_uint64, ctypes.POINTER(TourRecord), ctypes.c_int,
                                             ctypes.POINTER(ctypes.c_int)]
@@ -151,6 +162,8 @@ def lib():
                                          ctypes.c_uint64, ip]
         L.tspgpu_tie_tour.argtypes = [vp, ctypes.c_int, ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
                                       ip]
+        L.tspgpu_tie_tour_gpu.argtypes = [vp, vp, ctypes.c_int, ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64,
+                                          ctypes.c_uint64, ip]
         L.tspgpu_tie_key.argtypes = [ctypes.c_int, ip, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]
         cp = ctypes.POINTER(City)
         L.tspgpu_solve_instance.argtypes = [vp, dp, ctypes.c_int, dp, ip, dp]
@@ -566,6 +579,16 @@ def tie_tour(dist, w0: int, w1: int, cost):
     return rc, tour
 
 
+def tie_tour_gpu(ctx: "Context", dist, w0: int, w1: int, cost):
+    """tie_tour with the certificate's prefix DPs on the context's GPU
+    (tspgpu_tie_tour_gpu): (rc, tour)."""
+    d, dt = _search_dist(dist)
+    n = d.shape[0]
+    tour = np.zeros(n + 1, dtype=np.int32)
+    rc = lib().tspgpu_tie_tour_gpu(ctx.handle, d.ctypes.data, dt, n, w0, w1, cost_bits(cost, dt), _ip(tour))
+    return rc, tour
+
+
 class Search:
     """One instance (or shard `shard` of `nshards`) of the K2 search on a Context."""
 
@@ -612,6 +635,25 @@ class Search:
 
     def run_all(self):
         self._check(lib().tspgpu_search_run_all(self.handle), "tspgpu_search_run_all")
+
+    def chain(self, exchange_every: int = 0, hook=None) -> bool:
+        """This shard's whole search chained on the device with one
+        synchronisation (tspgpu_search_chain); False: too large to chain, the
+        shard is at its starting state (continue with start/step).  hook(stream,
+        word): called every `exchange_every` levels to enqueue an exchange of
+        the device incumbent word on the search's stream."""
+        done = ctypes.c_int()
+        cb = LEVEL_HOOK(lambda _u, st, w: hook(st, w)) if hook else LEVEL_HOOK()
+        self._check(lib().tspgpu_search_chain(self.handle, exchange_every if hook else 0, cb, None,
+                                              ctypes.byref(done)), "tspgpu_search_chain")
+        return bool(done.value)
+
+    def tie_slot(self, bits: int):
+        """The device tie rule's least key at cost word `bits` on this shard:
+        (found, w0, w1, overflow)."""
+        t = TieSlot()
+        self._check(lib().tspgpu_search_tie_slot(self.handle, bits, ctypes.byref(t)), "tspgpu_search_tie_slot")
+        return bool(t.found), int(t.w0), int(t.w1), bool(t.overflow)
 
     def timing(self):
         ms, rounds = ctypes.c_double(), ctypes.c_int()
