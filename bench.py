@@ -353,6 +353,59 @@ def cli_wall(n, reps=3):
     return best
 
 
+# the merge-dominated runs, where mergeBlocks
+# (tsp.cpp:202-269, O(L1*L2^2) through rotate) is the program; the reference's
+# own times on the survey's 8-core Xeon
+K3_CASES = ((4, 1024, 1, 7100), (4, 1024, 8, 30900), (8, 1024, 8, 237056))
+
+
+def k3_merge(reps=2):
+    """K3 (the GPU mergeBlocks) where it dominates: `bin/tsp n 1024 1000
+    1000` with TSP_NPROCS=P, the program's own clock (tsp.cpp:275-276,
+    360-363) and its TSP_STATS phase split (block search, merge), the final
+    cost checked against the reference's (tests/golden/cli_large.json), next
+    to the reference's measured time (237 s for ./tsp 8 1024
+    on 8 ranks)."""
+    if not os.path.exists(TSP_BIN):
+        return {"error": "bin/tsp not built"}
+    gold = {}
+    try:
+        with open(os.path.join(ROOT, "tests", "golden", "cli_large.json")) as f:
+            for c in json.load(f)["data"]:
+                gold[(tuple(c["args"]), c["P"])] = c["lines"][-1].rsplit(" ", 1)[1]
+    except (OSError, KeyError, ValueError):
+        pass
+    pat = re.compile(r"TSP ran in (\d+) ms for (\d+) cities and the trip cost ([0-9.]+)")
+    st = re.compile(r"block search ([0-9.]+) ms.*merge ([0-9.]+) ms, total ([0-9.]+) ms")
+    out = {}
+    for n, B, P, ref_ms in K3_CASES:
+        env = dict(os.environ, TSP_NPROCS=str(P), TSP_STATS="1")
+        for k in ("PMI_SIZE", "PMI_RANK", "OMPI_COMM_WORLD_SIZE", "OMPI_COMM_WORLD_RANK"):
+            env.pop(k, None)
+        best = None
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            p = subprocess.run([TSP_BIN, str(n), str(B), "1000", "1000"], capture_output=True, text=True,
+                               timeout=300, env=env)
+            wall = (time.perf_counter() - t0) * 1e3
+            m, q = pat.search(p.stdout), st.search(p.stderr)
+            if p.returncode != 0 or not m:
+                best = {"error": f"rc={p.returncode} {p.stderr[-200:]}"}
+                break
+            r = {"program_ms": int(m.group(1)), "process_wall_ms": wall, "cost": m.group(3),
+                 "block_search_ms": float(q.group(1)) if q else None, "merge_ms": float(q.group(2)) if q else None}
+            if best is None or r["program_ms"] < best["program_ms"]:
+                best = r
+        if "cost" in best:
+            g = gold.get(((n, B, 1000, 1000), P))
+            best["reference_cost"] = g
+            best["same_cost"] = g == best["cost"] if g else None
+            best["reference_ms_survey_xeon"] = ref_ms
+            best["speedup_vs_reference"] = ref_ms / max(best["program_ms"], 1)
+        out[f"./tsp {n} {B} 1000 1000 P={P}"] = best
+    return out
+
+
 def reference_multiblock(n=16, blocks=8, procs=(1, 2, 4, 8)):
     """The reference's own multi-block runs beside the drop-in, on this box:
     `mpirun -np P ./tsp n B 1000 1000` (the reference, oracle/_ref/tsp, one
@@ -771,6 +824,7 @@ def main():
     ap.add_argument("--no-pmc", action="store_true")
     ap.add_argument("--no-tto", action="store_true", help="skip the time-to-optimal probes")
     ap.add_argument("--no-k2", action="store_true", help="skip the K2 search probes")
+    ap.add_argument("--no-k3", action="store_true", help="skip the K3 merge-dominated CLI runs")
     ap.add_argument("--no-ref-multiblock", action="store_true",
                     help="skip the reference-vs-drop-in `./tsp 16 8` runs at P = 1/2/4/8")
     ap.add_argument("--plumbing", action="store_true", help=argparse.SUPPRESS)
@@ -968,7 +1022,12 @@ def main():
             k2["pmc"] = k2_pmc(cu, peaks, k2["bb_nodes_expanded"], k2["kernel_ms"])
         except Exception as e:  # noqa: BLE001
             k2["pmc"] = {"error": f"{type(e).__name__}: {e}"}
-    cpu = cpu_opt = refmb = None
+    cpu = cpu_opt = refmb = k3 = None
+    if world == 1 and not args.no_k3:
+        try:
+            k3 = k3_merge()
+        except Exception as e:  # noqa: BLE001
+            k3 = {"error": f"{type(e).__name__}: {e}"}
     if world == 1 and not args.no_ref_multiblock:
         try:
             refmb = reference_multiblock(n)
@@ -1017,6 +1076,7 @@ def main():
         "k2_single_instance": k2,
         "k2_strong_scaling": k2s,
         "k2_exhaustive_14": exh,
+        "k3_merge": k3,
         "config4_tsplib": tsplib,
         "k1_i32_extension": i32,
         "device": devname,

@@ -343,6 +343,25 @@ int tspgpu_merge(tspgpu_ctx *ctx, const tspgpu_city *p1, int L1, double c1, cons
 int tspgpu_reduce(tspgpu_ctx *ctx, const tspgpu_city *paths, int L, const double *costs, int nblocks, int nprocs,
                   double *final_cost, char *log, int logcap);
 
+/* ---------------------------------------------------------------------------
+ * Tuning and test knobs.  The defaults are the measured best; a knob changes
+ * how the kernels run (K1 variant / configuration, buffer sizes, a bound
+ * switched off for an A/B run, a fallback forced by a test), never the
+ * answer.  Process-wide, read where each is used (K1 knobs at context
+ * creation, K2 knobs at search creation).  The library reads no environment
+ * variable of its own: the documented TSP_* variables belong to bin/tsp.
+ * Names: K1, TILED_CFG, WG_PER_CU, THREADS, LDS_TABLE_MAX_N, WIDE_PULL,
+ * SEARCH_{KERNEL, HUNGRY, MIN_SPLIT, WALL_S, RING_LOG2, REFILL, TAIL, SUFFIX,
+ * TWO_EDGE, CHAIN, LAGRANGE, MST, MST_MINREM, TAIL_CAP_LOG2, EXPAND_LOG2,
+ * BUDGET, TIE, PAGEABLE, TAILS, CHAIN_CAP_LOG2, CHAIN_POISON, DEBUG, DEPTH,
+ * RECORD_CAP}, CHAIN_FPB, CHAIN_GRID, ENUM_KERNEL, ENUM_WG_PER_CU,
+ * HEURISTIC_THREADS, HEURISTIC_ALL_STARTS (csrc/tuning.cpp).
+ * ------------------------------------------------------------------------- */
+/* 0, -ENOENT (no such knob) or -EINVAL (not finite) */
+int tspgpu_tuning_set(const char *name, double value);
+/* back to the default (name NULL: every knob) */
+int tspgpu_tuning_clear(const char *name);
+
 #ifdef __cplusplus
 }
 #endif

@@ -22,3 +22,24 @@ def gpu_ctx():
     ctx = tspgpu.Context(device=0)
     yield ctx
     ctx.close()
+
+
+class Knobs:
+    """Tuning / test knobs of libtspgpu (tspgpu_tuning_set), reset after the test."""
+
+    def set(self, name, value):
+        import tspgpu
+
+        tspgpu.tune(name, float(value))
+
+    def clear(self, name=None):
+        import tspgpu
+
+        tspgpu.untune(name)
+
+
+@pytest.fixture
+def knobs():
+    k = Knobs()
+    yield k
+    k.clear()

@@ -99,3 +99,33 @@ def test_distance_matrix_threaded_batch_bit_exact():
     d = tspgpu.distance_matrix(blocks)
     for b in range(0, 1200, 37):
         assert np.array_equal(d[b], O.distance_matrix(blocks[b]))
+
+
+def test_tuning_knobs_abi():
+    """Knobs go through tspgpu_tuning_set only: unknown names are refused,
+    known ones set and cleared (the library reads no environment variable)."""
+    L = tspgpu.lib()
+    assert L.tspgpu_tuning_set(b"NO_SUCH_KNOB", 1.0) == -errno.ENOENT
+    assert L.tspgpu_tuning_set(b"SEARCH_CHAIN", float("nan")) == -errno.EINVAL
+    assert L.tspgpu_tuning_set(b"SEARCH_CHAIN", 0.0) == 0
+    assert L.tspgpu_tuning_clear(b"SEARCH_CHAIN") == 0
+    assert L.tspgpu_tuning_clear(b"NO_SUCH_KNOB") == -errno.ENOENT
+    assert L.tspgpu_tuning_clear(None) == 0
+
+
+def test_library_reads_no_environment():
+    """The product sources (libtspgpu, bin/tsp_search) read no TSPGPU_*
+    environment variable; bin/tsp reads only the documented TSP_* ones and the
+    launchers' rank variables."""
+    import glob
+    import re
+
+    pkg = os.path.join(ROOT, "tsp-mpi-reduction_amd")
+    srcs = glob.glob(os.path.join(pkg, "csrc", "*")) + glob.glob(os.path.join(pkg, "host", "*.cpp"))
+    for f in srcs:
+        if os.path.isdir(f):
+            continue
+        for name in re.findall(r'getenv\("([A-Z0-9_]+)"\)', open(f).read()):
+            assert name.startswith("TSP_") or name in ("PMI_SIZE", "PMI_RANK", "OMPI_COMM_WORLD_SIZE",
+                                                      "OMPI_COMM_WORLD_RANK", "PMIX_NAMESPACE", "SLURM_JOB_ID",
+                                                      "SLURM_STEP_ID", "PMI_ID", "PMIX_RANK"), (f, name)

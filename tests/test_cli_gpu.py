@@ -14,6 +14,10 @@ import tspgpu
 
 MS = re.compile(r"^TSP ran in \d+ ms ")
 CASES = O.load_golden("cli.json")
+# SURVEY Appendix B's merge-dominated runs, where K3 (the GPU mergeBlocks)
+# carries the program: ./tsp 4 1024 at P=1/8, ./tsp 8 1024 at P=8 (the
+# reference: 7.1 / 30.9 / 237 s on 8 cores)
+LARGE = O.load_golden("cli_large.json")
 
 
 def run_tsp(args, P):
@@ -42,6 +46,14 @@ def test_cli_argument_errors(case):
 @pytest.mark.parametrize("case", [c for c in CASES if not c.get("error_case")],
                          ids=lambda c: "-".join(map(str, c["args"])) + f"-P{c['P']}")
 def test_cli_matches_reference(case):
+    rc, lines, err = run_tsp(case["args"], case["P"])
+    assert rc == case["rc"], err
+    assert split(lines) == split(case["lines"])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", LARGE, ids=lambda c: "-".join(map(str, c["args"])) + f"-P{c['P']}")
+def test_cli_merge_dominated_matches_reference(case):
     rc, lines, err = run_tsp(case["args"], case["P"])
     assert rc == case["rc"], err
     assert split(lines) == split(case["lines"])

@@ -89,6 +89,9 @@ def test_merge_matches_reference_fold(case):
 
 
 CLI = [c for c in O.load_golden("cli.json") if not c.get("error_case")]
+# SURVEY Appendix B's merge-dominated runs (4 1024 at P=1/8, 8 1024 at P=8): the
+# reference needs minutes (O(L1*L2^2) mergeBlocks), the host replay seconds
+CLI += O.load_golden("cli_large.json")
 
 
 @pytest.mark.parametrize("case", CLI, ids=lambda c: "-".join(map(str, c["args"])) + f"-P{c['P']}")

@@ -4,9 +4,9 @@ switches that happen inside one call:
 
   * n = 16, B >= 2 x CUs: the restructured sub-cube kernel (variant 6,
     hk_sub.h) is the default; variant 5 (hk_tiled.h), variant 4 (ping-pong +
-    parent words) and variant 2 are forced through TSPGPU_K1 (read when a
+    parent words) and variant 2 are forced through the knob K1 (read when a
     context is created);
-  * every variant-5/6 configuration compiled in (k1_cfg.h, TSPGPU_TILED_CFG),
+  * every variant-5/6 configuration compiled in (k1_cfg.h, knob TILED_CFG),
     f64 and i32;
   * tie-heavy blocks (integer lattice 0..3, 0..39) mixed with random ones;
   * one block solved alone (variant 2: fewer blocks than CUs) equals its row
@@ -52,20 +52,17 @@ def _oracle_all(key, d):
 
 
 def _ctx(variant=None, cfg=None):
-    old = {k: os.environ.get(k) for k in ("TSPGPU_K1", "TSPGPU_TILED_CFG")}
+    # (K1 knobs are read at context creation)
     try:
-        for k, v in (("TSPGPU_K1", variant), ("TSPGPU_TILED_CFG", cfg)):
+        for k, v in (("K1", variant), ("TILED_CFG", cfg)):
             if v is None:
-                os.environ.pop(k, None)
+                tspgpu.untune(k)
             else:
-                os.environ[k] = str(v)
+                tspgpu.tune(k, v)
         return tspgpu.Context(device=0)
     finally:
-        for k, v in old.items():
-            if v is None:
-                os.environ.pop(k, None)
-            else:
-                os.environ[k] = v
+        tspgpu.untune("K1")
+        tspgpu.untune("TILED_CFG")
 
 
 def _check(ctx, d, ref, vb=8):

@@ -102,11 +102,11 @@ def test_k2_matches_k1(gpu_ctx):
 
 
 @pytest.mark.parametrize("budget", ["1", "64"])
-def test_tiny_budget_splits_everything(gpu_ctx, monkeypatch, budget):
+def test_tiny_budget_splits_everything(gpu_ctx, budget, knobs):
     """Round kernel (2), budgets of 1 and 64 iterations: nearly every item is
     cut and re-queued many times; the answer must not change."""
-    monkeypatch.setenv("TSPGPU_SEARCH_KERNEL", "2")
-    monkeypatch.setenv("TSPGPU_SEARCH_BUDGET", budget)
+    knobs.set("SEARCH_KERNEL", "2")
+    knobs.set("SEARCH_BUDGET", budget)
     rng = np.random.default_rng(int(budget))
     for n in (9, 12):
         xy = rng.uniform(0, 1000, size=(n, 2))
@@ -119,18 +119,17 @@ def test_tiny_budget_splits_everything(gpu_ctx, monkeypatch, budget):
 
 
 @pytest.mark.parametrize("mode", ["donate_always", "small_ring", "kernel1", "kernel2"])
-def test_search_kernels_and_hand_off_stress(gpu_ctx, monkeypatch, mode):
+def test_search_kernels_and_hand_off_stress(gpu_ctx, mode, knobs):
     """Persistent search with a donation at every chance (every busy lane
     splits its root level whenever it may), with a 64-item ring (donations
     mostly refused by the capacity check), and the two round kernels: same
     cost and tour as the oracle, tie-heavy and random instances."""
-    env = {"donate_always": {"TSPGPU_SEARCH_HUNGRY": "-1000000000", "TSPGPU_SEARCH_MIN_SPLIT": "0"},
-           "small_ring": {"TSPGPU_SEARCH_RING_LOG2": "6", "TSPGPU_SEARCH_HUNGRY": "-1000000000",
-                          "TSPGPU_SEARCH_MIN_SPLIT": "0"},
-           "kernel1": {"TSPGPU_SEARCH_KERNEL": "1"}, "kernel2": {"TSPGPU_SEARCH_KERNEL": "2"}}[mode]
+    env = {"donate_always": {"SEARCH_HUNGRY": "-1000000000", "SEARCH_MIN_SPLIT": "0"},
+           "small_ring": {"SEARCH_RING_LOG2": "6", "SEARCH_HUNGRY": "-1000000000", "SEARCH_MIN_SPLIT": "0"},
+           "kernel1": {"SEARCH_KERNEL": "1"}, "kernel2": {"SEARCH_KERNEL": "2"}}[mode]
     for k, v in env.items():
-        monkeypatch.setenv(k, v)
-    monkeypatch.setenv("TSPGPU_SEARCH_WALL_S", "30")
+        knobs.set(k, v)
+    knobs.set("SEARCH_WALL_S", "30")
     rng = np.random.default_rng(len(mode))
     for n in (5, 9, 12, 14):
         for kind in ("ties", "random"):
@@ -146,7 +145,7 @@ def test_search_kernels_and_hand_off_stress(gpu_ctx, monkeypatch, mode):
 
 @pytest.mark.parametrize("mode", [("0", None, None), ("5", None, None), ("6", None, None), ("6", "8", "2"),
                                   ("5", "8", "1"), ("6", None, "2")])
-def test_frontier_search_modes(gpu_ctx, monkeypatch, mode):
+def test_frontier_search_modes(gpu_ctx, mode, knobs):
     """Frontier search (expand_kernel level by level, then the prefixes with
     5/6 cities left folded by tail_kernel) against the DFS rounds ("0"):
     default seed depth, shallow seeds (depth 1-2: many expansion levels) and
@@ -154,11 +153,11 @@ def test_frontier_search_modes(gpu_ctx, monkeypatch, mode):
     Same cost and tour as the oracle on tie-heavy, random and integer
     instances, n = 8..14."""
     tail, cap, depth = mode
-    monkeypatch.setenv("TSPGPU_SEARCH_TAIL", tail)
+    knobs.set("SEARCH_TAIL", tail)
     if cap is not None:
-        monkeypatch.setenv("TSPGPU_SEARCH_TAIL_CAP_LOG2", cap)
+        knobs.set("SEARCH_TAIL_CAP_LOG2", cap)
     if depth is not None:
-        monkeypatch.setenv("TSPGPU_SEARCH_DEPTH", depth)
+        knobs.set("SEARCH_DEPTH", depth)
     rng = np.random.default_rng(17 + int(tail) + (0 if cap is None else 7) + (0 if depth is None else 3))
     for n in (8, 9, 11, 13, 14):
         for kind in ("ties", "random", "int"):
@@ -174,29 +173,29 @@ def test_frontier_search_modes(gpu_ctx, monkeypatch, mode):
             assert (float(cost), tour.tolist()) == (oc, ot), (mode, n, kind, st)
 
 
-def test_frontier_16_golden(gpu_ctx, monkeypatch):
+def test_frontier_16_golden(gpu_ctx, knobs):
     """The reference's own 16-city instance through the frontier search with
     5- and 6-city register tails: golden cost bits and tour."""
     case = next(c for c in O.load_golden("seed0_blocks.json") if c["n"] == 16 and c["B"] == 1 and c["X"] == 1000)
     blk = _cities(case["cities"][0])
     d = tspgpu.distance_matrix([blk])[0]
     for tail in ("5", "6"):
-        monkeypatch.setenv("TSPGPU_SEARCH_TAIL", tail)
+        knobs.set("SEARCH_TAIL", tail)
         cost, tour, st = tspgpu.search_solve(gpu_ctx, d)
         assert cost == O.hexf(case["solutions"][0]["cost_hex"]), st
         assert [blk[t][0] for t in tour] == case["solutions"][0]["ids"], st
 
 
 @pytest.mark.parametrize("mode", ["chain", "steps", "chain_overflow"])
-def test_chained_small_search(gpu_ctx, monkeypatch, mode):
+def test_chained_small_search(gpu_ctx, mode, knobs):
     """Small single-shard searches run as chained frontier levels (one
     synchronisation); a level that overflows the ping-pong buffers falls back
     to the stepwise search.  All three give the reference's golden 16-city
     answer, and random / tie-heavy instances equal the oracle."""
     if mode == "steps":
-        monkeypatch.setenv("TSPGPU_SEARCH_CHAIN", "0")
+        knobs.set("SEARCH_CHAIN", "0")
     if mode == "chain_overflow":
-        monkeypatch.setenv("TSPGPU_SEARCH_CHAIN_CAP_LOG2", "8")
+        knobs.set("SEARCH_CHAIN_CAP_LOG2", "8")
     case = next(c for c in O.load_golden("seed0_blocks.json") if c["n"] == 16 and c["B"] == 1 and c["X"] == 1000)
     blk = _cities(case["cities"][0])
     d = tspgpu.distance_matrix([blk])[0]
@@ -213,7 +212,7 @@ def test_chained_small_search(gpu_ctx, monkeypatch, mode):
 
 
 @pytest.mark.parametrize("n", [22, 28])
-def test_chained_search_with_tree_bound_above_18(gpu_ctx, monkeypatch, n):
+def test_chained_search_with_tree_bound_above_18(gpu_ctx, n, knobs):
     """With the tree bound the chained levels run up to 32 cities: the same
     cost and tour as the stepwise search.  A chain whose level buffers
     overflow reruns step by step from its starting state: after a 32-city
@@ -224,16 +223,16 @@ def test_chained_search_with_tree_bound_above_18(gpu_ctx, monkeypatch, n):
 
     d = np.asarray(k2_instance(n, 3))
     c0, t0, _ = tspgpu.search_solve(gpu_ctx, d)
-    monkeypatch.setenv("TSPGPU_SEARCH_CHAIN", "0")
+    knobs.set("SEARCH_CHAIN", "0")
     c1, t1, _ = tspgpu.search_solve(gpu_ctx, d)
-    monkeypatch.delenv("TSPGPU_SEARCH_CHAIN")
+    knobs.clear("SEARCH_CHAIN")
     assert c0 == c1 and t0.tolist() == t1.tolist()
     tspgpu.search_solve(gpu_ctx, np.asarray(k2_instance(32, 35)))
-    monkeypatch.setenv("TSPGPU_SEARCH_CHAIN_CAP_LOG2", "10")
+    knobs.set("SEARCH_CHAIN_CAP_LOG2", "10")
     c2, t2, _ = tspgpu.search_solve(gpu_ctx, d)
     assert c2 == c0 and t2.tolist() == t0.tolist()
     if n == 22:  # (without the tree bound the 28-city search takes seconds)
-        monkeypatch.setenv("TSPGPU_SEARCH_MST", "0")
+        knobs.set("SEARCH_MST", "0")
         c3, t3, _ = tspgpu.search_solve(gpu_ctx, d)
         assert c3 == c0 and t3.tolist() == t0.tolist()
 
@@ -261,7 +260,7 @@ def test_sharded_on_one_gpu(gpu_ctx, nshards):
         S.close()
 
 
-def test_solve_sharded_single_process(gpu_ctx, monkeypatch):
+def test_solve_sharded_single_process(gpu_ctx, knobs):
     """search_dist's driver with one rank (exchanges are no-ops): the shard as
     one device chain and the winner from the device tie key (one phase, no
     record read), also on tie-heavy lattices; step by step (chain off) with an
@@ -275,7 +274,7 @@ def test_solve_sharded_single_process(gpu_ctx, monkeypatch):
         assert cost == oc and tour.tolist() == ot, st
         assert st["chained"] == 1 and st["exchanges"] == 1, st
         assert st["phases"] == 1 and st["tie"] == 1 and st["record_gather"] == 0, st
-    monkeypatch.setenv("TSPGPU_SEARCH_CHAIN", "0")
+    knobs.set("SEARCH_CHAIN", "0")
     cost, tour, st = search_dist.solve_sharded(gpu_ctx, d, exchange_every=1)
     assert cost == oc and tour.tolist() == ot, st
     assert st["chained"] == 0 and st["exchanges"] == st["rounds"] >= 1 and st["tie"] == 1
@@ -304,27 +303,29 @@ def test_chain_tie_slot_abi(gpu_ctx):
     another: the MIN of the shards' keys at the MIN of their incumbents is
     tsp()'s tour (tspgpu_tie_tour certifies it)."""
     rng = np.random.default_rng(3)
-    xy = rng.integers(0, 4, size=(13, 2)).astype(np.float64)
-    d = O.distance_matrix([(i, xy[i, 0], xy[i, 1]) for i in range(13)])
+    xy = rng.integers(0, 4, size=(15, 2)).astype(np.float64)  # (15 cities: a frontier search, so chained)
+    d = O.distance_matrix([(i, xy[i, 0], xy[i, 1]) for i in range(15)])
     ub, _ = tspgpu.heuristic_tour(d)
     shards = [tspgpu.Search(gpu_ctx, d, shard=s, nshards=3) for s in range(3)]
-    for S in shards:
-        S.set_bound(ub)
-        assert S.chain()
-    opt = min(S.counters()[0] for S in shards)
-    slots = [S.tie_slot(opt) for S in shards]
-    assert not any(ovf for _, _, _, ovf in slots)
-    w0 = min(w for f, w, _, _ in slots if f)
-    rc, tour = tspgpu.tie_tour(d, w0, 0, tspgpu.bits_cost(opt, tspgpu.F64))
-    oc, ot = O.solve_block(d)
-    assert rc == 0 and tspgpu.bits_cost(opt, tspgpu.F64) == oc and tour.tolist() == ot
-    # the slot of a cost no shard recorded
-    assert all(not S.tie_slot(opt + 1)[0] for S in shards)
-    for S in shards:
-        S.close()
+    try:
+        for S in shards:
+            S.set_bound(ub)
+            assert S.chain()
+        opt = min(S.counters()[0] for S in shards)
+        slots = [S.tie_slot(opt) for S in shards]
+        assert not any(ovf for _, _, _, ovf in slots), slots
+        w0 = min(w for f, w, _, _ in slots if f)
+        rc, tour = tspgpu.tie_tour(d, w0, 0, tspgpu.bits_cost(opt, tspgpu.F64))
+        oc, ot = O.solve_block(d)
+        assert rc == 0 and tspgpu.bits_cost(opt, tspgpu.F64) == oc and tour.tolist() == ot
+        # the slot of a cost no shard recorded (every recorded tour costs at most the bound)
+        assert all(not S.tie_slot(tspgpu.cost_bits(2 * ub + 1, tspgpu.F64))[0] for S in shards)
+    finally:
+        for S in shards:
+            S.close()
 
 
-def test_overflow_falls_back_to_second_phase(gpu_ctx, monkeypatch):
+def test_overflow_falls_back_to_second_phase(gpu_ctx, knobs):
     """All-equal distances: every tour is optimal.  7! = 5040 fit the record
     buffer; 9! = 362880 at n = 10 do not, so (device tie rule off) the search
     runs a second phase with the optimum as the bound and a buffer of the
@@ -334,7 +335,7 @@ def test_overflow_falls_back_to_second_phase(gpu_ctx, monkeypatch):
     cost, tour, st = tspgpu.search_solve(gpu_ctx, d)
     oc, ot = O.solve_block(d.astype(np.float64))
     assert cost == int(oc) and tour.tolist() == ot and st["phases"] == 1 and st["tie"] == 1, st
-    monkeypatch.setenv("TSPGPU_SEARCH_TIE", "0")
+    knobs.set("SEARCH_TIE", "0")
     d = np.full((8, 8), 7, dtype=np.int32)
     np.fill_diagonal(d, 0)
     cost, tour, st = tspgpu.search_solve(gpu_ctx, d)  # 7! = 5040 optimal tours: fits
@@ -347,19 +348,19 @@ def test_overflow_falls_back_to_second_phase(gpu_ctx, monkeypatch):
     assert cost == int(oc) and tour.tolist() == ot and st["phases"] == 2 and st["optimal_tours"] == 362880
 
 
-def test_forced_second_phase_and_k1_fallback(gpu_ctx, monkeypatch):
+def test_forced_second_phase_and_k1_fallback(gpu_ctx, knobs):
     """A tiny record buffer forces the second phase on an ordinary lattice
     instance; coincident cities (12! optimal tours) fall back to K1."""
     rng = np.random.default_rng(11)
     xy = rng.integers(0, 3, size=(11, 2)).astype(np.float64)
     d = O.distance_matrix([(i, xy[i, 0], xy[i, 1]) for i in range(11)])
-    monkeypatch.setenv("TSPGPU_SEARCH_RECORD_CAP", "2")
+    knobs.set("SEARCH_RECORD_CAP", "2")
     cost, tour, st = tspgpu.search_solve(gpu_ctx, d)  # device tie rule: one phase
     oc, ot = O.solve_block(d)
     assert (cost, tour.tolist()) == (oc, ot) and st["phases"] == 1 and st["tie"] == 1, st
-    monkeypatch.setenv("TSPGPU_SEARCH_TIE", "0")
+    knobs.set("SEARCH_TIE", "0")
     cost, tour, st = tspgpu.search_solve(gpu_ctx, d)
-    monkeypatch.delenv("TSPGPU_SEARCH_RECORD_CAP")
+    knobs.clear("SEARCH_RECORD_CAP")
     assert (cost, tour.tolist()) == (oc, ot) and st["phases"] == 2, st
     d = np.zeros((13, 13))
     cost, tour, st = tspgpu.search_solve(gpu_ctx, d)
@@ -378,7 +379,7 @@ def test_coincident_cities_device_tie_rule(gpu_ctx):
 
 
 @pytest.mark.parametrize("n", [9, 12, 14, 17])
-def test_device_tie_rule_agrees_with_records(gpu_ctx, monkeypatch, n):
+def test_device_tie_rule_agrees_with_records(gpu_ctx, n, knobs):
     """Tie-heavy lattices and uniform cities.  Default: the records decide and
     the device answer, when certified cheaply, must agree (tie_checked != -1).
     With a 2-record buffer (as in a tie storm) the device tie rule decides in
@@ -397,9 +398,9 @@ def test_device_tie_rule_agrees_with_records(gpu_ctx, monkeypatch, n):
         if n <= 16:
             oc, ot = O.solve_block(d)
             assert (cost, tour.tolist()) == (oc, ot), (k, st)
-        monkeypatch.setenv("TSPGPU_SEARCH_RECORD_CAP", "2")
+        knobs.set("SEARCH_RECORD_CAP", "2")
         c2, t2, s2 = tspgpu.search_solve(gpu_ctx, d)
-        monkeypatch.delenv("TSPGPU_SEARCH_RECORD_CAP")
+        knobs.clear("SEARCH_RECORD_CAP")
         assert (c2, t2.tolist()) == (cost, tour.tolist()), (k, s2)
         if s2["tie"]:
             assert s2["phases"] == 1 and s2["fallback"] == 0, s2
@@ -410,7 +411,7 @@ def test_device_tie_rule_agrees_with_records(gpu_ctx, monkeypatch, n):
 
 
 @pytest.mark.parametrize("n", [22, 26])
-def test_device_tie_rule_two_word_keys(gpu_ctx, monkeypatch, n):
+def test_device_tie_rule_two_word_keys(gpu_ctx, n, knobs):
     """Above 21 cities the key takes two words (a sub-slot per first word): the
     device answer equals the records' rule on symmetric instances (two optimal
     orientations at least), uniform and on a 40 x 40 lattice; a two-record
@@ -419,12 +420,12 @@ def test_device_tie_rule_two_word_keys(gpu_ctx, monkeypatch, n):
     for k in range(3):
         xy = rng.uniform(0, 1000, size=(n, 2)) if k == 0 else rng.integers(0, 40, size=(n, 2)).astype(np.float64)
         d = O.distance_matrix([(i, xy[i, 0], xy[i, 1]) for i in range(n)])
-        monkeypatch.delenv("TSPGPU_SEARCH_TIE", raising=False)
+        knobs.clear("SEARCH_TIE")
         c1, t1, s1 = tspgpu.search_solve(gpu_ctx, d)
-        monkeypatch.setenv("TSPGPU_SEARCH_RECORD_CAP", "1")
+        knobs.set("SEARCH_RECORD_CAP", "1")
         c2, t2, s2 = tspgpu.search_solve(gpu_ctx, d)
-        monkeypatch.delenv("TSPGPU_SEARCH_RECORD_CAP")
-        monkeypatch.setenv("TSPGPU_SEARCH_TIE", "0")
+        knobs.clear("SEARCH_RECORD_CAP")
+        knobs.set("SEARCH_TIE", "0")
         c0, t0, s0 = tspgpu.search_solve(gpu_ctx, d)
         assert c1 == c0 and t1.tolist() == t0.tolist() and s1["tie_checked"] != -1, (k, s1, s0)
         assert c2 == c0 and t2.tolist() == t0.tolist(), (k, s2)
@@ -464,10 +465,10 @@ def _enum_nodes(n):
 
 
 @pytest.mark.parametrize("n", [7, 9, 12, 13])
-def test_enum_kernel_against_oracle_and_round_kernels(gpu_ctx, monkeypatch, n):
+def test_enum_kernel_against_oracle_and_round_kernels(gpu_ctx, n, knobs):
     """enum.hip (7 <= n <= 16: a lane per depth-(n-7) prefix, 720 completions
     in registers) against tsp()'s oracle, on random and tie-heavy lattice
-    cities; the round kernels with the bound off (TSPGPU_ENUM_KERNEL=0) give
+    cities; the round kernels with the bound off (knob ENUM_KERNEL=0) give
     the same answer; the node count is every partial path exactly."""
     rng = np.random.default_rng(9100 + n)
     for lattice in (False, True):
@@ -478,9 +479,9 @@ def test_enum_kernel_against_oracle_and_round_kernels(gpu_ctx, monkeypatch, n):
         assert (cost, tour.tolist()) == (oc, ot), (n, lattice, st)
         assert st["nodes"] == _enum_nodes(n) and st["depth"] == n - 7, st
         if n <= 12:
-            monkeypatch.setenv("TSPGPU_ENUM_KERNEL", "0")
+            knobs.set("ENUM_KERNEL", "0")
             c2, t2, st2 = tspgpu.search_solve(gpu_ctx, d, exhaustive=True)
-            monkeypatch.delenv("TSPGPU_ENUM_KERNEL")
+            knobs.clear("ENUM_KERNEL")
             assert (c2, t2.tolist()) == (oc, ot), (n, lattice, st2)
 
 
@@ -498,7 +499,7 @@ def test_enum_kernel_integer_matrix(gpu_ctx, n):
         assert (cost, tour.tolist()) == (int(oc), ot), (n, hi, st)
 
 
-def test_enum_kernel_record_overflow_second_phase(gpu_ctx, monkeypatch):
+def test_enum_kernel_record_overflow_second_phase(gpu_ctx, knobs):
     """Thousands of tied optima on a 3x3 lattice (n=10) with a 2-record
     buffer: the device tie rule answers in one phase; without it the
     enumeration runs a second phase with the optimum as the bound.  Both
@@ -506,18 +507,18 @@ def test_enum_kernel_record_overflow_second_phase(gpu_ctx, monkeypatch):
     xy = [(x, y) for x in range(3) for y in range(3)] + [(1.0, 0.5)]
     d = O.distance_matrix([(i, float(x), float(y)) for i, (x, y) in enumerate(xy)])
     oc, ot = O.solve_block(d)
-    monkeypatch.setenv("TSPGPU_SEARCH_RECORD_CAP", "2")
+    knobs.set("SEARCH_RECORD_CAP", "2")
     cost, tour, st = tspgpu.search_solve(gpu_ctx, d, exhaustive=True)
     assert (cost, tour.tolist()) == (oc, ot) and st["phases"] == 1 and st["tie"] == 1, st
-    monkeypatch.setenv("TSPGPU_SEARCH_TIE", "0")
+    knobs.set("SEARCH_TIE", "0")
     cost, tour, st = tspgpu.search_solve(gpu_ctx, d, exhaustive=True)
     assert (cost, tour.tolist()) == (oc, ot) and st["phases"] == 2, st
 
 
 @pytest.mark.parametrize("kind", ["random", "clustered", "ties"])
-def test_lagrangian_two_edge_bound_keeps_the_answer(gpu_ctx, monkeypatch, kind):
+def test_lagrangian_two_edge_bound_keeps_the_answer(gpu_ctx, kind, knobs):
     """The Lagrangian city weights only change which nodes are pruned: with
-    and without them (TSPGPU_SEARCH_LAGRANGE) the search returns the DP's cost
+    and without them (knob SEARCH_LAGRANGE) the search returns the DP's cost
     and tour (K1-wide) on random and clustered instances of 17-21 cities and
     tie-heavy ones of 13-17."""
     rng = np.random.default_rng({"random": 1, "clustered": 2, "ties": 3}[kind])
@@ -532,15 +533,15 @@ def test_lagrangian_two_edge_bound_keeps_the_answer(gpu_ctx, monkeypatch, kind):
         d = tspgpu.distance_matrix([[(i, xy[i, 0], xy[i, 1]) for i in range(n)]])[0]
         wc, wt, _ = gpu_ctx.solve_instance(d)
         for lag in ("1", "0"):
-            monkeypatch.setenv("TSPGPU_SEARCH_LAGRANGE", lag)
+            knobs.set("SEARCH_LAGRANGE", lag)
             cost, tour, st = tspgpu.search_solve(gpu_ctx, d)
             assert cost == wc and tour.tolist() == wt.tolist(), (kind, n, lag, st)
 
 
 @pytest.mark.parametrize("kind", ["random", "clustered", "ties", "integer"])
-def test_tree_bound_keeps_the_answer(gpu_ctx, monkeypatch, kind):
-    """The Held-Karp tree bound (TSPGPU_SEARCH_MST, on at paths with >= 12
-    cities left by default, TSPGPU_SEARCH_MST_MINREM=0: at every level) only
+def test_tree_bound_keeps_the_answer(gpu_ctx, kind, knobs):
+    """The Held-Karp tree bound (knob SEARCH_MST, on at paths with >= 12
+    cities left by default, SEARCH_MST_MINREM=0: at every level) only
     changes which paths are pruned: off, default and everywhere, the search
     returns the DP's cost and tie-broken tour (K1-wide) on random, clustered,
     tie-heavy and integer (i32 search) instances of 13-25 cities."""
@@ -558,16 +559,16 @@ def test_tree_bound_keeps_the_answer(gpu_ctx, monkeypatch, kind):
             d = np.rint(d).astype(np.int32)
         wc, wt, _ = gpu_ctx.solve_instance(np.asarray(d, dtype=np.float64))
         for mst, minrem in (("0", None), ("1", None), ("1", "0")):
-            monkeypatch.setenv("TSPGPU_SEARCH_MST", mst)
+            knobs.set("SEARCH_MST", mst)
             if minrem is None:
-                monkeypatch.delenv("TSPGPU_SEARCH_MST_MINREM", raising=False)
+                knobs.clear("SEARCH_MST_MINREM")
             else:
-                monkeypatch.setenv("TSPGPU_SEARCH_MST_MINREM", minrem)
+                knobs.set("SEARCH_MST_MINREM", minrem)
             cost, tour, st = tspgpu.search_solve(gpu_ctx, d)
             assert cost == wc and tour.tolist() == wt.tolist(), (kind, n, mst, minrem, st)
 
 
-def test_tree_bound_on_the_hard_32_city_seeds(gpu_ctx, monkeypatch):
+def test_tree_bound_on_the_hard_32_city_seeds(gpu_ctx, knobs):
     """bench.k2_instance(32, s) for the seeds whose two-edge bound left a
     heavy tail (35: 0.5 s without the tree bound; 14 and 20: 11-14 s): with
     the tree bound each is solved in well under a second, the same answer at
@@ -578,13 +579,13 @@ def test_tree_bound_on_the_hard_32_city_seeds(gpu_ctx, monkeypatch):
         d = k2_instance(32, seed)
         got = []
         for minrem in ("12", "0"):
-            monkeypatch.setenv("TSPGPU_SEARCH_MST_MINREM", minrem)
+            knobs.set("SEARCH_MST_MINREM", minrem)
             cost, tour, st = tspgpu.search_solve(gpu_ctx, d)
             assert st["kernel_ms"] < 500, st
             got.append((cost, tour.tolist()))
         assert got[0] == got[1], seed
         if seed == 35:
-            monkeypatch.setenv("TSPGPU_SEARCH_MST", "0")
+            knobs.set("SEARCH_MST", "0")
             cost, tour, _ = tspgpu.search_solve(gpu_ctx, d)
-            monkeypatch.delenv("TSPGPU_SEARCH_MST")
+            knobs.clear("SEARCH_MST")
             assert (cost, tour.tolist()) == got[0]

@@ -128,7 +128,7 @@ def test_heuristic_split_over_ranks_gives_the_same_bound(n):
 
 
 @pytest.mark.parametrize("n", [20, 27, 32])
-def test_heuristic_threads_give_the_serial_tour(monkeypatch, n):
+def test_heuristic_threads_give_the_serial_tour(n, knobs):
     """From 20 cities the multi-start runs on up to 8 host threads
     (TSPGPU_HEURISTIC_THREADS overrides); the results are combined in start
     order, so cost and tour equal the serial run's, f64 and i32."""
@@ -138,7 +138,7 @@ def test_heuristic_threads_give_the_serial_tour(monkeypatch, n):
     for m in (d, np.rint(d).astype(np.int32)):
         got = []
         for t in ("1", "3", "8"):
-            monkeypatch.setenv("TSPGPU_HEURISTIC_THREADS", t)
+            knobs.set("HEURISTIC_THREADS", t)
             c, tour = tspgpu.heuristic_tour(m)
             got.append((c, tour.tolist()))
         assert got[0] == got[1] == got[2]

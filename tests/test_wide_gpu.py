@@ -66,10 +66,10 @@ def test_rejects_bad_input(gpu_ctx):
 
 
 @pytest.mark.parametrize("form", ["0", "1"])
-def test_push_and_pull_forms(gpu_ctx, monkeypatch, form):
+def test_push_and_pull_forms(gpu_ctx, form, knobs):
     """Both layer forms (row-owner push, per-destination pull) on the goldens
     (tie-heavy included) and on random / lattice instances vs the oracle."""
-    monkeypatch.setenv("TSPGPU_WIDE_PULL", form)
+    knobs.set("WIDE_PULL", form)
     for inst in O.load_golden("tie_blocks.json"):
         cities = [(c[0], O.hexf(c[1]), O.hexf(c[2])) for c in inst["cities"]]
         if len(cities) < 3:

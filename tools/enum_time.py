@@ -5,6 +5,7 @@ import os, sys, time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [os.path.join(ROOT, "tsp-mpi-reduction_amd"), ROOT]
 import tspgpu  # noqa: E402
+tspgpu.tune_from_environ()  # (TSPGPU_<KNOB> variables of this tool -> library knobs)
 from bench import Shard  # noqa: E402
 
 ctx = tspgpu.Context(device=0)
@@ -13,7 +14,7 @@ for n in [int(a) for a in sys.argv[1:]] or [12, 13, 14, 15]:
     d = Shard(n, 1, 0, 1).distances()[0]
     res = {}
     for mode in (("enum", "old") if old and n <= 15 else ("enum",)):
-        os.environ["TSPGPU_ENUM_KERNEL"] = "1" if mode == "enum" else "0"
+        tspgpu.tune("ENUM_KERNEL", "1" if mode == "enum" else "0")
         best = None
         for rep in range(3):
             t = time.perf_counter()

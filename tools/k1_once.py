@@ -9,13 +9,14 @@ sys.path.insert(0, ROOT)
 import numpy as np  # noqa: E402
 
 import tspgpu  # noqa: E402
+tspgpu.tune_from_environ()  # (TSPGPU_<KNOB> variables of this tool -> library knobs)
 from bench import Shard  # noqa: E402
 
 n, B, vb = int(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3])
 v, _, cfg = sys.argv[4].partition(":")
-os.environ["TSPGPU_K1"] = v
+tspgpu.tune("K1", v)
 if cfg:
-    os.environ["TSPGPU_TILED_CFG"] = cfg
+    tspgpu.tune("TILED_CFG", cfg)
 d = Shard(n, B, 0, B).distances()
 if vb == 4:
     d = np.rint(d).astype(np.int32)

@@ -17,15 +17,16 @@ sys.path.insert(0, ROOT)
 import numpy as np  # noqa: E402
 
 import tspgpu  # noqa: E402
+tspgpu.tune_from_environ()  # (TSPGPU_<KNOB> variables of this tool -> library knobs)
 from bench import Shard  # noqa: E402
 
 
 def ctx_for(variant, cfg=None):
-    os.environ["TSPGPU_K1"] = str(variant)
+    tspgpu.tune("K1", str(variant))
     if cfg is None:
-        os.environ.pop("TSPGPU_TILED_CFG", None)
+        tspgpu.untune("TILED_CFG")
     else:
-        os.environ["TSPGPU_TILED_CFG"] = str(cfg)
+        tspgpu.tune("TILED_CFG", str(cfg))
     return tspgpu.Context(device=0)
 
 

@@ -12,6 +12,7 @@ CHILD = r'''
 import sys, time, json, numpy as np
 sys.path.insert(0, "{root}/tsp-mpi-reduction_amd"); sys.path.insert(0, "{root}")
 import tspgpu
+tspgpu.tune_from_environ()  # (TSPGPU_<KNOB> variables of this tool -> library knobs)
 from bench import k2_instance
 ctx = tspgpu.Context(device=0)
 out = {{}}

@@ -15,6 +15,7 @@ CHILD = r'''
 import sys, time, json, numpy as np
 sys.path.insert(0, "{root}/tsp-mpi-reduction_amd"); sys.path.insert(0, "{root}")
 import tspgpu
+tspgpu.tune_from_environ()  # (TSPGPU_<KNOB> variables of this tool -> library knobs)
 from bench import Shard
 ctx = tspgpu.Context(device=0)
 cases = {{"tsp16_1": Shard(16, 1, 0, 1).distances()[0]}}

@@ -11,6 +11,7 @@ CHILD = r'''
 import sys, time, json, numpy as np
 sys.path.insert(0, "{root}/tsp-mpi-reduction_amd")
 import tspgpu
+tspgpu.tune_from_environ()  # (TSPGPU_<KNOB> variables of this tool -> library knobs)
 n, seed_skip = {n}, {skip}
 rng = np.random.default_rng(12)
 for m in (18, 22, 25):

@@ -10,6 +10,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "tsp-mpi-reduction_amd"))
 sys.path.insert(0, ROOT)
 import tspgpu  # noqa: E402
+tspgpu.tune_from_environ()  # (TSPGPU_<KNOB> variables of this tool -> library knobs)
 from bench import Shard  # noqa: E402
 
 n = int(os.environ.get("K2_N", "16"))
@@ -17,7 +18,7 @@ d = Shard(n, 1, 0, 1).distances()[0]
 ctx = tspgpu.Context(device=0)
 reps = int(sys.argv[1]) if len(sys.argv) > 1 else 3
 if len(sys.argv) > 2:  # seed depth (the library reads TSPGPU_SEARCH_DEPTH when a search starts)
-    os.environ["TSPGPU_SEARCH_DEPTH"] = sys.argv[2]
+    tspgpu.tune("SEARCH_DEPTH", sys.argv[2])
 for _ in range(reps):
     t = time.perf_counter()
     cost, tour, st = tspgpu.search_solve(ctx, d)

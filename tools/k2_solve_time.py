@@ -15,6 +15,7 @@ sys.path.insert(0, ROOT)
 import numpy as np  # noqa: E402
 
 import tspgpu  # noqa: E402
+tspgpu.tune_from_environ()  # (TSPGPU_<KNOB> variables of this tool -> library knobs)
 from bench import Shard, k2_instance  # noqa: E402
 
 

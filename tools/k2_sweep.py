@@ -6,6 +6,7 @@ sys.path.insert(0, os.path.join(ROOT, "tsp-mpi-reduction_amd"))
 sys.path.insert(0, ROOT)
 import numpy as np  # noqa: E402
 import tspgpu  # noqa: E402
+tspgpu.tune_from_environ()  # (TSPGPU_<KNOB> variables of this tool -> library knobs)
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 20
 seeds = [int(s) for s in sys.argv[2:]] or [1]
@@ -15,9 +16,9 @@ for seed in seeds:
     xy = np.random.default_rng(seed).uniform(0, 1000, size=(n, 2))
     d = tspgpu.distance_matrix([[(i, xy[i, 0], xy[i, 1]) for i in range(n)]])[0]
     for kern, refill, budget in cfgs:
-        os.environ["TSPGPU_SEARCH_KERNEL"] = str(kern)
-        os.environ["TSPGPU_SEARCH_REFILL"] = str(refill)
-        os.environ["TSPGPU_SEARCH_BUDGET"] = str(budget)
+        tspgpu.tune("SEARCH_KERNEL", str(kern))
+        tspgpu.tune("SEARCH_REFILL", str(refill))
+        tspgpu.tune("SEARCH_BUDGET", str(budget))
         t = time.perf_counter()
         cost, tour, st = tspgpu.search_solve(ctx, d)
         wall = (time.perf_counter() - t) * 1e3

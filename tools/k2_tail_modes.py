@@ -6,6 +6,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "tsp-mpi-reduction_amd"))
 sys.path.insert(0, ROOT)
 import tspgpu
+tspgpu.tune_from_environ()  # (TSPGPU_<KNOB> variables of this tool -> library knobs)
 from bench import Shard  # noqa: E402  (reference generator)
 
 ctx = tspgpu.Context(device=0)
@@ -17,7 +18,7 @@ for n in ns:
     for b in range(4):
         want = (ref[0][b], ref[1][b][:n + 1].tolist()) if ref else ctx.solve_instance(d[b])[:2]
         for mode in ("0", "5", "6"):
-            os.environ["TSPGPU_SEARCH_TAIL"] = mode
+            tspgpu.tune("SEARCH_TAIL", mode)
             best = None
             for rep in range(3):
                 t = time.perf_counter()

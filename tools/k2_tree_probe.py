@@ -12,13 +12,14 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "tsp-mpi-reduction_amd"))
 sys.path.insert(0, ROOT)
 import tspgpu  # noqa: E402
+tspgpu.tune_from_environ()  # (TSPGPU_<KNOB> variables of this tool -> library knobs)
 from bench import k2_instance  # noqa: E402
 
 ctx = tspgpu.Context(device=0)
 
 
 def run(d, mst):
-    os.environ["TSPGPU_SEARCH_MST"] = "1" if mst else "0"
+    tspgpu.tune("SEARCH_MST", "1" if mst else "0")
     tspgpu.search_solve(ctx, d) if d.shape[0] <= 20 else None  # warm (small cases only)
     t = time.perf_counter()
     cost, tour, st = tspgpu.search_solve(ctx, d)

@@ -14,8 +14,8 @@ if sys.argv[1] == "--one":
     B = 16384
     d = Shard(16, B, 0, B).distances()
     for cfg in sys.argv[3].split(","):
-        os.environ["TSPGPU_K1"] = "5"
-        os.environ["TSPGPU_TILED_CFG"] = cfg
+        tspgpu.tune("K1", "5")
+        tspgpu.tune("TILED_CFG", cfg)
         ctx = tspgpu.Context(device=0)
         dd, dc, dt = ctx.upload(d), ctx.alloc(B * 8), ctx.alloc(B * 17 * 4)
         ctx.solve_device(dd, 16, B, dc, dt, ctx.stream)

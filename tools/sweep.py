@@ -14,6 +14,7 @@ sys.path.insert(0, ROOT)
 import numpy as np  # noqa: E402
 
 import tspgpu  # noqa: E402
+tspgpu.tune_from_environ()  # (TSPGPU_<KNOB> variables of this tool -> library knobs)
 from bench import Shard  # noqa: E402
 
 ns = [int(a) for a in sys.argv[1:]] or [16, 14, 12]
@@ -32,9 +33,9 @@ for n in ns:
     rows = []
     ctxs = []
     for v, th, wg in configs:
-        os.environ["TSPGPU_K1"] = str(v)
-        os.environ["TSPGPU_THREADS"] = str(th)
-        os.environ["TSPGPU_WG_PER_CU"] = str(wg)
+        tspgpu.tune("K1", str(v))
+        tspgpu.tune("THREADS", str(th))
+        tspgpu.tune("WG_PER_CU", str(wg))
         ctx = tspgpu.Context(device=0)
         ctxs.append((v, th, wg, ctx, ctx.upload(d), ctx.alloc(B * vb), ctx.alloc(B * (n + 1) * 4)))
     ref = None

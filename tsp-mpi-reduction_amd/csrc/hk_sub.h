@@ -162,6 +162,21 @@ __device__ __forceinline__ void relax_min2(double &a0, double g0, double d0, dou
         : [a0] "+v"(a0), [a1] "+v"(a1), [t0] "=&v"(t0), [t1] "=&v"(t1)
         : [g0] "v"(g0), [d0] "v"(d0), [g1] "v"(g1), [d1] "v"(d1));
 }
+// two relaxations of ONE destination: two adds and one v_min3_i32 (1.5 VALU
+// instructions per relaxation instead of 2; integer min is exact in any order)
+__device__ __forceinline__ void relax_min3(int32_t &a, int32_t g0, int32_t d0, int32_t g1, int32_t d1)
+{
+    int32_t t0, t1;
+    asm volatile(
+        "v_add_u32 %[t0], %[g0], %[d0]\n\t"
+        "v_add_u32 %[t1], %[g1], %[d1]\n\t"
+        "v_min3_i32 %[a], %[a], %[t0], %[t1]"
+        : [a] "+v"(a), [t0] "=&v"(t0), [t1] "=&v"(t1)
+        : [g0] "v"(g0), [d0] "v"(d0), [g1] "v"(g1), [d1] "v"(d1));
+}
+#ifndef TSPGPU_SUB_MIN3
+#define TSPGPU_SUB_MIN3 1  // i32 middle passes: member pairs per destination through v_min3_i32
+#endif
 __device__ __forceinline__ void relax_min2(int32_t &a0, int32_t g0, int32_t d0, int32_t &a1, int32_t g1, int32_t d1)
 {
     int32_t t0, t1;
@@ -252,16 +267,58 @@ __host__ __device__ constexpr int sub_lds_count()
             if (!(p >= J && C0 + qq >= QL)) ++n;
     return n;
 }
-template <int T, int J, int QL, int C0, int QN>
+// QP = false: member-major (p, then the destinations q: consecutive
+// relaxations have different destinations, independent min chains).  QP =
+// true (integer values): member 0's row first, then member PAIRS (p, p + 1)
+// destination by destination, so relaxations 2i-1 and 2i share q and fold
+// into one v_min3 (acc = min3(acc, g_p + d, g_(p+1) + d')).
+template <int T, int J, int QL, int C0, int QN, bool QP = false>
 __host__ __device__ constexpr int sub_lds_pair(int k)
 {
     int n = 0;
-    for (int p = 0; p < T; ++p)
+    if (!QP) {
+        for (int p = 0; p < T; ++p)
+            for (int qq = 0; qq < QN; ++qq)
+                if (!(p >= J && C0 + qq >= QL)) {
+                    if (n == k) return p * 64 + qq;
+                    ++n;
+                }
+        return -1;
+    }
+    for (int qq = 0; qq < QN; ++qq)
+        if (!(0 >= J && C0 + qq >= QL)) {
+            if (n == k) return qq;
+            ++n;
+        }
+    for (int p = 1; p < T; p += 2)
         for (int qq = 0; qq < QN; ++qq)
-            if (!(p >= J && C0 + qq >= QL)) {
-                if (n == k) return p * 64 + qq;
-                ++n;
-            }
+            for (int pp = p; pp < p + 2 && pp < T; ++pp)
+                if (!(pp >= J && C0 + qq >= QL)) {
+                    if (n == k) return pp * 64 + qq;
+                    ++n;
+                }
+    return -1;
+}
+
+// QP order: 1 = relaxation k opens a same-destination member pair (k, k + 1),
+// 2 = k closes one, 0 = a single relaxation (member 0, or a pair member whose
+// partner is a high-high relaxation, which is not in the LDS list)
+template <int T, int J, int QL, int C0, int QN>
+__host__ __device__ constexpr int sub_lds_role(int k)
+{
+    int n = 0;
+    for (int qq = 0; qq < QN; ++qq)
+        if (!(0 >= J && C0 + qq >= QL)) {
+            if (n == k) return 0;
+            ++n;
+        }
+    for (int p = 1; p < T; p += 2)
+        for (int qq = 0; qq < QN; ++qq) {
+            int in = 0;
+            for (int pp = p; pp < p + 2 && pp < T; ++pp) in += !(pp >= J && C0 + qq >= QL) ? 1 : 0;
+            for (int i = 0; i < in; ++i, ++n)
+                if (n == k) return in == 2 ? 1 + i : 0;
+        }
     return -1;
 }
 
@@ -341,11 +398,13 @@ __device__ __forceinline__ void sub_mid(const SubCtx<V, N, L> &c, uint32_t h, ui
         constexpr int QN = Q - C0 < QC ? Q - C0 : QC;
         constexpr int CNT = sub_lds_count<T, J, QL, C0, QN>();
         constexpr int AH = TSPGPU_SUB_AHEAD < CNT ? TSPGPU_SUB_AHEAD : CNT;
+        // integer min-only rows: member pairs per destination (v_min3_i32)
+        constexpr bool QP = TSPGPU_SUB_MIN3 && !ARG && std::is_same<V, int32_t>::value;
         V acc[QN];
         uint32_t arg[ARG ? QN : 1];
         // distance of LDS relaxation k (compile-time pair)
         auto dload = [&](auto kk) -> V {
-            constexpr int pq = sub_lds_pair<T, J, QL, C0, QN>(decltype(kk)::value);
+            constexpr int pq = sub_lds_pair<T, J, QL, C0, QN, QP>(decltype(kk)::value);
             constexpr int p = pq / 64, q = C0 + pq % 64;
             if constexpr (p < J && q < QL)
                 return lds_val<V>(c.img, mrow[p] + kof[q]);
@@ -359,7 +418,7 @@ __device__ __forceinline__ void sub_mid(const SubCtx<V, N, L> &c, uint32_t h, ui
         // relaxation k of the chunk (its distance from the load pipeline)
         auto relax_one = [&](auto kk) {
             constexpr int k = decltype(kk)::value;
-            constexpr int pq = sub_lds_pair<T, J, QL, C0, QN>(k);
+            constexpr int pq = sub_lds_pair<T, J, QL, C0, QN, QP>(k);
             constexpr int p = pq / 64, qq = pq % 64;
             const V d = dv[k % AH];
             if constexpr (k + AH < CNT) dv[k % AH] = dload(std::integral_constant<int, k + AH>{});
@@ -373,11 +432,31 @@ __device__ __forceinline__ void sub_mid(const SubCtx<V, N, L> &c, uint32_t h, ui
                 relax_min(acc[qq], g[p], d);
             }
         };
-        if constexpr (TSPGPU_SUB_PAIR && !ARG) {
+        if constexpr (QP) {
+            static_for<CNT>([&](auto kk) {
+                constexpr int k = decltype(kk)::value;
+                constexpr int role = sub_lds_role<T, J, QL, C0, QN>(k);
+                if constexpr (role == 1) {
+                    constexpr int pq0 = sub_lds_pair<T, J, QL, C0, QN, QP>(k);
+                    constexpr int pq1 = sub_lds_pair<T, J, QL, C0, QN, QP>(k + 1);
+                    static_assert(pq0 % 64 == pq1 % 64 && pq1 / 64 == pq0 / 64 + 1, "member pair");
+                    const V d0 = dv[k % AH];
+                    if constexpr (k + AH < CNT) dv[k % AH] = dload(std::integral_constant<int, k + AH>{});
+                    const V d1 = dv[(k + 1) % AH];
+                    if constexpr (k + 1 + AH < CNT) dv[(k + 1) % AH] = dload(std::integral_constant<int, k + 1 + AH>{});
+                    if constexpr (std::is_same<V, int32_t>::value)
+                        relax_min3(acc[pq0 % 64], g[pq0 / 64], d0, g[pq1 / 64], d1);
+                    __builtin_amdgcn_sched_barrier(0);
+                } else if constexpr (role == 0) {
+                    relax_one(kk);
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+            });
+        } else if constexpr (TSPGPU_SUB_PAIR && !ARG) {
             static_for<(CNT + 1) / 2>([&](auto kk2) {
                 constexpr int k0 = 2 * decltype(kk2)::value, k1 = k0 + 1;
-                constexpr int pq0 = sub_lds_pair<T, J, QL, C0, QN>(k0);
-                constexpr int pq1 = k1 < CNT ? sub_lds_pair<T, J, QL, C0, QN>(k1) : 0;
+                constexpr int pq0 = sub_lds_pair<T, J, QL, C0, QN, QP>(k0);
+                constexpr int pq1 = k1 < CNT ? sub_lds_pair<T, J, QL, C0, QN, QP>(k1) : 0;
                 constexpr int p0 = pq0 / 64, q0 = pq0 % 64, p1 = pq1 / 64, q1 = pq1 % 64;
                 if constexpr (k1 < CNT && p0 > 0 && p1 > 0 && q0 != q1) {
                     const V d0 = dv[k0 % AH];

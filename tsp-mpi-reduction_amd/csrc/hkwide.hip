@@ -26,6 +26,7 @@
 #include "ctx.h"
 #include "wave.h"
 #include "tspgpu.h"
+#include "tuning.h"
 
 namespace {
 
@@ -282,10 +283,9 @@ void enqueue_wide(const WideState *w, const WideInfo &h, int n, int cus, hipStre
     const int N = n - 1;
     hipLaunchKernelGGL(wide_layer1, dim3(1), dim3(64), 0, st, w->dist, n, w->tab);
     // per-destination (pull) form up to 17 cities, where both are bound by the
-    // ~8 us kernel boundary per layer and pull is a little faster; TSPGPU_WIDE_PULL
-    // = 0 / 1 forces either (measured: profiles/r01/k1wide_push_vs_pull.log)
-    const char *force = std::getenv("TSPGPU_WIDE_PULL");
-    const bool pull = force ? std::atoi(force) != 0 : n <= 17;
+    // ~8 us kernel boundary per layer and pull is a little faster; the knob
+    // WIDE_PULL = 0 / 1 forces either (measured: profiles/r01/k1wide_push_vs_pull.log)
+    const bool pull = tspgpu::tuned_or("WIDE_PULL", n <= 17 ? 1 : 0) != 0;
     if (!pull) {
         for (int t = 1; t < N; ++t) {
             const unsigned long long blocks = (h.cnt[t] + kWideThreads - 1) / kWideThreads;

@@ -34,11 +34,15 @@
 #include "search.h"
 #include "search_host.h"
 #include "tspgpu.h"
+#include "tuning.h"
 
 using namespace tspgpu;
 using tspgpu::host::held_karp_pi;
 using tspgpu::host::lagrange_pi;
 using tspgpu::host::validate_search;
+using tspgpu::tuned;
+using tspgpu::tuned_int;
+using tspgpu::tuned_or;
 
 static_assert(sizeof(SearchRecord) == sizeof(tspgpu_tour_record), "record layout");
 constexpr int kWords = 16;  // device counter words of a search (see tspgpu_search::d_words)
@@ -72,7 +76,7 @@ struct tspgpu_search {
     uint64_t pending = 0;        // items waiting for the next round
     uint32_t budget = 256;       // DFS iterations per item per round
     uint32_t refill = 16;        // v2/persistent: refill a wave once this many lanes wait
-    // round kernel (TSPGPU_SEARCH_KERNEL): 2 lock-step DFS (default), 1 branching DFS;
+    // round kernel (knob SEARCH_KERNEL): 2 lock-step DFS (default), 1 branching DFS;
     // 3 = run_all as ONE persistent launch with a device work ring (measured
     // 1.3-2x slower than rounds at n = 18: profiles/r01/k2_persistent.log)
     int kernel = 2;
@@ -86,7 +90,7 @@ struct tspgpu_search {
     int noprune = 0;             // exhaustive enumeration (tspgpu_search_enumerate)
     int enum_kernel = 0;         // enumeration by enum.hip (6-city register tails, 7 <= n <= 16)
     // Frontier search (default for the bounded search when n - 1 - tail_len >
-    // the seed depth; TSPGPU_SEARCH_TAIL = 0 selects the DFS rounds, 5 or 6 the
+    // the seed depth; knob SEARCH_TAIL = 0 selects the DFS rounds, 5 or 6 the
     // tail length): each step expands up to kExpandMax items of the frontier
     // (LIFO) by one level with the bound; prefixes with tail_len cities left
     // collect in d_tail and are folded by tail_kernel, all tail_len!
@@ -94,7 +98,7 @@ struct tspgpu_search {
     // frontier is empty.
     int tail_len = 6;
     bool frontier = false;
-    bool chain = true;  // run_all: small searches as chained levels (TSPGPU_SEARCH_CHAIN=0: step by step)
+    bool chain = true;  // run_all: small searches as chained levels (knob SEARCH_CHAIN=0: step by step)
     // stronger frontier bounds (SearchArgs::bnd2 / ::hsuf): the two-edge bound
     // for symmetric matrices and the suffix table for the last tail_len cities
     int sym = 0;
@@ -104,12 +108,12 @@ struct tspgpu_search {
     size_t hsuf_alloc = 0;      // bytes
     int hs_len = 0;             // sizes 1..hs_len built (0: none)
     uint32_t hs_off[8] = {};
-    int suffix_len = 6;         // TSPGPU_SEARCH_SUFFIX=0/5/6: table size (0: B0/B1 only)
-    bool use_two_edge = true;   // TSPGPU_SEARCH_TWO_EDGE=0: no B1
-    bool use_lagrange = true;   // TSPGPU_SEARCH_LAGRANGE=0: B1 without the Lagrangian city weights
-    bool use_mst = true;        // TSPGPU_SEARCH_MST=0: no Held-Karp tree bound in the expand kernel
+    int suffix_len = 6;         // knob SEARCH_SUFFIX=0/5/6: table size (0: B0/B1 only)
+    bool use_two_edge = true;   // knob SEARCH_TWO_EDGE=0: no B1
+    bool use_lagrange = true;   // knob SEARCH_LAGRANGE=0: B1 without the Lagrangian city weights
+    bool use_mst = true;        // knob SEARCH_MST=0: no Held-Karp tree bound in the expand kernel
     bool mst_on = false;        // (symmetric matrices only)
-    int mst_min_rem = 12;       // TSPGPU_SEARCH_MST_MINREM: paths with fewer cities left skip it (measured: profiles/r02/k2_tree_minrem.log)
+    int mst_min_rem = 12;       // knob SEARCH_MST_MINREM: paths with fewer cities left skip it (measured: profiles/r02/k2_tree_minrem.log)
     // The frontier is a LIFO stack of segments, each a run of paths in its own
     // buffer (fb): a step expands the top T items of the top segment and its
     // children become a new segment on top, written straight into a spare
@@ -131,7 +135,7 @@ struct tspgpu_search {
     // search spent 1.3 s in hipMalloc (1714 vs 524 ms warm), at 2^21 564 vs
     // 545 ms (profiles/r02/k2_expand_cap.log)
     uint64_t expand_max = (uint64_t)1 << 21;
-    uint64_t expand_steps = 0;  // frontier expansions so far (parity of the double-buffered child counter)  // frontier items one step expands, at most (TSPGPU_SEARCH_EXPAND_LOG2)
+    uint64_t expand_steps = 0;  // frontier expansions so far (parity of the double-buffered child counter)  // frontier items one step expands, at most (knob SEARCH_EXPAND_LOG2)
     uint64_t tails = 0;          // items waiting in d_tail
     int rounds = 0;
     double ms = 0.0;             // device time of all seed/round launches
@@ -143,7 +147,7 @@ struct tspgpu_search {
     // device tie rule (search.h): kTieSlots slots, then 8 words: [0..4] the
     // optimum's slot (tie_lookup_kernel), [5] the overflow flag
     TieSlot *d_tie = nullptr;
-    bool tie_on = true;  // TSPGPU_SEARCH_TIE=0: records and the host rule only
+    bool tie_on = true;  // knob SEARCH_TIE=0: records and the host rule only
     // pinned staging: the host tables of create (so their copies need no
     // synchronisation) and, at kStageSpec, the speculative records readback
     char *h_stage = nullptr;
@@ -322,42 +326,23 @@ static int search_create(tspgpu_ctx *c, const void *dist, int dtype, int n, int 
     s->dtype = dtype;
     s->shard = (uint32_t)shard;
     s->nshards = (uint32_t)nshards;
-    if (const char *e = std::getenv("TSPGPU_SEARCH_KERNEL")) {
-        const int v = std::atoi(e);
-        s->kernel = v == 1 ? 1 : (v == 3 ? 3 : 2);
-    }
-    if (const char *e = std::getenv("TSPGPU_SEARCH_HUNGRY")) s->hungry = (int32_t)std::atol(e);
-    if (const char *e = std::getenv("TSPGPU_SEARCH_MIN_SPLIT")) s->min_split = (uint32_t)std::max(0L, std::atol(e));
-    if (const char *e = std::getenv("TSPGPU_SEARCH_WALL_S")) s->wall_s = std::max(0.1, std::atof(e));
-    if (const char *e = std::getenv("TSPGPU_SEARCH_RING_LOG2")) {  // tests: a small ring
-        const int v = std::atoi(e);
-        if (v >= 6 && v <= 24) s->ring_cap = 1u << v;
-    }
-    if (const char *e = std::getenv("TSPGPU_SEARCH_REFILL")) {
-        const long v = std::atol(e);
-        if (v > 0) s->refill = (uint32_t)std::min<long>(v, 64);
-    }
-    if (const char *e = std::getenv("TSPGPU_SEARCH_TAIL")) {
-        const int v = std::atoi(e);
-        s->tail_len = (v == 5 || v == 6) ? v : 0;
-    }
-    if (const char *e = std::getenv("TSPGPU_SEARCH_SUFFIX")) {
-        const int v = std::atoi(e);
-        s->suffix_len = (v == 5 || v == 6) ? v : 0;
-    }
-    if (const char *e = std::getenv("TSPGPU_SEARCH_TWO_EDGE")) s->use_two_edge = std::atoi(e) != 0;
-    if (const char *e = std::getenv("TSPGPU_SEARCH_CHAIN")) s->chain = std::atoi(e) != 0;
-    if (const char *e = std::getenv("TSPGPU_SEARCH_LAGRANGE")) s->use_lagrange = std::atoi(e) != 0;
-    if (const char *e = std::getenv("TSPGPU_SEARCH_MST")) s->use_mst = std::atoi(e) != 0;
-    if (const char *e = std::getenv("TSPGPU_SEARCH_MST_MINREM")) s->mst_min_rem = std::atoi(e);
-    if (const char *e = std::getenv("TSPGPU_SEARCH_TAIL_CAP_LOG2")) {  // tests: many flushes, small steps
-        const int v = std::atoi(e);
-        if (v >= 8 && v <= 27) s->tail_cap = 1u << v;
-    }
-    if (const char *e = std::getenv("TSPGPU_SEARCH_EXPAND_LOG2")) {
-        const int v = std::atoi(e);
-        if (v >= 8 && v <= 26) s->expand_max = (uint64_t)1 << v;
-    }
+    // tuning knobs (tuning.h; tests and A/B runs only, the defaults above are the product)
+    double kv = 0.0;
+    if (tuned("SEARCH_KERNEL", &kv)) s->kernel = (int)kv == 1 ? 1 : ((int)kv == 3 ? 3 : 2);
+    if (tuned("SEARCH_HUNGRY", &kv)) s->hungry = (int32_t)kv;
+    if (tuned("SEARCH_MIN_SPLIT", &kv)) s->min_split = (uint32_t)std::max(0.0, kv);
+    if (tuned("SEARCH_WALL_S", &kv)) s->wall_s = std::max(0.1, kv);
+    if (tuned("SEARCH_RING_LOG2", &kv) && kv >= 6 && kv <= 24) s->ring_cap = 1u << (int)kv;  // tests: a small ring
+    if (tuned("SEARCH_REFILL", &kv) && kv > 0) s->refill = (uint32_t)std::min(kv, 64.0);
+    if (tuned("SEARCH_TAIL", &kv)) s->tail_len = ((int)kv == 5 || (int)kv == 6) ? (int)kv : 0;
+    if (tuned("SEARCH_SUFFIX", &kv)) s->suffix_len = ((int)kv == 5 || (int)kv == 6) ? (int)kv : 0;
+    if (tuned("SEARCH_TWO_EDGE", &kv)) s->use_two_edge = kv != 0;
+    if (tuned("SEARCH_CHAIN", &kv)) s->chain = kv != 0;
+    if (tuned("SEARCH_LAGRANGE", &kv)) s->use_lagrange = kv != 0;
+    if (tuned("SEARCH_MST", &kv)) s->use_mst = kv != 0;
+    if (tuned("SEARCH_MST_MINREM", &kv)) s->mst_min_rem = (int)kv;
+    if (tuned("SEARCH_TAIL_CAP_LOG2", &kv) && kv >= 8 && kv <= 27) s->tail_cap = 1u << (int)kv;  // tests: many flushes
+    if (tuned("SEARCH_EXPAND_LOG2", &kv) && kv >= 8 && kv <= 26) s->expand_max = (uint64_t)1 << (int)kv;
     const size_t lds = search_lds_bytes(n, f64, s->kernel == 1 ? 1 : 2);
     const int per_cu = std::max(1, std::min(8, (int)((160 * 1024) / lds)));
     s->grid = c->cu_count * per_cu;
@@ -372,10 +357,7 @@ static int search_create(tspgpu_ctx *c, const void *dist, int dtype, int n, int 
     }
     if (depth > N - 1) depth = N - 1;
     while (depth > 1 && falling(N, depth) >= (1ull << 31)) --depth;
-    if (const char *e = std::getenv("TSPGPU_SEARCH_BUDGET")) {
-        const long v = std::atol(e);
-        if (v > 0) s->budget = (uint32_t)v;
-    }
+    if (tuned("SEARCH_BUDGET", &kv) && kv > 0) s->budget = (uint32_t)kv;
     s->frontier = s->tail_len && s->kernel == 2 && N - s->tail_len > depth;
     // the frontier search expands level by level with its own bounds: a
     // smaller seed set (~64 prefixes per CU) costs less than the round
@@ -536,14 +518,14 @@ static int search_create(tspgpu_ctx *c, const void *dist, int dtype, int n, int 
         e = hipMalloc((void **)&s->d_rec, sizeof(SearchRecord) * s->rec_cap);
         if (e == hipSuccess) s->rec_alloc = s->rec_cap;
     }
-    if (const char *ev = std::getenv("TSPGPU_SEARCH_TIE")) s->tie_on = std::atoi(ev) != 0;
+    if (double v; tuned("SEARCH_TIE", &v)) s->tie_on = v != 0;
     constexpr size_t kTieBytes = sizeof(TieSlot) * kTieSlots;
     if (e == hipSuccess && !s->d_tie) e = hipMalloc((void **)&s->d_tie, kTieBytes + 8 * sizeof(unsigned long long));
     if (e == hipSuccess) e = hipMemsetAsync(s->d_tie, 0xFF, kTieBytes, st);
     if (e == hipSuccess)
         e = hipMemsetAsync(reinterpret_cast<char *>(s->d_tie) + kTieBytes, 0, 8 * sizeof(unsigned long long), st);
     if (e == hipSuccess) e = hipMemsetAsync(s->d_stats, 0, kStatBytes, st);
-    const bool pinned = !std::getenv("TSPGPU_SEARCH_PAGEABLE");
+    const bool pinned = tuned_or("SEARCH_PAGEABLE", 0) == 0;
     if (e == hipSuccess && pinned && !s->h_cnt)
         e = hipHostMalloc((void **)&s->h_cnt, 16 * sizeof(unsigned long long), hipHostMallocDefault);
     if (e == hipSuccess && pinned && !s->h_stats)
@@ -655,8 +637,8 @@ static SearchArgs args_of(tspgpu_search *s)
     a.refill = s->refill;
     a.kernel = s->kernel == 1 && !s->noprune ? 1 : 2;  // the round kernels (2 for enumeration)
     a.noprune = s->noprune;
-    a.tails = s->noprune;  // TSPGPU_SEARCH_TAILS=0/1 overrides
-    if (const char *e = std::getenv("TSPGPU_SEARCH_TAILS")) a.tails = std::atoi(e) != 0;
+    a.tails = s->noprune;  // knob SEARCH_TAILS=0/1 overrides
+    if (double v; tuned("SEARCH_TAILS", &v)) a.tails = v != 0;
     a.queue = reinterpret_cast<unsigned int *>(s->d_words);
     a.inc = s->d_words + 1;
     a.nodes = s->d_stats;
@@ -1085,12 +1067,9 @@ static int run_chain(tspgpu_search *s, bool *done, int every = 0, tspgpu_level_h
                      void *user = nullptr)
 {
     *done = false;
-    // ping-pong buffer capacity (TSPGPU_SEARCH_CHAIN_CAP_LOG2: tests force the overflow fallback)
+    // ping-pong buffer capacity (knob SEARCH_CHAIN_CAP_LOG2: tests force the overflow fallback)
     uint64_t kChainCap = (uint64_t)1 << 22;
-    if (const char *ev = std::getenv("TSPGPU_SEARCH_CHAIN_CAP_LOG2")) {
-        const int v = std::atoi(ev);
-        if (v >= 8 && v <= 24) kChainCap = (uint64_t)1 << v;
-    }
+    if (double v; tuned("SEARCH_CHAIN_CAP_LOG2", &v) && v >= 8 && v <= 24) kChainCap = (uint64_t)1 << (int)v;
     SearchArgs a0 = args_of(s);
     const int levels = a0.tail_level - s->depth;
     // a run of 256 paths per block (one per lane) and two blocks per CU:
@@ -1098,8 +1077,8 @@ static int run_chain(tspgpu_search *s, bool *done, int every = 0, tspgpu_level_h
     // 1024-path runs on one block per CU (profiles/r03/k2_chain_sweep.log)
     uint32_t chain_fpb = 256;
     int chain_grid = 2;
-    if (const char *ev = std::getenv("TSPGPU_CHAIN_FPB")) chain_fpb = (uint32_t)std::atoi(ev);  // (sweeps)
-    if (const char *ev = std::getenv("TSPGPU_CHAIN_GRID")) chain_grid = std::max(1, std::atoi(ev));
+    chain_fpb = (uint32_t)tuned_int("CHAIN_FPB", (int)chain_fpb);  // (sweeps)
+    chain_grid = std::max(1, tuned_int("CHAIN_GRID", chain_grid));
     hipStream_t st = s->ctx->stream;
     const int hooks = hook && every > 0 && levels > 1 ? (levels - 1) / every : 0;
     if (levels < 1 || s->local_items + 1 > kChainCap) {
@@ -1123,6 +1102,12 @@ static int run_chain(tspgpu_search *s, bool *done, int every = 0, tspgpu_level_h
         if (ob[k] < 0) return rc;
         s->seg_buf.push_back(ob[k]);  // (marked used so the second front_spare picks another)
         s->seg_n.push_back(0);
+    }
+    if (tuned_or("SEARCH_CHAIN_POISON", 0) != 0) {  // tests: no slot may be read that was not written
+        for (int k = 0; k < 2 && e == hipSuccess; ++k)
+            e = hipMemsetAsync(s->fb[ob[k]], 0xFF, sizeof(PathItem) * kChainCap, st);
+        if (e == hipSuccess) e = hipMemsetAsync(s->d_tail, 0xFF, sizeof(PathItem) * s->tail_cap, st);
+        if (e != hipSuccess) return herr(e);
     }
     // level l reads its input count from word 4 (the seeds, l = 0) or
     // 10 + l%3, writes 10 + (l+1)%3 and zeroes 10 + (l+2)%3
@@ -1241,7 +1226,7 @@ static int run_persist(tspgpu_search *s)
     if (hipEventElapsedTime(&ms, s->e0, s->e1) == hipSuccess) s->ms += ms;
     s->pending = 0;
     s->rounds = 1;
-    if (std::getenv("TSPGPU_SEARCH_DEBUG"))
+    if (tuned("SEARCH_DEBUG", nullptr))
         std::fprintf(stderr, "persist: grid %d seeds %llu/%llu head %llu tail %llu consumed %llu work %llu abort %llu ms %.3f\n",
                      grid, h.seed_cursor.v, (unsigned long long)s->local_items, h.head.v, h.tail.v, h.consumed.v,
                      h.work.v, h.abort.v, ms);
@@ -1266,7 +1251,7 @@ static int run_enum(tspgpu_search *s)
     a.items = (uint32_t)falling(N, G);
     const uint64_t blocks = (a.items + kSearchThreads - 1) / kSearchThreads;
     int per_cu = 8;
-    if (const char *e = std::getenv("TSPGPU_ENUM_WG_PER_CU")) per_cu = std::max(1, std::atoi(e));
+    per_cu = std::max(1, tuned_int("ENUM_WG_PER_CU", per_cu));
     const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>(blocks, (uint64_t)s->ctx->cu_count * per_cu));
     hipError_t e = hipMemcpyAsync(s->d_stats, &upper, 8, hipMemcpyHostToDevice, st);  // line 0, nodes
     if (e != hipSuccess) return herr(e);
@@ -1297,8 +1282,7 @@ int tspgpu_search_run_all(tspgpu_search *s)
     }
     int rc = tspgpu_search_start(s);
     uint64_t pending = 1;
-    const char *dbg = std::getenv("TSPGPU_SEARCH_DEBUG");
-    const bool trace = dbg && std::atoi(dbg) >= 2;
+    const bool trace = tuned_or("SEARCH_DEBUG", 0) >= 2;
     while (!rc && pending) {
         rc = tspgpu_search_step(s, &pending);
         if (trace)
@@ -1449,15 +1433,15 @@ static int search_solve(tspgpu_ctx *c, const void *dist, int dtype, int n, doubl
                         tspgpu_search_stats *stats, int noprune)
 {
     if (!c || !cost_out || !tour_out) return -EINVAL;
-    // TSPGPU_SEARCH_DEBUG: host phase times on stderr (development aid)
-    const bool dbg = std::getenv("TSPGPU_SEARCH_DEBUG") != nullptr;
+    // knob SEARCH_DEBUG: host phase times on stderr (development aid)
+    const bool dbg = tuned("SEARCH_DEBUG", nullptr);
     using clk = std::chrono::steady_clock;
     const clk::time_point T0 = clk::now();
     clk::time_point T1 = T0, T2 = T0, T3 = T0, T4 = T0;
     auto ms_of = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
     tspgpu_search *s = nullptr;
-    int depth = 0;  // automatic; TSPGPU_SEARCH_DEPTH (tests): a shallow seed, a deep frontier
-    if (const char *e = std::getenv("TSPGPU_SEARCH_DEPTH")) depth = std::max(0, std::atoi(e));
+    int depth = 0;  // automatic; knob SEARCH_DEPTH (tests): a shallow seed, a deep frontier
+    depth = std::max(0, tuned_int("SEARCH_DEPTH", depth));
     // the multi-start bound (host) while the search is created (host tables,
     // device buffers): both take ~1 ms at 32 cities
     double ub = 0.0;
@@ -1479,15 +1463,12 @@ static int search_solve(tspgpu_ctx *c, const void *dist, int dtype, int n, doubl
     s->noprune = noprune;
     // enumeration work is uniform and every lane reaches the register tails:
     // long budgets (fewer, fuller rounds) win (profiles/r01/k2_exhaustive_budget.log)
-    if (noprune && !std::getenv("TSPGPU_SEARCH_BUDGET")) s->budget = 16384;
+    if (noprune && !tuned("SEARCH_BUDGET", nullptr)) s->budget = 16384;
     // 7 <= n <= 16, one shard: the register-tail enumeration kernel (enum.hip);
-    // TSPGPU_ENUM_KERNEL=0 keeps the round kernels (tests compare both)
-    const char *ek = std::getenv("TSPGPU_ENUM_KERNEL");
-    s->enum_kernel = noprune && n >= 7 && n <= 16 && !(ek && std::atoi(ek) == 0);
-    if (const char *e = std::getenv("TSPGPU_SEARCH_RECORD_CAP")) {  // tests: force the second phase
-        const long v = std::atol(e);
-        if (v > 0) s->rec_cap = (unsigned int)std::min<long>(v, s->rec_cap);
-    }
+    // knob ENUM_KERNEL=0 keeps the round kernels (tests compare both)
+    s->enum_kernel = noprune && n >= 7 && n <= 16 && tuned_or("ENUM_KERNEL", 1) != 0;
+    if (double v; tuned("SEARCH_RECORD_CAP", &v) && v > 0)  // tests: force the second phase
+        s->rec_cap = (unsigned int)std::min<double>(v, s->rec_cap);
     rc = hrc;
     if (dbg) T1 = clk::now();
     if (!rc && threaded) rc = tspgpu_search_set_bound(s, ub);

@@ -1,6 +1,7 @@
 // Host-only parts of K2 (search_host.h): bound tour, city weights, input
 // check and the tie rule over the optimal set (tsp.cpp:457-470, 483-499).
 #include "search_host.h"
+#include "tuning.h"
 
 #include <algorithm>
 #include <cerrno>
@@ -260,7 +261,7 @@ bool heuristic(const V *d, int n, std::vector<int32_t> &best, V &cost, int first
     // ~7 us at 16 cities, all sixteen were a quarter of the whole in-process
     // search, and the device's suffix tests tighten the bound within the
     // first expansion anyway (profiles/r03/k2_variants.log)
-    if (n < 20 && (int)starts.size() > 4 && !std::getenv("TSPGPU_HEURISTIC_ALL_STARTS")) {
+    if (n < 20 && (int)starts.size() > 4 && tuned_or("HEURISTIC_ALL_STARTS", 0) == 0) {
         std::vector<int> few;
         for (int i = 0; i < 4; ++i) few.push_back(starts[(size_t)i * starts.size() / 4]);
         starts.swap(few);
@@ -289,7 +290,7 @@ bool heuristic(const V *d, int n, std::vector<int32_t> &best, V &cost, int first
         tours[i] = cb < cf ? std::move(bw) : std::move(fw);
     };
     int nt = n >= 20 ? std::min(ns, 8) : 1;
-    if (const char *e = std::getenv("TSPGPU_HEURISTIC_THREADS")) nt = std::max(1, std::min(ns, std::atoi(e)));
+    if (double v; tuned("HEURISTIC_THREADS", &v)) nt = std::max(1, std::min(ns, (int)v));
     bool done = false;
     if (nt > 1) {
         std::vector<std::thread> th;

@@ -6,6 +6,7 @@
 // host (computeDistanceMatrix, assignment2.h:184-200) because glibc pow(x,2)
 // differs from x*x in ~0.08% of inputs; the device never recomputes it.
 #include "tspgpu.h"
+#include "tuning.h"
 
 #include <hip/hip_runtime.h>
 
@@ -612,18 +613,16 @@ int tspgpu_ctx_create(const tspgpu_opts *opts, tspgpu_ctx **out)
         std::snprintf(c->name, sizeof c->name, "%s (%s, %d CUs)", nm[0] ? nm : "AMD GPU", prop.gcnArchName,
                       prop.multiProcessorCount);
     }
-    // tuning overrides for experiments (defaults are the measured best)
-    if (const char *e = std::getenv("TSPGPU_THREADS")) c->threads = std::atoi(e);
-    if (const char *e = std::getenv("TSPGPU_LDS_TABLE_MAX_N")) {
-        const int v = std::atoi(e);
-        c->lds_table_max_n = v < kLdsTableMaxN ? v : kLdsTableMaxN;
-    }
-    if (const char *e = std::getenv("TSPGPU_K1")) {
-        const int v = std::atoi(e);
+    // tuning knobs for experiments and tests (tuning.h; the defaults are the measured best)
+    double kv = 0.0;
+    if (tspgpu::tuned("THREADS", &kv)) c->threads = (int)kv;
+    if (tspgpu::tuned("LDS_TABLE_MAX_N", &kv)) c->lds_table_max_n = (int)kv < kLdsTableMaxN ? (int)kv : kLdsTableMaxN;
+    if (tspgpu::tuned("K1", &kv)) {
+        const int v = (int)kv;
         c->variant = v < 0 ? 1 : (v >= 6 ? 6 : (v >= 4 ? v : (v > 2 ? 2 : v)));
     }
-    if (const char *e = std::getenv("TSPGPU_TILED_CFG")) c->tiled_cfg = std::atoi(e);
-    if (const char *e = std::getenv("TSPGPU_WG_PER_CU")) c->wg_per_cu = std::atoi(e) > 0 ? std::atoi(e) : 0;
+    if (tspgpu::tuned("TILED_CFG", &kv)) c->tiled_cfg = (int)kv;
+    if (tspgpu::tuned("WG_PER_CU", &kv)) c->wg_per_cu = kv > 0 ? (int)kv : 0;
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
         delete c;
         return -EIO;

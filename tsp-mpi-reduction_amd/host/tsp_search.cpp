@@ -303,7 +303,7 @@ void chain_exchange(void *user, void *stream, void *word)
     if (ncclAllReduce(word, word, 1, ncclUint64, ncclMin, h->comm, (hipStream_t)stream) != ncclSuccess) h->rc = -EIO;
 }
 
-int search_multi(const Instance &in, int G, bool force_rccl, Result &res)
+int search_multi(const Instance &in, int G, bool force_rccl, int exchange_every, Result &res)
 {
     int ndev = tspgpu_device_count();
     if (ndev < 1) ndev = 1;
@@ -329,9 +329,8 @@ int search_multi(const Instance &in, int G, bool force_rccl, Result &res)
     uint64_t key[3] = {~0ull, ~0ull, 0};  // least w0, least w1 of its holders, any overflow
     std::vector<int32_t> tie_tour(in.n + 1, 0);
     std::atomic<int> tie_ok{0};
-    // frontier steps between two incumbent exchanges (TSPGPU_EXCHANGE_EVERY, default 4)
-    int every = 4;
-    if (const char *e = std::getenv("TSPGPU_EXCHANGE_EVERY")) every = std::max(1, std::atoi(e));
+    // frontier steps between two incumbent exchanges (--exchange-every, default 4)
+    const int every = std::max(1, exchange_every);
     const bool two = in.n - 1 > 20;
     std::barrier sync(G);
     std::vector<std::thread> th;
@@ -541,7 +540,7 @@ int main(int argc, char **argv)
 {
     Instance in;
     bool have = false, verify = false, tsplib_round = false, dump = false;
-    int gpus = 1, random_n = 0, clusters = 0;
+    int gpus = 1, random_n = 0, clusters = 0, exchange_every = 4;
     bool force_rccl = false;
     uint64_t seed = 1;
     std::string solver = "auto", cities_file, matrix_file, tsplib_file;
@@ -559,13 +558,14 @@ int main(int argc, char **argv)
         else if (a == "--tsplib") tsplib_file = next();
         else if (a == "--tsplib-round") tsplib_round = true;
         else if (a == "--gpus") gpus = std::atoi(next());
+        else if (a == "--exchange-every") exchange_every = std::atoi(next());  // frontier steps between exchanges
         else if (a == "--rccl") force_rccl = true;  // the RCCL exchange even on one GPU (one-rank communicator)
         else if (a == "--solver") solver = next();
         else if (a == "--verify") verify = true;
         else if (a == "--dump-matrix") dump = true;  // print the instance's matrix and exit (no GPU)
         else {
             std::fprintf(stderr, "usage: tsp_search (--random N [--seed S] [--clustered K] | --cities FILE "
-                                 "[--tsplib-round] | --matrix FILE | --tsplib FILE) [--gpus G] [--rccl] [--solver auto|wide|k1|k2|enum] [--verify]\n");
+                                 "[--tsplib-round] | --matrix FILE | --tsplib FILE) [--gpus G] [--rccl] [--exchange-every S] [--solver auto|wide|k1|k2|enum] [--verify]\n");
             return 1;
         }
     }
@@ -612,7 +612,7 @@ int main(int argc, char **argv)
     int rc = solver == "k1"     ? solve_k1(in, res)
              : solver == "wide" ? solve_wide(in, res)
              : solver == "enum" ? solve_enum(in, res)
-                                : search_multi(in, gpus, force_rccl, res);
+                                : search_multi(in, gpus, force_rccl, exchange_every, res);
     if (rc == -EOVERFLOW && in.n <= TSPGPU_WIDE_MAX_CITIES) {
         // more tied optima than the record buffers hold (e.g. coincident cities):
         // the DP returns the same tour directly

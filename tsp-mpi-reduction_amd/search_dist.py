@@ -23,7 +23,6 @@ min and its tie rule, across shards).
 from __future__ import annotations
 
 import errno
-import os
 import threading
 import time
 
@@ -59,8 +58,7 @@ def solve_sharded(ctx, dist, group=None, depth: int = 0, device=None, exchange_e
     2. Each rank runs its shard as ONE device chain (tspgpu_search_chain: the
        seeds, every frontier level and the tail fold back to back, one
        synchronisation).  A shard too large to chain runs step by step
-       instead, `exchange_every` steps between exchanges (default
-       TSPGPU_EXCHANGE_EVERY or 4).
+       instead, `exchange_every` steps between exchanges (default 4).
     3. Exchanges: ONE all-reduce(MIN) of the pair (incumbent word, -busy) —
        the same count on every rank, so the collectives pair up; after the
        last one (nobody busy) the MIN is the optimum.
@@ -97,9 +95,7 @@ def solve_sharded(ctx, dist, group=None, depth: int = 0, device=None, exchange_e
         ncoll[0] += 1
         return [int(x) for x in t.tolist()]
 
-    if exchange_every is None:
-        exchange_every = int(os.environ.get("TSPGPU_EXCHANGE_EVERY", "4"))
-    exchange_every = max(1, int(exchange_every))
+    exchange_every = max(1, int(exchange_every or 4))
 
     # the multi-start tour (host, split over the ranks: start cities r, r+W,
     # ...) on a thread while the search is created (ctypes releases the GIL)

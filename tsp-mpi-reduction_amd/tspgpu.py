@@ -39,6 +39,8 @@ EXPORTED_SYMBOLS = (
     "tspgpu_solve_instance",
     # K1 on integer distances
     "tspgpu_validate_i32", "tspgpu_solve_blocks_i32", "tspgpu_solve_blocks_i32_device",
+    # tuning / test knobs
+    "tspgpu_tuning_set", "tspgpu_tuning_clear",
 )
 
 F64, I32 = 0, 1
@@ -162,6 +164,8 @@ def lib():
                                          ctypes.c_uint64, ip]
         L.tspgpu_tie_tour.argtypes = [vp, ctypes.c_int, ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
                                       ip]
+        L.tspgpu_tuning_set.argtypes = [ctypes.c_char_p, ctypes.c_double]
+        L.tspgpu_tuning_clear.argtypes = [ctypes.c_char_p]
         L.tspgpu_tie_tour_gpu.argtypes = [vp, vp, ctypes.c_int, ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64,
                                           ctypes.c_uint64, ip]
         L.tspgpu_tie_key.argtypes = [ctypes.c_int, ip, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]
@@ -172,6 +176,31 @@ def lib():
                                     ctypes.c_int]
         _lib = L
     return _lib
+
+
+def tune(name: str, value) -> None:
+    """Set a tuning / test knob (tspgpu_tuning_set; include/tspgpu.h
+    "Tuning"): process-wide, read where the knob is used (K1 knobs at
+    Context creation, K2 knobs at search creation)."""
+    rc = lib().tspgpu_tuning_set(name.encode(), float(value))
+    if rc:
+        raise TspGpuError(rc, f"tspgpu_tuning_set({name})")
+
+
+def tune_from_environ() -> None:
+    """Development tools only (tools/*.py): every TSPGPU_<KNOB>=value of this
+    process's environment as tune(KNOB, value).  The library itself reads no
+    environment variable; neither the tests nor bench.py call this."""
+    for k, v in os.environ.items():
+        if k.startswith("TSPGPU_") and k != "TSPGPU_LIB":
+            tune(k[len("TSPGPU_"):], float(v))
+
+
+def untune(name: str | None = None) -> None:
+    """Back to the default (None: every knob)."""
+    rc = lib().tspgpu_tuning_clear(name.encode() if name else None)
+    if rc:
+        raise TspGpuError(rc, f"tspgpu_tuning_clear({name})")
 
 
 def _dp(a):
@@ -253,9 +282,14 @@ class Context:
         if rc:
             raise TspGpuError(rc, "tspgpu_ctx_create")
         self.handle = h
+        import weakref
+
+        self._searches = weakref.WeakSet()  # live Search objects: closed before the context
 
     def close(self):
         if self.handle:
+            for S in list(self._searches):
+                S.close()
             lib().tspgpu_ctx_destroy(self.handle)
             self.handle = None
 
@@ -601,6 +635,8 @@ class Search:
         if rc:
             raise TspGpuError(rc, "tspgpu_search_create")
         self.handle = h
+        if getattr(ctx, "_searches", None) is not None:
+            ctx._searches.add(self)
         dep, items, local = ctypes.c_int(), ctypes.c_uint64(), ctypes.c_uint64()
         lib().tspgpu_search_info(h, ctypes.byref(dep), ctypes.byref(items), ctypes.byref(local))
         self.depth, self.items, self.local_items = dep.value, items.value, local.value
