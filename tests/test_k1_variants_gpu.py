@@ -86,7 +86,10 @@ def test_n16_large_batch_every_variant(variant):
         used = _check(ctx, d, ref)
     finally:
         ctx.close()
-    assert used == (6 if variant is None else variant)
+    expect = 6 if variant is None else variant
+    if variant == 5 and not any(v == 5 for v, *_ in _k1_cfgs()):
+        expect = 4  # (no variant-5 forward kernel in a product build: the n = 16 fallback)
+    assert used == expect
 
 
 @pytest.mark.parametrize("n,vb,expect", [(13, 8, 6), (14, 8, 6), (15, 8, 6), (16, 8, 6), (12, 8, 2), (16, 4, 6),

@@ -589,3 +589,30 @@ def test_tree_bound_on_the_hard_32_city_seeds(gpu_ctx, knobs):
             cost, tour, _ = tspgpu.search_solve(gpu_ctx, d)
             knobs.clear("SEARCH_MST")
             assert (cost, tour.tolist()) == got[0]
+
+
+@pytest.mark.parametrize("n,cap", [(16, 8), (22, 10)])
+def test_chain_overflow_reads_no_unwritten_slot(knobs, n, cap):
+    """A chained level that overflows leaves output slots it reserved but never
+    wrote.  On a FRESH context whose level and tail buffers are filled with
+    0xFF bytes (knob SEARCH_CHAIN_POISON: paths of length 255, cities 255 —
+    out of range of every LDS table), a forced overflow (tiny level buffers)
+    must still return the stepwise search's answer: the chained kernels after
+    the overflow read no slot (they return at once) and the rerun starts from
+    the chain's starting state."""
+    from bench import Shard, k2_instance
+
+    d = Shard(16, 1, 0, 1).distances()[0] if n == 16 else np.asarray(k2_instance(n, 3))
+    ctx = tspgpu.Context(device=0)
+    try:
+        knobs.set("SEARCH_CHAIN_POISON", 1)
+        knobs.set("SEARCH_CHAIN_CAP_LOG2", cap)
+        c1, t1, s1 = tspgpu.search_solve(ctx, d)
+        knobs.clear()
+        knobs.set("SEARCH_CHAIN", 0)
+        c0, t0, _ = tspgpu.search_solve(ctx, d)
+    finally:
+        ctx.close()
+    assert c1 == c0 and t1.tolist() == t0.tolist(), s1
+    if n == 16:
+        assert c1 == 3871.1947567096445 and t1.tolist() == [0, 14, 2, 13, 10, 12, 6, 4, 9, 11, 3, 5, 15, 8, 1, 7, 0]

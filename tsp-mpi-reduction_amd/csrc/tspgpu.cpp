@@ -168,13 +168,29 @@ int ensure_tiled_info(tspgpu_ctx *c, int L)
 // n = 16) until its backtracking kernel has run, so a launch takes blocks in
 // chunks: up to 65536 (108 GB of the 288 GB at n = 16 — a persistent grid of
 // 1536 workgroups then idles a third of the chip for 0.67 of 42.7 rounds
-// instead of 0.67 of 10.7 at 16384), halved while the allocation fails.
+// instead of 0.67 of 10.7 at 16384), at most 3/4 of the device memory free
+// at that moment (other contexts or ranks on the same GPU keep theirs),
+// halved while the allocation fails, down to 64 blocks.  A slot area far
+// larger than a later launch needs (> 4x and > 8 GB) is given back first.
 int ensure_slots(tspgpu_ctx *c, int nblocks, size_t slot, int *chunk)
 {
     int ch = std::min(nblocks, 65536);
+    const size_t need = (size_t)ch * slot;
+    if (c->d_tslots && c->tslots_bytes > 4 * need && c->tslots_bytes > ((size_t)8 << 30)) {
+        (void)hipFree(c->d_tslots);
+        c->d_tslots = nullptr;
+        c->tslots_bytes = 0;
+    }
+    if (c->tslots_bytes < need) {
+        size_t free_b = 0, total_b = 0;
+        if (hipMemGetInfo(&free_b, &total_b) == hipSuccess) {
+            const size_t usable = (free_b + c->tslots_bytes) / 4 * 3;  // (the current area is freed first)
+            while (ch > 64 && (size_t)ch * slot > usable) ch /= 2;
+        }
+    }
     for (;;) {
         const int rc = ensure(&c->d_tslots, &c->tslots_bytes, (size_t)ch * slot);
-        if (rc == 0 || rc != -ENOMEM || ch <= 1024) {
+        if (rc == 0 || rc != -ENOMEM || ch <= 64) {
             *chunk = ch;
             return rc;
         }

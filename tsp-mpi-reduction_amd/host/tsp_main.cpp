@@ -212,8 +212,15 @@ int read_rank_files(const std::string &dir, uint64_t key, int P, int n, int B, i
             RankFileHeader h{};
             const bool hdr = std::fread(&h, sizeof h, 1, f) == 1 && h.magic == kMagic;
             if (!hdr || h.job != key || h.B != B || h.X != X || h.Y != Y || (int)h.n != n || (int)h.rank != r) {
-                std::fclose(f);  // stale (an earlier run's) or foreign: drop it, keep waiting for this job's
-                std::remove(fin.c_str());
+                // stale (an earlier run's) or foreign: drop it, keep waiting for
+                // this job's — but only if the path still names the file just
+                // read: the worker may have rename()d its fresh file over it
+                // meanwhile, and that one must not be deleted
+                struct stat open_st {}, path_st {};
+                const bool same = fstat(fileno(f), &open_st) == 0 && stat(fin.c_str(), &path_st) == 0 &&
+                                  open_st.st_ino == path_st.st_ino && open_st.st_dev == path_st.st_dev;
+                std::fclose(f);
+                if (same) std::remove(fin.c_str());
                 continue;
             }
             if (h.status != 0) {
