@@ -36,10 +36,11 @@ namespace tspgpu {
 // sub-cube-ordered high columns, odd so that the low-low gathers of a
 // half-wave spread over the banks (25: 1% faster than 21 and 23 at n = 16,
 // profiles/r03/k1_ab_table.log run 6)
+// (L = 9, 128-thread workgroups: 23, so that twelve workgroups' LDS fits a CU)
 #ifndef TSPGPU_SUB_DS
 #define TSPGPU_SUB_DS 25
 #endif
-constexpr int kSubDS = TSPGPU_SUB_DS;
+__host__ __device__ constexpr int sub_ds(int L) { return L >= 10 ? TSPGPU_SUB_DS : 23; }
 
 // one entry per L-bit mask (indexed like TiledInfo::mask, L <= 10): nibbles
 // 0..L-1 = the members ascending, then the non-members ascending; bytes
@@ -51,7 +52,7 @@ struct SubRow {
 
 __host__ __device__ constexpr size_t sub_img_bytes(int N, int L, int vb)
 {
-    return (size_t)(N + (N - L)) * kSubDS * vb;
+    return (size_t)(N + (N - L)) * sub_ds(L) * vb;
 }
 // One low layer in LDS at a time (TSPGPU_SUB_ONE_LAYER): a middle pass loads
 // its rows' values into registers, the workgroup passes a barrier, and the
@@ -322,6 +323,15 @@ __host__ __device__ constexpr int sub_lds_role(int k)
     return -1;
 }
 
+// Timing-only ablations (measurement builds, tools/ab_build.sh; the results
+// are WRONG): 1 = the middle passes take their high members' values from the
+// LDS region instead of the push loads, 2 = no LDS distance gathers (one
+// register value), 4 = no barrier between the middle passes, 8 = no push
+// stores in the middle passes, 16 = the sub-cube barriers wait for LDS only
+#ifndef TSPGPU_SUB_ABL
+#define TSPGPU_SUB_ABL 0
+#endif
+
 #ifndef TSPGPU_SUB_QC
 #define TSPGPU_SUB_QC 7  // destinations relaxed together (register budget)
 #endif
@@ -346,7 +356,7 @@ __device__ __forceinline__ void sub_mid(const SubCtx<V, N, L> &c, uint32_t h, ui
     constexpr int CUR = sub_layer_off(L, J);
     constexpr int NXT = sub_layer_off(L, J + 1);
     constexpr bool ARG = T >= N - TSPGPU_TILED_TA_OFF;
-    constexpr uint32_t DSB = (uint32_t)(kSubDS * VB);
+    constexpr uint32_t DSB = (uint32_t)(sub_ds(L) * VB);
     constexpr uint32_t HR0 = (uint32_t)N * DSB;  // image row N: the first sub-cube-ordered high row
     constexpr uint32_t HC0 = (uint32_t)N * VB;   // image column N
     uint32_t hm[HC > 0 ? HC : 1], hn[QH > 0 ? QH : 1];
@@ -381,7 +391,9 @@ __device__ __forceinline__ void sub_mid(const SubCtx<V, N, L> &c, uint32_t h, ui
     if (!act) return;
     const uint32_t voff = (BASE + r) * VB;  // the row's offset in a push column
 #pragma unroll
-    for (int i = 0; i < HC; ++i) g[J + i] = c.push.load(voff, (h * H + hm[i]) * (uint32_t)(NL * VB));
+    for (int i = 0; i < HC; ++i)
+        g[J + i] = (TSPGPU_SUB_ABL & 1) ? c.region[CUR + (i % J) * ROWS + r]
+                                        : c.push.load(voff, (h * H + hm[i]) * (uint32_t)(NL * VB));
     uint32_t mrow[J], kof[QL];
 #pragma unroll
     for (int p = 0; p < J; ++p) mrow[p] = sub_nib(ent, p) * DSB;
@@ -406,7 +418,9 @@ __device__ __forceinline__ void sub_mid(const SubCtx<V, N, L> &c, uint32_t h, ui
         auto dload = [&](auto kk) -> V {
             constexpr int pq = sub_lds_pair<T, J, QL, C0, QN, QP>(decltype(kk)::value);
             constexpr int p = pq / 64, q = C0 + pq % 64;
-            if constexpr (p < J && q < QL)
+            if constexpr (TSPGPU_SUB_ABL & 2)
+                return g[p] + g[0];  // (ablation: no gather)
+            else if constexpr (p < J && q < QL)
                 return lds_val<V>(c.img, mrow[p] + kof[q]);
             else if constexpr (p < J)
                 return lds_val<V>(c.img, mrow[p] + HC0 + (q - QL) * VB);
@@ -500,7 +514,7 @@ __device__ __forceinline__ void sub_mid(const SubCtx<V, N, L> &c, uint32_t h, ui
             } else {
                 // high k -> push column (h | k, k) of sub-cube h | k, same row index
                 const uint32_t cb = hn[q - QL];
-                c.push.store(voff, ((h | (1u << cb)) * H + cb) * (uint32_t)(NL * VB), acc[qq]);
+                if (!(TSPGPU_SUB_ABL & 8)) c.push.store(voff, ((h | (1u << cb)) * H + cb) * (uint32_t)(NL * VB), acc[qq]);
             }
             if constexpr (ARG) {
                 const uint32_t pos = arg[qq] / DSB;  // image row of the argmin member = its city bit
@@ -527,7 +541,7 @@ __device__ __forceinline__ void sub_first(const SubCtx<V, N, L> &c, uint32_t h, 
 {
     constexpr int H = N - L, QH = H - C, Q1 = N - 1 - C;
     constexpr int NL = 1 << L, VB = sizeof(V);
-    constexpr uint32_t DSB = (uint32_t)(kSubDS * VB);
+    constexpr uint32_t DSB = (uint32_t)(sub_ds(L) * VB);
     constexpr int ROWS2 = cbinom(L, 2);
     static_assert(C + 1 < N - TSPGPU_TILED_TA_OFF, "first passes are min-only");
     if (tid >= (uint32_t)(L * Q1 + (C > 0 ? QH : 0))) return;
@@ -593,7 +607,7 @@ __device__ __forceinline__ void sub_last(const SubCtx<V, N, L> &c, uint32_t h, u
     constexpr bool ARG = T >= N - TSPGPU_TILED_TA_OFF;
     constexpr int QP = pow2_at_least(Q);
     constexpr int NL = 1 << L, VB = sizeof(V);
-    constexpr uint32_t DSB = (uint32_t)(kSubDS * VB);
+    constexpr uint32_t DSB = (uint32_t)(sub_ds(L) * VB);
     if (lane >= (uint32_t)QP) return;
     uint32_t hm[C > 0 ? C : 1];
     {
@@ -635,7 +649,7 @@ __device__ __forceinline__ void sub_penult(const SubCtx<V, N, L> &c, uint32_t h,
     constexpr bool ARG = T >= N - TSPGPU_TILED_TA_OFF;
     constexpr int QP = pow2_at_least(Q);
     constexpr int NL = 1 << L, VB = sizeof(V);
-    constexpr uint32_t DSB = (uint32_t)(kSubDS * VB);
+    constexpr uint32_t DSB = (uint32_t)(sub_ds(L) * VB);
     constexpr int ROWS = L, BASE = tiled_moff(L, J);
     constexpr int CUR = sub_layer_off(L, J);
     if (tid >= (uint32_t)(L * QP)) return;
@@ -687,7 +701,7 @@ template <typename V, int N, int L>
 __device__ __forceinline__ void sub_build_high(const SubCtx<V, N, L> &c, uint32_t h, uint32_t e)
 {
     constexpr int H = N - L, VB = sizeof(V);
-    constexpr uint32_t DSB = (uint32_t)(kSubDS * VB);
+    constexpr uint32_t DSB = (uint32_t)(sub_ds(L) * VB);
     const uint32_t cc = (uint32_t)__builtin_popcount(h);
     const uint32_t nh = ~h & ((1u << H) - 1u);
     char *img = c.img;
@@ -782,10 +796,14 @@ __global__ __launch_bounds__(THREADS, tiled_waves(THREADS, sub_wg(WG))) void hk_
     constexpr int NL = 1 << L;
     constexpr int n = N + 1;
     constexpr int VB = sizeof(V);
-    constexpr uint32_t DSB = (uint32_t)(kSubDS * VB);
+    constexpr uint32_t DSB = (uint32_t)(sub_ds(L) * VB);
     static_assert(H >= 1 && H <= 6 && L >= 5 && L <= 10, "variant 6 sizes");
-    static_assert(kSubDS >= N + H, "image stride");
-    static_assert(THREADS >= 256 && L * (N - 1) + H <= 192, "edge passes: lanes 0..191, pass L at 192..");
+    static_assert(sub_ds(L) >= N + H, "image stride");
+    // a middle pass gives each of its rows a thread; the edge intervals loop
+    // their virtual lanes (pass 0/1 lanes 0..191, pass L 192..; pass L-1
+    // lanes 0..127, the next sub-cube's image rows 128..) over the workgroup
+    static_assert(THREADS % 64 == 0 && THREADS >= cbinom(L, L / 2), "one row per thread in a middle pass");
+    static_assert(L * (N - 1) + H <= 192 && L * 8 <= 128, "edge intervals: virtual lane layout");
     // static LDS: image/region offsets fold into immediates (A/B against
     // dynamic LDS: equal within noise, profiles/r03/k1_ab_table.log)
     __shared__ __attribute__((aligned(16))) char smem[sub_lds_bytes(N, L, VB)];
@@ -829,11 +847,15 @@ __global__ __launch_bounds__(THREADS, tiled_waves(THREADS, sub_wg(WG))) void hk_
                 constexpr int M2 = tiled_moff(L, 2), C2 = cbinom(L, 2);
                 ent = rowtab[M2 + (t < (uint32_t)C2 ? t : 0u)];
             }
-            if (t < 192u)
-                sub_dispatch_first<V, N, L>(c, h, hc, t);
-            else if (h > 0)
-                sub_dispatch_last<V, N, L>(c, h - 1, __builtin_popcount(h - 1), t - 192u);
-            __syncthreads();
+#pragma unroll
+            for (uint32_t v0 = 0; v0 < 256u; v0 += THREADS) {  // (one iteration at 256 threads)
+                const uint32_t v = t + v0;
+                if (v < 192u)
+                    sub_dispatch_first<V, N, L>(c, h, hc, v);
+                else if (h > 0)
+                    sub_dispatch_last<V, N, L>(c, h - 1, __builtin_popcount(h - 1), v - 192u);
+            }
+            if (TSPGPU_SUB_ABL & 16) lds_barrier(); else __syncthreads();
             // middle passes j = 2..L-2, unrolled (every offset a compile-time
             // constant); the next pass's row entry is loaded one pass ahead
             static_for<L - 3>([&](auto jj) {
@@ -845,15 +867,19 @@ __global__ __launch_bounds__(THREADS, tiled_waves(THREADS, sub_wg(WG))) void hk_
                     ent = rowtab[MN + (tj < (uint32_t)CN ? tj : 0u)];
                 }
                 sub_dispatch_mid_j<V, N, L, j>(c, h, hc, tj, cur);
-                lds_barrier();
+                if (!(TSPGPU_SUB_ABL & 4)) lds_barrier();
             });
             // pass L - 1 (lanes < 128) beside the next sub-cube's high image rows/columns (lanes 128..)
             t = opaque_u32(tid);
-            if (t < 128u)
-                sub_dispatch_penult<V, N, L>(c, h, hc, t);
-            else if (h + 1 < (uint32_t)NH)
-                sub_build_high<V, N, L>(c, h + 1, t - 128u);
-            __syncthreads();
+#pragma unroll
+            for (uint32_t v0 = 0; v0 < 256u; v0 += THREADS) {
+                const uint32_t v = t + v0;
+                if (v < 128u)
+                    sub_dispatch_penult<V, N, L>(c, h, hc, v);
+                else if (h + 1 < (uint32_t)NH)
+                    sub_build_high<V, N, L>(c, h + 1, v - 128u);
+            }
+            if (TSPGPU_SUB_ABL & 16) lds_barrier(); else __syncthreads();
         }
 
         // closing min (tsp.cpp:483-499): G[full][m] + d[m][0], first strict min
