@@ -327,7 +327,10 @@ __host__ __device__ constexpr int sub_lds_role(int k)
 // are WRONG): 1 = the middle passes take their high members' values from the
 // LDS region instead of the push loads, 2 = no LDS distance gathers (one
 // register value), 4 = no barrier between the middle passes, 8 = no push
-// stores in the middle passes, 16 = the sub-cube barriers wait for LDS only
+// stores in the middle passes, 16 = the sub-cube barriers wait for LDS only,
+// 32 = the middle passes' push loads all read one L2-resident row (the loads
+// stay, their memory traffic goes), 64 = the middle passes' push stores all
+// write one L2-resident row (likewise)
 #ifndef TSPGPU_SUB_ABL
 #define TSPGPU_SUB_ABL 0
 #endif
@@ -339,8 +342,68 @@ __host__ __device__ constexpr int sub_lds_role(int k)
 #define TSPGPU_SUB_AHEAD 6  // distance loads in flight per lane
 #endif
 
+// Push columns recycled (TSPGPU_SUB_RECYCLE).  Column (h', x) is written by
+// sub-cube h' \ x and read by sub-cube h' only, so in the numeric sub-cube
+// order it is live over [h' \ x, h']; first-fit over those intervals gives
+// 23 columns at H = 5 instead of 80 (184 KB per block instead of 640 KB), and
+// the six resident blocks of a CU then touch ~280 MB of pushes instead of ~1
+// GB — close to the 256 MB Infinity Cache.  (Ablations, profiles/r04: push
+// loads and stores redirected to one L2-resident row -18% forward time.)
+#ifndef TSPGPU_SUB_RECYCLE
+#define TSPGPU_SUB_RECYCLE 0
+#endif
+template <int H>
+struct SubColMap {
+    uint32_t slot[(1 << H) * H];
+    int count;
+};
+template <int H>
+constexpr SubColMap<H> sub_col_map()
+{
+    SubColMap<H> m{};
+    int until[(1 << H) * H] = {};  // per column slot: the consumer sub-cube of its current column
+    int n = 0;
+    for (int p = 0; p < (1 << H); ++p)  // producers in the forward order
+        for (int x = 0; x < H; ++x) {
+            if ((p >> x) & 1) continue;
+            const int hp = p | (1 << x);
+            int s = -1;
+            for (int k = 0; k < n && s < 0; ++k)
+                if (until[k] < p) s = k;  // (its consumer has finished)
+            if (s < 0) s = n++;
+            until[s] = hp;
+            m.slot[hp * H + x] = (uint32_t)s;
+        }
+    m.count = n;
+    return m;
+}
+template <int H>
+__constant__ SubColMap<H> g_sub_cols = sub_col_map<H>();
+// the push column of (sub-cube hp, high city x)
+template <int H>
+__device__ __forceinline__ uint32_t sub_col(uint32_t hp, uint32_t x)
+{
+    // (wave-uniform: a scalar load from the constant table)
+    if constexpr (TSPGPU_SUB_RECYCLE) return g_sub_cols<H>.slot[__builtin_amdgcn_readfirstlane(hp * H + x)];
+    return hp * H + x;
+}
+
+// Deferred push stores (TSPGPU_SUB_DEFER).  Vector-memory operations retire
+// in issue order (one vmcnt per wave), so a pass's push loads, issued after
+// the previous pass's push stores, could only be used once those stores had
+// completed: every pass waited for the last one's write acknowledgements.  A
+// middle pass now keeps its high-destination results in registers (at most
+// H - |h| values per thread), issues the NEXT pass's push loads first and only
+// then these stores — the loads no longer queue behind them.  (Ablations,
+// profiles/r04: no middle push stores -18% forward time, no push loads -11%.)
+#ifndef TSPGPU_SUB_DEFER
+#define TSPGPU_SUB_DEFER 0  // measured slower: +14% forward time (62 VGPR spills), profiles/r04/k1_defer_ab.log
+#endif
+constexpr int kSubPend = 6;  // >= H - |h|
+
 template <typename V, int N, int L, int T, int J>
-__device__ __forceinline__ void sub_mid(const SubCtx<V, N, L> &c, uint32_t h, uint32_t tid, const uint4 &ent)
+__device__ __forceinline__ void sub_mid(const SubCtx<V, N, L> &c, uint32_t h, uint32_t tid, const uint4 &ent,
+                                        V (&pend)[kSubPend])
 {
     constexpr int H = N - L;
     constexpr int Q = N - T;
@@ -388,12 +451,25 @@ __device__ __forceinline__ void sub_mid(const SubCtx<V, N, L> &c, uint32_t h, ui
     // (one layer in LDS: every wave has its row's values before any of the
     // next layer overwrites them)
     if (TSPGPU_SUB_ONE_LAYER) lds_barrier();
-    if (!act) return;
     const uint32_t voff = (BASE + r) * VB;  // the row's offset in a push column
+    if (act) {
 #pragma unroll
-    for (int i = 0; i < HC; ++i)
-        g[J + i] = (TSPGPU_SUB_ABL & 1) ? c.region[CUR + (i % J) * ROWS + r]
-                                        : c.push.load(voff, (h * H + hm[i]) * (uint32_t)(NL * VB));
+        for (int i = 0; i < HC; ++i)
+            g[J + i] = (TSPGPU_SUB_ABL & 1)    ? c.region[CUR + (i % J) * ROWS + r]
+                       : (TSPGPU_SUB_ABL & 32) ? c.push.load(r * VB, 0)
+                                               : c.push.load(voff, sub_col<H>(h, hm[i]) * (uint32_t)(NL * VB));
+    }
+    // the previous middle pass's pushes, behind this pass's loads
+    constexpr bool DEFER_IN = TSPGPU_SUB_DEFER && J > 2, DEFER_OUT = TSPGPU_SUB_DEFER && J < L - 2;
+    if constexpr (DEFER_IN) {
+        constexpr int ROWS_P = cbinom(L, J - 1), BASE_P = tiled_moff(L, J - 1);
+        if (r < (uint32_t)ROWS_P) {
+#pragma unroll
+            for (int u = 0; u < QH; ++u)
+                c.push.store((BASE_P + r) * VB, sub_col<H>(h | (1u << hn[u]), hn[u]) * (uint32_t)(NL * VB), pend[u]);
+        }
+    }
+    if (!act) return;
     uint32_t mrow[J], kof[QL];
 #pragma unroll
     for (int p = 0; p < J; ++p) mrow[p] = sub_nib(ent, p) * DSB;
@@ -514,7 +590,12 @@ __device__ __forceinline__ void sub_mid(const SubCtx<V, N, L> &c, uint32_t h, ui
             } else {
                 // high k -> push column (h | k, k) of sub-cube h | k, same row index
                 const uint32_t cb = hn[q - QL];
-                if (!(TSPGPU_SUB_ABL & 8)) c.push.store(voff, ((h | (1u << cb)) * H + cb) * (uint32_t)(NL * VB), acc[qq]);
+                if (TSPGPU_SUB_ABL & 64)
+                    c.push.store(r * VB, 8192u, acc[qq]);
+                else if (DEFER_OUT)
+                    pend[q - QL] = acc[qq];  // (stored by the next pass, after its loads)
+                else if (!(TSPGPU_SUB_ABL & 8))
+                    c.push.store(voff, sub_col<H>(h | (1u << cb), cb) * (uint32_t)(NL * VB), acc[qq]);
             }
             if constexpr (ARG) {
                 const uint32_t pos = arg[qq] / DSB;  // image row of the argmin member = its city bit
@@ -557,7 +638,7 @@ __device__ __forceinline__ void sub_first(const SubCtx<V, N, L> &c, uint32_t h, 
     const uint32_t nh = ~h & ((1u << H) - 1u);
     V g0[C > 0 ? C : 1];  // G[h][hm_i]: row 0 of sub-cube h (wave-uniform)
 #pragma unroll
-    for (int i = 0; i < C; ++i) g0[i] = c.push.load(0, (h * H + hm[i]) * (uint32_t)(NL * VB));
+    for (int i = 0; i < C; ++i) g0[i] = c.push.load(0, sub_col<H>(h, hm[i]) * (uint32_t)(NL * VB));
     if (tid < (uint32_t)(L * Q1)) {
         const uint32_t a = tid / Q1, q = tid % Q1;
         const uint32_t kk = q < (uint32_t)(L - 1) ? q + (q >= a ? 1u : 0u) : L + nth_bit(nh, q - (L - 1));
@@ -574,7 +655,7 @@ __device__ __forceinline__ void sub_first(const SubCtx<V, N, L> &c, uint32_t h, 
         const uint32_t voff = (1u + a) * VB;  // row {a}: index 1 + a in the mask list
 #pragma unroll
         for (int i = 0; i < C; ++i) {
-            const V g1 = c.push.load(voff, (h * H + hm[i]) * (uint32_t)(NL * VB));
+            const V g1 = c.push.load(voff, sub_col<H>(h, hm[i]) * (uint32_t)(NL * VB));
             relax_min(acc, g1, lds_val<V>(c.img, (L + hm[i]) * DSB + kk * VB));
         }
         if (kk < (uint32_t)L) {
@@ -583,7 +664,7 @@ __device__ __forceinline__ void sub_first(const SubCtx<V, N, L> &c, uint32_t h, 
             c.region[(kk > a ? ROWS2 : 0) + hi * (hi - 1) / 2 + lo] = acc;
         } else {
             const uint32_t x = kk - L;
-            c.push.store(voff, ((h | (1u << x)) * H + x) * (uint32_t)(NL * VB), acc);
+            c.push.store(voff, sub_col<H>(h | (1u << x), x) * (uint32_t)(NL * VB), acc);
         }
     } else if constexpr (C > 0) {
         // pass j = 0, high destination: G[h + x][x] -> push row 0 of sub-cube h | x
@@ -591,7 +672,7 @@ __device__ __forceinline__ void sub_first(const SubCtx<V, N, L> &c, uint32_t h, 
         V acc = g0[0] + lds_val<V>(c.img, (L + hm[0]) * DSB + (L + x) * VB);
 #pragma unroll
         for (int i = 1; i < C; ++i) relax_min(acc, g0[i], lds_val<V>(c.img, (L + hm[i]) * DSB + (L + x) * VB));
-        c.push.store(0, ((h | (1u << x)) * H + x) * (uint32_t)(NL * VB), acc);
+        c.push.store(0, sub_col<H>(h | (1u << x), x) * (uint32_t)(NL * VB), acc);
     }
 }
 
@@ -627,10 +708,10 @@ __device__ __forceinline__ void sub_last(const SubCtx<V, N, L> &c, uint32_t h, u
     for (int m = 0; m < L; ++m) relax_any<ARG>(m == 0, acc, arg, c.layerL[m], lds_val<V>(c.img, m * DSB + kk * VB), (uint32_t)m);
 #pragma unroll
     for (int i = 0; i < C; ++i) {
-        const V g = c.push.load((NL - 1) * VB, (h * H + hm[i]) * (uint32_t)(NL * VB));
+        const V g = c.push.load((NL - 1) * VB, sub_col<H>(h, hm[i]) * (uint32_t)(NL * VB));
         relax_any<ARG>(false, acc, arg, g, lds_val<V>(c.img, (L + hm[i]) * DSB + kk * VB), L + hm[i]);
     }
-    if (act) c.push.store((NL - 1) * VB, ((h | (1u << x)) * H + x) * (uint32_t)(NL * VB), acc);
+    if (act) c.push.store((NL - 1) * VB, sub_col<H>(h | (1u << x), x) * (uint32_t)(NL * VB), acc);
     if constexpr (ARG) {
         const uint64_t w = group_or<QP>(act ? (uint64_t)arg << (4 * lane) : 0ull);
         if (lane == 0) c.par.store((NL - 1) * 8u, h * (uint32_t)(NL * 8), w);
@@ -676,14 +757,14 @@ __device__ __forceinline__ void sub_penult(const SubCtx<V, N, L> &c, uint32_t h,
     }
 #pragma unroll
     for (int i = 0; i < C; ++i) {
-        const V g = c.push.load(voff, (h * H + hm[i]) * (uint32_t)(NL * VB));
+        const V g = c.push.load(voff, sub_col<H>(h, hm[i]) * (uint32_t)(NL * VB));
         relax_any<ARG>(false, acc, arg, g, lds_val<V>(c.img, (L + hm[i]) * DSB + kk * VB), L + hm[i]);
     }
     if (act) {
         if (q == 0)
             c.layerL[b] = acc;
         else
-            c.push.store(voff, ((h | (1u << x)) * H + x) * (uint32_t)(NL * VB), acc);
+            c.push.store(voff, sub_col<H>(h | (1u << x), x) * (uint32_t)(NL * VB), acc);
     }
     if constexpr (ARG) {
         const uint64_t w = group_or<QP>(act ? (uint64_t)arg << (4 * q) : 0ull);
@@ -723,12 +804,12 @@ __device__ __forceinline__ void sub_build_high(const SubCtx<V, N, L> &c, uint32_
 
 template <typename V, int N, int L, int J>
 __device__ __forceinline__ void sub_dispatch_mid_j(const SubCtx<V, N, L> &c, uint32_t h, int hc, uint32_t tid,
-                                                   const uint4 &ent)
+                                                   const uint4 &ent, V (&pend)[kSubPend])
 {
     constexpr int H = N - L;
-#define TSPGPU_SM(HC)                                                                       \
-    case HC:                                                                                \
-        if constexpr (HC <= H) sub_mid<V, N, L, J + (HC <= H ? HC : 0), J>(c, h, tid, ent);  \
+#define TSPGPU_SM(HC)                                                                             \
+    case HC:                                                                                      \
+        if constexpr (HC <= H) sub_mid<V, N, L, J + (HC <= H ? HC : 0), J>(c, h, tid, ent, pend);  \
         break;
     switch (hc) {
         TSPGPU_SM(0) TSPGPU_SM(1) TSPGPU_SM(2) TSPGPU_SM(3) TSPGPU_SM(4) TSPGPU_SM(5) TSPGPU_SM(6) TSPGPU_SM(7)
@@ -835,10 +916,13 @@ __global__ __launch_bounds__(THREADS, tiled_waves(THREADS, sub_wg(WG))) void hk_
             dc[tid] = dsrc[(tid + 1) * n];
         }
         // layer 1 of the high cities: G[{x}][x] = d[0][x] (tsp.cpp:435), pushed to sub-cube {x}, row 0
-        if (tid < H) c.push.store(0, (((1u << tid) * H + tid) * NL) * VB, dsrc[L + tid + 1]);
+        if (tid < H) c.push.store(0, (sub_col<H>(1u << tid, tid) * NL) * VB, dsrc[L + tid + 1]);
         __syncthreads();
 
         uint4 ent = make_uint4(0, 0, 0, 0);
+        V pend[kSubPend];  // deferred push stores of the last middle pass (TSPGPU_SUB_DEFER)
+#pragma unroll
+        for (int u = 0; u < kSubPend; ++u) pend[u] = V(0);
         for (uint32_t h = 0; h < (uint32_t)NH; ++h) {
             const int hc = __builtin_popcount(h);
             // interval A(h): passes 0/1 of h (lanes < 192) beside pass L of h - 1 (lanes 192..)
@@ -866,7 +950,7 @@ __global__ __launch_bounds__(THREADS, tiled_waves(THREADS, sub_wg(WG))) void hk_
                     constexpr int MN = tiled_moff(L, j + 1), CN = cbinom(L, j + 1);
                     ent = rowtab[MN + (tj < (uint32_t)CN ? tj : 0u)];
                 }
-                sub_dispatch_mid_j<V, N, L, j>(c, h, hc, tj, cur);
+                sub_dispatch_mid_j<V, N, L, j>(c, h, hc, tj, cur, pend);
                 if (!(TSPGPU_SUB_ABL & 4)) lds_barrier();
             });
             // pass L - 1 (lanes < 128) beside the next sub-cube's high image rows/columns (lanes 128..)
@@ -891,7 +975,7 @@ __global__ __launch_bounds__(THREADS, tiled_waves(THREADS, sub_wg(WG))) void hk_
                 if (m <= L)
                     gl = c.layerL[m - 1];
                 else
-                    gl = c.push.load((NL - 1) * VB, ((uint32_t)((NH - 1) * H + (m - 1 - L)) * NL) * VB);
+                    gl = c.push.load((NL - 1) * VB, (sub_col<H>(NH - 1, m - 1 - L) * NL) * VB);
             }
             const V cand = valid ? gl + dc[m - 1] : ValT<V>::invalid;
             const V best = ValT<V>::vmin(wave_min(cand), ValT<V>::inf);
@@ -908,6 +992,145 @@ __global__ __launch_bounds__(THREADS, tiled_waves(THREADS, sub_wg(WG))) void hk_
         __syncthreads();
     }
 }
+
+// ---------------------------------------------------------------------------
+// Backtracking of variant 6 with recycled push columns (TSPGPU_SUB_RECYCLE:
+// the forward pass no longer keeps every pushed value, so the rows below the
+// parent words cannot be recomputed from them).  One wave per block:
+// (1) the rows with >= N - TSPGPU_TILED_TA_OFF members: their parent words,
+//     as hk_tiled_backtrack;
+// (2) below: the first prefix set T0 = {t1..tK} (K = N - TA_OFF - 1 cities)
+//     gets its own Held-Karp, G[S][m] for every S within T0, in the slot's
+//     recompute area (2^K x K values) — the same recurrence over the same
+//     IEEE adds and mins, so the forward pass's bits (G[S][m] depends on S
+//     and m only; min is order-free) — and the walk continues with the first
+//     strict minimum over the members ascending (tsp.cpp:457-470), cities of
+//     T0 ascending = local indices ascending.
+// 10 * 9 * 2^8 = 23 K relaxations per 16-city block (1.3% of the forward
+// pass), against a recompute of whole sub-cube rows before.
+// ---------------------------------------------------------------------------
+constexpr int kSubBtWaves = 4;
+__host__ __device__ constexpr int sub_bt_k(int N) { return N - TSPGPU_TILED_TA_OFF - 1; }
+__host__ __device__ constexpr size_t sub_rec_bytes(int N, int vb) { return ((size_t)vb * sub_bt_k(N)) << sub_bt_k(N); }
+// one block's global slot for variant 6: push area, parent words and the
+// recompute area of either backtracking kernel
+__host__ __device__ constexpr size_t sub_slot_bytes(int N, int L, int vb)
+{
+    const size_t rec = tiled_recomp_bytes(L, vb) > sub_rec_bytes(N, vb) ? tiled_recomp_bytes(L, vb) : sub_rec_bytes(N, vb);
+    return tiled_push_bytes(N, L, vb) + tiled_parent_bytes(N, L) + ((rec + 255) & ~(size_t)255);
+}
+
+namespace {  // (internal linkage, like hk_tiled_backtrack)
+template <typename V, int N, int L>
+__global__ __launch_bounds__(64 * kSubBtWaves) void hk_sub_backtrack(int nblocks, int blk0,
+                                                                     const char *__restrict__ slots, uint32_t slot_bytes,
+                                                                     const TiledInfo *__restrict__ info,
+                                                                     const V *__restrict__ dist,
+                                                                     V *__restrict__ cost_out,
+                                                                     int32_t *__restrict__ tour_out)
+{
+    constexpr int NL = 1 << L, n = N + 1, VB = sizeof(V), K = sub_bt_k(N), NK = 1 << K;
+    static_assert(K >= 1 && K <= 12 && K < N, "prefix DP size");
+    __shared__ uint16_t lrank[NL];
+    __shared__ int smoff[L + 2];
+    __shared__ V drs[kSubBtWaves][N * N + N];  // per wave: d[m][k] (inner cities), then d[0][k]
+    for (int i = threadIdx.x; i < NL; i += 64 * kSubBtWaves) lrank[i] = info->rank[i];
+    if (threadIdx.x < (uint32_t)(L + 2)) smoff[threadIdx.x] = info->moff[threadIdx.x];
+    __syncthreads();
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    V *dr = drs[wave];
+    const V *d0 = dr + N * N;
+    auto wave_sync = [] {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    };
+    for (int blk = blk0 + (int)(blockIdx.x * kSubBtWaves + wave); blk < nblocks;
+         blk += (int)(gridDim.x * kSubBtWaves)) {
+        const V *dsrc = dist + (size_t)blk * n * n;
+        for (int i = lane; i < N * N; i += 64) dr[i] = dsrc[(i / N + 1) * n + (i % N + 1)];
+        if (lane < (uint32_t)N) dr[N * N + lane] = dsrc[lane + 1];
+        wave_sync();
+        int32_t *tour = tour_out + (size_t)blk * (n + 1);
+        const int bestM = tour[n - 1];
+        if (bestM < 1) continue;  // no tour (cost already -1)
+        char *slot = const_cast<char *>(slots) + (size_t)(blk - blk0) * slot_bytes;
+        Rsrc<uint64_t> par;
+        par.rs = uniform_rsrc(slot + tiled_push_bytes(N, L, VB), (uint32_t)tiled_parent_bytes(N, L));
+        Rsrc<V> rec;
+        rec.rs = uniform_rsrc(slot + tiled_push_bytes(N, L, VB) + tiled_parent_bytes(N, L),
+                              (uint32_t)sub_rec_bytes(N, VB));
+        uint32_t S = (1u << N) - 1u;
+        int k = bestM - 1;
+        bool ok = bestM >= 1 && bestM <= N;
+        int pos = n - 2;
+        // (1) parent words
+        for (; ok && pos >= 1 && __builtin_popcount(S) - 1 >= N - TSPGPU_TILED_TA_OFF; --pos) {
+            const uint32_t T = S & ~(1u << k);
+            const uint32_t hT = T >> L, lT = T & (uint32_t)(NL - 1);
+            const uint32_t idx = (uint32_t)smoff[__builtin_popcount(lT)] + lrank[lT];
+            const uint64_t w = par.load(idx * 8u, hT * (uint32_t)(NL * 8));
+            const int q = k - __builtin_popcount(T & ((1u << k) - 1u));  // k's place among T's non-members
+            const int pm = (int)((w >> (4 * q)) & 15u);
+            ok = pm < N && ((T >> pm) & 1u);
+            if (lane == 0) tour[pos] = ok ? pm + 1 : 0;
+            S = T;
+            k = pm;
+        }
+        if (ok && pos >= 1) {
+            // (2) the prefix set's own DP, local city i = the i-th member of T0 ascending
+            const uint32_t T0 = S & ~(1u << k);
+            ok = __builtin_popcount(T0) == K;
+            int city[K];
+            {
+                uint32_t b = T0;
+#pragma unroll
+                for (int i = 0; i < K; ++i) {
+                    city[i] = b ? __builtin_ctz(b) : 0;
+                    b &= b - 1u;
+                }
+            }
+            // layer 1: G[{i}][i] = d[0][city i] (tsp.cpp:435)
+            if (ok && lane < (uint32_t)K) rec.store(((1u << lane) * K + lane) * VB, 0, d0[city[lane]]);
+            for (int j = 2; ok && j <= K; ++j) {
+                wave_sync();
+                for (uint32_t M = lane; M < (uint32_t)NK; M += 64) {
+                    if (__builtin_popcount(M) != j) continue;
+#pragma unroll
+                    for (int kk = 0; kk < K; ++kk) {
+                        if (!((M >> kk) & 1u)) continue;
+                        const uint32_t P = M & ~(1u << kk);
+                        V acc = ValT<V>::inf;
+#pragma unroll
+                        for (int m = 0; m < K; ++m)
+                            if ((P >> m) & 1u)
+                                acc = ValT<V>::vmin(acc, rec.load((P * K + m) * VB, 0) + dr[city[m] * N + city[kk]]);
+                        rec.store((M * K + kk) * VB, 0, acc);
+                    }
+                }
+            }
+            wave_sync();
+            // the walk below T0: first strict minimum over the members ascending
+            uint32_t Mloc = (uint32_t)NK - 1u;
+            for (; ok && pos >= 1; --pos) {
+                const bool mem = lane < (uint32_t)K && ((Mloc >> lane) & 1u);
+                V cand = ValT<V>::invalid;
+                if (mem) cand = rec.load((Mloc * K + lane) * VB, 0) + dr[city[lane < (uint32_t)K ? lane : 0] * N + k];
+                const V best = wave_min(cand);
+                const unsigned long long hit = __ballot(mem && cand == best);
+                const int li = hit ? __ffsll(hit) - 1 : K;
+                ok = li < K;
+                const int pm = ok ? city[li < K ? li : 0] : N;
+                if (lane == 0) tour[pos] = ok ? pm + 1 : 0;
+                if (ok) Mloc &= ~(1u << li);
+                k = pm;
+            }
+        }
+        if (!ok && lane == 0) cost_out[blk] = V(-1);
+        wave_sync();  // dr is reloaded for the next block
+    }
+}
+}  // namespace
 
 struct SubArgs {
     const void *dist;
@@ -932,9 +1155,14 @@ hipError_t launch_sub_n(const SubArgs &a)
     hipError_t e = hipGetLastError();
     if (e == hipSuccess && a.ev_mid) e = hipEventRecord(a.ev_mid, a.stream);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL((hk_tiled_backtrack<V, N, L>), dim3(a.bt_grid), dim3(64 * kTiledBtWaves), 0, a.stream, a.blk1,
-                       a.blk0, a.slots, a.slot_bytes, a.info, static_cast<const V *>(a.dist), static_cast<V *>(a.cost),
-                       a.tour);
+    if constexpr (TSPGPU_SUB_RECYCLE)
+        hipLaunchKernelGGL((hk_sub_backtrack<V, N, L>), dim3(a.bt_grid), dim3(64 * kSubBtWaves), 0, a.stream, a.blk1,
+                           a.blk0, a.slots, a.slot_bytes, a.info, static_cast<const V *>(a.dist),
+                           static_cast<V *>(a.cost), a.tour);
+    else
+        hipLaunchKernelGGL((hk_tiled_backtrack<V, N, L>), dim3(a.bt_grid), dim3(64 * kTiledBtWaves), 0, a.stream,
+                           a.blk1, a.blk0, a.slots, a.slot_bytes, a.info, static_cast<const V *>(a.dist),
+                           static_cast<V *>(a.cost), a.tour);
     return hipGetLastError();
 }
 

@@ -291,9 +291,10 @@ int solve_sub(tspgpu_ctx *c, const SubCfg *cfg, const void *d_dist, int n, int n
     if (rc) return rc;
     // (TSPGPU_WG_PER_CU: measurement builds with another occupancy, hk_sub.h)
     const int grid = std::min(nblocks, c->cu_count * (c->wg_per_cu > 0 ? c->wg_per_cu : cfg->wg));
-    // the same per-block slot as variant 5 (push area, parent words,
-    // recompute area), kept until the backtracking kernel has run
-    const size_t slot = tiled_slot_bytes(N, L, cfg->vbytes);
+    // variant 5's per-block slot (push area, parent words, recompute area,
+    // large enough for either backtracking kernel), kept until the
+    // backtracking kernel has run
+    const size_t slot = sub_slot_bytes(N, L, cfg->vbytes);
     int chunk = 0;
     if ((rc = ensure_slots(c, nblocks, slot, &chunk))) return rc;
     for (int b0 = 0; b0 < nblocks; b0 += chunk) {
