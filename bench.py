@@ -573,7 +573,7 @@ def k2_group(world, local_rank):
     return dist.new_group(backend="gloo"), "gloo"
 
 
-def k2_single_instance(ctx, n, group, backend, world, reps=3):
+def k2_single_instance(ctx, n, group, backend, world, reps=5):
     """K2 on the reference's own instance `./tsp n 1 1000 1000` (config 3's
     16 cities): time to the optimal tour and B&B nodes (sharded over the ranks
     with RCCL between rounds when N > 1)."""
@@ -584,6 +584,10 @@ def k2_single_instance(ctx, n, group, backend, world, reps=3):
     def best_of(fn):
         best = None
         for _ in range(reps):
+            if group is not None:  # (the ranks start each search together)
+                import torch.distributed as dist
+
+                dist.barrier(group=group)
             t = time.perf_counter()
             cost, tour, st = fn()
             wall = (time.perf_counter() - t) * 1e3

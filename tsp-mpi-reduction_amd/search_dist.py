@@ -54,22 +54,26 @@ def solve_sharded(ctx, dist, group=None, depth: int = 0, device=None, exchange_e
     """Search one instance over the ranks of `group` (None: the default group,
     or a single process when torch.distributed is not initialised).
 
-    1. The multi-start bound: each rank runs 1/W of the starts, all-reduce MIN.
+    1. The multi-start bound: from 20 cities each rank runs 1/W of the starts
+       and the ranks all-reduce MIN; below, every rank computes the same
+       four-start bound itself.
     2. Each rank runs its shard as ONE device chain (tspgpu_search_chain: the
        seeds, every frontier level and the tail fold back to back, one
-       synchronisation).  A shard too large to chain runs step by step
-       instead, `exchange_every` steps between exchanges (default 4).
-    3. Exchanges: ONE all-reduce(MIN) of the pair (incumbent word, -busy) —
-       the same count on every rank, so the collectives pair up; after the
-       last one (nobody busy) the MIN is the optimum.
-    4. The winner: each rank reads its device tie slot at the
-       optimum (the reverse-lex least optimal tour it found), all-reduce MIN
-       of w0 (ranks without one send the maximum), then of w1 among the
-       holders of that w0 (two-word keys, n > 21), and every rank certifies
-       the winning key once (tspgpu_tie_tour): tsp()'s tour with no record
-       leaving any rank.  Only when a tie table overflowed or the certificate
-       fails do the ranks fall back to gathering their optimal records for the
-       host tie rule (a second search first if records were lost).
+       synchronisation that also reads back the counters and the shard's tie
+       slot at its incumbent).
+    3. The winner (MIN of the cost, then MIN of the
+       reverse-lex key among the holders of that cost): when every shard
+       finished its chain, ONE all-gather of 7-word records (incumbent,
+       chained, tie slot w0/w1/found/overflow, nodes) and the same
+       lexicographic MIN on every rank; otherwise the stepwise search with one
+       all-reduce MIN of (incumbent, -busy) every `exchange_every` steps
+       (default 4; the same count on every rank, so the collectives pair up)
+       followed by all-reduce MIN of w0 (ranks without one send the maximum)
+       and of w1 among its holders.  Every rank certifies the winning key once
+       (tspgpu_tie_tour_gpu): tsp()'s tour with no record leaving any rank.
+       Only when a tie table overflowed or the certificate fails do the ranks
+       gather their optimal records for the host tie rule (a second search
+       first if records were lost).
 
     Returns (cost, tour (n+1,), stats dict); identical on every rank."""
     import torch
@@ -97,13 +101,25 @@ def solve_sharded(ctx, dist, group=None, depth: int = 0, device=None, exchange_e
 
     exchange_every = max(1, int(exchange_every or 4))
 
-    # the multi-start tour (host, split over the ranks: start cities r, r+W,
-    # ...) on a thread while the search is created (ctypes releases the GIL)
+    def allgather(vals):
+        """Every rank's record (a list of int64) -> [record of rank 0, ...]."""
+        t = torch.tensor(vals, dtype=torch.int64, device=device)
+        if not collective:
+            return [[int(x) for x in t.tolist()]]
+        parts = [torch.empty_like(t) for _ in range(world)]
+        tdist.all_gather(parts, t, group=group)
+        ncoll[0] += 1
+        return [[int(x) for x in p.tolist()] for p in parts]
+
+    # the multi-start tour.  From 20 cities it is split over the ranks (start
+    # cities r, r+W, ...; all-reduce MIN of the costs) and computed on a thread
+    # while the search is created (ctypes releases the GIL); below, every rank
+    # computes the same four-start bound itself (microseconds; no collective)
+    split = collective and world > 1 and len(dist) >= 20
     heur = {}
 
     def _heuristic():
-        heur["v"] = tspgpu.heuristic_tour(dist, first=rank, step=world) if world > 1 else \
-            tspgpu.heuristic_tour(dist)
+        heur["v"] = tspgpu.heuristic_tour(dist, first=rank, step=world) if split else tspgpu.heuristic_tour(dist)
 
     th = threading.Thread(target=_heuristic) if len(dist) >= 20 else None  # (smaller: not worth a thread)
     if th is not None:
@@ -116,8 +132,7 @@ def solve_sharded(ctx, dist, group=None, depth: int = 0, device=None, exchange_e
     if "v" not in heur:
         _heuristic()  # (no thread, or it raised: here, so an error surfaces)
     try:
-        if collective:
-            # then the MIN of the ranks' costs: all starts' bound at 1/W of the host time
+        if split:
             ub_r, _ = heur["v"]
             word = tspgpu.cost_bits(ub_r, S.dtype) if ub_r is not None else _I64_MAX
             ub = tspgpu.bits_cost(allmin([word])[0], S.dtype)
@@ -125,43 +140,59 @@ def solve_sharded(ctx, dist, group=None, depth: int = 0, device=None, exchange_e
             ub, _ = heur["v"]
         S.set_bound(ub)
         t0 = time.perf_counter()
+        two = S.n - 1 > 20
         exchanges = 0
         chained = S.chain()
-        busy = 0
-        if not chained:
-            S.start()
-            busy = 1
-        while True:
-            # up to exchange_every steps on this rank (while it has work), then
-            # the exchange: incumbent MIN and "anyone still busy" (MIN of the
-            # negated flag) in one all-reduce
-            for _ in range(exchange_every):
-                if not busy:
+        inc, nodes, recs = S.counters()  # (a finished chain: from its own readback)
+        # Fast path, every rank one finished chain: ONE collective.  Each rank
+        # contributes (incumbent, chained, its tie slot at that incumbent,
+        # nodes); the optimum is the MIN of the incumbents, the winner the
+        # (w0, w1)-MIN over the ranks that hold a tour of that cost — the
+        # all-reduce MIN of the cost and then of the key in
+        # one all-gather of 7-word records, the same MIN computed on every rank.
+        f, w0, w1, ovf = S.tie_slot(inc) if chained else (False, 0, 0, False)
+        rec = allgather([inc, int(chained), int(f), _key_i64(w0) if f else _I64_MAX,
+                         _key_i64(w1) if f and two else _I64_MAX, int(ovf), int(nodes)])
+        exchanges = 1
+        fast = all(r[1] for r in rec)
+        if fast:
+            opt = min(r[0] for r in rec)
+            total_nodes = sum(r[6] for r in rec)
+            at_opt = [r for r in rec if r[0] == opt]  # (only a rank at the optimum can hold an optimal tour)
+            holders = [r for r in at_opt if r[2]]
+            nov = -1 if any(r[5] for r in at_opt) else 0
+            K0, K1 = min((r[3], r[4]) for r in holders) if holders else (_I64_MAX, _I64_MAX)
+        else:
+            # some shard was too large to chain: step by step, one all-reduce
+            # MIN of (incumbent, -busy) every exchange_every steps, the same
+            # count on every rank (ranks whose chain finished only join)
+            busy, exchanges = 0, 0
+            if not chained:
+                S.start()
+                busy = 1
+            while True:
+                for _ in range(exchange_every):
+                    if not busy:
+                        break
+                    busy = 1 if S.step() else 0
+                inc, _, _ = S.counters()
+                best, anybusy = allmin([inc, -busy])
+                exchanges += 1
+                if best < inc:
+                    S.set_bound(tspgpu.bits_cost(best, S.dtype))
+                if anybusy == 0:
                     break
-                busy = 1 if S.step() else 0
-            inc, _, _ = S.counters()
-            best, anybusy = allmin([inc, -busy])
-            exchanges += 1
-            if best < inc:
-                S.set_bound(tspgpu.bits_cost(best, S.dtype))
-            if anybusy == 0:
-                break
-        opt = best  # (the last exchange: every rank finished, so the MIN is the optimum)
-        _, nodes, recs = S.counters()
-        node_t = None
-        if collective:  # (overlaps the tie exchange)
-            node_t = torch.tensor([int(nodes)], dtype=torch.int64, device=device)
-            node_w = tdist.all_reduce(node_t, op=tdist.ReduceOp.SUM, group=group, async_op=True)
+            opt = best  # (the last exchange: every rank finished, so the MIN is the optimum)
+            _, nodes, recs = S.counters()
+            total_nodes = None
+            # the device tie rule across ranks: MIN of w0, then of w1 among its holders
+            found, w0, w1, ovf = S.tie_slot(opt) if inc <= opt else (False, 0, 0, False)
+            k0 = _key_i64(w0) if found else _I64_MAX
+            K0, nov = allmin([k0, -int(ovf)])
+            K1 = 0
+            if two:
+                (K1,) = allmin([_key_i64(w1) if found and k0 == K0 else _I64_MAX])
         cost = tspgpu.bits_cost(opt, S.dtype)
-
-        # the device tie rule across ranks: MIN of w0, then of w1 among its holders
-        found, w0, w1, ovf = S.tie_slot(opt) if inc <= opt else (False, 0, 0, False)
-        two = S.n - 1 > 20
-        k0 = _key_i64(w0) if found else _I64_MAX
-        K0, nov = allmin([k0, -int(ovf)])
-        K1 = 0
-        if two:
-            (K1,) = allmin([_key_i64(w1) if found and k0 == K0 else _I64_MAX])
         tie, tour = 0, None
         if nov == 0 and K0 != _I64_MAX:
             w = (_key_u64(K0), _key_u64(K1) if two else 0, cost)
@@ -173,13 +204,16 @@ def solve_sharded(ctx, dist, group=None, depth: int = 0, device=None, exchange_e
             tour, phases, fallback, nodes, n_opt = _records_winner(S, ctx, dist, opt, recs, nodes, allmin,
                                                                   collective, group)
             gathered = 1
-        total_nodes = int(nodes)
-        if node_t is not None:
-            node_w.wait()
-            if phases == 1:
-                total_nodes = int(node_t.item())
-            # (phases 2: _records_winner summed phase 1 + 2 over the ranks; the
+        if total_nodes is None or phases == 2 or fallback:
+            # (stepwise path: one SUM; phases 2: _records_winner summed phase 1 + 2 over the ranks; the
             # K1-wide fallback reports this rank's nodes)
+            if phases == 1 and not fallback and collective:
+                node_t = torch.tensor([int(nodes)], dtype=torch.int64, device=device)
+                tdist.all_reduce(node_t, op=tdist.ReduceOp.SUM, group=group)
+                ncoll[0] += 1
+                total_nodes = int(node_t.item())
+            else:
+                total_nodes = int(nodes)
         wall = time.perf_counter() - t0
         kernel_ms, rounds = S.timing()
         stats = {"nodes": total_nodes, "rank_nodes": int(S.counters()[1]),
