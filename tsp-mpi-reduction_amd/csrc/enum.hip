@@ -443,17 +443,19 @@ __global__ __launch_bounds__(256) void tail_kernel(SearchArgs a)
     const int n = a.n;
     const V *gd = static_cast<const V *>(a.dist);
     const V *ga = static_cast<const V *>(a.amin);
-    for (int i = threadIdx.x; i < n * n; i += blockDim.x) dl[(i / n) * kTRow + i % n] = gd[i];
-    for (int i = threadIdx.x; i < n; i += blockDim.x) am[i] = ga[i];
     // a chained search whose level overflowed is abandoned: its tail slots may
-    // hold paths nobody wrote (stale or uninitialised memory), so none is read
+    // hold paths nobody wrote (stale or uninitialised memory), so none is read;
+    // and a block beyond the waiting tails leaves before staging its tables
     __shared__ uint32_t dead;
-    if (threadIdx.x == 0) dead = a.overflow ? __hip_atomic_load(a.overflow, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
-    __syncthreads();
-    if (dead) return;  // (block-uniform)
-
     const unsigned int claimed = __hip_atomic_load(a.tail_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const uint32_t count = claimed < a.tail_cap ? claimed : a.tail_cap;
+    if (threadIdx.x == 0) dead = a.overflow ? __hip_atomic_load(a.overflow, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+    __syncthreads();
+    if (dead || blockIdx.x * 256u >= count) return;  // (block-uniform: count is one load of one word)
+    for (int i = threadIdx.x; i < n * n; i += blockDim.x) dl[(i / n) * kTRow + i % n] = gd[i];
+    for (int i = threadIdx.x; i < n; i += blockDim.x) am[i] = ga[i];
+    __syncthreads();
+
     const uint32_t full = (uint32_t)((1ull << n) - 1ull) & ~1u;
     const int lane = __lane_id();
     uint32_t *q = wq[threadIdx.x >> 6];
@@ -855,6 +857,21 @@ __global__ __launch_bounds__(256) void expand_kernel(SearchArgs a)
     const int n = a.n;
     const V *gd = static_cast<const V *>(a.dist);
     const V *ga = static_cast<const V *>(a.amin);
+    // chained levels: once a level has overflowed, the later ones return at
+    // once — the input slots an overflowing block reserved were never written
+    // (they hold stale or uninitialised paths) and must not be read
+    __shared__ uint32_t dead;
+    if (threadIdx.x == 0) dead = a.overflow ? __hip_atomic_load(a.overflow, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+    // the next step counts its children into the other counter word (no host memset per step)
+    if (a.out_next && blockIdx.x == 0 && threadIdx.x == 0) *a.out_next = 0u;
+    uint32_t fin_count = a.fin_count;
+    if (a.fin_count_dev) {  // chained level: the previous level's child count, at most its buffer
+        const uint32_t c = __hip_atomic_load(a.fin_count_dev, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        fin_count = c < a.fout_cap ? c : a.fout_cap;
+    }
+    __syncthreads();
+    // (a block without a run of this level leaves before staging its tables)
+    if (dead || blockIdx.x * a.fin_per_block >= fin_count) return;  // (block-uniform)
     for (int i = threadIdx.x; i < n * n; i += blockDim.x) dl[(i / n) * kTRow + i % n] = gd[i];
     for (int i = threadIdx.x; i < n; i += blockDim.x) am[i] = ga[i];
     if (a.sym)
@@ -867,23 +884,10 @@ __global__ __launch_bounds__(256) void expand_kernel(SearchArgs a)
         for (int i = threadIdx.x; i < n; i += blockDim.x) dm[kSearchMaxN * kTRow + i] = a.mst[n * n + i];
         if (threadIdx.x == 0) dm[kSearchMaxN * kTRow + kSearchMaxN] = a.mst[n * n + n];
     }
-    // chained levels: once a level has overflowed, the later ones return at
-    // once — the input slots an overflowing block reserved were never written
-    // (they hold stale or uninitialised paths) and must not be read
-    __shared__ uint32_t dead;
-    if (threadIdx.x == 0) dead = a.overflow ? __hip_atomic_load(a.overflow, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
     __syncthreads();
-    if (dead) return;  // (block-uniform)
 
-    // the next step counts its children into the other counter word (no host memset per step)
-    if (a.out_next && blockIdx.x == 0 && threadIdx.x == 0) *a.out_next = 0u;
     const uint32_t full = (uint32_t)((1ull << n) - 1ull) & ~1u;
     const V thr = EThr<V>::of(ENum<V>::val(__hip_atomic_load(a.inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)));
-    uint32_t fin_count = a.fin_count;
-    if (a.fin_count_dev) {  // chained level: the previous level's child count, at most its buffer
-        const uint32_t c = __hip_atomic_load(a.fin_count_dev, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        fin_count = c < a.fout_cap ? c : a.fout_cap;
-    }
     const int lane = __lane_id(), wv = threadIdx.x >> 6;
     __shared__ uint32_t bskip;
     // every run of fin_per_block input paths (one per block, or a fixed grid looping)

@@ -265,6 +265,21 @@ hipError_t launch_tie_lookup(const SearchArgs &a, unsigned long long *out, const
 hipError_t launch_fetch(const SearchArgs &a, const unsigned long long *words, unsigned long long *out,
                         uint32_t spec_cap);
 constexpr int kFetchWords = 32;  // fetch_kernel's words before the records
+// search_create's device state in ONE launch (search.hip init_kernel): the
+// host tables copied from pinned host memory (read by the kernel directly),
+// the tie table filled with 0xFF, its trailing words and the statistics
+// lines zeroed — instead of a dozen memsets and copies of a few KB each
+struct SearchInit {
+    const uint32_t *src[6];
+    uint32_t *dst[6];
+    uint32_t words[6];  // 4-byte words per copy
+    int ncopy;
+    uint32_t *fill_ff;  // 0xFF words (the tie slots)
+    uint32_t n_ff;
+    uint32_t *zero[2];  // zero words (tie words, statistics)
+    uint32_t n_zero[2];
+};
+hipError_t launch_init(const SearchInit &init, hipStream_t stream);
 // suffix table (enum.hip): size a.hs_len of a.hsuf, one thread per set
 hipError_t launch_suffix(const SearchArgs &a, bool f64, uint32_t sets);
 // seeds (seed_grid blocks) and the suffix table in one launch (enum.hip)

@@ -1182,7 +1182,24 @@ __global__ __launch_bounds__(256) void fetch_kernel(SearchArgs a, const unsigned
     for (uint32_t i = (uint32_t)t; i < cnt * kW; i += 256) out[32 + i] = src[i];
 }
 
+__global__ __launch_bounds__(256) void init_kernel(SearchInit in)
+{
+    const uint32_t stride = gridDim.x * 256u;
+    const uint32_t t0 = blockIdx.x * 256u + threadIdx.x;
+    for (int c = 0; c < in.ncopy; ++c)
+        for (uint32_t i = t0; i < in.words[c]; i += stride) in.dst[c][i] = in.src[c][i];
+    for (uint32_t i = t0; i < in.n_ff; i += stride) in.fill_ff[i] = 0xFFFFFFFFu;
+    for (int z = 0; z < 2; ++z)
+        for (uint32_t i = t0; i < in.n_zero[z]; i += stride) in.zero[z][i] = 0u;
+}
+
 }  // namespace
+
+hipError_t launch_init(const SearchInit &init, hipStream_t stream)
+{
+    hipLaunchKernelGGL(init_kernel, dim3(64), dim3(256), 0, stream, init);
+    return hipGetLastError();
+}
 
 hipError_t launch_fetch(const SearchArgs &a, const unsigned long long *words, unsigned long long *out,
                         uint32_t spec_cap)

@@ -157,6 +157,9 @@ struct tspgpu_search {
     // the fetch buffer still reflects the device state (a finished chain and
     // nothing run or written since): counters, tie slot and records read from it
     bool fresh = false;
+    // straight from create's init launch: the counter words 0, 4 and 8..13 are
+    // zero, so the first start / chain skips its memsets of them
+    bool pristine = false;
 };
 
 namespace {
@@ -521,35 +524,12 @@ static int search_create(tspgpu_ctx *c, const void *dist, int dtype, int n, int 
     if (double v; tuned("SEARCH_TIE", &v)) s->tie_on = v != 0;
     constexpr size_t kTieBytes = sizeof(TieSlot) * kTieSlots;
     if (e == hipSuccess && !s->d_tie) e = hipMalloc((void **)&s->d_tie, kTieBytes + 8 * sizeof(unsigned long long));
-    if (e == hipSuccess) e = hipMemsetAsync(s->d_tie, 0xFF, kTieBytes, st);
-    if (e == hipSuccess)
-        e = hipMemsetAsync(reinterpret_cast<char *>(s->d_tie) + kTieBytes, 0, 8 * sizeof(unsigned long long), st);
-    if (e == hipSuccess) e = hipMemsetAsync(s->d_stats, 0, kStatBytes, st);
     const bool pinned = tuned_or("SEARCH_PAGEABLE", 0) == 0;
     if (e == hipSuccess && pinned && !s->h_cnt)
         e = hipHostMalloc((void **)&s->h_cnt, 16 * sizeof(unsigned long long), hipHostMallocDefault);
     if (e == hipSuccess && pinned && !s->h_stats)
         e = hipHostMalloc((void **)&s->h_stats, kStatBytes + 8 * sizeof(unsigned long long), hipHostMallocDefault);
     if (e == hipSuccess && pinned && !s->h_stage) e = hipHostMalloc((void **)&s->h_stage, kStageBytes, hipHostMallocDefault);
-    // the tables go through the pinned staging area, so the copies are
-    // asynchronous and create returns without a synchronisation (pageable:
-    // synchronised below)
-    size_t soff = 0;
-    auto put = [&](void *dst, const void *src, size_t bytes) {
-        const void *from = src;
-        if (s->h_stage && soff + bytes <= kStageSpec) {
-            std::memcpy(s->h_stage + soff, src, bytes);
-            from = s->h_stage + soff;
-            soff += (bytes + 15) & ~(size_t)15;
-        } else if (s->h_stage) {
-            soff = kStageSpec + 1;  // (does not fit: synchronise below)
-        }
-        return hipMemcpyAsync(dst, from, bytes, hipMemcpyHostToDevice, st);
-    };
-    if (e == hipSuccess) e = put(s->d_dist, dist, vb * n * n);
-    if (e == hipSuccess) e = put(s->d_amin, f64 ? (const void *)ad.data() : (const void *)ai.data(), vb * n);
-    if (e == hipSuccess && s->sym) e = put(s->d_bnd2, f64 ? (const void *)bd.data() : (const void *)bi.data(), vb * 2 * n);
-    if (e == hipSuccess && s->mst_on) e = put(s->d_mst, mt.data(), sizeof(double) * mt.size());
     unsigned long long w[kWords] = {};
     if (f64) {
         const double inf = INFINITY;
@@ -557,8 +537,54 @@ static int search_create(tspgpu_ctx *c, const void *dist, int dtype, int n, int 
     } else {
         w[1] = bound ? (unsigned long long)std::min<double>(*bound, (double)INT32_MAX) : (unsigned long long)INT32_MAX;
     }
-    if (e == hipSuccess) e = put(s->d_words, w, sizeof w);
-    if (e == hipSuccess && (!s->h_stage || soff > kStageSpec)) e = hipStreamSynchronize(st);
+    // the host tables and the counter words, with the sizes
+    struct Part {
+        void *dst;
+        const void *src;
+        size_t bytes;
+    };
+    Part parts[5];
+    int np = 0;
+    parts[np++] = {s->d_dist, dist, vb * n * n};
+    parts[np++] = {s->d_amin, f64 ? (const void *)ad.data() : (const void *)ai.data(), vb * n};
+    if (s->sym) parts[np++] = {s->d_bnd2, f64 ? (const void *)bd.data() : (const void *)bi.data(), vb * 2 * n};
+    if (s->mst_on) parts[np++] = {s->d_mst, mt.data(), sizeof(double) * mt.size()};
+    parts[np++] = {s->d_words, w, sizeof w};
+    size_t need = 0;
+    for (int i = 0; i < np; ++i) need += (parts[i].bytes + 15) & ~(size_t)15;
+    if (e == hipSuccess && s->h_stage && need <= kStageSpec) {
+        // ONE launch: the tables staged in pinned host memory, read by the
+        // kernel directly (no copy commands), the tie slots filled and the
+        // statistics zeroed beside them (a dozen memsets and copies took
+        // ~70 us of the 16-city search's timeline, profiles/r04)
+        SearchInit in{};
+        size_t soff = 0;
+        for (int i = 0; i < np; ++i) {
+            std::memcpy(s->h_stage + soff, parts[i].src, parts[i].bytes);
+            in.src[i] = reinterpret_cast<const uint32_t *>(s->h_stage + soff);
+            in.dst[i] = static_cast<uint32_t *>(parts[i].dst);
+            in.words[i] = (uint32_t)(parts[i].bytes / 4);
+            soff += (parts[i].bytes + 15) & ~(size_t)15;
+        }
+        in.ncopy = np;
+        in.fill_ff = reinterpret_cast<uint32_t *>(s->d_tie);
+        in.n_ff = (uint32_t)(kTieBytes / 4);
+        in.zero[0] = reinterpret_cast<uint32_t *>(reinterpret_cast<char *>(s->d_tie) + kTieBytes);
+        in.n_zero[0] = 16;
+        in.zero[1] = reinterpret_cast<uint32_t *>(s->d_stats);
+        in.n_zero[1] = (uint32_t)(kStatBytes / 4);
+        e = launch_init(in, st);
+        s->pristine = e == hipSuccess;  // (words 0, 4, 8..13 are zero: the first run skips its memsets)
+    } else if (e == hipSuccess) {
+        // pageable staging (knob SEARCH_PAGEABLE): memsets, copies and a synchronisation
+        e = hipMemsetAsync(s->d_tie, 0xFF, kTieBytes, st);
+        if (e == hipSuccess)
+            e = hipMemsetAsync(reinterpret_cast<char *>(s->d_tie) + kTieBytes, 0, 8 * sizeof(unsigned long long), st);
+        if (e == hipSuccess) e = hipMemsetAsync(s->d_stats, 0, kStatBytes, st);
+        for (int i = 0; i < np && e == hipSuccess; ++i)
+            e = hipMemcpyAsync(parts[i].dst, parts[i].src, parts[i].bytes, hipMemcpyHostToDevice, st);
+        if (e == hipSuccess) e = hipStreamSynchronize(st);
+    }
     if (e == hipSuccess && !s->e0) e = hipEventCreate(&s->e0);
     if (e == hipSuccess && !s->e1) e = hipEventCreate(&s->e1);
     if (e == hipSuccess && !s->e2) e = hipEventCreate(&s->e2);
@@ -749,8 +775,12 @@ static int launch_and_count(tspgpu_search *s, bool seed, int grid, SearchArgs &a
                             bool sync = true)
 {
     hipStream_t st = s->ctx->stream;
-    hipError_t e = hipMemsetAsync(s->d_words, 0, 8, st);  // queue
-    if (e == hipSuccess) e = hipMemsetAsync(s->d_words + 4, 0, 8, st);  // items out
+    hipError_t e = hipSuccess;
+    if (!s->pristine) {
+        e = hipMemsetAsync(s->d_words, 0, 8, st);  // queue
+        if (e == hipSuccess) e = hipMemsetAsync(s->d_words + 4, 0, 8, st);  // items out
+    }
+    s->pristine = false;
     if (e != hipSuccess) return herr(e);
     (void)hipEventRecord(s->e0, st);
     if (seed && suffix_sets)  // the frontier's seeds and its suffix table, side by side in one launch
@@ -824,7 +854,7 @@ static int search_start(tspgpu_search *s, bool sync)
     s->rounds = 0;
     s->tails = 0;
     if (s->frontier) {  // tails (word 8) and the odd steps' child counter (word 9)
-        hipError_t e = hipMemsetAsync(s->d_words + 8, 0, 16, s->ctx->stream);
+        hipError_t e = s->pristine ? hipSuccess : hipMemsetAsync(s->d_words + 8, 0, 16, s->ctx->stream);
         if (e != hipSuccess) return herr(e);
         s->expand_steps = 0;
     }
@@ -1089,7 +1119,7 @@ static int run_chain(tspgpu_search *s, bool *done, int every = 0, tspgpu_level_h
     const bool f64 = s->dtype == TSPGPU_F64;
     // words 10..13 zeroed before the seeds (10..12: level counters, 13:
     // overflow); word 14 keeps the incumbent the chain starts from
-    hipError_t e = hipMemsetAsync(s->d_words + 10, 0, 4 * sizeof(unsigned long long), st);
+    hipError_t e = s->pristine ? hipSuccess : hipMemsetAsync(s->d_words + 10, 0, 4 * sizeof(unsigned long long), st);
     if (e == hipSuccess)
         e = hipMemcpyAsync(s->d_words + 14, s->d_words + 1, sizeof(unsigned long long), hipMemcpyDeviceToDevice, st);
     if (e != hipSuccess) return herr(e);
