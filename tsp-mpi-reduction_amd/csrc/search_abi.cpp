@@ -63,8 +63,11 @@ struct tspgpu_search {
     std::vector<double> hd;    // host copy (f64 view) for the selection
     std::vector<int32_t> hi;
     void *d_dist = nullptr, *d_amin = nullptr;
-    // [0] queue (u32), [1] incumbent, [2] nodes, [3] record count (u32), [4] items out (u32),
-    // [5..7] utilisation counters, [8] tail items (u32)
+    // [0] queue (u32), [1] incumbent, [2] nodes, [3] record count (u32), [4] items out / seed
+    // count (u32), [5..7] utilisation counters, [8] tail items (u32), [9] odd frontier steps'
+    // child count (u32), [10..12] chained level counters (u32, in rotation), [13] chained
+    // overflow flag (u32), [14] the incumbent a chain started from (its rerun restores it),
+    // [15] unused
     unsigned long long *d_words = nullptr;
     unsigned long long *d_stats = nullptr;  // kStatLines x kStatStride: [0] nodes, [1..3] lane-step counters
     SearchRecord *d_rec = nullptr;
@@ -1031,10 +1034,13 @@ int tspgpu_search_step(tspgpu_search *s, uint64_t *pending)
 // buffers of kChainCap paths — then the tail fold, and ONE synchronisation.
 // No host round trip per level (the stepwise search pays ~30 us each: 0.2 of
 // the 16-city search's 0.45 ms, profiles/r03/k2_variants.log).  A level whose
-// children or tails would not fit sets an overflow word; the search is then
-// rerun step by step (records and tails reset; the incumbent, a real tour's
-// cost, is kept).  Breadth first instead of the stepwise LIFO: the same
-// bounds, the same optimal set, a different node count.
+// children or tails would not fit sets an overflow word (13); every later
+// chained kernel then returns at once (the slots an overflowing block
+// reserved were never written and are not read), and the search reruns step
+// by step from the chain's starting state: records, tails, tie slots and
+// statistics reset, the incumbent restored from word 14.  Breadth first
+// instead of the stepwise LIFO: the same bounds, the same optimal set, a
+// different node count.
 // search_solve's readbacks, enqueued behind the search: one kernel writes
 // the statistics, counter words, tie slot and first records straight into
 // the pinned h_stage + kStageSpec (fetch_kernel's layout)
