@@ -45,7 +45,7 @@ def test_file_fixtures(gpu_ctx, name):
         assert [cities[t][0] for t in tour] == inst["solution"]["ids"], (name, len(cities), st)
 
 
-@pytest.mark.parametrize("n", [3, 4, 5, 7, 9, 11, 13, 15, 16, 17, 18])
+@pytest.mark.parametrize("n", [3, 4, 5, 7, 9, 11, 13, 15, 16, 17, 18, 20])
 def test_f64_against_oracle(gpu_ctx, n):
     rng = np.random.default_rng(4000 + n)
     for k in range(6 if n <= 14 else 2):
@@ -60,7 +60,7 @@ def test_f64_against_oracle(gpu_ctx, n):
         assert tour.tolist() == ot, (n, k, st)
 
 
-@pytest.mark.parametrize("n", [4, 8, 12, 14, 16])
+@pytest.mark.parametrize("n", [4, 8, 12, 14, 16, 18])
 def test_i32_against_oracle(gpu_ctx, n):
     """Integer-matrix extension (configs 1 and 4): symmetric and asymmetric."""
     rng = np.random.default_rng(7000 + n)
