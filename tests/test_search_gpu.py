@@ -60,6 +60,33 @@ def test_f64_against_oracle(gpu_ctx, n):
         assert tour.tolist() == ot, (n, k, st)
 
 
+@pytest.mark.parametrize("n", [13, 16, 19])
+def test_device_bound_against_host_bound(gpu_ctx, n, knobs):
+    """search_solve below 20 cities takes its initial bound from the device
+    heuristic in the init launch (search.hip init_heuristic): same answers as
+    with the host heuristic's bound (knob SEARCH_DEVICE_BOUND=0) and as the
+    oracle, on f64 points, lattice ties and asymmetric integer matrices."""
+    rng = np.random.default_rng(9100 + n)
+    for k in range(3):
+        if k == 0:
+            xy = rng.uniform(0, 1000, size=(n, 2))
+            d = O.distance_matrix([(i, xy[i, 0], xy[i, 1]) for i in range(n)])
+        elif k == 1:
+            xy = rng.integers(0, 4, size=(n, 2)).astype(np.float64)
+            d = O.distance_matrix([(i, xy[i, 0], xy[i, 1]) for i in range(n)])
+        else:
+            d = rng.integers(1, 1000, size=(n, n)).astype(np.int32)
+            np.fill_diagonal(d, 0)
+        cost, tour, st = tspgpu.search_solve(gpu_ctx, d)
+        knobs.set("SEARCH_DEVICE_BOUND", 0)
+        hcost, htour, hst = tspgpu.search_solve(gpu_ctx, d)
+        knobs.clear("SEARCH_DEVICE_BOUND")
+        assert cost == hcost and tour.tolist() == htour.tolist(), (n, k)
+        if n <= 16:
+            oc, ot = O.solve_block(np.asarray(d, dtype=np.float64))
+            assert float(cost) == oc and tour.tolist() == ot, (n, k)
+
+
 @pytest.mark.parametrize("n", [4, 8, 12, 14, 16, 18])
 def test_i32_against_oracle(gpu_ctx, n):
     """Integer-matrix extension (configs 1 and 4): symmetric and asymmetric."""

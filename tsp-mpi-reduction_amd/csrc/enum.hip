@@ -666,6 +666,7 @@ __global__ __launch_bounds__(256) void suffix_kernel(SearchArgs a, uint32_t sets
 template <typename V, int TL>
 __global__ __launch_bounds__(256) void prologue_kernel(SearchArgs a, uint32_t sets, uint32_t seed_blocks)
 {
+    if (a.t_start && blockIdx.x == 0 && threadIdx.x == 0) *a.t_start = wall_clock64();
     if (blockIdx.x < seed_blocks)
         seed_body<V>(a, blockIdx.x, seed_blocks);
     else

@@ -142,6 +142,11 @@ struct SearchArgs {
     struct TieSlot *tie;
     uint32_t tie_mask;         // slots - 1 (power of two)
     unsigned int *tie_overflow;
+    // chained searches: the prologue's block 0 stores the device wall clock
+    // (wall_clock64) here at its start, the fetch kernel its own beside it, so
+    // the chain is timed without events (an event costs ~5 us of the GPU's
+    // timeline between two launches); null: not stored
+    unsigned long long *t_start;
     hipStream_t stream;
 };
 
@@ -270,14 +275,24 @@ constexpr int kFetchWords = 32;  // fetch_kernel's words before the records
 // the tie table filled with 0xFF, its trailing words and the statistics
 // lines zeroed — instead of a dozen memsets and copies of a few KB each
 struct SearchInit {
-    const uint32_t *src[6];
-    uint32_t *dst[6];
-    uint32_t words[6];  // 4-byte words per copy
+    const uint32_t *src[8];
+    uint32_t *dst[8];
+    uint32_t words[8];  // 4-byte words per copy
     int ncopy;
     uint32_t *fill_ff;  // 0xFF words (the tie slots)
     uint32_t n_ff;
     uint32_t *zero[2];  // zero words (tie words, statistics)
     uint32_t n_zero[2];
+    // the incumbent words (counter words 1 and 14; the copies above leave them
+    // out): block 0 stores inc_init there or, with heur_n > 0, the smaller of
+    // it and the device heuristic's tour cost (search.hip init_heuristic)
+    unsigned long long *inc_word[2];
+    unsigned long long inc_init;  // f64 bits or a non-negative int32 cost
+    const void *heur_dist;        // heur_n x heur_n, f64 or i32 (host staging, read by the kernel)
+    int heur_n;                   // 0: no device heuristic; else 4 <= heur_n <= 20
+    int heur_f64;
+    int heur_sym;                 // the matrix is symmetric (2-opt deltas are then exact)
+    int heur_starts;              // start cities, spread over 0..n-1 (at most 16)
 };
 hipError_t launch_init(const SearchInit &init, hipStream_t stream);
 // suffix table (enum.hip): size a.hs_len of a.hsuf, one thread per set

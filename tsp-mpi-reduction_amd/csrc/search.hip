@@ -32,6 +32,7 @@
 #include <hip/hip_runtime.h>
 
 #include "search.h"
+#include "wave.h"
 
 namespace tspgpu {
 namespace {
@@ -1140,11 +1141,13 @@ __global__ __launch_bounds__(64) void tie_lookup_kernel(SearchArgs a, unsigned l
 // search_solve's readbacks in ONE launch, written straight into pinned host
 // memory (no copy commands): out[0..3] the summed statistics lines, out[4..19]
 // the 16 counter words, out[20..24] the optimum's tie slot (as
-// tie_lookup_kernel), out[32..] the first min(records, spec_cap) records.
+// tie_lookup_kernel), out[25] the device wall clock at its start, out[32..]
+// the first min(records, spec_cap) records.
 __global__ __launch_bounds__(256) void fetch_kernel(SearchArgs a, const unsigned long long *words,
                                                     unsigned long long *out, uint32_t spec_cap)
 {
     const int t = (int)threadIdx.x;
+    if (t == 0) out[25] = wall_clock64();  // (the chain's end: see SearchArgs::t_start)
     __shared__ unsigned long long part[4][kStatLines];
     __shared__ unsigned long long tie[4];
     part[t & 3][t >> 2] = a.nodes[(t >> 2) * kStatStride + (t & 3)];  // 256 threads = 64 lines x 4
@@ -1182,22 +1185,169 @@ __global__ __launch_bounds__(256) void fetch_kernel(SearchArgs a, const unsigned
     for (uint32_t i = (uint32_t)t; i < cnt * kW; i += 256) out[32 + i] = src[i];
 }
 
-__global__ __launch_bounds__(256) void init_kernel(SearchInit in)
+// The search's upper bound computed on the device, in the init launch (block
+// 0, sixteen waves), instead of by the host before the search: the host
+// heuristic's construction (search_host.cpp: nearest neighbour from four
+// spread start cities, local search, the smaller exact left fold of either
+// direction) with one wave per start city.  Nearest neighbour (ties: the lowest city),
+// then best-improvement 2-opt over all position pairs at once (up to three
+// per lane): on symmetric matrices the four-edge delta is exact; otherwise the
+// chosen move's reversed edges are priced and a move that does not gain ends
+// the descent.  The distances are read from the host staging (pinned) into
+// LDS once.  Any tour's cost is a valid incumbent, so a tour that is not a
+// permutation (never expected) is dropped rather than published.
+__device__ __forceinline__ double wave_sum(double x)
 {
-    const uint32_t stride = gridDim.x * 256u;
-    const uint32_t t0 = blockIdx.x * 256u + threadIdx.x;
+    for (int off = 32; off >= 1; off >>= 1) x += __shfl_xor(x, off);
+    return x;
+}
+
+__device__ __forceinline__ void init_heuristic(const SearchInit &in)
+{
+    constexpr int kWaves = 16, kPairs = 3;  // 1024 threads (heur_starts of them work); heur_n <= 20: <= 171 pairs
+    __shared__ double hd[kSearchMaxN * kSearchMaxN];
+    __shared__ int ht[kWaves][kSearchMaxN];
+    __shared__ double hbest[kWaves];
+    const int n = in.heur_n;
+    for (int i = threadIdx.x; i < n * n; i += blockDim.x)
+        hd[i] = in.heur_f64 ? static_cast<const double *>(in.heur_dist)[i]
+                            : (double)static_cast<const int32_t *>(in.heur_dist)[i];
+    __syncthreads();
+    const int lane = __lane_id(), wv = (int)(threadIdx.x >> 6);
+    int *t = ht[wv];
+    // this lane's moves: reverse positions i..j, 1 <= i < j <= n-1 (pair lane + 64 r)
+    int mi[kPairs], mj[kPairs];
+#pragma unroll
+    for (int r = 0; r < kPairs; ++r) {
+        int rem = lane + 64 * r;
+        mi[r] = 0;
+        mj[r] = 0;
+        for (int i = 1; i <= n - 2; ++i) {
+            const int c = n - 1 - i;
+            if (rem < c) {
+                mi[r] = i;
+                mj[r] = i + 1 + rem;
+                break;
+            }
+            rem -= c;
+        }
+    }
+    double wbest = 1.0e300;
+    // start cities spread over the tour like the host's (search_host.cpp
+    // heuristic: 0, n/4, n/2, 3n/4 for four), one wave each on its own SIMD
+    const int ns = in.heur_starts < n ? in.heur_starts : n;
+    for (int w = wv; w < ns; w += kWaves) {  // (wave-uniform)
+        const int s0 = w * n / ns;
+        if (lane == 0) t[0] = s0;
+        uint32_t used = 1u << s0;
+        int cur = s0;
+        for (int k = 1; k < n; ++k) {
+            const bool cand = lane < n && !((used >> (lane & 31)) & 1u);
+            const double v = cand ? hd[cur * n + lane] : 1.0e300;
+            const double m = wave_min_dpp(v);
+            const int j = __builtin_ctzll(__ballot(cand && v == m));
+            if (lane == 0) t[k] = j;
+            used |= 1u << j;
+            cur = j;
+        }
+        double total = wave_sum(lane < n ? hd[t[lane] * n + t[lane + 1 < n ? lane + 1 : 0]] : 0.0);
+        for (int it = 0; it < 8 * n; ++it) {
+            double best = 0.0;
+            int bi = 0, bj = 0;
+#pragma unroll
+            for (int r = 0; r < kPairs; ++r) {
+                if (!mi[r]) continue;
+                const int i = mi[r], j = mj[r];
+                const int a = t[i - 1], b = t[i], c = t[j], e = t[j + 1 < n ? j + 1 : 0];
+                const double dlt = (hd[a * n + c] + hd[b * n + e]) - (hd[a * n + b] + hd[c * n + e]);
+                if (dlt < best) best = dlt, bi = i, bj = j;
+            }
+            const double m = wave_min_dpp(best);
+            const double tol = -1e-9 * (1.0 + total);
+            if (!(m < tol)) break;  // (wave-uniform)
+            const int wl = __builtin_ctzll(__ballot(bi > 0 && best == m));
+            const int i = __builtin_amdgcn_readlane(bi, wl), j = __builtin_amdgcn_readlane(bj, wl);
+            double gain = m;
+            if (!in.heur_sym) {  // the segment's own edges, reversed
+                const double x = lane >= i && lane < j ? hd[t[lane + 1] * n + t[lane]] - hd[t[lane] * n + t[lane + 1]] : 0.0;
+                gain += wave_sum(x);
+                if (!(gain < tol)) break;
+            }
+            const bool in_seg = lane >= i && lane <= j;
+            const int v = in_seg ? t[i + j - lane] : 0;
+            if (in_seg) t[lane] = v;
+            total += gain;
+        }
+        // the left fold from city 0: lane 0 forward, lane 1 backward
+        const int p0 = __builtin_ctzll(__ballot(lane < n && t[lane] == 0));
+        const int dir = lane == 1 ? n - 1 : 1;
+        double c = 0.0;
+        int prev = 0;
+        for (int q = 1; q < n; ++q) {
+            const int x = t[(p0 + q * dir) % n];
+            c = c + hd[prev * n + x];
+            prev = x;
+        }
+        c = c + hd[prev * n];
+        const uint32_t bit = lane < n ? 1u << (t[lane] & 31) : 0u;
+        uint32_t seen = bit;
+        for (int off = 32; off >= 1; off >>= 1) seen |= (uint32_t)__shfl_xor((int)seen, off);
+        const bool perm = seen == (uint32_t)((1ull << n) - 1ull);
+        const double c0 = __shfl(c, 0), c1 = __shfl(c, 1);
+        if (perm) wbest = fmin(wbest, fmin(c0, c1));
+    }
+    if (lane == 0) hbest[wv] = wbest;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double b = hbest[0];
+        for (int w = 1; w < kWaves; ++w) b = fmin(b, hbest[w]);
+        unsigned long long u = in.inc_init;
+        if (b < 1.0e300) {
+            const unsigned long long hb = in.heur_f64 ? (unsigned long long)__double_as_longlong(b)
+                                                      : (unsigned long long)(uint32_t)(int32_t)b;
+            u = hb < u ? hb : u;  // (non-negative costs: the encodings order like the values)
+        }
+        *in.inc_word[0] = u;
+        *in.inc_word[1] = u;
+    }
+}
+
+__global__ __launch_bounds__(1024) void init_kernel(SearchInit in)
+{
+    const uint32_t stride = gridDim.x * blockDim.x;
+    const uint32_t t0 = blockIdx.x * blockDim.x + threadIdx.x;
+    // every table's first word of this thread loaded before any store: the
+    // sources are pinned host memory, one PCIe round trip instead of one per
+    // table (the tables are far below one stride; the loops below are the rest)
+    uint32_t v[8];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) v[c] = c < in.ncopy && t0 < in.words[c] ? in.src[c][t0] : 0u;
+#pragma unroll
+    for (int c = 0; c < 8; ++c)
+        if (c < in.ncopy && t0 < in.words[c]) in.dst[c][t0] = v[c];
     for (int c = 0; c < in.ncopy; ++c)
-        for (uint32_t i = t0; i < in.words[c]; i += stride) in.dst[c][i] = in.src[c][i];
+        for (uint32_t i = t0 + stride; i < in.words[c]; i += stride) in.dst[c][i] = in.src[c][i];
     for (uint32_t i = t0; i < in.n_ff; i += stride) in.fill_ff[i] = 0xFFFFFFFFu;
     for (int z = 0; z < 2; ++z)
         for (uint32_t i = t0; i < in.n_zero[z]; i += stride) in.zero[z][i] = 0u;
+    if (blockIdx.x != 0) return;  // (block-uniform)
+    if (in.heur_n > 0) {
+        init_heuristic(in);
+    } else if (threadIdx.x == 0) {
+        *in.inc_word[0] = in.inc_init;
+        *in.inc_word[1] = in.inc_init;
+    }
 }
 
 }  // namespace
 
 hipError_t launch_init(const SearchInit &init, hipStream_t stream)
 {
-    hipLaunchKernelGGL(init_kernel, dim3(64), dim3(256), 0, stream, init);
+    if (init.ncopy < 0 || init.ncopy > 8 || init.heur_n < 0 || init.heur_n > 20 ||
+        (init.heur_n && (init.heur_n < 4 || init.heur_starts < 1 || init.heur_starts > 16)))
+        return hipErrorInvalidValue;
+    // 16 blocks of 1024 (block 0's sixteen waves: the heuristic's start cities)
+    hipLaunchKernelGGL(init_kernel, dim3(16), dim3(1024), 0, stream, init);
     return hipGetLastError();
 }
 

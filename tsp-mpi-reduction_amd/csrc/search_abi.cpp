@@ -25,6 +25,8 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <map>
+#include <mutex>
 #include <thread>
 #include <vector>
 
@@ -67,7 +69,7 @@ struct tspgpu_search {
     // count (u32), [5..7] utilisation counters, [8] tail items (u32), [9] odd frontier steps'
     // child count (u32), [10..12] chained level counters (u32, in rotation), [13] chained
     // overflow flag (u32), [14] the incumbent a chain started from (its rerun restores it),
-    // [15] unused
+    // [15] a chain's start: the device wall clock (SearchArgs::t_start)
     unsigned long long *d_words = nullptr;
     unsigned long long *d_stats = nullptr;  // kStatLines x kStatStride: [0] nodes, [1..3] lane-step counters
     SearchRecord *d_rec = nullptr;
@@ -163,6 +165,9 @@ struct tspgpu_search {
     // straight from create's init launch: the counter words 0, 4 and 8..13 are
     // zero, so the first start / chain skips its memsets of them
     bool pristine = false;
+    bool inc_shared = false;  // tspgpu_search_incumbent_device handed word 1 out
+    bool stamp = false;       // the next prologue stores the chain's start clock in word 15
+    int dev_heur = 0;  // create's init launch computed the initial bound on the device (its n)
 };
 
 namespace {
@@ -314,8 +319,10 @@ static void front_release(tspgpu_search *s);
 extern "C" {
 
 // (bound: the initial incumbent, written with the counter words; null: none)
+// (dev_bound: the init launch computes the bound on the device, search.hip
+// init_heuristic; s->dev_heur says whether it did)
 static int search_create(tspgpu_ctx *c, const void *dist, int dtype, int n, int shard, int nshards, int depth,
-                         const double *bound, tspgpu_search **out)
+                         const double *bound, tspgpu_search **out, bool dev_bound = false)
 {
     if (!c || !out) return -EINVAL;
     *out = nullptr;
@@ -540,6 +547,7 @@ static int search_create(tspgpu_ctx *c, const void *dist, int dtype, int n, int 
     } else {
         w[1] = bound ? (unsigned long long)std::min<double>(*bound, (double)INT32_MAX) : (unsigned long long)INT32_MAX;
     }
+    w[14] = w[1];  // the incumbent a chain starts from (run_chain copies it only after a run)
     // the host tables and the counter words, with the sizes
     struct Part {
         void *dst;
@@ -560,16 +568,41 @@ static int search_create(tspgpu_ctx *c, const void *dist, int dtype, int n, int 
         // kernel directly (no copy commands), the tie slots filled and the
         // statistics zeroed beside them (a dozen memsets and copies took
         // ~70 us of the 16-city search's timeline, profiles/r04)
+        // (the counter words without 1 and 14, the incumbent: block 0 stores those)
+        Part ip[8];
+        int ni = 0;
+        for (int i = 0; i + 1 < np; ++i) ip[ni++] = parts[i];
+        ip[ni++] = {s->d_words, w, 8};
+        ip[ni++] = {s->d_words + 2, w + 2, 12 * 8};
+        ip[ni++] = {s->d_words + 15, w + 15, 8};
         SearchInit in{};
         size_t soff = 0;
-        for (int i = 0; i < np; ++i) {
-            std::memcpy(s->h_stage + soff, parts[i].src, parts[i].bytes);
+        for (int i = 0; i < ni; ++i) {
+            std::memcpy(s->h_stage + soff, ip[i].src, ip[i].bytes);
             in.src[i] = reinterpret_cast<const uint32_t *>(s->h_stage + soff);
-            in.dst[i] = static_cast<uint32_t *>(parts[i].dst);
-            in.words[i] = (uint32_t)(parts[i].bytes / 4);
-            soff += (parts[i].bytes + 15) & ~(size_t)15;
+            in.dst[i] = static_cast<uint32_t *>(ip[i].dst);
+            in.words[i] = (uint32_t)(ip[i].bytes / 4);
+            soff += (ip[i].bytes + 15) & ~(size_t)15;
         }
-        in.ncopy = np;
+        in.ncopy = ni;
+        in.inc_word[0] = s->d_words + 1;
+        in.inc_word[1] = s->d_words + 14;
+        in.inc_init = w[1];
+        if (dev_bound && n >= 4 && n <= 20) {
+            bool msym = true;
+            for (int i = 0; i < n && msym; ++i)
+                for (int j = 0; j < i && msym; ++j)
+                    msym = f64 ? static_cast<const double *>(dist)[i * n + j] == static_cast<const double *>(dist)[j * n + i]
+                               : static_cast<const int32_t *>(dist)[i * n + j] == static_cast<const int32_t *>(dist)[j * n + i];
+            in.heur_dist = in.src[0];  // (the distances, staged first)
+            in.heur_n = n;
+            in.heur_f64 = f64 ? 1 : 0;
+            in.heur_sym = msym ? 1 : 0;
+            // four spread starts, as the host's (search_host.cpp heuristic): at
+            // 14/16/19 cities the same bound and nodes as 8 or 16 starts, and
+            // each wave has a SIMD to itself (profiles/r04/k2_device_bound.log)
+            in.heur_starts = 4;
+        }
         in.fill_ff = reinterpret_cast<uint32_t *>(s->d_tie);
         in.n_ff = (uint32_t)(kTieBytes / 4);
         in.zero[0] = reinterpret_cast<uint32_t *>(reinterpret_cast<char *>(s->d_tie) + kTieBytes);
@@ -578,6 +611,7 @@ static int search_create(tspgpu_ctx *c, const void *dist, int dtype, int n, int 
         in.n_zero[1] = (uint32_t)(kStatBytes / 4);
         e = launch_init(in, st);
         s->pristine = e == hipSuccess;  // (words 0, 4, 8..13 are zero: the first run skips its memsets)
+        s->dev_heur = e == hipSuccess ? in.heur_n : 0;
     } else if (e == hipSuccess) {
         // pageable staging (knob SEARCH_PAGEABLE): memsets, copies and a synchronisation
         e = hipMemsetAsync(s->d_tie, 0xFF, kTieBytes, st);
@@ -643,6 +677,8 @@ int tspgpu_search_set_bound(tspgpu_search *s, double bound)
     (void)hipSetDevice(s->ctx->device);
     // on the search's stream: ordered after create's (asynchronous) counter words
     hipError_t e = hipMemcpyAsync(s->d_words + 1, &w, 8, hipMemcpyHostToDevice, s->ctx->stream);
+    if (e == hipSuccess)  // word 14: a chain's starting incumbent (read by its overflow rerun)
+        e = hipMemcpyAsync(s->d_words + 14, &w, 8, hipMemcpyHostToDevice, s->ctx->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(s->ctx->stream);
     return herr(e);
 }
@@ -694,8 +730,24 @@ static SearchArgs args_of(tspgpu_search *s)
         a.tie_mask = kTieSlots - 1;
         a.tie_overflow = reinterpret_cast<unsigned int *>(tie_words(s) + 5);
     }
+    a.t_start = s->stamp ? s->d_words + 15 : nullptr;
     a.stream = s->ctx->stream;
     return a;
+}
+
+// the device wall clock's rate (wall_clock64 ticks per ms), per device
+static double wall_clock_khz(int device)
+{
+    static std::mutex mu;
+    static std::map<int, double> rate;
+    std::lock_guard<std::mutex> g(mu);
+    auto it = rate.find(device);
+    if (it != rate.end()) return it->second;
+    int khz = 0;
+    if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device) != hipSuccess || khz <= 0)
+        khz = 100000;  // (gfx9: 100 MHz)
+    rate[device] = (double)khz;
+    return (double)khz;
 }
 
 static int ensure_items(tspgpu_search *s, int which, size_t count)
@@ -785,12 +837,12 @@ static int launch_and_count(tspgpu_search *s, bool seed, int grid, SearchArgs &a
     }
     s->pristine = false;
     if (e != hipSuccess) return herr(e);
-    (void)hipEventRecord(s->e0, st);
+    if (sync) (void)hipEventRecord(s->e0, st);  // (a chain times itself: SearchArgs::t_start)
     if (seed && suffix_sets)  // the frontier's seeds and its suffix table, side by side in one launch
         e = launch_prologue(a, s->dtype == TSPGPU_F64, grid, suffix_sets);
     else
         e = seed ? launch_seed(a, s->dtype == TSPGPU_F64, grid) : launch_round(a, s->dtype == TSPGPU_F64, grid);
-    (void)hipEventRecord(s->e1, st);
+    if (sync) (void)hipEventRecord(s->e1, st);
     if (e != hipSuccess) return herr(e);
     if (!sync) return 0;
     unsigned long long out = 0;
@@ -1125,12 +1177,18 @@ static int run_chain(tspgpu_search *s, bool *done, int every = 0, tspgpu_level_h
     const bool f64 = s->dtype == TSPGPU_F64;
     // words 10..13 zeroed before the seeds (10..12: level counters, 13:
     // overflow); word 14 keeps the incumbent the chain starts from
+    // (pristine: create wrote them, word 14 = word 1; set_bound keeps that)
     hipError_t e = s->pristine ? hipSuccess : hipMemsetAsync(s->d_words + 10, 0, 4 * sizeof(unsigned long long), st);
-    if (e == hipSuccess)
+    if (e == hipSuccess && (!s->pristine || s->inc_shared))
         e = hipMemcpyAsync(s->d_words + 14, s->d_words + 1, sizeof(unsigned long long), hipMemcpyDeviceToDevice, st);
     if (e != hipSuccess) return herr(e);
-    (void)hipEventRecord(s->e2, st);
+    // timed by the device clock when the fetch carries it (prologue start to
+    // fetch start), else by events around the chain
+    const bool fetch = s->fetch && s->h_stage;
+    if (!fetch) (void)hipEventRecord(s->e2, st);
+    s->stamp = fetch;
     int rc = search_start(s, false);  // the seeds, enqueued: their count stays in word 4
+    s->stamp = false;
     if (rc) return rc;
     int ob[2];
     for (int k = 0; k < 2; ++k) {
@@ -1171,11 +1229,10 @@ static int run_chain(tspgpu_search *s, bool *done, int every = 0, tspgpu_level_h
         a.overflow = reinterpret_cast<unsigned int *>(s->d_words + 13);  // (an abandoned chain folds no tails)
         e = launch_tail(a, f64, s->ctx->cu_count * 8);
     }
-    (void)hipEventRecord(s->e1, st);
+    if (!fetch) (void)hipEventRecord(s->e1, st);
     unsigned long long local[8] = {};
     unsigned long long *h = s->h_cnt ? s->h_cnt : local;
     // (search_solve: its readbacks ride on this synchronisation, words 8..13 among them)
-    const bool fetch = s->fetch && s->h_stage;
     if (e == hipSuccess && fetch) {
         e = enqueue_fetch(s);
         h = fetch_buf(s) + 4 + 8;
@@ -1184,8 +1241,14 @@ static int run_chain(tspgpu_search *s, bool *done, int every = 0, tspgpu_level_h
     }
     if (e == hipSuccess) e = hipStreamSynchronize(st);
     if (e != hipSuccess) return herr(e);
-    float ms = 0.f;
-    if (hipEventElapsedTime(&ms, s->e2, s->e1) == hipSuccess) s->ms += ms;  // seeds through the tail fold
+    if (fetch) {  // seeds through the tail fold: device wall clock, prologue start to fetch start
+        const unsigned long long *f = fetch_buf(s);
+        const unsigned long long t0 = f[4 + 15], t1 = f[25];
+        if (t1 > t0) s->ms += (double)(t1 - t0) / wall_clock_khz(s->ctx->device);
+    } else {
+        float ms = 0.f;
+        if (hipEventElapsedTime(&ms, s->e2, s->e1) == hipSuccess) s->ms += ms;
+    }
     s->rounds += levels + 1;
     front_release(s);
     s->pending = 0;
@@ -1393,7 +1456,12 @@ int tspgpu_search_timing(const tspgpu_search *s, double *kernel_ms, int *rounds)
     return 0;
 }
 
-void *tspgpu_search_incumbent_device(tspgpu_search *s) { return s ? (void *)(s->d_words + 1) : nullptr; }
+void *tspgpu_search_incumbent_device(tspgpu_search *s)
+{
+    if (!s) return nullptr;
+    s->inc_shared = true;  // (the caller may write word 1: a chain then saves it itself)
+    return (void *)(s->d_words + 1);
+}
 
 int tspgpu_search_counters(tspgpu_search *s, uint64_t *incumbent_bits, uint64_t *nodes, uint64_t *records)
 {
@@ -1484,6 +1552,11 @@ static int search_solve(tspgpu_ctx *c, const void *dist, int dtype, int n, doubl
     int hrc = 0;
     std::thread ht;
     bool threaded = false;
+    // 13..19 cities: the bound computed on the device by the search's init
+    // launch (search.hip init_heuristic, one wave per start city) instead of
+    // by the host before the search (~35 us of the ~0.2 ms at 16 cities);
+    // knob SEARCH_DEVICE_BOUND=0: the host
+    const bool dev_bound = !noprune && n >= 13 && n < 20 && tuned_or("SEARCH_DEVICE_BOUND", 1) != 0;
     if (n >= 20) {  // (smaller: a thread costs more than it saves)
         try {
             ht = std::thread([&] { hrc = tspgpu_heuristic_tour(dist, dtype, n, &ub, nullptr); });
@@ -1492,11 +1565,16 @@ static int search_solve(tspgpu_ctx *c, const void *dist, int dtype, int n, doubl
         }
     }
     // (n < 20: the bound first, then written with the counter words at create)
-    if (!threaded) hrc = tspgpu_heuristic_tour(dist, dtype, n, &ub, nullptr);
-    int rc = search_create(c, dist, dtype, n, 0, 1, depth, threaded || hrc ? nullptr : &ub, &s);
+    if (!threaded && !dev_bound) hrc = tspgpu_heuristic_tour(dist, dtype, n, &ub, nullptr);
+    int rc = search_create(c, dist, dtype, n, 0, 1, depth, threaded || hrc || dev_bound ? nullptr : &ub, &s,
+                           dev_bound);
     if (threaded) ht.join();
     if (rc) return rc;
     s->noprune = noprune;
+    if (dev_bound && !s->dev_heur) {  // (pageable staging: no init launch, the host's bound)
+        hrc = tspgpu_heuristic_tour(dist, dtype, n, &ub, nullptr);
+        if (!hrc) hrc = tspgpu_search_set_bound(s, ub);
+    }
     // enumeration work is uniform and every lane reaches the register tails:
     // long budgets (fewer, fuller rounds) win (profiles/r01/k2_exhaustive_budget.log)
     if (noprune && !tuned("SEARCH_BUDGET", nullptr)) s->budget = 16384;
