@@ -303,11 +303,26 @@ __device__ __forceinline__ void fold_path(const V *dl, const uint32_t (&w)[8], i
         }
 }
 
+// byte l of a path's words (a select chain: no dynamically indexed registers)
+__device__ __forceinline__ int path_byte(const uint32_t (&w)[8], int l)
+{
+    uint32_t v = 0;
+#pragma unroll
+    for (int b = 0; b < 8; ++b) v = (l >> 2) == b ? w[b] : v;
+    return (int)((v >> (8 * (l & 3))) & 255u);
+}
+
 // One handed-over prefix (slot idx of a.ftail): refold, bound test, all
 // TL! completions; `act` false = a lane with nothing to do (wave-uniform code).
+// wide (wave-uniform; a wave with only a few prefixes, e.g. the two tails of
+// the reference's 16-city instance): no per-lane straight-line completion —
+// every first-city group of every live prefix goes to the group loop below,
+// where the whole wave folds each prefix's TL! orders (TL!/64 per lane): the
+// prefixes' latency instead of the per-lane 720-order chain (~15 us at one
+// live lane).  The same tours are offered: all those within the incumbent.
 template <typename V, int TL>
 __device__ __forceinline__ void tail_one(const SearchArgs &a, const V *dl, const V *am, uint32_t full, uint32_t idx,
-                                         bool act, unsigned long long &lanes, TieCache &tcache)
+                                         bool act, unsigned long long &lanes, TieCache &tcache, bool wide = false)
 {
     uint32_t w[8];
     load_path(a.ftail + idx, act, w);
@@ -334,6 +349,11 @@ __device__ __forceinline__ void tail_one(const SearchArgs &a, const V *dl, const
     const unsigned long long am_ = __ballot(act);
     if (am_ == 0) return;
     lanes += (unsigned long long)__popcll(am_);
+    constexpr int kGroup = TL == 6 ? 120 : 24;  // (TL-1)!
+    uint32_t gm = 0;  // groups of this lane within the incumbent
+    if (wide) {
+        gm = act ? (1u << TL) - 1u : 0u;
+    } else {
     V s[TL][TL], d0[TL], dk[TL];
 #pragma unroll
     for (int i = 0; i < TL; ++i) {
@@ -360,21 +380,26 @@ __device__ __forceinline__ void tail_one(const SearchArgs &a, const V *dl, const
     // lanes that have such groups are served one at a time by the whole wave,
     // each lane folding every 64th of the group's (TL-1)! orders.
     (void)best;
-    constexpr int kGroup = TL == 6 ? 120 : 24;  // (TL-1)!
-    uint32_t gm = 0;  // groups of this lane within the incumbent
 #pragma unroll
     for (int g = 0; g < TL; ++g) gm |= (act && bg[g] <= inc) ? (1u << g) : 0u;
+    }
     for (unsigned long long owners = __ballot(gm != 0); owners; owners &= owners - 1ull) {
         const int o = __ffsll((long long)owners) - 1;
         const uint32_t ogm = (uint32_t)__shfl((int)gm, o);
         const uint32_t otp = (uint32_t)__shfl((int)tpack, o);
         const int oprev = __shfl(prev, o), olen = __shfl(len, o);
-        const uint32_t oidx = (uint32_t)__shfl((int)idx, o);
+        uint32_t ow[8];  // the owner's path words (its record's and tie key's first cities)
+#pragma unroll
+        for (int b = 0; b < 8; ++b) ow[b] = (uint32_t)__shfl((int)w[b], o);
         V ocp;
         if constexpr (sizeof(V) == 8)
             ocp = __longlong_as_double(__shfl((long long)__double_as_longlong(cp), o));
         else
             ocp = (V)__shfl((int)cp, o);
+        // the incumbent read once per owner (a tour is still recorded iff its
+        // atomicMin finds it within the incumbent: a stale read only costs
+        // attempts), then lowered by every attempt's answer
+        V cur = ENum<V>::val(__hip_atomic_load(a.inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
         for (uint32_t gg = ogm; gg; gg &= gg - 1u) {
             const int g = __builtin_ctz(gg);
             for (int p = g * kGroup + __lane_id(); p < (g + 1) * kGroup; p += 64) {
@@ -403,28 +428,28 @@ __device__ __forceinline__ void tail_one(const SearchArgs &a, const V *dl, const
                     k = ord[l];
                 }
                 const V total = c + dl[k * kTRow];
-                const V cur = ENum<V>::val(__hip_atomic_load(a.inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
                 if (total <= cur) {
                     const uint64_t tb = ENum<V>::bits(total);
+                    // the record slot claimed beside the incumbent's atomicMin (one
+                    // round trip, not two); a tour the incumbent passed meanwhile
+                    // leaves a record above the optimum, which the host ignores
                     const unsigned long long old = atomicMin(a.inc, (unsigned long long)tb);
-                    if (tb <= old) {
-                        const unsigned int slot = atomicAdd(a.rec_count, 1u);
-                        if (slot < a.rec_cap) {
-                            SearchRecord *R = a.rec + slot;
-                            R->cost = tb;
-                            const uint8_t *pb = a.ftail[oidx].b;
-                            for (int l = 1; l < olen; ++l) R->city[l - 1] = pb[l];
+                    const unsigned int slot = atomicAdd(a.rec_count, 1u);
+                    cur = ENum<V>::vmin(ENum<V>::val(old), total);
+                    if (slot < a.rec_cap) {
+                        SearchRecord *R = a.rec + slot;
+                        R->cost = tb;
+                        for (int l = 1; l < olen; ++l) R->city[l - 1] = (uint8_t)path_byte(ow, l);
 #pragma unroll
-                            for (int l = 0; l < TL; ++l) R->city[olen - 1 + l] = (uint8_t)ord[l];
-                        }
-                        const uint8_t *pb = a.ftail[oidx].b;
+                        for (int l = 0; l < TL; ++l) R->city[olen - 1 + l] = (uint8_t)ord[l];
+                    }
+                    if (tb <= old)
                         tie_offer(a, tcache, tb, [&](int q) {
                             int v = 0;
 #pragma unroll
                             for (int l = 0; l < TL; ++l) v = q == olen + l ? ord[l] : v;
-                            return q < olen ? (int)pb[q] : v;
+                            return q < olen ? path_byte(ow, q) : v;
                         });
-                    }
                 }
             }
         }
@@ -433,7 +458,9 @@ __device__ __forceinline__ void tail_one(const SearchArgs &a, const V *dl, const
 
 // Every wave reads 64 slots at a time, queues the non-empty ones (len > 0) in
 // LDS and folds them 64 at a time, so a producer may leave holes without
-// idling lanes here.
+// idling lanes here.  A batch of at most kTailWide prefixes is folded wide
+// (tail_one: the wave over each prefix's orders).
+constexpr uint32_t kTailWide = 4;
 template <typename V, int TL>
 __global__ __launch_bounds__(256) void tail_kernel(SearchArgs a)
 {
@@ -481,7 +508,10 @@ __global__ __launch_bounds__(256) void tail_kernel(SearchArgs a)
             const uint32_t idx = act ? q[qn - take + lane] : 0u;
             __builtin_amdgcn_wave_barrier();
             qn -= take;
-            tail_one<V, TL>(a, dl, am, full, idx, act, lanes, tcache);
+            if (take <= kTailWide)
+                tail_one<V, TL>(a, dl, am, full, idx, act, lanes, tcache, true);
+            else
+                tail_one<V, TL>(a, dl, am, full, idx, act, lanes, tcache);
         }
         if (!more) break;
     }
@@ -624,7 +654,16 @@ __device__ __forceinline__ void suffix_body(const SearchArgs &a, uint32_t sets, 
     load_binom(bn);
     __syncthreads();
     double *H = const_cast<double *>(a.hsuf) + a.hs_off[TL];
-    for (uint32_t r0 = block * 256u + threadIdx.x; r0 < sets; r0 += nblocks * 256u) {
+    // one thread per (set, place x): wave w serves place I = w % TL of 64
+    // sets (I wave-uniform: one straight-line `complete` per wave), so the
+    // table's (TL-1)!-order chains spread over TL times the waves (the
+    // prologue's critical path: 14 us at 16 cities with a thread per set)
+    for (uint32_t g0 = block * 256u + (threadIdx.x & ~63u);; g0 += nblocks * 256u) {
+        const uint32_t wv = g0 >> 6;
+        const int I = (int)(wv % (uint32_t)TL);
+        const uint32_t r0 = (wv / (uint32_t)TL) * 64u + (uint32_t)__lane_id();
+        if ((wv / (uint32_t)TL) * 64u >= sets) break;  // (wave-uniform)
+        if (r0 >= sets) continue;
         // unrank U (colex): the largest place c with C(c, i) <= r, i = TL .. 1
         int c[TL];
         uint32_t r = r0;
@@ -646,10 +685,11 @@ __device__ __forceinline__ void suffix_body(const SearchArgs &a, uint32_t sets, 
         }
         static_for(
             [&](auto i) {
-                constexpr int I = decltype(i)::value;
+                constexpr int J = decltype(i)::value;
+                if (J != I) return;
                 double best = ENum<double>::big();
-                complete<double, TL, (((1 << TL) - 1) & ~(1 << I)), I>(sm, d0, 0.0, best);
-                H[(size_t)r0 * TL + I] = best;
+                complete<double, TL, (((1 << TL) - 1) & ~(1 << J)), J>(sm, d0, 0.0, best);
+                H[(size_t)r0 * TL + J] = best;
             },
             std::make_integer_sequence<int, TL>{});
     }
@@ -787,11 +827,16 @@ __device__ __forceinline__ double tree_bound(const double *dm, const double *pim
 template <typename V, int TL>
 __device__ __forceinline__ Expand<V> expand_eval(const SearchArgs &a, const V *dl, const V *am, const V *b2,
                                                  const uint32_t (*bn)[8], const double *dm, uint32_t full,
-                                                 uint32_t idx, uint32_t end, V thr)
+                                                 uint32_t idx, uint32_t end, V thr, const uint32_t *pre = nullptr)
 {
     Expand<V> e;
     const bool act = idx < end;
-    load_path(fin_at(a, idx), act, e.w);
+    if (pre) {  // (read before the count was known: only an active lane's words count)
+#pragma unroll
+        for (int b = 0; b < 8; ++b) e.w[b] = act ? pre[b] : 0u;
+    } else {
+        load_path(fin_at(a, idx), act, e.w);
+    }
     e.len = act ? (int)(e.w[0] & 255u) : 0;
     V c = 0;  // the reference's left fold of the path
     int k = 0;
@@ -862,6 +907,10 @@ __global__ __launch_bounds__(256) void expand_kernel(SearchArgs a)
     // once — the input slots an overflowing block reserved were never written
     // (they hold stale or uninitialised paths) and must not be read
     __shared__ uint32_t dead;
+    // every device read of the launch's set-up in flight together (the
+    // level's count, the overflow flag, the incumbent, the tables): one
+    // memory round trip and one barrier before the work, not three of each —
+    // a chained level is a latency chain of such round trips (~2 us each)
     if (threadIdx.x == 0) dead = a.overflow ? __hip_atomic_load(a.overflow, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
     // the next step counts its children into the other counter word (no host memset per step)
     if (a.out_next && blockIdx.x == 0 && threadIdx.x == 0) *a.out_next = 0u;
@@ -870,9 +919,15 @@ __global__ __launch_bounds__(256) void expand_kernel(SearchArgs a)
         const uint32_t c = __hip_atomic_load(a.fin_count_dev, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         fin_count = c < a.fout_cap ? c : a.fout_cap;
     }
-    __syncthreads();
-    // (a block without a run of this level leaves before staging its tables)
-    if (dead || blockIdx.x * a.fin_per_block >= fin_count) return;  // (block-uniform)
+    const V thr = EThr<V>::of(ENum<V>::val(__hip_atomic_load(a.inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)));
+    // chained: this block's first path read beside them, before its count is
+    // known (inside the input buffer; the words of lanes beyond the count are
+    // never used)
+    uint32_t pre[8];
+    const bool spec = a.fin_cap && a.nseg == 1 && blockIdx.x * a.fin_per_block + threadIdx.x < a.fin_cap;
+    load_path(a.fseg[0] + blockIdx.x * a.fin_per_block + threadIdx.x, spec, pre);
+    // (a block without a run of this level stages its tables all the same: it
+    // leaves at the barrier, and the tables are a few hundred bytes of L2)
     for (int i = threadIdx.x; i < n * n; i += blockDim.x) dl[(i / n) * kTRow + i % n] = gd[i];
     for (int i = threadIdx.x; i < n; i += blockDim.x) am[i] = ga[i];
     if (a.sym)
@@ -886,9 +941,9 @@ __global__ __launch_bounds__(256) void expand_kernel(SearchArgs a)
         if (threadIdx.x == 0) dm[kSearchMaxN * kTRow + kSearchMaxN] = a.mst[n * n + n];
     }
     __syncthreads();
+    if (dead || blockIdx.x * a.fin_per_block >= fin_count) return;  // (block-uniform)
 
     const uint32_t full = (uint32_t)((1ull << n) - 1ull) & ~1u;
-    const V thr = EThr<V>::of(ENum<V>::val(__hip_atomic_load(a.inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)));
     const int lane = __lane_id(), wv = threadIdx.x >> 6;
     __shared__ uint32_t bskip;
     // every run of fin_per_block input paths (one per block, or a fixed grid looping)
@@ -903,13 +958,19 @@ __global__ __launch_bounds__(256) void expand_kernel(SearchArgs a)
     uint32_t cT = 0, cF = 0;
     unsigned long long nodes = 0;
     uint32_t lv[kExpandTiles];
+    uint32_t w0[8];  // the first tile's path, kept for pass 2 (one fewer memory round trip)
 #pragma unroll
     for (int t = 0; t < kExpandTiles; ++t) {
         const uint32_t base = b0 + 256u * t;
         lv[t] = 0;
         if (base >= b1) continue;
-        const Expand<V> e = expand_eval<V, TL>(a, dl, am, b2, bn, dm, full, base + threadIdx.x, b1, thr);
+        const bool first = t == 0 && spec && runi == blockIdx.x;  // (the path read before the barrier)
+        const Expand<V> e = expand_eval<V, TL>(a, dl, am, b2, bn, dm, full, base + threadIdx.x, b1, thr,
+                                               first ? pre : nullptr);
         lv[t] = e.live;
+        if (t == 0)
+#pragma unroll
+            for (int b = 0; b < 8; ++b) w0[b] = e.w[b];
         const uint32_t cnt = (uint32_t)__builtin_popcount(e.live);
         if (e.len == a.tail_level) cT += cnt; else cF += cnt;  // children have len inner cities
         nodes += (unsigned long long)__builtin_popcount(e.rem) + e.hnodes;
@@ -949,7 +1010,12 @@ __global__ __launch_bounds__(256) void expand_kernel(SearchArgs a)
         if (base >= b1) break;  // block-uniform
         Expand<V> e;
         const bool act = base + threadIdx.x < b1;
-        load_path(fin_at(a, base + threadIdx.x), act, e.w);
+        if (t == 0) {
+#pragma unroll
+            for (int b = 0; b < 8; ++b) e.w[b] = w0[b];
+        } else {
+            load_path(fin_at(a, base + threadIdx.x), act, e.w);
+        }
         e.len = act ? (int)(e.w[0] & 255u) : 0;
         e.live = lv[t];
         const bool tail = e.len == a.tail_level;
@@ -1074,7 +1140,7 @@ hipError_t launch_seed(const SearchArgs &a, bool f64, int grid)
 hipError_t launch_prologue(const SearchArgs &a, bool f64, int seed_grid, uint32_t sets)
 {
     if (a.n > kSearchMaxN || !a.hsuf || (a.hs_len != 5 && a.hs_len != 6)) return hipErrorInvalidValue;
-    const int grid = seed_grid + (int)std::min<uint32_t>((sets + 255u) / 256u, 4096u);
+    const int grid = seed_grid + (int)std::min<uint32_t>((sets * (uint32_t)a.hs_len + 255u) / 256u, 4096u);
     const uint32_t sb = (uint32_t)seed_grid;
 #define TSPGPU_PRO(VT, TLV) hipLaunchKernelGGL((prologue_kernel<VT, TLV>), dim3(grid), dim3(256), 0, a.stream, a, sets, sb)
     if (a.hs_len == 5) {
@@ -1090,7 +1156,7 @@ hipError_t launch_suffix(const SearchArgs &a, bool f64, uint32_t sets)
 {
     if (a.n > kSearchMaxN || !a.hsuf || (a.hs_len != 5 && a.hs_len != 6)) return hipErrorInvalidValue;
     if (sets == 0) return hipSuccess;
-    const int grid = (int)std::min<uint32_t>((sets + 255u) / 256u, 4096u);
+    const int grid = (int)std::min<uint32_t>((sets * (uint32_t)a.hs_len + 255u) / 256u, 4096u);
     if (a.hs_len == 5) {
         if (f64)
             hipLaunchKernelGGL((suffix_kernel<double, 5>), dim3(grid), dim3(256), 0, a.stream, a, sets);

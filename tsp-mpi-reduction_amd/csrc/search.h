@@ -112,6 +112,7 @@ struct SearchArgs {
     // and outputs checked against fout_cap / tail_cap (*overflow = 1, the
     // block's children dropped) instead of sized on the host
     const unsigned int *fin_count_dev;
+    unsigned int fin_cap;      // chained: paths the input buffer holds (its first tile is read before the count; 0: not)
     unsigned int fout_cap;
     unsigned int *overflow;
     int max_grid;
@@ -230,10 +231,15 @@ __device__ __forceinline__ void tie_offer(const SearchArgs &a, TieCache &tc, uns
         atomicOr(a.tie_overflow, 1u);
         return;
     }
-    const unsigned long long o0 = atomicMin(&e->w0, w0);
     tc.cost = tb;
+    if (!two) {  // (the old key is not waited for: the cache keeps our own, an upper bound of the slot's)
+        atomicMin(&e->w0, w0);
+        tc.w0 = w0;
+        return;
+    }
+    const unsigned long long o0 = atomicMin(&e->w0, w0);
     tc.w0 = o0 < w0 ? o0 : w0;
-    if (!two || w0 > o0) return;
+    if (w0 > o0) return;
     // second word: the sub-slot of this w0 (lock-free: CAS claim, atomicMin)
     for (int i = 0; i < kTieSub; ++i) {
         const unsigned long long old = atomicCAS(&e->sub[i][0], kTieEmpty, w0);

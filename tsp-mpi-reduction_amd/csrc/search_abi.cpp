@@ -1213,6 +1213,8 @@ static int run_chain(tspgpu_search *s, bool *done, int every = 0, tspgpu_level_h
         a.fin = a.fseg[0];
         a.fin_count = l == 0 ? (uint32_t)s->local_items : (uint32_t)kChainCap;  // (the grid's bound)
         a.fin_count_dev = reinterpret_cast<const unsigned int *>(s->d_words + (l == 0 ? 4 : 10 + l % 3));
+        a.fin_cap = (uint32_t)std::min<size_t>(l == 0 ? s->fb_cap[s->seg_buf[0]] : s->fb_cap[ob[(l - 1) & 1]],
+                                               UINT32_MAX);
         a.out_count = reinterpret_cast<unsigned int *>(s->d_words + 10 + (l + 1) % 3);
         a.out_next = reinterpret_cast<unsigned int *>(s->d_words + 10 + (l + 2) % 3);
         a.fout = s->fb[ob[l & 1]];
