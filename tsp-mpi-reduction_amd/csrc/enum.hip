@@ -312,20 +312,18 @@ __device__ __forceinline__ int path_byte(const uint32_t (&w)[8], int l)
     return (int)((v >> (8 * (l & 3))) & 255u);
 }
 
-// One handed-over prefix (slot idx of a.ftail): refold, bound test, all
+// One handed-over prefix (its words, queued by tail_kernel): refold, bound test, all
 // TL! completions; `act` false = a lane with nothing to do (wave-uniform code).
-// wide (wave-uniform; a wave with only a few prefixes, e.g. the two tails of
-// the reference's 16-city instance): no per-lane straight-line completion —
-// every first-city group of every live prefix goes to the group loop below,
-// where the whole wave folds each prefix's TL! orders (TL!/64 per lane): the
-// prefixes' latency instead of the per-lane 720-order chain (~15 us at one
-// live lane).  The same tours are offered: all those within the incumbent.
+// (A wave with only a few prefixes takes tail_wide below instead.)
 template <typename V, int TL>
-__device__ __forceinline__ void tail_one(const SearchArgs &a, const V *dl, const V *am, uint32_t full, uint32_t idx,
-                                         bool act, unsigned long long &lanes, TieCache &tcache, bool wide = false)
+__device__ __forceinline__ void tail_one(const SearchArgs &a, const V *dl, const V *am, uint32_t full,
+                                         const uint32_t (&win)[8], bool act, unsigned long long &lanes,
+                                         TieCache &tcache)
 {
+    V inc = ENum<V>::val(__hip_atomic_load(a.inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
     uint32_t w[8];
-    load_path(a.ftail + idx, act, w);
+#pragma unroll
+    for (int b = 0; b < 8; ++b) w[b] = act ? win[b] : 0u;
     const int len = act ? (int)(w[0] & 255u) : 1;
     // ---- the prefix 0, t1..t(len-1): the reference's left fold
     V cp = 0;
@@ -344,16 +342,10 @@ __device__ __forceinline__ void tail_one(const SearchArgs &a, const V *dl, const
         ra += am[t[i]];
         tpack |= (uint32_t)t[i] << (5 * i);
     }
-    V inc = ENum<V>::val(__hip_atomic_load(a.inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
     if (!a.noprune && cp + ra > EThr<V>::of(inc)) act = false;
     const unsigned long long am_ = __ballot(act);
     if (am_ == 0) return;
     lanes += (unsigned long long)__popcll(am_);
-    constexpr int kGroup = TL == 6 ? 120 : 24;  // (TL-1)!
-    uint32_t gm = 0;  // groups of this lane within the incumbent
-    if (wide) {
-        gm = act ? (1u << TL) - 1u : 0u;
-    } else {
     V s[TL][TL], d0[TL], dk[TL];
 #pragma unroll
     for (int i = 0; i < TL; ++i) {
@@ -380,9 +372,10 @@ __device__ __forceinline__ void tail_one(const SearchArgs &a, const V *dl, const
     // lanes that have such groups are served one at a time by the whole wave,
     // each lane folding every 64th of the group's (TL-1)! orders.
     (void)best;
+    constexpr int kGroup = TL == 6 ? 120 : 24;  // (TL-1)!
+    uint32_t gm = 0;  // groups of this lane within the incumbent
 #pragma unroll
     for (int g = 0; g < TL; ++g) gm |= (act && bg[g] <= inc) ? (1u << g) : 0u;
-    }
     for (unsigned long long owners = __ballot(gm != 0); owners; owners &= owners - 1ull) {
         const int o = __ffsll((long long)owners) - 1;
         const uint32_t ogm = (uint32_t)__shfl((int)gm, o);
@@ -456,17 +449,177 @@ __device__ __forceinline__ void tail_one(const SearchArgs &a, const V *dl, const
     }
 }
 
+// permutation idx (0..23, lexicographic) of {0,1,2,3}: element at position pos
+__host__ __device__ constexpr int perm4(int idx, int pos)
+{
+    int avail[4] = {0, 1, 2, 3};
+    const int f[4] = {6, 2, 1, 1};
+    int n = 4, res = 0;
+    for (int p = 0; p <= pos; ++p) {
+        const int d = idx / f[p];
+        idx %= f[p];
+        res = avail[d];
+        for (int k = d; k < n - 1; ++k) avail[k] = avail[k + 1];
+        --n;
+    }
+    return res;
+}
+struct Perm4Table {
+    uint8_t p[24];  // 2 bits per position
+};
+constexpr Perm4Table make_perm4()
+{
+    Perm4Table t{};
+    for (int i = 0; i < 24; ++i)
+        t.p[i] = (uint8_t)(perm4(i, 0) | perm4(i, 1) << 2 | perm4(i, 2) << 4 | perm4(i, 3) << 6);
+    return t;
+}
+__constant__ Perm4Table g_perm4 = make_perm4();
+// v[i] / m[i][j] for a runtime i, j by selects (no dynamically indexed registers)
+template <typename T>
+__device__ __forceinline__ T sel4(const T (&v)[4], int i)
+{
+    return i == 0 ? v[0] : (i == 1 ? v[1] : (i == 2 ? v[2] : v[3]));
+}
+template <typename T>
+__device__ __forceinline__ T sel44(const T (&m)[4][4], int i, int j)
+{
+    const T r[4] = {sel4(m[0], j), sel4(m[1], j), sel4(m[2], j), sel4(m[3], j)};
+    return sel4(r, i);
+}
+
+// A wave with only a few prefixes (<= kTailWide; e.g. the two tails of the
+// reference's 16-city instance): tail_one's per-lane TL! chain would leave 63
+// lanes idle for ~20 us, so the prefixes' completions are split over the
+// lanes instead — one lane per (prefix, first tail city, second tail city),
+// each folding the (TL-2)! = 24 orders of the other four by the same
+// straight-line `complete` — and the tours within the incumbent are recorded
+// and offered to the tie rule exactly as in tail_one (TL = 6 only).
+template <typename V, int TL>
+__device__ __forceinline__ void tail_wide(const SearchArgs &a, const V *dl, const V *am, uint32_t full,
+                                          const uint32_t (&win)[8], bool act, unsigned long long &lanes,
+                                          TieCache &tcache)
+{
+    static_assert(TL == 6, "tail_wide: six tail cities");
+    V cur = ENum<V>::val(__hip_atomic_load(a.inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    uint32_t w[8];
+#pragma unroll
+    for (int b = 0; b < 8; ++b) w[b] = act ? win[b] : 0u;
+    const int len = act ? (int)(w[0] & 255u) : 1;
+    V cp = 0;
+    int prev = 0;
+    uint32_t mem = 0;
+    fold_path<V>(dl, w, len, cp, prev, mem);
+    const uint32_t rest = full & ~mem;
+    uint32_t tpack = 0;
+    V ra = am[0];
+    uint32_t x = rest;
+#pragma unroll
+    for (int i = 0; i < TL; ++i) {
+        const int t = x ? __builtin_ctz(x) : 0;
+        x &= x - 1u;
+        ra += am[t];
+        tpack |= (uint32_t)t << (5 * i);
+    }
+    if (!a.noprune && cp + ra > EThr<V>::of(cur)) act = false;
+    const unsigned long long owners = __ballot(act);
+    if (owners == 0) return;
+    const int nown = __popcll(owners);
+    lanes += (unsigned long long)nown;
+    constexpr int kPairs = TL * (TL - 1);
+    for (int base = 0; base < nown * kPairs; base += 64) {  // (wave-uniform)
+        const int combo = base + __lane_id();
+        const bool on = combo < nown * kPairs;
+        const int oi = on ? combo / kPairs : 0, pr = on ? combo % kPairs : 0;
+        int o = 0;  // the oi-th owner lane
+        {
+            unsigned long long m = owners;
+            for (int k = 0; k < oi; ++k) m &= m - 1ull;
+            o = __ffsll((long long)m) - 1;
+        }
+        const uint32_t otp = (uint32_t)__shfl((int)tpack, o);
+        const int oprev = __shfl(prev, o), olen = __shfl(len, o);
+        V ocp;
+        if constexpr (sizeof(V) == 8)
+            ocp = __longlong_as_double(__shfl((long long)__double_as_longlong(cp), o));
+        else
+            ocp = (V)__shfl((int)cp, o);
+        uint32_t ow[8];
+#pragma unroll
+        for (int b = 0; b < 8; ++b) ow[b] = (uint32_t)__shfl((int)w[b], o);
+        const int i = pr / (TL - 1), jj = pr % (TL - 1), j = jj < i ? jj : jj + 1;
+        const int ti = (int)((otp >> (5 * i)) & 31u), tj = (int)((otp >> (5 * j)) & 31u);
+        const int lo = i < j ? i : j, hi = i < j ? j : i;
+        int r[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            int p = k;
+            p += p >= lo ? 1 : 0;
+            p += p >= hi ? 1 : 0;
+            r[k] = (int)((otp >> (5 * p)) & 31u);
+        }
+        V s4[4][4], d04[4], dk4[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            d04[u] = dl[r[u] * kTRow];
+            dk4[u] = dl[tj * kTRow + r[u]];
+#pragma unroll
+            for (int v = 0; v < 4; ++v) s4[u][v] = u == v ? (V)0 : dl[r[u] * kTRow + r[v]];
+        }
+        const V pj = (ocp + dl[oprev * kTRow + ti]) + dl[ti * kTRow + tj];
+        V best = ENum<V>::big();
+        static_for(
+            [&](auto q) {
+                constexpr int Q = decltype(q)::value;
+                complete<V, 4, (15 & ~(1 << Q)), Q>(s4, d04, pj + dk4[Q], best);
+            },
+            std::make_integer_sequence<int, 4>{});
+        // rare: this lane's orders within the incumbent, recorded one by one
+        if (!(on && best <= cur)) continue;
+#pragma unroll 1
+        for (int pi = 0; pi < 24; ++pi) {
+            const uint32_t pm = g_perm4.p[pi];
+            const int a0 = (int)(pm & 3u), a1 = (int)((pm >> 2) & 3u), a2 = (int)((pm >> 4) & 3u), a3 = (int)(pm >> 6);
+            V c = pj + sel4(dk4, a0);
+            c = c + sel44(s4, a0, a1);
+            c = c + sel44(s4, a1, a2);
+            c = c + sel44(s4, a2, a3);
+            const V total = c + sel4(d04, a3);
+            if (!(total <= cur)) continue;
+            const uint64_t tb = ENum<V>::bits(total);
+            const unsigned long long old = atomicMin(a.inc, (unsigned long long)tb);
+            const unsigned int slot = atomicAdd(a.rec_count, 1u);
+            cur = ENum<V>::vmin(ENum<V>::val(old), total);
+            const int ord[TL] = {ti, tj, sel4(r, a0), sel4(r, a1), sel4(r, a2), sel4(r, a3)};
+            if (slot < a.rec_cap) {
+                SearchRecord *R = a.rec + slot;
+                R->cost = tb;
+                for (int l = 1; l < olen; ++l) R->city[l - 1] = (uint8_t)path_byte(ow, l);
+#pragma unroll
+                for (int l = 0; l < TL; ++l) R->city[olen - 1 + l] = (uint8_t)ord[l];
+            }
+            if (tb <= old)
+                tie_offer(a, tcache, tb, [&](int q) {
+                    int v = 0;
+#pragma unroll
+                    for (int l = 0; l < TL; ++l) v = q == olen + l ? ord[l] : v;
+                    return q < olen ? path_byte(ow, q) : v;
+                });
+        }
+    }
+}
+
 // Every wave reads 64 slots at a time, queues the non-empty ones (len > 0) in
 // LDS and folds them 64 at a time, so a producer may leave holes without
 // idling lanes here.  A batch of at most kTailWide prefixes is folded wide
-// (tail_one: the wave over each prefix's orders).
+// (tail_wide: the lanes over each prefix's first two tail cities).
 constexpr uint32_t kTailWide = 4;
 template <typename V, int TL>
 __global__ __launch_bounds__(256) void tail_kernel(SearchArgs a)
 {
     __shared__ V dl[kSearchMaxN * kTRow];
     __shared__ V am[kSearchMaxN];
-    __shared__ uint32_t wq[4][128];
+    __shared__ uint4 wq[4][128][2];  // per wave: the queued paths' words
     const int n = a.n;
     const V *gd = static_cast<const V *>(a.dist);
     const V *ga = static_cast<const V *>(a.amin);
@@ -485,7 +638,7 @@ __global__ __launch_bounds__(256) void tail_kernel(SearchArgs a)
 
     const uint32_t full = (uint32_t)((1ull << n) - 1ull) & ~1u;
     const int lane = __lane_id();
-    uint32_t *q = wq[threadIdx.x >> 6];
+    uint4 (*q)[2] = wq[threadIdx.x >> 6];
     uint32_t qn = 0;               // wave-uniform: live slots queued
     unsigned long long lanes = 0;  // wave-uniform
     TieCache tcache;
@@ -494,9 +647,15 @@ __global__ __launch_bounds__(256) void tail_kernel(SearchArgs a)
         const bool more = base < count;
         if (more) {
             const uint32_t idx = base + lane;
-            const bool live = idx < count && a.ftail[idx].b[0] != 0;
+            uint32_t pw[8];  // (the whole path: its fold needs it, one read instead of two)
+            load_path(a.ftail + idx, idx < count, pw);
+            const bool live = idx < count && (pw[0] & 255u) != 0;
             const unsigned long long m = __ballot(live);
-            if (live) q[qn + __popcll(m & ((1ull << lane) - 1ull))] = idx;
+            if (live) {
+                const uint32_t at = qn + __popcll(m & ((1ull << lane) - 1ull));
+                q[at][0] = make_uint4(pw[0], pw[1], pw[2], pw[3]);
+                q[at][1] = make_uint4(pw[4], pw[5], pw[6], pw[7]);
+            }
             qn += (uint32_t)__popcll(m);
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
@@ -505,13 +664,21 @@ __global__ __launch_bounds__(256) void tail_kernel(SearchArgs a)
         while (qn >= 64u || (!more && qn > 0u)) {
             const uint32_t take = qn < 64u ? qn : 64u;
             const bool act = (uint32_t)lane < take;
-            const uint32_t idx = act ? q[qn - take + lane] : 0u;
+            uint32_t w[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
+            if (act) {
+                const uint4 lo = q[qn - take + lane][0], hi = q[qn - take + lane][1];
+                w[0] = lo.x, w[1] = lo.y, w[2] = lo.z, w[3] = lo.w;
+                w[4] = hi.x, w[5] = hi.y, w[6] = hi.z, w[7] = hi.w;
+            }
             __builtin_amdgcn_wave_barrier();
             qn -= take;
-            if (take <= kTailWide)
-                tail_one<V, TL>(a, dl, am, full, idx, act, lanes, tcache, true);
-            else
-                tail_one<V, TL>(a, dl, am, full, idx, act, lanes, tcache);
+            if constexpr (TL == 6) {
+                if (take <= kTailWide) {
+                    tail_wide<V, TL>(a, dl, am, full, w, act, lanes, tcache);
+                    continue;
+                }
+            }
+            tail_one<V, TL>(a, dl, am, full, w, act, lanes, tcache);
         }
         if (!more) break;
     }
@@ -920,12 +1087,6 @@ __global__ __launch_bounds__(256) void expand_kernel(SearchArgs a)
         fin_count = c < a.fout_cap ? c : a.fout_cap;
     }
     const V thr = EThr<V>::of(ENum<V>::val(__hip_atomic_load(a.inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)));
-    // chained: this block's first path read beside them, before its count is
-    // known (inside the input buffer; the words of lanes beyond the count are
-    // never used)
-    uint32_t pre[8];
-    const bool spec = a.fin_cap && a.nseg == 1 && blockIdx.x * a.fin_per_block + threadIdx.x < a.fin_cap;
-    load_path(a.fseg[0] + blockIdx.x * a.fin_per_block + threadIdx.x, spec, pre);
     // (a block without a run of this level stages its tables all the same: it
     // leaves at the barrier, and the tables are a few hundred bytes of L2)
     for (int i = threadIdx.x; i < n * n; i += blockDim.x) dl[(i / n) * kTRow + i % n] = gd[i];
@@ -958,19 +1119,13 @@ __global__ __launch_bounds__(256) void expand_kernel(SearchArgs a)
     uint32_t cT = 0, cF = 0;
     unsigned long long nodes = 0;
     uint32_t lv[kExpandTiles];
-    uint32_t w0[8];  // the first tile's path, kept for pass 2 (one fewer memory round trip)
 #pragma unroll
     for (int t = 0; t < kExpandTiles; ++t) {
         const uint32_t base = b0 + 256u * t;
         lv[t] = 0;
         if (base >= b1) continue;
-        const bool first = t == 0 && spec && runi == blockIdx.x;  // (the path read before the barrier)
-        const Expand<V> e = expand_eval<V, TL>(a, dl, am, b2, bn, dm, full, base + threadIdx.x, b1, thr,
-                                               first ? pre : nullptr);
+        const Expand<V> e = expand_eval<V, TL>(a, dl, am, b2, bn, dm, full, base + threadIdx.x, b1, thr);
         lv[t] = e.live;
-        if (t == 0)
-#pragma unroll
-            for (int b = 0; b < 8; ++b) w0[b] = e.w[b];
         const uint32_t cnt = (uint32_t)__builtin_popcount(e.live);
         if (e.len == a.tail_level) cT += cnt; else cF += cnt;  // children have len inner cities
         nodes += (unsigned long long)__builtin_popcount(e.rem) + e.hnodes;
@@ -1010,12 +1165,7 @@ __global__ __launch_bounds__(256) void expand_kernel(SearchArgs a)
         if (base >= b1) break;  // block-uniform
         Expand<V> e;
         const bool act = base + threadIdx.x < b1;
-        if (t == 0) {
-#pragma unroll
-            for (int b = 0; b < 8; ++b) e.w[b] = w0[b];
-        } else {
-            load_path(fin_at(a, base + threadIdx.x), act, e.w);
-        }
+        load_path(fin_at(a, base + threadIdx.x), act, e.w);
         e.len = act ? (int)(e.w[0] & 255u) : 0;
         e.live = lv[t];
         const bool tail = e.len == a.tail_level;
@@ -1065,6 +1215,166 @@ __global__ __launch_bounds__(256) void expand_kernel(SearchArgs a)
     }  // runs
 }
 
+// Chained frontier levels, block-local (SearchArgs::local_levels): a block
+// takes a run of fin_per_block input paths and expands its subtree level after
+// level inside the launch — the paths between two levels stay in an LDS queue
+// (kLocalCap per level), with the block's own barriers between levels instead
+// of a launch per level.  The chain's level launches cost ~11 us each at 16
+// cities whatever their size, nearly all of it latency (set-up reads, the
+// path reads, the slot atomics: profiles/r04/k2_chain_costs.log), and a grid
+// barrier costs more than a launch (5-21 us), so the levels are folded per
+// block instead.  Children that reach the tail level go to ftail as before;
+// children the queue cannot hold (or those of the last local level) go to
+// fout, which the chain's next launch expands: every launch still advances
+// every path at least one level, so the chain's launch count bounds the depth
+// as before (the later launches mostly find nothing and leave).
+constexpr uint32_t kLocalCap = 512;
+
+template <typename V, int TL>
+__global__ __launch_bounds__(256) void expand_local_kernel(SearchArgs a)
+{
+    __shared__ V dl[kSearchMaxN * kTRow];
+    __shared__ V am[kSearchMaxN];
+    __shared__ V b2[2 * kSearchMaxN];
+    __shared__ uint32_t bn[32][8];
+    __shared__ double dm[kSearchMaxN * kTRow + kSearchMaxN + 1];
+    __shared__ uint4 q[2][kLocalCap][2];  // the level queues (32-byte paths)
+    __shared__ uint32_t wtot[2][4];
+    __shared__ uint32_t bbase[2];
+    __shared__ uint32_t dead, bskip;
+    const int n = a.n;
+    const V *gd = static_cast<const V *>(a.dist);
+    const V *ga = static_cast<const V *>(a.amin);
+    if (threadIdx.x == 0) dead = a.overflow ? __hip_atomic_load(a.overflow, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+    if (a.out_next && blockIdx.x == 0 && threadIdx.x == 0) *a.out_next = 0u;
+    uint32_t fin_count = a.fin_count;
+    if (a.fin_count_dev) {
+        const uint32_t c = __hip_atomic_load(a.fin_count_dev, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        fin_count = c < a.fout_cap ? c : a.fout_cap;
+    }
+    V thr = EThr<V>::of(ENum<V>::val(__hip_atomic_load(a.inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)));
+    const uint32_t fpb = a.fin_per_block;
+    uint32_t pre[8];  // the first run's paths, read beside the set-up (see expand_kernel)
+    const bool spec = a.fin_cap && a.nseg == 1 && threadIdx.x < fpb && blockIdx.x * fpb + threadIdx.x < a.fin_cap;
+    load_path(a.fseg[0] + blockIdx.x * fpb + threadIdx.x, spec, pre);
+    for (int i = threadIdx.x; i < n * n; i += blockDim.x) dl[(i / n) * kTRow + i % n] = gd[i];
+    for (int i = threadIdx.x; i < n; i += blockDim.x) am[i] = ga[i];
+    if (a.sym)
+        for (int i = threadIdx.x; i < 2 * n; i += blockDim.x) b2[i] = static_cast<const V *>(a.bnd2)[i];
+    load_binom(bn);
+    if (a.mst) {
+        for (int i = threadIdx.x; i < n * n; i += blockDim.x) dm[(i / n) * kTRow + i % n] = a.mst[i];
+        for (int i = threadIdx.x; i < n; i += blockDim.x) dm[kSearchMaxN * kTRow + i] = a.mst[n * n + i];
+        if (threadIdx.x == 0) dm[kSearchMaxN * kTRow + kSearchMaxN] = a.mst[n * n + n];
+    }
+    __syncthreads();
+    if (dead || blockIdx.x * fpb >= fin_count) return;  // (block-uniform)
+
+    const uint32_t full = (uint32_t)((1ull << n) - 1ull) & ~1u;
+    const int lane = __lane_id(), wv = threadIdx.x >> 6;
+    unsigned long long nodes = 0;
+    for (uint32_t runi = blockIdx.x; runi * fpb < fin_count; runi += gridDim.x) {
+        const uint32_t b0 = runi * fpb;
+        uint32_t qn = fin_count - b0 < fpb ? fin_count - b0 : fpb;  // this level's paths (block-uniform)
+        int cur = 0;
+        for (int L = 0; L < a.local_levels && qn > 0; ++L) {
+            // the incumbent for the next level, read now (its latency under this level's work)
+            const V thr_next = EThr<V>::of(ENum<V>::val(__hip_atomic_load(a.inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)));
+            const bool last = L + 1 >= a.local_levels;
+            uint32_t qnext = 0;  // block-uniform
+            for (uint32_t t0 = 0; t0 < qn; t0 += 256u) {
+                const uint32_t i = t0 + threadIdx.x;
+                const bool act = i < qn;
+                uint32_t w[8];
+                if (L == 0 && t0 == 0 && runi == blockIdx.x && spec) {
+#pragma unroll
+                    for (int b = 0; b < 8; ++b) w[b] = pre[b];
+                } else if (L == 0) {
+                    load_path(fin_at(a, b0 + i), act, w);
+                } else if (act) {
+                    const uint4 lo = q[cur][i][0], hi = q[cur][i][1];
+                    w[0] = lo.x, w[1] = lo.y, w[2] = lo.z, w[3] = lo.w;
+                    w[4] = hi.x, w[5] = hi.y, w[6] = hi.z, w[7] = hi.w;
+                } else {
+#pragma unroll
+                    for (int b = 0; b < 8; ++b) w[b] = 0u;
+                }
+                const Expand<V> e = expand_eval<V, TL>(a, dl, am, b2, bn, dm, full, i, qn, thr, w);
+                nodes += (unsigned long long)__builtin_popcount(e.rem) + e.hnodes;
+                publish_ub<V>(a, e.ub);
+                const uint32_t cnt = (uint32_t)__builtin_popcount(e.live);
+                const bool tail = e.len == a.tail_level;  // children with tail_level inner cities
+                const uint32_t v[2] = {tail ? cnt : 0u, tail ? 0u : cnt};
+                uint32_t incl[2] = {v[0], v[1]};
+#pragma unroll
+                for (int off = 1; off < 64; off <<= 1)
+#pragma unroll
+                    for (int k = 0; k < 2; ++k) {
+                        const uint32_t y = __shfl_up(incl[k], off);
+                        if (lane >= off) incl[k] += y;
+                    }
+                if (lane == 63) {
+                    wtot[0][wv] = incl[0];
+                    wtot[1][wv] = incl[1];
+                }
+                __syncthreads();
+                uint32_t wofs[2] = {0u, 0u}, ttot[2] = {0u, 0u};
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    wofs[0] += u < wv ? wtot[0][u] : 0u;
+                    wofs[1] += u < wv ? wtot[1][u] : 0u;
+                    ttot[0] += wtot[0][u];
+                    ttot[1] += wtot[1][u];
+                }
+                // the non-tail children stay in the block unless this is the
+                // last local level or the queue cannot take the tile's
+                const bool local = !last && qnext + ttot[1] <= kLocalCap;  // (block-uniform)
+                if (threadIdx.x == 0) {
+                    bbase[0] = ttot[0] ? atomicAdd(a.tail_count, ttot[0]) : 0u;
+                    bbase[1] = !local && ttot[1] ? atomicAdd(a.out_count, ttot[1]) : 0u;
+                    bskip = 0u;
+                    if (a.overflow && ((ttot[0] && (uint64_t)bbase[0] + ttot[0] > a.tail_cap) ||
+                                       (!local && ttot[1] && (uint64_t)bbase[1] + ttot[1] > a.fout_cap))) {
+                        *a.overflow = 1u;  // the chain is abandoned (the host reruns it step by step)
+                        bskip = 1u;
+                    }
+                }
+                __syncthreads();
+                if (bskip) return;  // (block-uniform; nothing this block reserved is read: see expand_kernel)
+                uint32_t slot = tail ? bbase[0] + wofs[0] + incl[0] - v[0]
+                                     : (local ? qnext : bbase[1]) + wofs[1] + incl[1] - v[1];
+                const int cb = e.len >> 2, cs = 8 * (e.len & 3);
+                uint32_t cw[8];
+#pragma unroll
+                for (int b = 0; b < 8; ++b) cw[b] = b == 0 ? ((e.w[0] & ~255u) | (uint32_t)(e.len + 1)) : e.w[b];
+                for (uint32_t x = e.live; x; x &= x - 1u, ++slot) {
+                    const uint32_t j = (uint32_t)__builtin_ctz(x);
+                    uint32_t o[8];
+#pragma unroll
+                    for (int b = 0; b < 8; ++b) o[b] = b == cb ? ((cw[b] & ~(255u << cs)) | (j << cs)) : cw[b];
+                    const uint4 lo = make_uint4(o[0], o[1], o[2], o[3]), hi = make_uint4(o[4], o[5], o[6], o[7]);
+                    if (!tail && local) {
+                        q[cur ^ 1][slot][0] = lo;
+                        q[cur ^ 1][slot][1] = hi;
+                    } else {
+                        uint4 *dst = reinterpret_cast<uint4 *>((tail ? a.ftail : a.fout) + slot);
+                        dst[0] = lo;
+                        dst[1] = hi;
+                    }
+                }
+                if (local) qnext += ttot[1];
+                __syncthreads();  // (wtot reused; the queue's writes before the next level reads them)
+            }
+            cur ^= 1;
+            qn = qnext;
+            thr = thr_next < thr ? thr_next : thr;
+        }
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) nodes += __shfl_xor(nodes, off);
+    if (lane == 0 && nodes) atomicAdd(stat_line(a), nodes);
+}
+
 // Seeds (SearchItem, from seed_kernel) -> frontier paths.
 __global__ __launch_bounds__(256) void to_paths_kernel(SearchArgs a)
 {
@@ -1110,10 +1420,21 @@ hipError_t launch_to_paths(const SearchArgs &a)
 hipError_t launch_expand(const SearchArgs &a, bool f64)
 {
     if (a.n > kSearchMaxN || a.fin_count == 0) return a.fin_count ? hipErrorInvalidValue : hipSuccess;
-    if (a.fin_per_block == 0 || a.fin_per_block % 256u || a.fin_per_block > 256u * kExpandTiles)
+    if (a.fin_per_block == 0 || (a.local_levels <= 0 && (a.fin_per_block % 256u || a.fin_per_block > 256u * kExpandTiles)))
         return hipErrorInvalidValue;
     int grid = (int)((a.fin_count + a.fin_per_block - 1u) / a.fin_per_block);
     if (a.max_grid > 0 && grid > a.max_grid) grid = a.max_grid;  // chained: the blocks loop over the runs
+    if (a.local_levels > 0) {
+        if (a.fin_per_block > 256u) return hipErrorInvalidValue;
+#define TSPGPU_LOC(VT, TLV) hipLaunchKernelGGL((expand_local_kernel<VT, TLV>), dim3(grid), dim3(256), 0, a.stream, a)
+        if (a.tail_len == 5) {
+            if (f64) TSPGPU_LOC(double, 5); else TSPGPU_LOC(int32_t, 5);
+        } else {
+            if (f64) TSPGPU_LOC(double, 6); else TSPGPU_LOC(int32_t, 6);
+        }
+#undef TSPGPU_LOC
+        return hipGetLastError();
+    }
     if (a.tail_len == 5) {
         if (f64)
             hipLaunchKernelGGL((expand_kernel<double, 5>), dim3(grid), dim3(256), 0, a.stream, a);

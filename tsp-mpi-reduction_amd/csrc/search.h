@@ -100,7 +100,12 @@ struct SearchArgs {
     const PathItem *fseg[4];
     uint32_t fseg_start[4];
     int nseg;
-    uint32_t fin_per_block;    // expand_kernel: paths per block (multiple of 256)
+    uint32_t fin_per_block;    // expand_kernel: paths per block (multiple of 256; expand_local_kernel: of 64)
+    // chained levels expanded block-locally (expand_local_kernel, > 0): up to
+    // this many levels of a run's subtree inside one launch, the levels between
+    // kept in LDS; children that reach the tail level, that the LDS queue
+    // cannot hold or that the last local level makes go to ftail / fout
+    int local_levels;
     PathItem *fout;
     PathItem *ftail;
     unsigned int *tail_count;  // items in ftail (tail_kernel reads it on the device)

@@ -1167,6 +1167,12 @@ static int run_chain(tspgpu_search *s, bool *done, int every = 0, tspgpu_level_h
     int chain_grid = 2;
     chain_fpb = (uint32_t)tuned_int("CHAIN_FPB", (int)chain_fpb);  // (sweeps)
     chain_grid = std::max(1, tuned_int("CHAIN_GRID", chain_grid));
+    // the levels expanded block-locally (expand_local_kernel; knob
+    // CHAIN_LOCAL), runs of 64 input paths per block
+    // (from 20 cities: 7-11% fewer kernel-us at 20-32 cities; at 14-16 cities
+    // the per-level launches win, profiles/r04/k2_local_sweep.log)
+    const bool chain_local = tuned_or("CHAIN_LOCAL", s->n >= 20 ? 1 : 0) != 0;
+    const uint32_t chain_local_fpb = (uint32_t)std::max(1, std::min(256, tuned_int("CHAIN_LOCAL_FPB", 64)));
     hipStream_t st = s->ctx->stream;
     const int hooks = hook && every > 0 && levels > 1 ? (levels - 1) / every : 0;
     if (levels < 1 || s->local_items + 1 > kChainCap) {
@@ -1220,7 +1226,8 @@ static int run_chain(tspgpu_search *s, bool *done, int every = 0, tspgpu_level_h
         a.fout = s->fb[ob[l & 1]];
         a.fout_cap = (uint32_t)kChainCap;
         a.overflow = reinterpret_cast<unsigned int *>(s->d_words + 13);
-        a.fin_per_block = chain_fpb;
+        a.fin_per_block = chain_local ? chain_local_fpb : chain_fpb;
+        a.local_levels = chain_local ? levels - l : 0;  // (block-local: every level left, in LDS where it fits)
         a.max_grid = s->ctx->cu_count * chain_grid;  // (blocks beyond the level's runs only stage tables and leave)
         e = launch_expand(a, f64);
         if (e == hipSuccess && hooks && (l + 1) % every == 0 && (l + 1) / every <= hooks)

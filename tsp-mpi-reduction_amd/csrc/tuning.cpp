@@ -51,6 +51,8 @@ Knob g_knobs[] = {
     {"SEARCH_CHAIN_POISON", false, 0},    // 1: fill the chain's level buffers with 0xFF first (tests)
     {"CHAIN_FPB", false, 0},
     {"CHAIN_GRID", false, 0},
+    {"CHAIN_LOCAL", false, 0},      // 0: a launch per chained level (no block-local levels)
+    {"CHAIN_LOCAL_FPB", false, 0},
     {"SEARCH_DEBUG", false, 0},    // host phase times on stderr
     {"SEARCH_DEPTH", false, 0},
     {"SEARCH_RECORD_CAP", false, 0},  // tests: force the second phase
