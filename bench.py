@@ -720,7 +720,8 @@ def k2_pmc(cus, peaks, nodes_per_search, kernel_ms):
         out["roofline"] = {"bound": "valu (issue)", "achieved": ach / 1e12, "peak": peak / 1e12,
                            "unit": "T VALU lane-instructions/s", "frac": ach / peak,
                            "note": "VALU lane-instructions of the search kernels (PMC SQ_INSTS_VALU x 64) per search / "
-                                   "the search's device time (the chained launches' event span, gaps included), "
+                                   "the search's device time (device wall clock from the prologue's start to the "
+                                   "readback kernel's, gaps included), "
                                    "against the f64 add issue rate (bin/ubench); "
                                    "a node costs valu_lane_instructions_per_node of them"}
     return out
