@@ -1012,10 +1012,14 @@ __device__ __forceinline__ Expand<V> expand_eval(const SearchArgs &a, const V *d
     e.rem = act ? (full & ~mem) : 0u;
     V remA = am[0];  // every city still to be entered: its cheapest incoming edge (exact sums)
     V remB = 0;      // B1: the rem cities' half sums (exact sums)
-    for (uint32_t x = e.rem; x; x &= x - 1u) {
-        const int t = __builtin_ctz(x);
-        remA += am[t];
-        if (a.sym) remB += b2[2 * t];
+    // (over every city with a wave-uniform trip count and uniform LDS
+    // addresses, the member test as a select: the reads pipeline instead of
+    // one LDS round trip per member as in a per-lane bit loop; same sums, in
+    // the same ascending order)
+    for (int t = 1; t < a.n; ++t) {
+        const bool in = (e.rem >> t) & 1u;
+        remA += in ? am[t] : (V)0;
+        if (a.sym) remB += in ? b2[2 * t] : (V)0;
     }
     const bool htest = a.hs_len == TL && a.tail_len == TL && e.len == a.tail_level && !a.noprune;
     e.live = 0;
@@ -1026,12 +1030,11 @@ __device__ __forceinline__ Expand<V> expand_eval(const SearchArgs &a, const V *d
         e.hnodes = act ? (uint32_t)((TL + 1) * TL) : 0u;
         return e;
     }
-    for (uint32_t x = e.rem; x; x &= x - 1u) {
-        const int j = __builtin_ctz(x);
+    for (int j = 1; j < a.n; ++j) {  // (uniform trip count, as above)
         const V cj = c + dl[k * kTRow + j];
         bool ok = a.noprune || !(cj + (remA - am[j]) > thr);
         if (ok && a.sym && !a.noprune) ok = !(cj + (((remB - b2[2 * j]) + b2[2 * j + 1]) + b2[1]) > thr);
-        if (ok) e.live |= 1u << j;
+        if (ok && ((e.rem >> j) & 1u)) e.live |= 1u << j;
     }
     // the tree bound of the whole rest (all children at once), only for paths
     // the cheaper bounds left children of; its margin

@@ -198,23 +198,32 @@ __host__ __device__ constexpr int tiled_moff(int L, int J)
 
 // Buffer-resource access with the uniform part of the offset in soffset (an
 // SGPR) and the per-lane part in voffset: no VALU address arithmetic.
+// (cache-policy bits of the pushes' loads and stores: A/B builds only)
+#ifndef TSPGPU_RS_LOAD_AUX
+#define TSPGPU_RS_LOAD_AUX 0
+#endif
+#ifndef TSPGPU_RS_STORE_AUX
+#define TSPGPU_RS_STORE_AUX 0
+#endif
 template <typename V>
 struct Rsrc {
     __amdgpu_buffer_rsrc_t rs;
     __device__ __forceinline__ V load(uint32_t voff, uint32_t soff) const
     {
         if constexpr (sizeof(V) == 8)
-            return __builtin_bit_cast(V, __builtin_amdgcn_raw_buffer_load_b64(rs, (int)voff, (int)soff, 0));
+            return __builtin_bit_cast(V, __builtin_amdgcn_raw_buffer_load_b64(rs, (int)voff, (int)soff,
+                                                                                  TSPGPU_RS_LOAD_AUX));
         else
-            return (V)__builtin_amdgcn_raw_buffer_load_b32(rs, (int)voff, (int)soff, 0);
+            return (V)__builtin_amdgcn_raw_buffer_load_b32(rs, (int)voff, (int)soff, TSPGPU_RS_LOAD_AUX);
     }
     __device__ __forceinline__ void store(uint32_t voff, uint32_t soff, V v) const
     {
         if constexpr (sizeof(V) == 8) {
             using u2 = decltype(__builtin_amdgcn_raw_buffer_load_b64(rs, 0, 0, 0));
-            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2, v), rs, (int)voff, (int)soff, 0);
+            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2, v), rs, (int)voff, (int)soff,
+                                                  TSPGPU_RS_STORE_AUX);
         } else {
-            __builtin_amdgcn_raw_buffer_store_b32((uint32_t)v, rs, (int)voff, (int)soff, 0);
+            __builtin_amdgcn_raw_buffer_store_b32((uint32_t)v, rs, (int)voff, (int)soff, TSPGPU_RS_STORE_AUX);
         }
     }
     // non-temporal 8-byte store (parent words: read back only by the backtracking)
