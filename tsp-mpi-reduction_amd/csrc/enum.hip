@@ -312,18 +312,15 @@ __device__ __forceinline__ int path_byte(const uint32_t (&w)[8], int l)
     return (int)((v >> (8 * (l & 3))) & 255u);
 }
 
-// One handed-over prefix (its words, queued by tail_kernel): refold, bound test, all
+// One handed-over prefix (slot idx of a.ftail): refold, bound test, all
 // TL! completions; `act` false = a lane with nothing to do (wave-uniform code).
 // (A wave with only a few prefixes takes tail_wide below instead.)
 template <typename V, int TL>
-__device__ __forceinline__ void tail_one(const SearchArgs &a, const V *dl, const V *am, uint32_t full,
-                                         const uint32_t (&win)[8], bool act, unsigned long long &lanes,
-                                         TieCache &tcache)
+__device__ __forceinline__ void tail_one(const SearchArgs &a, const V *dl, const V *am, uint32_t full, uint32_t idx,
+                                         bool act, unsigned long long &lanes, TieCache &tcache)
 {
-    V inc = ENum<V>::val(__hip_atomic_load(a.inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
     uint32_t w[8];
-#pragma unroll
-    for (int b = 0; b < 8; ++b) w[b] = act ? win[b] : 0u;
+    load_path(a.ftail + idx, act, w);
     const int len = act ? (int)(w[0] & 255u) : 1;
     // ---- the prefix 0, t1..t(len-1): the reference's left fold
     V cp = 0;
@@ -342,6 +339,7 @@ __device__ __forceinline__ void tail_one(const SearchArgs &a, const V *dl, const
         ra += am[t[i]];
         tpack |= (uint32_t)t[i] << (5 * i);
     }
+    V inc = ENum<V>::val(__hip_atomic_load(a.inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
     if (!a.noprune && cp + ra > EThr<V>::of(inc)) act = false;
     const unsigned long long am_ = __ballot(act);
     if (am_ == 0) return;
@@ -496,15 +494,12 @@ __device__ __forceinline__ T sel44(const T (&m)[4][4], int i, int j)
 // straight-line `complete` — and the tours within the incumbent are recorded
 // and offered to the tie rule exactly as in tail_one (TL = 6 only).
 template <typename V, int TL>
-__device__ __forceinline__ void tail_wide(const SearchArgs &a, const V *dl, const V *am, uint32_t full,
-                                          const uint32_t (&win)[8], bool act, unsigned long long &lanes,
-                                          TieCache &tcache)
+__device__ __forceinline__ void tail_wide(const SearchArgs &a, const V *dl, const V *am, uint32_t full, uint32_t idx,
+                                          bool act, unsigned long long &lanes, TieCache &tcache)
 {
     static_assert(TL == 6, "tail_wide: six tail cities");
-    V cur = ENum<V>::val(__hip_atomic_load(a.inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
     uint32_t w[8];
-#pragma unroll
-    for (int b = 0; b < 8; ++b) w[b] = act ? win[b] : 0u;
+    load_path(a.ftail + idx, act, w);
     const int len = act ? (int)(w[0] & 255u) : 1;
     V cp = 0;
     int prev = 0;
@@ -521,6 +516,7 @@ __device__ __forceinline__ void tail_wide(const SearchArgs &a, const V *dl, cons
         ra += am[t];
         tpack |= (uint32_t)t << (5 * i);
     }
+    V cur = ENum<V>::val(__hip_atomic_load(a.inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
     if (!a.noprune && cp + ra > EThr<V>::of(cur)) act = false;
     const unsigned long long owners = __ballot(act);
     if (owners == 0) return;
@@ -619,7 +615,7 @@ __global__ __launch_bounds__(256) void tail_kernel(SearchArgs a)
 {
     __shared__ V dl[kSearchMaxN * kTRow];
     __shared__ V am[kSearchMaxN];
-    __shared__ uint4 wq[4][128][2];  // per wave: the queued paths' words
+    __shared__ uint32_t wq[4][128];
     const int n = a.n;
     const V *gd = static_cast<const V *>(a.dist);
     const V *ga = static_cast<const V *>(a.amin);
@@ -638,7 +634,7 @@ __global__ __launch_bounds__(256) void tail_kernel(SearchArgs a)
 
     const uint32_t full = (uint32_t)((1ull << n) - 1ull) & ~1u;
     const int lane = __lane_id();
-    uint4 (*q)[2] = wq[threadIdx.x >> 6];
+    uint32_t *q = wq[threadIdx.x >> 6];
     uint32_t qn = 0;               // wave-uniform: live slots queued
     unsigned long long lanes = 0;  // wave-uniform
     TieCache tcache;
@@ -647,15 +643,9 @@ __global__ __launch_bounds__(256) void tail_kernel(SearchArgs a)
         const bool more = base < count;
         if (more) {
             const uint32_t idx = base + lane;
-            uint32_t pw[8];  // (the whole path: its fold needs it, one read instead of two)
-            load_path(a.ftail + idx, idx < count, pw);
-            const bool live = idx < count && (pw[0] & 255u) != 0;
+            const bool live = idx < count && a.ftail[idx].b[0] != 0;
             const unsigned long long m = __ballot(live);
-            if (live) {
-                const uint32_t at = qn + __popcll(m & ((1ull << lane) - 1ull));
-                q[at][0] = make_uint4(pw[0], pw[1], pw[2], pw[3]);
-                q[at][1] = make_uint4(pw[4], pw[5], pw[6], pw[7]);
-            }
+            if (live) q[qn + __popcll(m & ((1ull << lane) - 1ull))] = idx;
             qn += (uint32_t)__popcll(m);
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
@@ -664,21 +654,16 @@ __global__ __launch_bounds__(256) void tail_kernel(SearchArgs a)
         while (qn >= 64u || (!more && qn > 0u)) {
             const uint32_t take = qn < 64u ? qn : 64u;
             const bool act = (uint32_t)lane < take;
-            uint32_t w[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
-            if (act) {
-                const uint4 lo = q[qn - take + lane][0], hi = q[qn - take + lane][1];
-                w[0] = lo.x, w[1] = lo.y, w[2] = lo.z, w[3] = lo.w;
-                w[4] = hi.x, w[5] = hi.y, w[6] = hi.z, w[7] = hi.w;
-            }
+            const uint32_t idx = act ? q[qn - take + lane] : 0u;
             __builtin_amdgcn_wave_barrier();
             qn -= take;
             if constexpr (TL == 6) {
                 if (take <= kTailWide) {
-                    tail_wide<V, TL>(a, dl, am, full, w, act, lanes, tcache);
+                    tail_wide<V, TL>(a, dl, am, full, idx, act, lanes, tcache);
                     continue;
                 }
             }
-            tail_one<V, TL>(a, dl, am, full, w, act, lanes, tcache);
+            tail_one<V, TL>(a, dl, am, full, idx, act, lanes, tcache);
         }
         if (!more) break;
     }
@@ -1012,14 +997,10 @@ __device__ __forceinline__ Expand<V> expand_eval(const SearchArgs &a, const V *d
     e.rem = act ? (full & ~mem) : 0u;
     V remA = am[0];  // every city still to be entered: its cheapest incoming edge (exact sums)
     V remB = 0;      // B1: the rem cities' half sums (exact sums)
-    // (over every city with a wave-uniform trip count and uniform LDS
-    // addresses, the member test as a select: the reads pipeline instead of
-    // one LDS round trip per member as in a per-lane bit loop; same sums, in
-    // the same ascending order)
-    for (int t = 1; t < a.n; ++t) {
-        const bool in = (e.rem >> t) & 1u;
-        remA += in ? am[t] : (V)0;
-        if (a.sym) remB += in ? b2[2 * t] : (V)0;
+    for (uint32_t x = e.rem; x; x &= x - 1u) {
+        const int t = __builtin_ctz(x);
+        remA += am[t];
+        if (a.sym) remB += b2[2 * t];
     }
     const bool htest = a.hs_len == TL && a.tail_len == TL && e.len == a.tail_level && !a.noprune;
     e.live = 0;
@@ -1030,11 +1011,12 @@ __device__ __forceinline__ Expand<V> expand_eval(const SearchArgs &a, const V *d
         e.hnodes = act ? (uint32_t)((TL + 1) * TL) : 0u;
         return e;
     }
-    for (int j = 1; j < a.n; ++j) {  // (uniform trip count, as above)
+    for (uint32_t x = e.rem; x; x &= x - 1u) {
+        const int j = __builtin_ctz(x);
         const V cj = c + dl[k * kTRow + j];
         bool ok = a.noprune || !(cj + (remA - am[j]) > thr);
         if (ok && a.sym && !a.noprune) ok = !(cj + (((remB - b2[2 * j]) + b2[2 * j + 1]) + b2[1]) > thr);
-        if (ok && ((e.rem >> j) & 1u)) e.live |= 1u << j;
+        if (ok) e.live |= 1u << j;
     }
     // the tree bound of the whole rest (all children at once), only for paths
     // the cheaper bounds left children of; its margin
