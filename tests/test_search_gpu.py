@@ -586,6 +586,11 @@ def test_tree_bound_keeps_the_answer(gpu_ctx, kind, knobs):
             d = np.rint(d).astype(np.int32)
         wc, wt, _ = gpu_ctx.solve_instance(np.asarray(d, dtype=np.float64))
         for mst, minrem in (("0", None), ("1", None), ("1", "0")):
+            if mst == "0" and n >= 25:
+                # (bound off at 25 clustered cities: 7e13 nodes, ~160 s of one
+                # GPU — the answer is pinned by K1-wide with the bound on and at
+                # 18 / 22 cities with it off; tools/k2_mst0_probe.py times it)
+                continue
             knobs.set("SEARCH_MST", mst)
             if minrem is None:
                 knobs.clear("SEARCH_MST_MINREM")
