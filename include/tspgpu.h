@@ -70,6 +70,11 @@ int tspgpu_distance_matrix(const tspgpu_city *cities, int n, int nblocks, double
 int tspgpu_validate(const double *dist, int n, int nblocks, int strict);
 
 int tspgpu_ctx_create(const tspgpu_opts *opts, tspgpu_ctx **out);
+/* Destroy order is free: every tspgpu_search holds a reference on its
+ * context, so destroying the context while searches are alive only marks it
+ * closing (no new search may be created on it: -EINVAL) and the last
+ * tspgpu_search_destroy releases it.  Searches never destroyed keep their
+ * context (a leak, never a use-after-free). */
 int tspgpu_ctx_destroy(tspgpu_ctx *ctx);
 
 /* Batched replacement for tsp() on host buffers; synchronous.
@@ -270,7 +275,10 @@ int tspgpu_search_step(tspgpu_search *s, uint64_t *pending);
 int tspgpu_search_run_all(tspgpu_search *s);
 /* device time of all seed/round launches so far, and the rounds run */
 int tspgpu_search_timing(const tspgpu_search *s, double *kernel_ms, int *rounds);
-/* device address of the 64-bit incumbent word (f64 bits or integer cost) */
+/* device address of the 64-bit incumbent word (f64 bits or integer cost).
+ * The caller may write it (an RCCL all-reduce MIN in place): from this call
+ * on tspgpu_search_counters / tspgpu_search_tie_slot read the device, not the
+ * last chain's readback. */
 void *tspgpu_search_incumbent_device(tspgpu_search *s);
 int tspgpu_search_counters(tspgpu_search *s, uint64_t *incumbent_bits, uint64_t *nodes, uint64_t *records);
 /* forget the records (and grow the buffer to `capacity` if larger) */
@@ -287,10 +295,13 @@ int tspgpu_search_records(tspgpu_search *s, uint64_t cost_bits, tspgpu_tour_reco
  * incumbent word) is called to enqueue an exchange of the device incumbent on
  * that stream — e.g. ncclAllReduce(word, word, 1, ncclUint64, ncclMin, comm,
  * stream): the same number of calls on every shard, chained or not.
- * *done = 1: the shard's search is complete.  *done = 0: the search is too
- * large to chain (a level overflowed, or n is above the chain's limit) and is
- * back at its starting state (incumbent restored, no records): continue with
- * tspgpu_search_start / tspgpu_search_step. */
+ * *done = 1: the shard's search is complete.  *done = 0: the search is not
+ * a chain — too large (a level overflowed, or n is above the chain's limit;
+ * it is back at its starting state: incumbent restored, no records) or too
+ * small to have a frontier level (below ~15 cities the seed depth, one prefix
+ * per lane of the grid, already reaches the register tails: e.g. 13 cities,
+ * seed depth 7 >= 12 - 6) — continue with tspgpu_search_start /
+ * tspgpu_search_step.  The hooks are enqueued either way (same count). */
 typedef void (*tspgpu_level_hook)(void *user, void *stream, void *incumbent_word);
 int tspgpu_search_chain(tspgpu_search *s, int exchange_every, tspgpu_level_hook hook, void *user, int *done);
 

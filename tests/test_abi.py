@@ -38,6 +38,17 @@ def test_host_library_exports():
     assert names and all(hasattr(L, n) for n in names)
 
 
+def test_comm_library_exports():
+    """libtspcomm (the RCCL side of search_dist.py) exports what
+    include/tspcomm.h declares; without a GPU only loading is checked."""
+    path = os.path.join(os.path.dirname(tspgpu.LIB_PATH), "libtspcomm.so")
+    L = ctypes.CDLL(path)
+    src = re.sub(r"/\*.*?\*/", "", open(os.path.join(ROOT, "include", "tspcomm.h")).read(), flags=re.S)
+    names = sorted(set(re.findall(r"\b(tspcomm_[a-z_0-9]+)\s*\(", src)))
+    assert len(names) == 7 and all(hasattr(L, n) for n in names), names
+    assert L.tspcomm_unique_id_bytes() == 128
+
+
 def test_version_and_tour_length():
     assert tspgpu.lib().tspgpu_version() == 100
     assert tspgpu.tour_length(2) == 2 and tspgpu.tour_length(16) == 17

@@ -97,7 +97,13 @@ xy = rng.integers(0, 4, size=(14, 2)) * 1.0
 dl = tspgpu.distance_matrix([[(i, xy[i, 0], xy[i, 1]) for i in range(14)]])[0]
 cl, tl, sl = search_dist.solve_sharded(ctx, dl, group=dist.group.WORLD)
 c1, t1, _ = tspgpu.search_solve(ctx, dl)
+from bench import k2_instance
+d24 = np.asarray(k2_instance(24, 3))
+c24, t24, s24 = search_dist.solve_sharded(ctx, d24, group=dist.group.WORLD)
+c24b, t24b, _ = tspgpu.search_solve(ctx, d24)
 print(json.dumps({"cost": cost, "tour": [int(x) for x in tour], "backend": st["backend"],
+                  "hooks": st["hooks"], "chained": st["chained"], "hooks24": s24["hooks"],
+                  "exchanges24": s24["exchanges"], "same24": bool(c24 == c24b and list(t24) == list(t24b)),
                   "exchanges": st["exchanges"], "world": st["world"], "phases": st["phases"], "tie": st["tie"],
                   "record_gather": st["record_gather"], "lattice_same": bool(cl == c1 and list(tl) == list(t1)),
                   "lattice_tie": sl["tie"], "lattice_gather": sl["record_gather"]}))
@@ -115,6 +121,10 @@ def test_search_dist_world1_nccl_group():
     r = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
     assert r["backend"] == "nccl" and r["world"] == 1 and r["exchanges"] >= 1
     assert r["cost"] == GOLD_COST and r["tour"] == GOLD_TOUR
+    # the in-stream RCCL incumbent exchange between chained levels (libtspcomm's
+    # hook, every 2 levels), then the one exchange after the chain
+    assert r["chained"] == 1 and r["hooks"] >= 2 and r["exchanges"] == 1 + r["hooks"], r
+    assert r["hooks24"] >= 2 and r["exchanges24"] == 1 + r["hooks24"] and r["same24"], r
     # the winner from the RCCL all-reduce of the device tie key: one phase, no record gather
     assert r["phases"] == 1 and r["tie"] == 1 and r["record_gather"] == 0
     assert r["lattice_same"] and r["lattice_tie"] == 1 and r["lattice_gather"] == 0

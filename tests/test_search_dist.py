@@ -83,12 +83,29 @@ class FakeSearch:
                 self.keys[bits] = min(self.keys.get(bits, k), k)
         return len(self.queue)
 
-    def chain(self):
+    LEVELS = 5  # the stand-in's "frontier levels": its tours in five runs
+
+    def chain(self, exchange_every=0, hook=None, native_hook=None):
+        """As tspgpu_search_chain: hook(stream, word) between levels every
+        `exchange_every` levels, (LEVELS - 1) // every times on every shard,
+        chained or not."""
+        assert native_hook is None  # (gloo)
+        hooks = (self.LEVELS - 1) // exchange_every if hook and exchange_every > 0 else 0
         if not self.chainable:
+            for _ in range(hooks):
+                hook(None, None)
             return False
         self.start()
-        while self.step():
-            pass
+        runs = np.array_split(np.arange(len(self.queue)), self.LEVELS)
+        done = 0
+        for lvl, run in enumerate(runs):
+            for _ in run:
+                self.step()
+            if hooks and (lvl + 1) % exchange_every == 0 and done < hooks:
+                hook(None, None)
+                done += 1
+        for _ in range(hooks - done):
+            hook(None, None)
         return True
 
     def tie_slot(self, bits):
@@ -150,7 +167,7 @@ def _cpu_worker(rank, world, port, dist, cap, chainable, tie_on, out):
     tdist.init_process_group("gloo", rank=rank, world_size=world)
     cost, tour, st = search_dist.solve_sharded(None, dist)
     out.put((rank, cost, tour.tolist(), st["optimal_tours"], st["phases"], st["nodes"], st["tie"],
-             st["record_gather"], st["exchanges"]))
+             st["record_gather"], st["exchanges"], st["hooks"]))
     tdist.destroy_process_group()
 
 
@@ -193,7 +210,7 @@ def test_driver_collectives_cpu(world, cap, chainable, tie_on):
         d = _lattice(7, seed)
         res = _run(_cpu_worker, world, d, cap, chainable, tie_on)
         oc, ot = O.solve_block(d)
-        for rank, cost, tour, n_opt, phases, nodes, tie, gathered, exchanges in res:
+        for rank, cost, tour, n_opt, phases, nodes, tie, gathered, exchanges, hooks in res:
             assert cost == oc and tour == ot
             assert nodes == 720 * phases  # every tour folded once per phase, over all ranks
             assert tie == (1 if tie_on else 0) and gathered == (0 if tie_on else 1)
@@ -202,9 +219,12 @@ def test_driver_collectives_cpu(world, cap, chainable, tie_on):
                 assert n_opt == 0  # (no record left any rank)
             else:
                 assert n_opt >= 1
+            # the incumbent exchanged inside the chain every 2 levels (2 hooks
+            # over 5 levels), then the one exchange after the chains
+            assert hooks == 2
             if chainable:
-                assert exchanges == 1  # one exchange after the chains
-        assert len({r[8] for r in res}) == 1
+                assert exchanges == 1 + hooks
+        assert len({r[8] for r in res}) == 1 and len({r[9] for r in res}) == 1  # the same count on every rank
 
 
 def _gpu_worker(rank, world, port, dist, out):

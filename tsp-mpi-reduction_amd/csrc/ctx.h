@@ -60,7 +60,17 @@ struct tspgpu_ctx {
     // K1-wide per-context cache (buffers + captured launch graph of the last n), hkwide.hip
     void *wide_cache = nullptr;
     void (*wide_free)(void *) = nullptr;
-    // K2 device buffers kept between searches (search_abi.cpp)
+    // K2 device buffers kept between searches (search_abi.cpp); null while a
+    // live search holds them
     void *search_pool = nullptr;
     void (*search_pool_free)(void *) = nullptr;
+    // Lifetime: every tspgpu_search holds a reference on its context (it uses
+    // the stream, the device, the mutex and the pool).  tspgpu_ctx_destroy
+    // with searches still alive only marks the context closing; the last
+    // tspgpu_search_destroy then releases it.  Both under mu.
+    int live_searches = 0;
+    bool closing = false;
 };
+
+// frees every resource of c and c itself (no live search may remain)
+void tspgpu_ctx_release(tspgpu_ctx *c);

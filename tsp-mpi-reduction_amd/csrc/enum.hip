@@ -421,11 +421,12 @@ __device__ __forceinline__ void tail_one(const SearchArgs &a, const V *dl, const
                 const V total = c + dl[k * kTRow];
                 if (total <= cur) {
                     const uint64_t tb = ENum<V>::bits(total);
-                    // the record slot claimed beside the incumbent's atomicMin (one
-                    // round trip, not two); a tour the incumbent passed meanwhile
-                    // leaves a record above the optimum, which the host ignores
+                    // a record slot only for a tour still within the incumbent
+                    // the atomicMin returns (a stale read must not fill the
+                    // record buffer with tours above the optimum: rec_count
+                    // decides the -EOVERFLOW / second-phase fallback)
                     const unsigned long long old = atomicMin(a.inc, (unsigned long long)tb);
-                    const unsigned int slot = atomicAdd(a.rec_count, 1u);
+                    const unsigned int slot = tb <= old ? atomicAdd(a.rec_count, 1u) : ~0u;
                     cur = ENum<V>::vmin(ENum<V>::val(old), total);
                     if (slot < a.rec_cap) {
                         SearchRecord *R = a.rec + slot;
@@ -584,7 +585,7 @@ __device__ __forceinline__ void tail_wide(const SearchArgs &a, const V *dl, cons
             if (!(total <= cur)) continue;
             const uint64_t tb = ENum<V>::bits(total);
             const unsigned long long old = atomicMin(a.inc, (unsigned long long)tb);
-            const unsigned int slot = atomicAdd(a.rec_count, 1u);
+            const unsigned int slot = tb <= old ? atomicAdd(a.rec_count, 1u) : ~0u;  // (as tail_one)
             cur = ENum<V>::vmin(ENum<V>::val(old), total);
             const int ord[TL] = {ti, tj, sel4(r, a0), sel4(r, a1), sel4(r, a2), sel4(r, a3)};
             if (slot < a.rec_cap) {
@@ -792,6 +793,8 @@ __device__ __forceinline__ void seed_body(const SearchArgs &a, uint32_t block, u
 template <typename V>
 __global__ __launch_bounds__(kSearchThreads) void seed_kernel(SearchArgs a)
 {
+    // (a chain without the suffix table starts here: its clock, as the prologue's)
+    if (a.t_start && blockIdx.x == 0 && threadIdx.x == 0) *a.t_start = wall_clock64();
     seed_body<V>(a, blockIdx.x, gridDim.x);
 }
 

@@ -334,6 +334,16 @@ static int search_create(tspgpu_ctx *c, const void *dist, int dtype, int n, int 
     if (hipSetDevice(c->device) != hipSuccess) return -ENODEV;
     auto *s = new (std::nothrow) tspgpu_search();
     if (!s) return -ENOMEM;
+    {
+        // the search's reference on its context (ctx.h "Lifetime"); dropped by
+        // tspgpu_search_destroy, also on the failure path below
+        std::lock_guard<std::mutex> g(c->mu);
+        if (c->closing) {
+            delete s;
+            return -EINVAL;
+        }
+        ++c->live_searches;
+    }
     s->ctx = c;
     s->n = n;
     s->dtype = dtype;
@@ -649,7 +659,17 @@ int tspgpu_search_destroy(tspgpu_search *s)
     free_buffers(*s);
     if (s->d_ps) (void)hipFree(s->d_ps);
     if (s->d_ring) (void)hipFree(s->d_ring);
+    tspgpu_ctx *c = s->ctx;
     delete s;
+    // dropping the reference is the last use of the context: when
+    // tspgpu_ctx_destroy came first, the last search releases it (with the
+    // pool just given back)
+    bool last = false;
+    {
+        std::lock_guard<std::mutex> g(c->mu);
+        last = --c->live_searches == 0 && c->closing;
+    }
+    if (last) tspgpu_ctx_release(c);
     return 0;
 }
 
@@ -1175,11 +1195,21 @@ static int run_chain(tspgpu_search *s, bool *done, int every = 0, tspgpu_level_h
     const uint32_t chain_local_fpb = (uint32_t)std::max(1, std::min(256, tuned_int("CHAIN_LOCAL_FPB", 64)));
     hipStream_t st = s->ctx->stream;
     const int hooks = hook && every > 0 && levels > 1 ? (levels - 1) / every : 0;
-    if (levels < 1 || s->local_items + 1 > kChainCap) {
-        // (not chained: the exchanges still pair up with the other shards')
-        for (int k = 0; k < hooks; ++k) hook(user, st, s->d_words + 1);
-        return 0;
-    }
+    // Every return enqueues all `hooks` exchanges, also after a failure
+    // halfway (the other shards block in theirs otherwise): the guard
+    // enqueues whatever the level loop did not.
+    struct HookGuard {
+        tspgpu_level_hook hook;
+        void *user;
+        hipStream_t st;
+        void *word;
+        int want, done = 0;
+        ~HookGuard()
+        {
+            for (; done < want; ++done) hook(user, st, word);
+        }
+    } guard{hook, user, st, s->d_words + 1, hooks};
+    if (levels < 1 || s->local_items + 1 > kChainCap) return 0;  // (not chained: the guard's exchanges pair up)
     const bool f64 = s->dtype == TSPGPU_F64;
     // words 10..13 zeroed before the seeds (10..12: level counters, 13:
     // overflow); word 14 keeps the incumbent the chain starts from
@@ -1230,8 +1260,10 @@ static int run_chain(tspgpu_search *s, bool *done, int every = 0, tspgpu_level_h
         a.local_levels = chain_local ? levels - l : 0;  // (block-local: every level left, in LDS where it fits)
         a.max_grid = s->ctx->cu_count * chain_grid;  // (blocks beyond the level's runs only stage tables and leave)
         e = launch_expand(a, f64);
-        if (e == hipSuccess && hooks && (l + 1) % every == 0 && (l + 1) / every <= hooks)
+        if (e == hipSuccess && hooks && (l + 1) % every == 0 && (l + 1) / every <= hooks) {
             hook(user, st, s->d_words + 1);  // (enqueued between two levels)
+            ++guard.done;
+        }
     }
     if (e == hipSuccess) {
         SearchArgs a = args_of(s);
@@ -1253,7 +1285,7 @@ static int run_chain(tspgpu_search *s, bool *done, int every = 0, tspgpu_level_h
     if (fetch) {  // seeds through the tail fold: device wall clock, prologue start to fetch start
         const unsigned long long *f = fetch_buf(s);
         const unsigned long long t0 = f[4 + 15], t1 = f[25];
-        if (t1 > t0) s->ms += (double)(t1 - t0) / wall_clock_khz(s->ctx->device);
+        if (t0 != 0 && t1 > t0) s->ms += (double)(t1 - t0) / wall_clock_khz(s->ctx->device);
     } else {
         float ms = 0.f;
         if (hipEventElapsedTime(&ms, s->e2, s->e1) == hipSuccess) s->ms += ms;
@@ -1469,6 +1501,10 @@ void *tspgpu_search_incumbent_device(tspgpu_search *s)
 {
     if (!s) return nullptr;
     s->inc_shared = true;  // (the caller may write word 1: a chain then saves it itself)
+    // ... and the last chain's readback may no longer hold it: counters and
+    // tie_slot read the device from now on (an all-reduce after the chain
+    // lowers word 1 below the shard's own incumbent)
+    s->fresh = false;
     return (void *)(s->d_words + 1);
 }
 

@@ -651,6 +651,21 @@ int tspgpu_ctx_create(const tspgpu_opts *opts, tspgpu_ctx **out)
 int tspgpu_ctx_destroy(tspgpu_ctx *c)
 {
     if (!c) return 0;
+    {
+        // searches still alive keep the context: the last one's destroy
+        // releases it (ctx.h "Lifetime")
+        std::lock_guard<std::mutex> g(c->mu);
+        c->closing = true;
+        if (c->live_searches > 0) return 0;
+    }
+    tspgpu_ctx_release(c);
+    return 0;
+}
+
+}  // extern "C"
+
+void tspgpu_ctx_release(tspgpu_ctx *c)
+{
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     for (int i = 0; i <= kMaxN; ++i) {
@@ -658,7 +673,9 @@ int tspgpu_ctx_destroy(tspgpu_ctx *c)
         if (c->d_info[i]) (void)hipFree(c->d_info[i]);
     }
     if (c->wide_free) c->wide_free(c->wide_cache);
-    if (c->search_pool_free) c->search_pool_free(c->search_pool);
+    // (null while a search holds the pool: round 4's segfault was
+    // pool_free(nullptr) when the context went first)
+    if (c->search_pool_free && c->search_pool) c->search_pool_free(c->search_pool);
     if (c->d_slots) (void)hipFree(c->d_slots);
     for (void *p : c->d_tinfo)
         if (p) (void)hipFree(p);
@@ -674,8 +691,9 @@ int tspgpu_ctx_destroy(tspgpu_ctx *c)
     for (auto ev : c->ev_split) (void)hipEventDestroy(ev);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
-    return 0;
 }
+
+extern "C" {
 
 int tspgpu_solve_blocks_device(tspgpu_ctx *c, const double *d_dist, int n, int nblocks, double *d_cost,
                                int32_t *d_tour, void *hip_stream)

@@ -345,6 +345,13 @@ int search_multi(const Instance &in, int G, bool force_rccl, int exchange_every,
             if (!rc) rc = tspgpu_search_create(ctx, dist_ptr(in), in.dtype, in.n, g, G, 0, &s);
             if (!rc) rc = tspgpu_search_set_bound(s, ub);
             hipStream_t st = ctx ? (hipStream_t)tspgpu_stream(ctx) : nullptr;
+            // the key exchange's device words, allocated up front: a shard that
+            // fails later still joins every collective (with neutral words)
+            unsigned long long *dk = nullptr;
+            if (!rc && rccl && hipMalloc((void **)&dk, 2 * sizeof(unsigned long long)) != hipSuccess) {
+                dk = nullptr;
+                rc = -ENOMEM;
+            }
             // every shard must join every all-reduce: if one could not start, none goes on
             if (rc) failed.store(1);
             sync.arrive_and_wait();
@@ -404,31 +411,31 @@ int search_multi(const Instance &in, int G, bool force_rccl, int exchange_every,
             tspgpu_tie_slot &ts = slots[g];
             std::memset(&ts, 0, sizeof ts);
             if (!rc) rc = tspgpu_search_tie_slot(s, inc, &ts);
-            if (rccl) {
-                unsigned long long *dk = nullptr;
-                unsigned long long hk[2] = {ts.found ? ts.w0 : ~0ull, ts.overflow ? 0ull : 1ull};
-                if (!rc && hipMalloc((void **)&dk, sizeof hk) != hipSuccess) rc = -ENOMEM;
-                // (a failed shard still joins the collectives, with neutral words)
-                if (dk) (void)hipMemcpyAsync(dk, hk, sizeof hk, hipMemcpyHostToDevice, st);
-                if (dk && ncclAllReduce(dk, dk, 2, ncclUint64, ncclMin, comms[g], st) != ncclSuccess) rc = -EIO;
-                if (dk) (void)hipMemcpyAsync(hk, dk, sizeof hk, hipMemcpyDeviceToHost, st);
-                if (st) (void)hipStreamSynchronize(st);
+            if (rccl && !failed.load()) {
+                // (failed is the same for every shard after the start barrier;
+                // otherwise every shard has dk and joins both collectives, a
+                // shard whose counters or tie slot failed with neutral words:
+                // no key, "overflow" so nobody certifies)
+                unsigned long long hk[2] = {!rc && ts.found ? ts.w0 : ~0ull, !rc && !ts.overflow ? 1ull : 0ull};
+                (void)hipMemcpyAsync(dk, hk, sizeof hk, hipMemcpyHostToDevice, st);
+                if (ncclAllReduce(dk, dk, 2, ncclUint64, ncclMin, comms[g], st) != ncclSuccess && !rc) rc = -EIO;
+                (void)hipMemcpyAsync(hk, dk, sizeof hk, hipMemcpyDeviceToHost, st);
+                (void)hipStreamSynchronize(st);
                 const uint64_t W0 = hk[0];
                 const bool clean = hk[1] == 1;
-                unsigned long long h1 = ts.found && ts.w0 == W0 ? ts.w1 : ~0ull;
-                if (two && dk) {
+                unsigned long long h1 = !rc && ts.found && ts.w0 == W0 ? ts.w1 : ~0ull;
+                if (two) {
                     (void)hipMemcpyAsync(dk, &h1, 8, hipMemcpyHostToDevice, st);
-                    if (ncclAllReduce(dk, dk, 1, ncclUint64, ncclMin, comms[g], st) != ncclSuccess) rc = -EIO;
+                    if (ncclAllReduce(dk, dk, 1, ncclUint64, ncclMin, comms[g], st) != ncclSuccess && !rc) rc = -EIO;
                     (void)hipMemcpyAsync(&h1, dk, 8, hipMemcpyDeviceToHost, st);
                     (void)hipStreamSynchronize(st);
                 }
-                if (dk) (void)hipFree(dk);
                 if (g == 0) {
                     key[0] = W0;
                     key[1] = two ? h1 : 0;
                     key[2] = clean ? 0 : 1;
                 }
-            } else {
+            } else if (!rccl) {
                 sync.arrive_and_wait();
                 if (g == 0) {
                     for (int q = 0; q < G; ++q) {
@@ -454,6 +461,7 @@ int search_multi(const Instance &in, int G, bool force_rccl, int exchange_every,
                 recs[g].resize(cnt);
             }
             if (s) tspgpu_search_timing(s, &ms[g], &rounds[g]);
+            if (dk) (void)hipFree(dk);
             if (s) tspgpu_search_destroy(s);
             if (ctx) tspgpu_ctx_destroy(ctx);
             rcs[g] = rc;

@@ -23,6 +23,7 @@ min and its tie rule, across shards).
 from __future__ import annotations
 
 import errno
+import os
 import threading
 import time
 
@@ -31,10 +32,86 @@ import numpy as np
 import tspgpu
 
 
-def _word_tensor(value: int, device):
-    import torch
+_COMM_LIB = None
 
-    return torch.tensor([value], dtype=torch.int64, device=device)
+
+def comm_lib():
+    """libtspcomm (include/tspcomm.h): the RCCL communicator and the
+    in-stream incumbent exchange hook; loaded only by multi-GPU drivers."""
+    global _COMM_LIB
+    if _COMM_LIB is None:
+        import ctypes
+
+        path = os.path.join(os.path.dirname(tspgpu.LIB_PATH), "libtspcomm.so")
+        if not os.path.exists(path):
+            raise RuntimeError(f"{path} missing: build it (make -C tsp-mpi-reduction_amd)")
+        L = ctypes.CDLL(path)
+        vp, ip = ctypes.c_void_p, ctypes.c_int
+        L.tspcomm_unique_id.argtypes = [ctypes.c_char_p, ip]
+        L.tspcomm_create.argtypes = [ctypes.c_char_p, ip, ip, ip, ctypes.POINTER(vp)]
+        L.tspcomm_destroy.argtypes = [vp]
+        L.tspcomm_hook_stats.argtypes = [vp, ctypes.POINTER(ip), ctypes.POINTER(ip), ip]
+        L.tspcomm_allreduce_min_u64.argtypes = [vp, ctypes.POINTER(ctypes.c_uint64), ip, vp]
+        _COMM_LIB = L
+    return _COMM_LIB
+
+
+class RcclComm:
+    """An RCCL communicator over the ranks of a torch.distributed group
+    (rank 0's ncclUniqueId broadcast over the group), for the in-stream
+    incumbent exchange: `native_hook` is the (function, user) pair that
+    tspgpu_search_chain calls between levels (tspcomm_level_hook: an
+    ncclAllReduce MIN of the device incumbent word on the search's stream)."""
+
+    def __init__(self, group, rank: int, world: int, device_index: int):
+        import ctypes
+
+        import torch
+        import torch.distributed as tdist
+
+        L = comm_lib()
+        nb = L.tspcomm_unique_id_bytes()
+        uid = ctypes.create_string_buffer(nb)
+        if rank == 0:
+            rc = L.tspcomm_unique_id(uid, nb)
+            if rc:
+                raise tspgpu.TspGpuError(rc, "tspcomm_unique_id")
+        dev = torch.device("cuda", device_index) if tdist.get_backend(group) == "nccl" else torch.device("cpu")
+        t = torch.tensor(list(uid.raw), dtype=torch.uint8, device=dev)
+        src = tdist.get_global_rank(group, 0) if group is not None else 0
+        tdist.broadcast(t, src=src, group=group)
+        raw = bytes(t.cpu().tolist())
+        h = ctypes.c_void_p()
+        rc = L.tspcomm_create(raw, world, rank, device_index, ctypes.byref(h))
+        if rc:
+            raise tspgpu.TspGpuError(rc, "tspcomm_create")
+        self.handle = h
+        self.native_hook = (ctypes.cast(L.tspcomm_level_hook, ctypes.c_void_p).value, h)
+
+    def hook_stats(self, reset: bool = True):
+        """(hooks enqueued, hooks that failed to enqueue) since the last reset."""
+        import ctypes
+
+        c, e = ctypes.c_int(), ctypes.c_int()
+        comm_lib().tspcomm_hook_stats(self.handle, ctypes.byref(c), ctypes.byref(e), int(reset))
+        return c.value, e.value
+
+    def close(self):
+        if self.handle:
+            comm_lib().tspcomm_destroy(self.handle)
+            self.handle = None
+
+
+_COMMS = {}
+
+
+def rccl_comm(group, rank: int, world: int, device_index: int) -> RcclComm:
+    """The process's communicator for this group and device (created once:
+    ncclCommInitRank costs far more than a search)."""
+    key = (id(group), rank, world, device_index)
+    if key not in _COMMS:
+        _COMMS[key] = RcclComm(group, rank, world, device_index)
+    return _COMMS[key]
 
 
 _I64_MAX = (1 << 63) - 1
@@ -50,7 +127,8 @@ def _key_u64(v: int) -> int:
     return ((v + (1 << 64)) % (1 << 64)) ^ (1 << 63)
 
 
-def solve_sharded(ctx, dist, group=None, depth: int = 0, device=None, exchange_every: int | None = None):
+def solve_sharded(ctx, dist, group=None, depth: int = 0, device=None, exchange_every: int | None = None,
+                  exchange_levels: int = 2):
     """Search one instance over the ranks of `group` (None: the default group,
     or a single process when torch.distributed is not initialised).
 
@@ -60,7 +138,12 @@ def solve_sharded(ctx, dist, group=None, depth: int = 0, device=None, exchange_e
     2. Each rank runs its shard as ONE device chain (tspgpu_search_chain: the
        seeds, every frontier level and the tail fold back to back, one
        synchronisation that also reads back the counters and the shard's tie
-       slot at its incumbent).
+       slot at its incumbent), and every `exchange_levels` levels the
+       incumbent is exchanged INSIDE the chain: with the "nccl" backend an
+       RCCL all-reduce MIN of the device word enqueued on the search's stream
+       between two levels (libtspcomm's hook, no host round trip); with gloo
+       (CPU tests, ranks sharing a GPU) a host all-reduce MIN at the level
+       boundary.  The hook count is the same on every rank.
     3. The winner (MIN of the cost, then MIN of the
        reverse-lex key among the holders of that cost): when every shard
        finished its chain, ONE all-gather of 7-word records (incumbent,
@@ -142,7 +225,32 @@ def solve_sharded(ctx, dist, group=None, depth: int = 0, device=None, exchange_e
         t0 = time.perf_counter()
         two = S.n - 1 > 20
         exchanges = 0
-        chained = S.chain()
+        # the periodic incumbent exchange inside the chain (north_star: "the
+        # incumbent bound is exchanged periodically")
+        hooks = 0
+        if backend == "nccl":
+            comm = rccl_comm(group, rank, world, device.index if device.index is not None else 0)
+            comm.hook_stats(reset=True)
+            chained = S.chain(exchange_levels, native_hook=comm.native_hook)
+            hooks, herr = comm.hook_stats(reset=True)
+            if herr:
+                raise tspgpu.TspGpuError(-errno.EIO, f"{herr} in-stream RCCL exchanges failed to enqueue")
+        elif collective:
+            nh = [0]
+
+            def host_exchange(_stream, _word):
+                # (gloo: the word through the host at the level boundary —
+                # counters synchronises the stream up to here)
+                nh[0] += 1
+                cur = S.counters()[0]
+                best = allmin([cur])[0]
+                if best < cur:
+                    S.set_bound(tspgpu.bits_cost(best, S.dtype))
+
+            chained = S.chain(exchange_levels, hook=host_exchange)
+            hooks = nh[0]
+        else:
+            chained = S.chain()
         inc, nodes, recs = S.counters()  # (a finished chain: from its own readback)
         # Fast path, every rank one finished chain: ONE collective.  Each rank
         # contributes (incumbent, chained, its tie slot at that incumbent,
@@ -153,7 +261,7 @@ def solve_sharded(ctx, dist, group=None, depth: int = 0, device=None, exchange_e
         f, w0, w1, ovf = S.tie_slot(inc) if chained else (False, 0, 0, False)
         rec = allgather([inc, int(chained), int(f), _key_i64(w0) if f else _I64_MAX,
                          _key_i64(w1) if f and two else _I64_MAX, int(ovf), int(nodes)])
-        exchanges = 1
+        exchanges = 1 + hooks
         fast = all(r[1] for r in rec)
         if fast:
             opt = min(r[0] for r in rec)
@@ -166,7 +274,7 @@ def solve_sharded(ctx, dist, group=None, depth: int = 0, device=None, exchange_e
             # some shard was too large to chain: step by step, one all-reduce
             # MIN of (incumbent, -busy) every exchange_every steps, the same
             # count on every rank (ranks whose chain finished only join)
-            busy, exchanges = 0, 0
+            busy, exchanges = 0, hooks  # (the in-chain exchanges, then the loop's)
             if not chained:
                 S.start()
                 busy = 1
@@ -195,8 +303,21 @@ def solve_sharded(ctx, dist, group=None, depth: int = 0, device=None, exchange_e
         cost = tspgpu.bits_cost(opt, S.dtype)
         tie, tour = 0, None
         if nov == 0 and K0 != _I64_MAX:
-            w = (_key_u64(K0), _key_u64(K1) if two else 0, cost)
-            rc, t = tspgpu.tie_tour_gpu(ctx, dist, *w) if ctx is not None else tspgpu.tie_tour(dist, *w)
+            # certified ONCE, on rank 0, and broadcast: every rank then takes
+            # the same branch below (a certificate that failed on one rank
+            # only — ENOMEM on a shared GPU — would otherwise split the ranks
+            # between the record gather's collectives and returning)
+            rc, t = -errno.EAGAIN, np.zeros(S.n + 1, dtype=np.int32)
+            if rank == 0:
+                w = (_key_u64(K0), _key_u64(K1) if two else 0, cost)
+                rc, t = tspgpu.tie_tour_gpu(ctx, dist, *w) if ctx is not None else tspgpu.tie_tour(dist, *w)
+            if collective:
+                buf = torch.tensor([1 if rc == 0 else 0, *[int(x) for x in t]], dtype=torch.int64, device=device)
+                src = tdist.get_global_rank(group, 0) if group is not None else 0
+                tdist.broadcast(buf, src=src, group=group)
+                ncoll[0] += 1
+                vals = [int(x) for x in buf.tolist()]
+                rc, t = (0 if vals[0] else -errno.EAGAIN), np.asarray(vals[1:], dtype=np.int32)
             if rc == 0:
                 tie, tour = 1, t
         phases, fallback, gathered, n_opt = 1, 0, 0, 0
@@ -220,7 +341,8 @@ def solve_sharded(ctx, dist, group=None, depth: int = 0, device=None, exchange_e
                  "optimal_tours": n_opt, "depth": S.depth,
                  "items": S.items, "phases": phases, "fallback": fallback, "kernel_ms": kernel_ms, "rounds": rounds,
                  "wall_s": wall, "tie": tie, "record_gather": gathered, "chained": int(chained),
-                 "collectives": ncoll[0], "exchanges": exchanges, "exchange_every": exchange_every, "world": world,
+                 "collectives": ncoll[0], "exchanges": exchanges, "hooks": hooks, "exchange_levels": exchange_levels,
+                 "exchange_every": exchange_every, "world": world,
                  "backend": backend}
         return cost, tour, stats
     finally:

@@ -282,14 +282,11 @@ class Context:
         if rc:
             raise TspGpuError(rc, "tspgpu_ctx_create")
         self.handle = h
-        import weakref
-
-        self._searches = weakref.WeakSet()  # live Search objects: closed before the context
 
     def close(self):
+        # (destroy order is free in the C ABI: live searches keep the
+        # context, the last Search.close releases it — include/tspgpu.h)
         if self.handle:
-            for S in list(self._searches):
-                S.close()
             lib().tspgpu_ctx_destroy(self.handle)
             self.handle = None
 
@@ -635,8 +632,6 @@ class Search:
         if rc:
             raise TspGpuError(rc, "tspgpu_search_create")
         self.handle = h
-        if getattr(ctx, "_searches", None) is not None:
-            ctx._searches.add(self)
         dep, items, local = ctypes.c_int(), ctypes.c_uint64(), ctypes.c_uint64()
         lib().tspgpu_search_info(h, ctypes.byref(dep), ctypes.byref(items), ctypes.byref(local))
         self.depth, self.items, self.local_items = dep.value, items.value, local.value
@@ -672,16 +667,26 @@ class Search:
     def run_all(self):
         self._check(lib().tspgpu_search_run_all(self.handle), "tspgpu_search_run_all")
 
-    def chain(self, exchange_every: int = 0, hook=None) -> bool:
+    def chain(self, exchange_every: int = 0, hook=None, native_hook=None) -> bool:
         """This shard's whole search chained on the device with one
-        synchronisation (tspgpu_search_chain); False: too large to chain, the
-        shard is at its starting state (continue with start/step).  hook(stream,
-        word): called every `exchange_every` levels to enqueue an exchange of
-        the device incumbent word on the search's stream."""
+        synchronisation (tspgpu_search_chain); False: not a chain (too large:
+        the shard is at its starting state; or too small to have a frontier
+        level) — continue with start/step.  Every `exchange_every` levels an
+        exchange of the device incumbent word is enqueued on the search's
+        stream, by hook(stream, word) (Python) or native_hook = (address of a
+        C tspgpu_level_hook, its user pointer), e.g. libtspcomm's in-stream
+        RCCL all-reduce MIN; the same count on every shard either way."""
         done = ctypes.c_int()
-        cb = LEVEL_HOOK(lambda _u, st, w: hook(st, w)) if hook else LEVEL_HOOK()
-        self._check(lib().tspgpu_search_chain(self.handle, exchange_every if hook else 0, cb, None,
-                                              ctypes.byref(done)), "tspgpu_search_chain")
+        user = None
+        if native_hook is not None:
+            cb, user = LEVEL_HOOK(native_hook[0]), native_hook[1]
+        elif hook is not None:
+            cb = LEVEL_HOOK(lambda _u, st, w: hook(st, w))
+        else:
+            cb = LEVEL_HOOK()
+        every = exchange_every if (hook is not None or native_hook is not None) else 0
+        self._check(lib().tspgpu_search_chain(self.handle, every, cb, user, ctypes.byref(done)),
+                    "tspgpu_search_chain")
         return bool(done.value)
 
     def tie_slot(self, bits: int):
