@@ -53,6 +53,11 @@ import tspgpu  # noqa: E402  (lazy: loads libtspgpu on first use, no HIP call at
 METRIC = "search nodes/sec (whole node) + time-to-optimal tour, 16-city, 1/2/4/8 GPU"
 UNIT = "Held-Karp DP relaxations/s"
 HBM_PEAK = 8.0e12  # B/s, MI355X_MICROARCH.md chip table (spec)
+# VALU lane-instruction rates at the 2.4 GHz spec clock (MI355X_MICROARCH.md
+# chip table: 256 CUs x 4 SIMDs, 157.3 TFLOPS f32 vector = 32 lanes/clk/SIMD
+# x 2 for FMA): 32-bit integer ops at the f32 rate, f64 add/min at half of it
+VALU_SPEC_I32 = 256 * 4 * 32 * 2.4e9  # 78.6 T lane-instructions/s
+VALU_SPEC_F64 = 256 * 4 * 16 * 2.4e9  # 39.3 T lane-instructions/s
 KERNEL_NAMES = {5: "hk_tiled_kernel", 6: "hk_sub_kernel"}  # K1 variant -> kernel symbol (others: heldkarp_kernel)
 UBENCH = os.path.join(PKG, "bin", "ubench")
 TSP_BIN = os.path.join(PKG, "bin", "tsp")
@@ -643,7 +648,11 @@ def k2_strong_scaling(ctx, n, seed, group, backend, world, rank, reps=2):
             "ranks": world, "backend": backend, "cost": cost, "tour": [int(x) for x in tour],
             "rank_wall_ms": wall, "rank_kernel_ms": st["kernel_ms"], "rank_nodes": st["rank_nodes"],
             "bb_nodes_expanded": st["nodes"], "rounds": st.get("rounds"), "exchanges": st["exchanges"],
-            "optimal_tours": st["optimal_tours"]}
+            "in_chain_exchanges": st.get("hooks", 0), "exchange_levels": st.get("exchange_levels"),
+            "chained": st.get("chained"), "optimal_tours": st["optimal_tours"],
+            "exchange": "RCCL all-reduce MIN of the device incumbent inside the chain every "
+                        f"{st.get('exchange_levels')} levels (libtspcomm), then one all-gather" if backend == "nccl"
+                        else ("host all-reduce MIN at level boundaries (gloo)" if world > 1 else "none (one rank)")}
 
 
 # --------------------------------------------------------------------------
@@ -1016,9 +1025,12 @@ def main():
         # the forward kernel's time as for the f64 headline
         pk = peaks["i32 relaxation min-only (add,min)"]
         ach = i32.get("forward_relaxations_per_s", i32["relaxations_per_s"])
-        i32["valu_roofline"] = {"bound": "valu (int32)", "achieved_relax_per_s": ach, "peak_relax_per_s": pk,
-                                "frac": ach / pk,
-                                "note": "forward kernel alone (HIP events around it in each chunk), like the f64 line"}
+        spec = VALU_SPEC_I32 / 2  # 2 lane-instructions (v_add_u32, v_min_i32) per relaxation
+        i32["valu_roofline"] = {"bound": "valu (int32)", "achieved_relax_per_s": ach, "peak_relax_per_s": spec,
+                                "frac": ach / spec, "peak_source": "spec: 78.6 T int32 lane-instructions/s / 2",
+                                "measured_peak_relax_per_s": pk, "frac_of_measured_peak": ach / pk,
+                                "note": "forward kernel alone (HIP events around it in each chunk), like the f64 line; "
+                                        "measured peak = bin/ubench's add+min mix on this GPU"}
     dom_ms = split["forward_kernel_ms"] if split else kernel_ms  # the dominant kernel's own time
     relax_s_kernel = Bp * relax / (dom_ms * 1e-3)
     roof = roofline(variant, kname, n, Bp, dom_ms, relax_s_kernel, alg_bytes_per_block, prof, peaks)
@@ -1044,10 +1056,26 @@ def main():
             cpu_opt = cpu_optimized(n)
         except Exception as e:  # noqa: BLE001
             cpu_opt = {"error": f"{type(e).__name__}: {e}"}
+    # both halves of the metric, first class (the headline `value` is K1's
+    # relaxations/s; the B&B search's nodes/s and time to the optimal tour
+    # of the 16-city instance are K2's)
+    headline = {
+        "k1_dp_relaxations_per_s": value,
+        "k1_roofline_frac": (roof or {}).get("frac"),
+        "k2_search_nodes_per_s": (k2 or {}).get("bb_nodes_per_s"),
+        "k2_time_to_optimal_ms_in_process": (k2 or {}).get("time_to_optimal_ms"),
+        "k2_kernel_ms": (k2 or {}).get("kernel_ms"),
+        "k2_instance": (k2 or {}).get("instance"),
+        "time_to_optimal_ms_program": ((tto or {}).get("cli_wall_ms") or {}).get("n16", {}).get("program_ms")
+        if isinstance(((tto or {}).get("cli_wall_ms") or {}).get("n16"), dict) else None,
+        "k2_strong_scaling_time_to_optimal_ms": (k2s or {}).get("time_to_optimal_ms"),
+        "k2_strong_scaling_nodes_per_s": (k2s or {}).get("bb_nodes_per_s"),
+    }
     line = {
         "metric": METRIC,
         "value": value,
         "unit": UNIT,
+        "headline": headline,
         # GPUs actually used: ranks sharing a device (a rehearsal on a smaller
         # box) do not add GPUs, and the line says so
         "n_gpus": min(world, ndev),
@@ -1115,14 +1143,18 @@ def roofline(variant, kname, n, Bp, kernel_ms, relax_s, alg_bytes_per_block, pro
     fabric = None
     if prof and "fabric_read_bytes" in prof:
         fabric = (prof["fabric_read_bytes"] + prof["fabric_write_bytes"]) * scale
-    valu = None
-    if peak_relax:
-        valu = {"bound": "valu", "achieved": per * relax_s / 1e12, "peak": per * peak_relax / 1e12,
-                "unit": "T VALU lane-instructions/s", "frac": relax_s / peak_relax, "traffic": hbm,
-                "note": f"{kname} (n={n}): {per} VALU instructions per DP relaxation ({mix}) x {Bp} blocks x "
-                        f"{tspgpu.relaxations_per_block(n):.0f} relaxations / the kernel's own HIP-event time "
-                        f"({kernel_ms:.3f} ms); peak = the same mix measured by bin/ubench on this GPU "
-                        f"({peak_relax:.3e} relaxations/s); traffic = memory-side bytes per launch (PMC)"}
+    # the f64 VALU spec (MI355X_MICROARCH.md: half the f32 vector rate) is the
+    # peak; the same mix measured by bin/ubench on this GPU rides along
+    spec_relax = VALU_SPEC_F64 / per
+    valu = {"bound": "valu", "achieved": per * relax_s / 1e12, "peak": VALU_SPEC_F64 / 1e12,
+            "unit": "T VALU lane-instructions/s", "frac": relax_s / spec_relax, "traffic": hbm,
+            "peak_source": "spec: 256 CU x 4 SIMD x 16 f64 lanes/clk x 2.4 GHz",
+            "measured_peak": per * peak_relax / 1e12 if peak_relax else None,
+            "frac_of_measured_peak": relax_s / peak_relax if peak_relax else None,
+            "note": f"{kname} (n={n}): {per} VALU instructions per DP relaxation ({mix}) x {Bp} blocks x "
+                    f"{tspgpu.relaxations_per_block(n):.0f} relaxations / the kernel's own HIP-event time "
+                    f"({kernel_ms:.3f} ms); measured_peak = the same mix by bin/ubench on this GPU; "
+                    f"traffic = memory-side bytes per launch (PMC)"}
     mem = None
     if hbm is not None:
         mem = {"bound": "hbm (upper bound: Infinity-Cache hits included)", "achieved": hbm / (kernel_ms * 1e-3) / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",

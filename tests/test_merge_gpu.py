@@ -88,3 +88,42 @@ def test_large_merge_matches_host(gpu_ctx):
     g, gc = gpu_ctx.merge(p1, c1, p2, c2)
     h, hc = host_merge(p1, c1, p2, c2)
     assert gc == hc and [c[0] for c in g] == [c[0] for c in h]
+
+
+def _host_reduce(sols, P):
+    B, L = len(sols), len(sols[0][0])
+    flat = (tspgpu.City * (B * L))()
+    costs = (ctypes.c_double * B)()
+    for b, (path, cost) in enumerate(sols):
+        costs[b] = cost
+        for i, (cid, x, y) in enumerate(path):
+            flat[b * L + i].id, flat[b * L + i].x, flat[b * L + i].y = cid, x, y
+    final = ctypes.c_double()
+    log = ctypes.create_string_buffer(1 << 16)
+    assert H.tsphost_reduce(flat, L, costs, B, P, ctypes.byref(final), log, len(log)) == 0
+    return final.value, log.value.decode()
+
+
+@pytest.mark.parametrize("kind,n,B,P", [("lattice", 6, 48, 1), ("lattice", 9, 40, 3), ("random", 8, 300, 8),
+                                        ("random", 5, 1100, 1)])
+def test_persistent_fold_matches_host(gpu_ctx, knobs, kind, n, B, P):
+    """The per-rank persistent fold (fold_persist_kernel, one launch for every
+    rank's fold) against the host replay and against the per-merge kernels:
+    tie-heavy lattice blocks (near-tied candidates stall a rank: the host
+    merges exactly and the kernel resumes), random blocks over 8 ranks, and a
+    fold that outgrows the 4096-city LDS path (4 x 1100 cities at P = 1: the
+    per-merge kernels finish it)."""
+    rng = np.random.default_rng(n * 1000 + B + P)
+    blocks = []
+    for b in range(B):
+        xy = (rng.integers(0, 3, size=(n, 2)) + 3 * np.array([b % 7, b // 7])).astype(np.float64) \
+            if kind == "lattice" else rng.uniform(0, 1000, size=(n, 2))
+        blocks.append([(b * n + i, xy[i, 0], xy[i, 1]) for i in range(n)])
+    sols = _solve_all(blocks)
+    hf, hlog = _host_reduce(sols, P)
+    paths, costs = [p for p, _ in sols], [c for _, c in sols]
+    f1, log1 = gpu_ctx.reduce(paths, costs, P)
+    knobs.set("K3_PERSIST", "0")
+    f0, log0 = gpu_ctx.reduce(paths, costs, P)
+    assert f1 == hf and f0 == hf, (f1, f0, hf)
+    assert log1 == log0 and sorted(log1.splitlines()) == sorted(hlog.splitlines())

@@ -4,7 +4,7 @@
 # (one process per library per round; bit-exactness vs variant 5 reported).
 set -u
 cd "$(dirname "$0")/.."
-OUT=gpurun_out/r04/ab
+OUT=${OUT:-gpurun_out/r05/ab}
 mkdir -p $OUT
 N=${N:-16}; VB=${VB:-8}
 for r in $(seq 1 ${ROUNDS:-2}); do

@@ -75,9 +75,22 @@ __host__ __device__ constexpr int sub_layer_off(int L, int j)
 {
     return (!TSPGPU_SUB_ONE_LAYER && (j & 1)) ? tiled_region_vals(L) - tiled_layer_vals(L, j) : 0;
 }
+// Overlapped edge passes (TSPGPU_SUB_OVERLAP): passes 0/1 of sub-cube h + 1
+// run during the last middle pass of h and pass L of h during the first middle
+// pass of h + 1, on the waves those passes leave idle, and pass L - 1's push
+// values are staged into LDS during middle pass L - 3 — the separate edge
+// interval A(h) and its exposed memory round trips go away (diagnostic stamps:
+// the two edge intervals took 33% of a block's time for 13% of its
+// relaxations).  Needs layer 2 of the next sub-cube outside the region
+// (C(L,2) x 2 values) and the staged values (L rows x H).
+#ifndef TSPGPU_SUB_OVERLAP
+#define TSPGPU_SUB_OVERLAP 0
+#endif
+__host__ __device__ constexpr int sub_l2_vals(int L) { return cbinom(L, 2) * 2; }
 __host__ __device__ constexpr size_t sub_lds_bytes(int N, int L, int vb)
 {
-    return sub_img_bytes(N, L, vb) + (size_t)2 * 16 * vb + (size_t)sub_region_vals(L) * vb + (size_t)16 * vb;
+    return sub_img_bytes(N, L, vb) + (size_t)2 * 16 * vb + (size_t)sub_region_vals(L) * vb + (size_t)16 * vb +
+           (TSPGPU_SUB_OVERLAP ? (size_t)(sub_l2_vals(L) + L * (N - L)) * vb : 0);
 }
 
 template <typename V, int N, int L>
@@ -86,6 +99,9 @@ struct SubCtx {
     const V *d0;       // d[0][k], k = 1..N at [k-1]
     V *region;         // live low layers (as variant 5)
     V *layerL;         // G[h | full low][m], m low: written by pass L-1, read by pass L
+    V *layer2;         // layer 2 (passes 0/1 write it, middle pass 2 reads it): the region's
+                       // bottom, or its own area when the edge passes overlap (TSPGPU_SUB_OVERLAP)
+    V *pst;            // pass L-1's push values staged in LDS (TSPGPU_SUB_OVERLAP): [row][i]
     Rsrc<V> push;      // this block's push area
     Rsrc<uint64_t> par;  // this block's parent words
 };
@@ -401,9 +417,36 @@ __device__ __forceinline__ uint32_t sub_col(uint32_t hp, uint32_t x)
 #endif
 constexpr int kSubPend = 6;  // >= H - |h|
 
+// Early push loads (TSPGPU_SUB_EARLY).  A middle pass's high members' values
+// (push loads, memory latency) were issued at its start and needed after the
+// first J x QC relaxations: every pass exposed most of a memory round trip.
+// Thread r owns row r in every pass of a sub-cube and the high members of
+// pass J + 1 are pass J's (same h), so pass J issues pass J + 1's push loads
+// itself, AFTER its own relaxations and stores (registers are free there),
+// and they land during the barrier and the next pass's LDS reads.
+#ifndef TSPGPU_SUB_EARLY
+#define TSPGPU_SUB_EARLY 0
+#endif
+// Diagnostic build (TSPGPU_SUB_STAMP): per wave, the shader clock spent in the
+// middle-pass bodies, at their barriers, in the edge intervals and in the whole
+// block, written over the block's tour words (tour_out[blk*(n+1) + 4*wave + k],
+// k = body, barrier, edge, total; the backtracking kernel is skipped).  The
+// results are not tours in such a build.
+#ifndef TSPGPU_SUB_STAMP
+#define TSPGPU_SUB_STAMP 0
+#endif
+__device__ __forceinline__ uint32_t sub_clock()
+{
+    return (uint32_t)__builtin_amdgcn_s_memtime();
+}
+// one |h| dispatch per sub-cube around all middle passes (instead of one per pass)
+#ifndef TSPGPU_SUB_MIDSWITCH
+#define TSPGPU_SUB_MIDSWITCH 0
+#endif
+
 template <typename V, int N, int L, int T, int J>
 __device__ __forceinline__ void sub_mid(const SubCtx<V, N, L> &c, uint32_t h, uint32_t tid, const uint4 &ent,
-                                        V (&pend)[kSubPend])
+                                        V (&pend)[kSubPend], V (&pre)[kSubPend])
 {
     constexpr int H = N - L;
     constexpr int Q = N - T;
@@ -446,19 +489,40 @@ __device__ __forceinline__ void sub_mid(const SubCtx<V, N, L> &c, uint32_t h, ui
     const uint32_t r = tid;
     const bool act = r < (uint32_t)ROWS;
     V g[T];
+    {
+        const V *src = J == 2 ? c.layer2 : c.region + CUR;
 #pragma unroll
-    for (int p = 0; p < J; ++p) g[p] = act ? c.region[CUR + p * ROWS + r] : V(0);
+        for (int p = 0; p < J; ++p) g[p] = act ? src[p * ROWS + r] : V(0);
+    }
     // (one layer in LDS: every wave has its row's values before any of the
     // next layer overwrites them)
     if (TSPGPU_SUB_ONE_LAYER) lds_barrier();
     const uint32_t voff = (BASE + r) * VB;  // the row's offset in a push column
+    constexpr bool PRE_IN = TSPGPU_SUB_EARLY && J > 2, PRE_OUT = TSPGPU_SUB_EARLY && J < L - 2;
     if (act) {
 #pragma unroll
         for (int i = 0; i < HC; ++i)
             g[J + i] = (TSPGPU_SUB_ABL & 1)    ? c.region[CUR + (i % J) * ROWS + r]
                        : (TSPGPU_SUB_ABL & 32) ? c.push.load(r * VB, 0)
+                       : PRE_IN                ? pre[i]
                                                : c.push.load(voff, sub_col<H>(h, hm[i]) * (uint32_t)(NL * VB));
     }
+    // pass J + 1's push loads (TSPGPU_SUB_EARLY): by this thread, which owns
+    // row r there too; after everything else of this pass
+    auto prefetch = [&] {
+        if constexpr (PRE_OUT && HC > 0) {
+            constexpr int ROWS_X = cbinom(L, J + 1), BASE_X = tiled_moff(L, J + 1);
+            __builtin_amdgcn_sched_barrier(0);
+            if (r < (uint32_t)ROWS_X) {
+#pragma unroll
+                for (int i = 0; i < HC; ++i)
+                    pre[i] = c.push.load((BASE_X + r) * VB, sub_col<H>(h, hm[i]) * (uint32_t)(NL * VB));
+            }
+        }
+        // (every entry redefined here: none stays live through a pass)
+#pragma unroll
+        for (int i = PRE_OUT ? HC : kSubPend; i < kSubPend; ++i) pre[i] = V(0);
+    };
     // the previous middle pass's pushes, behind this pass's loads
     constexpr bool DEFER_IN = TSPGPU_SUB_DEFER && J > 2, DEFER_OUT = TSPGPU_SUB_DEFER && J < L - 2;
     if constexpr (DEFER_IN) {
@@ -469,7 +533,10 @@ __device__ __forceinline__ void sub_mid(const SubCtx<V, N, L> &c, uint32_t h, ui
                 c.push.store((BASE_P + r) * VB, sub_col<H>(h | (1u << hn[u]), hn[u]) * (uint32_t)(NL * VB), pend[u]);
         }
     }
-    if (!act) return;
+    if (!act) {
+        prefetch();
+        return;
+    }
     uint32_t mrow[J], kof[QL];
 #pragma unroll
     for (int p = 0; p < J; ++p) mrow[p] = sub_nib(ent, p) * DSB;
@@ -607,6 +674,7 @@ __device__ __forceinline__ void sub_mid(const SubCtx<V, N, L> &c, uint32_t h, ui
         }
     });
     if constexpr (ARG) c.par.store((BASE + r) * 8u, h * (uint32_t)(NL * 8), ((uint64_t)whi << 32) | wlo);
+    prefetch();
 }
 
 // ---------------------------------------------------------------------------
@@ -661,7 +729,7 @@ __device__ __forceinline__ void sub_first(const SubCtx<V, N, L> &c, uint32_t h, 
         if (kk < (uint32_t)L) {
             // layer 2 (even: bottom of the region): position of kk in {a, kk}, colex rank
             const uint32_t lo = a < kk ? a : kk, hi = a < kk ? kk : a;
-            c.region[(kk > a ? ROWS2 : 0) + hi * (hi - 1) / 2 + lo] = acc;
+            c.layer2[(kk > a ? ROWS2 : 0) + hi * (hi - 1) / 2 + lo] = acc;
         } else {
             const uint32_t x = kk - L;
             c.push.store(voff, sub_col<H>(h | (1u << x), x) * (uint32_t)(NL * VB), acc);
@@ -757,7 +825,7 @@ __device__ __forceinline__ void sub_penult(const SubCtx<V, N, L> &c, uint32_t h,
     }
 #pragma unroll
     for (int i = 0; i < C; ++i) {
-        const V g = c.push.load(voff, sub_col<H>(h, hm[i]) * (uint32_t)(NL * VB));
+        const V g = TSPGPU_SUB_OVERLAP ? c.pst[r * H + i] : c.push.load(voff, sub_col<H>(h, hm[i]) * (uint32_t)(NL * VB));
         relax_any<ARG>(false, acc, arg, g, lds_val<V>(c.img, (L + hm[i]) * DSB + kk * VB), L + hm[i]);
     }
     if (act) {
@@ -769,6 +837,25 @@ __device__ __forceinline__ void sub_penult(const SubCtx<V, N, L> &c, uint32_t h,
     if constexpr (ARG) {
         const uint64_t w = group_or<QP>(act ? (uint64_t)arg << (4 * q) : 0ull);
         if (q == 0) c.par.store((BASE + r) * 8u, h * (uint32_t)(NL * 8), w);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Pass L-1's push values of sub-cube h (|h| = C) into LDS (TSPGPU_SUB_OVERLAP):
+// lane e < L * C loads row r = e / C (layer L-1, rank r) of push column
+// (h, hm_i), i = e % C, into pst[r * H + i] — by a wave that is idle in the
+// middle pass it runs beside, so the load's round trip is off the critical path.
+// ---------------------------------------------------------------------------
+template <typename V, int N, int L, int C>
+__device__ __forceinline__ void sub_stage_penult(const SubCtx<V, N, L> &c, uint32_t h, uint32_t lane)
+{
+    constexpr int H = N - L, NL = 1 << L, VB = sizeof(V);
+    constexpr int BASE = tiled_moff(L, L - 1);
+    if constexpr (C > 0) {
+        if (lane >= (uint32_t)(L * C)) return;
+        const uint32_t r = lane / C, i = lane % C;
+        const uint32_t x = nth_bit(h, i);
+        c.pst[r * H + i] = c.push.load((BASE + r) * VB, sub_col<H>(h, x) * (uint32_t)(NL * VB));
     }
 }
 
@@ -804,12 +891,12 @@ __device__ __forceinline__ void sub_build_high(const SubCtx<V, N, L> &c, uint32_
 
 template <typename V, int N, int L, int J>
 __device__ __forceinline__ void sub_dispatch_mid_j(const SubCtx<V, N, L> &c, uint32_t h, int hc, uint32_t tid,
-                                                   const uint4 &ent, V (&pend)[kSubPend])
+                                                   const uint4 &ent, V (&pend)[kSubPend], V (&pre)[kSubPend])
 {
     constexpr int H = N - L;
-#define TSPGPU_SM(HC)                                                                             \
-    case HC:                                                                                      \
-        if constexpr (HC <= H) sub_mid<V, N, L, J + (HC <= H ? HC : 0), J>(c, h, tid, ent, pend);  \
+#define TSPGPU_SM(HC)                                                                                  \
+    case HC:                                                                                           \
+        if constexpr (HC <= H) sub_mid<V, N, L, J + (HC <= H ? HC : 0), J>(c, h, tid, ent, pend, pre);  \
         break;
     switch (hc) {
         TSPGPU_SM(0) TSPGPU_SM(1) TSPGPU_SM(2) TSPGPU_SM(3) TSPGPU_SM(4) TSPGPU_SM(5) TSPGPU_SM(6) TSPGPU_SM(7)
@@ -841,6 +928,12 @@ __device__ __forceinline__ void sub_dispatch_penult(const SubCtx<V, N, L> &c, ui
 {
     constexpr int H = N - L;
     TSPGPU_SUB_SWITCH_C(hc, sub_penult, c, h, tid)
+}
+template <typename V, int N, int L>
+__device__ __forceinline__ void sub_dispatch_stage(const SubCtx<V, N, L> &c, uint32_t h, int hc, uint32_t lane)
+{
+    constexpr int H = N - L;
+    TSPGPU_SUB_SWITCH_C(hc, sub_stage_penult, c, h, lane)
 }
 template <typename V, int N, int L>
 __device__ __forceinline__ void sub_dispatch_last(const SubCtx<V, N, L> &c, uint32_t h, int hc, uint32_t lane)
@@ -895,6 +988,8 @@ __global__ __launch_bounds__(THREADS, tiled_waves(THREADS, sub_wg(WG))) void hk_
     c.d0 = d0;
     c.region = dc + 16;
     c.layerL = c.region + sub_region_vals(L);
+    c.layer2 = TSPGPU_SUB_OVERLAP ? c.layerL + 16 : c.region + sub_layer_off(L, 2);
+    c.pst = c.layerL + 16 + sub_l2_vals(L);
     const uint32_t tid = threadIdx.x;
     const uint4 *rowtab = reinterpret_cast<const uint4 *>(rows);
 
@@ -921,38 +1016,103 @@ __global__ __launch_bounds__(THREADS, tiled_waves(THREADS, sub_wg(WG))) void hk_
 
         uint4 ent = make_uint4(0, 0, 0, 0);
         V pend[kSubPend];  // deferred push stores of the last middle pass (TSPGPU_SUB_DEFER)
+        V pre[kSubPend];   // the next middle pass's push values (TSPGPU_SUB_EARLY)
 #pragma unroll
-        for (int u = 0; u < kSubPend; ++u) pend[u] = V(0);
+        for (int u = 0; u < kSubPend; ++u) pend[u] = pre[u] = V(0);
+        uint32_t st_body = 0, st_bar = 0, st_edge = 0, st_t0 = 0, st_a = 0;
+        if (TSPGPU_SUB_STAMP) st_t0 = sub_clock();
         for (uint32_t h = 0; h < (uint32_t)NH; ++h) {
             const int hc = __builtin_popcount(h);
+            if (TSPGPU_SUB_STAMP) st_a = sub_clock();
             // interval A(h): passes 0/1 of h (lanes < 192) beside pass L of h - 1 (lanes 192..)
+            // (TSPGPU_SUB_OVERLAP: at h = 0 only; later they run inside the middle passes)
             uint32_t t = opaque_u32(tid);
             {
                 constexpr int M2 = tiled_moff(L, 2), C2 = cbinom(L, 2);
                 ent = rowtab[M2 + (t < (uint32_t)C2 ? t : 0u)];
             }
+            if (!TSPGPU_SUB_OVERLAP || h == 0) {
 #pragma unroll
-            for (uint32_t v0 = 0; v0 < 256u; v0 += THREADS) {  // (one iteration at 256 threads)
-                const uint32_t v = t + v0;
-                if (v < 192u)
-                    sub_dispatch_first<V, N, L>(c, h, hc, v);
-                else if (h > 0)
-                    sub_dispatch_last<V, N, L>(c, h - 1, __builtin_popcount(h - 1), v - 192u);
+                for (uint32_t v0 = 0; v0 < 256u; v0 += THREADS) {  // (one iteration at 256 threads)
+                    const uint32_t v = t + v0;
+                    if (v < 192u)
+                        sub_dispatch_first<V, N, L>(c, h, hc, v);
+                    else if (h > 0)
+                        sub_dispatch_last<V, N, L>(c, h - 1, __builtin_popcount(h - 1), v - 192u);
+                }
+                if (TSPGPU_SUB_ABL & 16) lds_barrier(); else __syncthreads();
             }
-            if (TSPGPU_SUB_ABL & 16) lds_barrier(); else __syncthreads();
+            if (TSPGPU_SUB_STAMP) {
+                const uint32_t tb = sub_clock();
+                st_edge += tb - st_a;
+                st_a = tb;
+            }
             // middle passes j = 2..L-2, unrolled (every offset a compile-time
             // constant); the next pass's row entry is loaded one pass ahead
-            static_for<L - 3>([&](auto jj) {
-                constexpr int j = 2 + decltype(jj)::value;
-                const uint4 cur = ent;
-                const uint32_t tj = opaque_u32(tid);
-                if constexpr (j + 1 <= L - 2) {
-                    constexpr int MN = tiled_moff(L, j + 1), CN = cbinom(L, j + 1);
-                    ent = rowtab[MN + (tj < (uint32_t)CN ? tj : 0u)];
+            if constexpr (TSPGPU_SUB_MIDSWITCH) {
+                // one dispatch on |h| per sub-cube around all middle passes:
+                // each case is one straight-line sequence (the compiler's
+                // wait counters and register lifetimes see across passes)
+                auto mids = [&](auto hcc) {
+                    constexpr int HC = decltype(hcc)::value;
+                    static_for<L - 3>([&](auto jj) {
+                        constexpr int j = 2 + decltype(jj)::value;
+                        const uint4 cur = ent;
+                        const uint32_t tj = opaque_u32(tid);
+                        if constexpr (j + 1 <= L - 2) {
+                            constexpr int MN = tiled_moff(L, j + 1), CN = cbinom(L, j + 1);
+                            ent = rowtab[MN + (tj < (uint32_t)CN ? tj : 0u)];
+                        }
+                        sub_mid<V, N, L, j + HC, j>(c, h, tj, cur, pend, pre);
+                        if (!(TSPGPU_SUB_ABL & 4)) lds_barrier();
+                    });
+                };
+                switch (hc) {
+                case 0: mids(std::integral_constant<int, 0>{}); break;
+                case 1: if constexpr (H >= 1) mids(std::integral_constant<int, (H >= 1 ? 1 : 0)>{}); break;
+                case 2: if constexpr (H >= 2) mids(std::integral_constant<int, (H >= 2 ? 2 : 0)>{}); break;
+                case 3: if constexpr (H >= 3) mids(std::integral_constant<int, (H >= 3 ? 3 : 0)>{}); break;
+                case 4: if constexpr (H >= 4) mids(std::integral_constant<int, (H >= 4 ? 4 : 0)>{}); break;
+                case 5: if constexpr (H >= 5) mids(std::integral_constant<int, (H >= 5 ? 5 : 0)>{}); break;
+                case 6: if constexpr (H >= 6) mids(std::integral_constant<int, (H >= 6 ? 6 : 0)>{}); break;
+                default: break;
                 }
-                sub_dispatch_mid_j<V, N, L, j>(c, h, hc, tj, cur, pend);
-                if (!(TSPGPU_SUB_ABL & 4)) lds_barrier();
-            });
+            } else {
+                static_for<L - 3>([&](auto jj) {
+                    constexpr int j = 2 + decltype(jj)::value;
+                    const uint4 cur = ent;
+                    const uint32_t tj = opaque_u32(tid);
+                    if constexpr (j + 1 <= L - 2) {
+                        constexpr int MN = tiled_moff(L, j + 1), CN = cbinom(L, j + 1);
+                        ent = rowtab[MN + (tj < (uint32_t)CN ? tj : 0u)];
+                    }
+                    sub_dispatch_mid_j<V, N, L, j>(c, h, hc, tj, cur, pend, pre);
+                    if constexpr (TSPGPU_SUB_OVERLAP) {
+                        // edge passes on the waves this middle pass leaves idle
+                        static_assert(cbinom(L, 2) <= 64 && cbinom(L, L - 3) <= 128, "overlap: idle waves");
+                        if constexpr (j == 2) {  // pass L of h - 1 (its layerL is still in LDS)
+                            if (h > 0 && tj >= 64u) sub_dispatch_last<V, N, L>(c, h - 1, __builtin_popcount(h - 1), tj - 64u);
+                        }
+                        if constexpr (j == L - 3) {  // pass L - 1's push values into LDS
+                            if (tj >= 128u) sub_dispatch_stage<V, N, L>(c, h, hc, tj - 128u);
+                        }
+                        if constexpr (j == L - 2) {  // passes 0/1 of h + 1 (layer 2 in its own area)
+                            if (h + 1 < (uint32_t)NH && tj >= 64u)
+                                sub_dispatch_first<V, N, L>(c, h + 1, __builtin_popcount(h + 1), tj - 64u);
+                        }
+                    }
+                    uint32_t tm = 0;
+                    if (TSPGPU_SUB_STAMP) {
+                        tm = sub_clock();
+                        st_body += tm - st_a;
+                    }
+                    if (!(TSPGPU_SUB_ABL & 4)) lds_barrier();
+                    if (TSPGPU_SUB_STAMP) {
+                        st_a = sub_clock();
+                        st_bar += st_a - tm;
+                    }
+                });
+            }
             // pass L - 1 (lanes < 128) beside the next sub-cube's high image rows/columns (lanes 128..)
             t = opaque_u32(tid);
 #pragma unroll
@@ -964,6 +1124,16 @@ __global__ __launch_bounds__(THREADS, tiled_waves(THREADS, sub_wg(WG))) void hk_
                     sub_build_high<V, N, L>(c, h + 1, v - 128u);
             }
             if (TSPGPU_SUB_ABL & 16) lds_barrier(); else __syncthreads();
+            if (TSPGPU_SUB_STAMP) st_edge += sub_clock() - st_a;
+        }
+        if (TSPGPU_SUB_STAMP) {
+            const uint32_t tot = sub_clock() - st_t0;
+            if ((tid & 63u) == 0) {
+                int32_t *w = tour_out + (size_t)blk * (n + 1) + 4 * (tid >> 6);
+                w[0] = (int32_t)st_body, w[1] = (int32_t)st_bar, w[2] = (int32_t)st_edge, w[3] = (int32_t)tot;
+            }
+            __syncthreads();
+            continue;
         }
 
         // closing min (tsp.cpp:483-499): G[full][m] + d[m][0], first strict min
@@ -1155,6 +1325,7 @@ hipError_t launch_sub_n(const SubArgs &a)
     hipError_t e = hipGetLastError();
     if (e == hipSuccess && a.ev_mid) e = hipEventRecord(a.ev_mid, a.stream);
     if (e != hipSuccess) return e;
+    if constexpr (TSPGPU_SUB_STAMP) return hipSuccess;  // (diagnostic build: the tour words hold the stamps)
     if constexpr (TSPGPU_SUB_RECYCLE)
         hipLaunchKernelGGL((hk_sub_backtrack<V, N, L>), dim3(a.bt_grid), dim3(64 * kSubBtWaves), 0, a.stream, a.blk1,
                            a.blk0, a.slots, a.slot_bytes, a.info, static_cast<const V *>(a.dist),

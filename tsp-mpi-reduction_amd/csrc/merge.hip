@@ -35,6 +35,7 @@
 #include <vector>
 
 #include "ctx.h"
+#include "tuning.h"
 #include "wave.h"
 #include "tspgpu.h"
 
@@ -364,6 +365,201 @@ __global__ __launch_bounds__(kMergeThreads) void splice_kernel(const tspgpu_city
     }
 }
 
+// ---- persistent per-rank fold (tsp.cpp:348-352) --------------------------------
+//
+// The local fold s = ((b0 ⊕ b1) ⊕ b2) ... of every logical rank's contiguous
+// blocks is a chain of small dependent merges (path 1 grows by one block tour
+// of M = L2 - 1 cities per merge).  As separate launches it was 2 kernels per
+// merge in strict sequence (./tsp 8 1024 at P = 8: 1,016 fold_pick + 1,023
+// splice launches, ~10 us each, profiles/r04/k3_kernel_stats.csv).  Here ONE
+// launch runs every rank's whole fold: a workgroup per rank keeps its path in
+// LDS (structure of arrays), and each merge is three phases between workgroup
+// barriers — the swap-cost minimum (dx*dx, IEEE sqrt, the reference's order of
+// operations), the candidates within eps2 of it, and, with exactly one
+// candidate (then it is the reference's pair, as for fold_pick_kernel), the
+// splice in LDS.  The pick (A, B, C, D) of every merge is logged for the
+// host's exact cost fold (glibc pow, tsp.cpp:263).  A merge with several
+// candidates, or one whose result would not fit the LDS path, stops the rank:
+// its path goes to global memory with the index of the merge, for the host
+// (exact pick, then the remaining merges by the general path or a relaunch).
+constexpr int kFoldThreads = 1024;
+constexpr int kFoldCap = 4096;   // cities of a rank's path held in LDS (20 B each)
+constexpr int kFoldL2 = 33;      // block tours up to 32 cities + the closing copy
+
+struct FoldJob {
+    int first;     // block of the rank's running path when the kernel starts (path = that block's tour if k0 == 0)
+    int count;     // blocks of the rank: merges k0 .. count-2 fold blocks first + 1 + k
+    int k0;        // next merge (0: start from the block; > 0: from path/len, a relaunch)
+    int len;       // running path length when k0 > 0 (in `path`)
+    tspgpu_city *path;  // the rank's running path (global; capacity >= all cities)
+    Pick *picks;        // one per merge of this rank (count - 1)
+};
+struct FoldOut {
+    int status;  // 0 done, 1 stalled (several candidates) at merge `at`, 2 path cap reached before merge `at`
+    int at;
+    int len;     // running path length written to path (status != 0: before merge `at`)
+    int count;   // candidates of the stalled merge
+};
+
+// (key, pair) of the smallest swap cost and the second-smallest key of a set
+// of pairs: exactly one pair is within eps2 of the minimum iff the second key
+// lies above min + eps2 — one pass over the pairs decides what fold_pick's
+// two passes did
+struct Top2 {
+    unsigned long long k1, k2;
+    unsigned i1;
+};
+__device__ __forceinline__ void top2_add(Top2 &a, unsigned long long k, unsigned i)
+{
+    if (k < a.k1) {
+        a.k2 = a.k1;
+        a.k1 = k;
+        a.i1 = i;
+    } else if (k < a.k2) {
+        a.k2 = k;
+    }
+}
+__device__ __forceinline__ Top2 top2_merge(const Top2 &a, const Top2 &b)
+{
+    Top2 r;
+    const bool lo = a.k1 < b.k1 || (a.k1 == b.k1 && a.i1 < b.i1);
+    r.k1 = lo ? a.k1 : b.k1;
+    r.i1 = lo ? a.i1 : b.i1;
+    const unsigned long long hi = lo ? b.k1 : a.k1;
+    r.k2 = min(hi, min(a.k2, b.k2));
+    return r;
+}
+__device__ __forceinline__ unsigned long long shfl_u64(unsigned long long v, int m)
+{
+    const int lo = __shfl_xor((int)(unsigned)v, m), hi = __shfl_xor((int)(unsigned)(v >> 32), m);
+    return ((unsigned long long)(unsigned)hi << 32) | (unsigned)lo;
+}
+
+__global__ __launch_bounds__(kFoldThreads) void fold_persist_kernel(const tspgpu_city *blocks, int L2, double eps2,
+                                                                    const FoldJob *jobs, FoldOut *outs)
+{
+    __shared__ double px[kFoldCap], py[kFoldCap];
+    __shared__ int pid[kFoldCap];
+    __shared__ double cx[kFoldL2], cy[kFoldL2], ce[kFoldL2];
+    __shared__ int cid[kFoldL2];
+    __shared__ Top2 wtop[kFoldThreads / 64];
+    const FoldJob J = jobs[blockIdx.x];
+    const int t = threadIdx.x;
+    const int M = L2 - 1;
+    int len;
+    if (J.k0 == 0) {
+        len = L2;
+        const tspgpu_city *b = blocks + (size_t)J.first * L2;
+        for (int k = t; k < L2; k += kFoldThreads) {
+            const tspgpu_city c = b[k];
+            px[k] = c.x, py[k] = c.y, pid[k] = c.id;
+        }
+    } else {
+        len = J.len;
+        for (int k = t; k < len; k += kFoldThreads) {
+            const tspgpu_city c = J.path[k];
+            px[k] = c.x, py[k] = c.y, pid[k] = c.id;
+        }
+    }
+    int status = 0, at = J.count - 1, nc = 1;
+    for (int m = J.k0; m < J.count - 1; ++m) {
+        if (len + M > kFoldCap) {
+            status = 2, at = m;
+            break;
+        }
+        // stage the block (cities and edge lengths, read straight from memory:
+        // one barrier, which also orders the previous splice's LDS writes)
+        const tspgpu_city *c2 = blocks + (size_t)(J.first + 1 + m) * L2;
+        if (t < L2) {
+            const tspgpu_city c = c2[t], d = c2[t + 1 == L2 ? 0 : t + 1];
+            cx[t] = c.x, cy[t] = c.y, cid[t] = c.id;
+            ce[t] = ddist(c.x, c.y, d.x, d.y);
+        }
+        __syncthreads();
+        // one pass: the two smallest order keys of every swap cost (i over path
+        // edges, j over block edges, pair index i * L2 + j = row-major order)
+        Top2 tp{~0ull, ~0ull, ~0u};
+        for (int i = t; i < len; i += kFoldThreads) {
+            const int i1 = i + 1 == len ? 0 : i + 1;
+            const double ax = px[i], ay = py[i], bx = px[i1], by = py[i1];
+            const double eab = ddist(ax, ay, bx, by);
+            for (int j = 0; j < L2; ++j) {
+                const int j1 = j + 1 == L2 ? 0 : j + 1;
+                const double sc = ((ddist(ax, ay, cx[j1], cy[j1]) + ddist(bx, by, cx[j], cy[j])) - eab) - ce[j];
+                top2_add(tp, order_key(sc), (unsigned)(i * L2 + j));
+            }
+        }
+#pragma unroll
+        for (int o = 1; o < 64; o *= 2) {
+            Top2 q;
+            q.k1 = shfl_u64(tp.k1, o);
+            q.k2 = shfl_u64(tp.k2, o);
+            q.i1 = (unsigned)__shfl_xor((int)tp.i1, o);
+            tp = top2_merge(tp, q);
+        }
+        if (__lane_id() == 0) wtop[t / 64] = tp;
+        __syncthreads();
+        Top2 g = wtop[0];
+#pragma unroll
+        for (int w = 1; w < kFoldThreads / 64; ++w) g = top2_merge(g, wtop[w]);
+        // exactly one pair within eps2 of the minimum (then it is the
+        // reference's pair, as in fold_pick_kernel), else the host decides
+        const double thr = key_value(g.k1) + eps2;
+        if (!(g.k2 == ~0ull || g.k2 > order_key(thr))) {
+            status = 1, at = m, nc = 2;
+            break;
+        }
+        const int pi = (int)(g.i1 / (unsigned)L2), pj = (int)(g.i1 % (unsigned)L2);
+        const int pi1 = pi + 1 == len ? 0 : pi + 1, pj1 = pj + 1 == L2 ? 0 : pj + 1;
+        if (t == 0) {
+            Cand k;
+            k.i = pi, k.j = pj;
+            k.a = tspgpu_city{pid[pi], px[pi], py[pi]};
+            k.b = tspgpu_city{pid[pi1], px[pi1], py[pi1]};
+            k.c = tspgpu_city{cid[pj], cx[pj], cy[pj]};
+            k.d = tspgpu_city{cid[pj1], cx[pj1], cy[pj1]};
+            J.picks[m].c = k;
+        }
+        // splice (tsp.cpp:240-259): p = first index of A or B in path 1 (0 when
+        // either is its first city: the path closes on it), C's first index in
+        // path 2 (0 for the closing copy); out = path[0..p] ++ reversed rotation
+        // of the block after C ++ path[p+1..]
+        const int first = pid[0];
+        const int p = (pid[pi] == first || pid[pi1] == first) ? 0 : pi;
+        const int sw = pj == L2 - 1 ? 0 : pj;
+        const int start = (sw + 1) % M;
+        // shift path[p+1 .. len) up by M: through registers (4 per thread at the cap)
+        constexpr int kPer = kFoldCap / kFoldThreads;
+        double sx[kPer], sy[kPer];
+        int sid[kPer];
+#pragma unroll
+        for (int q = 0; q < kPer; ++q) {
+            const int k = p + 1 + t + q * kFoldThreads;
+            if (k < len) sx[q] = px[k], sy[q] = py[k], sid[q] = pid[k];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < kPer; ++q) {
+            const int k = p + 1 + t + q * kFoldThreads;
+            if (k < len) px[k + M] = sx[q], py[k + M] = sy[q], pid[k + M] = sid[q];
+        }
+        if (t < M) {
+            const int k = p + 1 + t;
+            const int q = start + (M - 1 - t);
+            const int src = q >= M ? q - M : q;
+            px[k] = cx[src], py[k] = cy[src], pid[k] = cid[src];
+        }
+        len += M;
+    }
+    __syncthreads();
+    for (int k = t; k < len; k += kFoldThreads) J.path[k] = tspgpu_city{pid[k], px[k], py[k]};
+    if (t == 0) {
+        FoldOut o;
+        o.status = status, o.at = at, o.len = len, o.count = nc;
+        outs[blockIdx.x] = o;
+    }
+}
+
 // ---- host side ---------------------------------------------------------------
 
 double (*volatile g_pow)(double, double) = ::pow;
@@ -624,6 +820,168 @@ struct Merger {
     }
 };
 
+// mergeBlocks (tsp.cpp:202-269) on the host, exactly: glibc distances, first
+// strict minimum in row-major order from INT_MAX, then the splice; for a fold
+// merge that stalled the persistent kernel (several near-tied candidates).
+// -> the pick (for the cost fold) and the new path in `path`.
+int host_fold_merge(std::vector<tspgpu_city> &path, const tspgpu_city *c2, int L2, Cand &pick)
+{
+    const int L1 = (int)path.size(), M = L2 - 1;
+    double best = (double)INT_MAX;  // tsp.cpp:204
+    bool found = false;
+    for (int i = 0; i < L1; ++i)
+        for (int j = 0; j < L2; ++j) {
+            const tspgpu_city &a = path[i], &b = path[(i + 1) % L1], &c = c2[j], &d = c2[(j + 1) % L2];
+            const double sc = hswap(a, b, c, d);
+            if (sc < best) {
+                best = sc;
+                pick = Cand{i, j, a, b, c, d};
+                found = true;
+            }
+        }
+    if (!found) return -EIO;
+    // tsp.cpp:229-239: first index of A or B in path 1, of C in path 2 (without its closing copy)
+    int p = -1, sw = -1;
+    for (int k = 0; k < L1 && p < 0; ++k)
+        if (path[k].id == pick.a.id || path[k].id == pick.b.id) p = k;
+    for (int k = 0; k < M && sw < 0; ++k)
+        if (c2[k].id == pick.c.id) sw = k;
+    if (p < 0) return -EIO;
+    if (sw < 0) return -EDEADLK;
+    std::vector<tspgpu_city> out;
+    out.reserve((size_t)L1 + M);
+    const int start = (sw + 1) % M;
+    for (int k = 0; k <= p; ++k) out.push_back(path[k]);
+    for (int t = 0; t < M; ++t) {
+        const int q = start + (M - 1 - t);
+        out.push_back(c2[q >= M ? q - M : q]);
+    }
+    for (int k = p + 1; k < L1; ++k) out.push_back(path[k]);
+    path.swap(out);
+    return 0;
+}
+
+// The fold of every logical rank (tsp.cpp:348-352) by fold_persist_kernel.
+// Ranks that stall (several near-tied candidates) get the merge exactly on the
+// host and are relaunched from the next one; ranks whose path outgrows LDS
+// finish through the Merger's per-merge kernels.  rank[r] holds the path and
+// rcost[r] the cost on return (costs folded in merge order, tsp.cpp:263, with
+// glibc swap costs of the logged picks).
+int persist_folds(Merger &m, const tspgpu_city *blocks, int L, const double *costs, const std::vector<int> &cnt,
+                  std::vector<DVec> &rank, DVec &tmp, std::vector<double> &rcost)
+{
+    const int P = (int)cnt.size();
+    int nb = 0;
+    for (int c : cnt) nb += c;
+    const size_t ncity = (size_t)nb * L;
+    FoldJob *djobs = nullptr;
+    FoldOut *douts = nullptr;
+    Pick *dpicks = nullptr;
+    hipError_t e = hipMalloc((void **)&djobs, P * sizeof(FoldJob));
+    if (e == hipSuccess) e = hipMalloc((void **)&douts, P * sizeof(FoldOut));
+    if (e == hipSuccess) e = hipMalloc((void **)&dpicks, (size_t)std::max(nb, 1) * sizeof(Pick));
+    auto release = [&] {
+        if (djobs) (void)hipFree(djobs);
+        if (douts) (void)hipFree(douts);
+        if (dpicks) (void)hipFree(dpicks);
+    };
+    if (e != hipSuccess) {
+        release();
+        return herr(e);
+    }
+    std::vector<FoldJob> jobs(P);
+    std::vector<int> firstb(P), cap_at(P, -1);
+    std::vector<Pick> hpick((size_t)nb);
+    std::vector<char> host_picked((size_t)nb, 0);
+    int rc = 0;
+    for (int r = 0, b = 0; r < P && !rc; b += cnt[r], ++r) {
+        rc = rank[r].reserve(ncity, m.st);
+        firstb[r] = b;
+        jobs[r] = FoldJob{b, cnt[r], 0, 0, rank[r].p, dpicks + b};
+    }
+    std::vector<int> active(P);
+    for (int r = 0; r < P; ++r) active[r] = r;
+    std::vector<FoldOut> outs(P);
+    while (!rc && !active.empty()) {
+        std::vector<FoldJob> aj;
+        for (int r : active) aj.push_back(jobs[r]);
+        e = hipMemcpyAsync(djobs, aj.data(), aj.size() * sizeof(FoldJob), hipMemcpyHostToDevice, m.st);
+        if (e == hipSuccess)
+            hipLaunchKernelGGL(fold_persist_kernel, dim3((unsigned)aj.size()), dim3(kFoldThreads), 0, m.st, blocks, L,
+                               m.eps2, djobs, douts);
+        if (e == hipSuccess) e = hipGetLastError();
+        if (e == hipSuccess) e = hipMemcpyAsync(outs.data(), douts, aj.size() * sizeof(FoldOut), hipMemcpyDeviceToHost, m.st);
+        if (e == hipSuccess) e = hipStreamSynchronize(m.st);
+        if (e != hipSuccess) {
+            rc = herr(e);
+            break;
+        }
+        std::vector<int> again;
+        for (size_t q = 0; q < active.size() && !rc; ++q) {
+            const int r = active[q];
+            const FoldOut &o = outs[q];
+            rank[r].len = (size_t)o.len;
+            if (o.status == 0) continue;
+            if (o.status == 2) {  // the path outgrew LDS: the per-merge kernels take over at merge o.at
+                cap_at[r] = o.at;
+                continue;
+            }
+            // several candidates: merge o.at exactly on the host, then relaunch
+            std::vector<tspgpu_city> path((size_t)o.len), blk((size_t)L);
+            e = hipMemcpyAsync(path.data(), rank[r].p, path.size() * sizeof(tspgpu_city), hipMemcpyDeviceToHost, m.st);
+            if (e == hipSuccess)
+                e = hipMemcpyAsync(blk.data(), blocks + (size_t)(firstb[r] + 1 + o.at) * L, L * sizeof(tspgpu_city),
+                                   hipMemcpyDeviceToHost, m.st);
+            if (e == hipSuccess) e = hipStreamSynchronize(m.st);
+            if (e != hipSuccess) {
+                rc = herr(e);
+                break;
+            }
+            Cand pk{};
+            rc = host_fold_merge(path, blk.data(), L, pk);
+            if (rc) break;
+            hpick[(size_t)firstb[r] + o.at].c = pk;
+            host_picked[(size_t)firstb[r] + o.at] = 1;
+            e = hipMemcpyAsync(rank[r].p, path.data(), path.size() * sizeof(tspgpu_city), hipMemcpyHostToDevice, m.st);
+            if (e != hipSuccess) {
+                rc = herr(e);
+                break;
+            }
+            rank[r].len = path.size();
+            jobs[r].k0 = o.at + 1;
+            jobs[r].len = (int)path.size();
+            if (jobs[r].k0 < cnt[r] - 1) again.push_back(r);
+        }
+        active.swap(again);
+    }
+    if (!rc) {
+        // the logged picks -> exact costs in merge order (tsp.cpp:263)
+        std::vector<Pick> dp((size_t)nb);
+        e = hipMemcpyAsync(dp.data(), dpicks, dp.size() * sizeof(Pick), hipMemcpyDeviceToHost, m.st);
+        if (e == hipSuccess) e = hipStreamSynchronize(m.st);
+        rc = herr(e);
+        for (int r = 0; r < P && !rc; ++r) {
+            const int b0 = firstb[r];
+            rcost[r] = costs[b0];
+            const int done = cap_at[r] >= 0 ? cap_at[r] : cnt[r] - 1;
+            for (int k = 0; k < done; ++k) {
+                const size_t idx = (size_t)b0 + k;
+                const Cand &c = host_picked[idx] ? hpick[idx].c : dp[idx].c;
+                rcost[r] = (rcost[r] + costs[b0 + 1 + k]) + hswap(c.a, c.b, c.c, c.d);
+            }
+        }
+        // the rest of an outgrown rank through the per-merge kernels
+        for (int r = 0; r < P && !rc; ++r)
+            for (int k = cap_at[r]; k >= 0 && k < cnt[r] - 1 && !rc; ++k)
+                rc = m.merge(rank[r], tmp, &rcost[r], blocks + (size_t)(firstb[r] + 1 + k) * L, L,
+                             &costs[firstb[r] + 1 + k], true);
+    }
+    if (!rc) rc = m.sync();  // (the picks buffer is freed below: nothing in flight may use it)
+    (void)hipStreamSynchronize(m.st);
+    release();
+    return rc;
+}
+
 double bbox_diagonal(const tspgpu_city *c, size_t n)
 {
     double x0 = INFINITY, x1 = -INFINITY, y0 = INFINITY, y1 = -INFINITY;
@@ -725,7 +1083,13 @@ int tspgpu_reduce(tspgpu_ctx *ctx, const tspgpu_city *paths, int L, const double
     std::vector<double> rcost(nprocs, 0.0);
     if (!rc) rc = tmp.reserve(ncity, m.st);
     int next = 0;
-    for (int r = 0; r < nprocs && !rc; ++r) {
+    if (!rc && fold_ok && L <= kFoldL2 && tspgpu::tuned_or("K3_PERSIST", 1) != 0) {
+        // (tuning knob K3_PERSIST = 0: the per-merge launches instead; tests compare both)
+        // every rank's fold in one persistent launch (fold_persist_kernel)
+        rc = persist_folds(m, blocks.p, L, costs, cnt, rank, tmp, rcost);
+        next = nblocks;
+    }
+    for (int r = 0; r < nprocs && !rc && next < nblocks; ++r) {
         rc = rank[r].reserve(ncity, m.st);
         if (rc) break;
         rc = herr(hipMemcpyAsync(rank[r].p, blocks.p + (size_t)next * L, L * sizeof(tspgpu_city),

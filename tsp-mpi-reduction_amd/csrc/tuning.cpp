@@ -58,6 +58,8 @@ Knob g_knobs[] = {
     {"SEARCH_RECORD_CAP", false, 0},  // tests: force the second phase
     {"ENUM_KERNEL", false, 0},     // 0: enumeration through the round kernels
     {"ENUM_WG_PER_CU", false, 0},
+    // K3 (merge.hip)
+    {"K3_PERSIST", false, 0},      // 0: per-merge fold launches instead of the persistent per-rank fold
     // host heuristics (search_host.cpp)
     {"HEURISTIC_THREADS", false, 0},
     {"HEURISTIC_ALL_STARTS", false, 0},

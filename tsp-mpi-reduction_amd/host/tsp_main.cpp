@@ -73,8 +73,11 @@ int visible_devices()
 
 // Blocks [lo, lo + count) on `gpus` devices: contiguous ranges, one context +
 // thread each; device (first_dev + g) mod visible devices.
+// (keep: the context of device first_dev stays open and is returned, for the
+// merges that follow on it — a second context costs a HIP stream and device
+// queries; null: every context is destroyed)
 int solve_range(const std::vector<tspgpu_city> &cities, int n, int lo, int count, int gpus, int first_dev,
-                double *cost, int32_t *tour)
+                double *cost, int32_t *tour, tspgpu_ctx **keep = nullptr)
 {
     const int B = count;
     if (B <= 0) return 0;
@@ -95,7 +98,10 @@ int solve_range(const std::vector<tspgpu_city> &cities, int n, int lo, int count
             if (!rc)
                 rc = tspgpu_solve_cities(ctx, cities.data() + (size_t)(lo + a) * n, n, b - a, cost + a,
                                          tour + (size_t)a * (n + 1));
-            if (ctx) tspgpu_ctx_destroy(ctx);
+            if (ctx && g == 0 && keep && !rc)
+                *keep = ctx;
+            else if (ctx)
+                tspgpu_ctx_destroy(ctx);
             rcs[g] = rc;
         });
     }
@@ -321,6 +327,7 @@ int main(int argc, char **argv)
     std::vector<int32_t> tour((size_t)B * (n + 1), -1);
     int rc;
     timespec ts_solve0, ts_solve1, ts_merge1;
+    tspgpu_ctx *kept = nullptr;  // the block search's context on TSP_GPU, reused by the merges
     clock_gettime(CLOCK_MONOTONIC_RAW, &ts_solve0);
     if (multi) {
         // rank 0's own share here, the other ranks' shares from their files
@@ -329,7 +336,8 @@ int main(int argc, char **argv)
         for (int r = 1; r < P; ++r) off[r] = off[r - 1] + cnt[r - 1];
         const uint64_t key = job_key(n, B, X, Y);
         int failed = 0;
-        rc = solve_range(cities, n, 0, cnt[0], env_int("TSP_GPUS", 1), env_int("TSP_GPU", 0), cost.data(), tour.data());
+        rc = solve_range(cities, n, 0, cnt[0], env_int("TSP_GPUS", 1), env_int("TSP_GPU", 0), cost.data(), tour.data(),
+                         &kept);
         if (!rc) rc = read_rank_files(gather_dir(key), key, P, n, B, X, Y, cnt, off, cost.data(), tour.data(), &failed);
         if (rc && failed) {
             std::fflush(stdout);
@@ -337,7 +345,8 @@ int main(int argc, char **argv)
             return 3;
         }
     } else {
-        rc = solve_range(cities, n, 0, B, env_int("TSP_GPUS", 1), env_int("TSP_GPU", 0), cost.data(), tour.data());
+        rc = solve_range(cities, n, 0, B, env_int("TSP_GPUS", 1), env_int("TSP_GPU", 0), cost.data(), tour.data(),
+                         &kept);
     }
     if (rc) {
         std::fflush(stdout);
@@ -358,14 +367,17 @@ int main(int argc, char **argv)
     std::vector<char> log(1 << 20);
     int red = 0;
     if (env_int("TSP_HOST_MERGE", 0)) {
+        if (kept) tspgpu_ctx_destroy(kept);
+        kept = nullptr;
         red = tsphost_reduce(paths.data(), L, cost.data(), B, P, &final_cost, log.data(), (int)log.size()) ? -EDEADLK
                                                                                                           : 0;
     } else {
         tspgpu_opts o;
         std::memset(&o, 0, sizeof o);
         o.device = env_int("TSP_GPU", 0);
-        tspgpu_ctx *ctx = nullptr;
-        red = tspgpu_ctx_create(&o, &ctx);
+        tspgpu_ctx *ctx = kept;
+        kept = nullptr;
+        red = ctx ? 0 : tspgpu_ctx_create(&o, &ctx);
         if (!red) red = tspgpu_reduce(ctx, paths.data(), L, cost.data(), B, P, &final_cost, log.data(), (int)log.size());
         if (ctx) tspgpu_ctx_destroy(ctx);
     }
