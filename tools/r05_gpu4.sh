@@ -8,3 +8,8 @@ for so in tsp-mpi-reduction_amd/lib_ab/stamp*.so; do
 done
 cat gpurun_out/r05/stamp2.txt
 bash tools/r05_k3trace.sh
+for dl in default 0 1; do
+  if [ $dl = default ]; then ./tsp-mpi-reduction_amd/bin/init_probe2 > gpurun_out/r05/init_probe_$dl.txt 2>&1;
+  else HIP_ENABLE_DEFERRED_LOADING=$dl ./tsp-mpi-reduction_amd/bin/init_probe2 > gpurun_out/r05/init_probe_$dl.txt 2>&1; fi
+  echo "== deferred=$dl rc=$?"; cat gpurun_out/r05/init_probe_$dl.txt
+done

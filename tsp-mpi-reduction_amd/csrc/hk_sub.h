@@ -84,13 +84,14 @@ __host__ __device__ constexpr int sub_layer_off(int L, int j)
 // relaxations).  Needs layer 2 of the next sub-cube outside the region
 // (C(L,2) x 2 values) and the staged values (L rows x H).
 #ifndef TSPGPU_SUB_OVERLAP
-#define TSPGPU_SUB_OVERLAP 0
+#define TSPGPU_SUB_OVERLAP 2  // 2: with the edge passes' push values staged in LDS (-3% forward, profiles/r05)
 #endif
 __host__ __device__ constexpr int sub_l2_vals(int L) { return cbinom(L, 2) * 2; }
 __host__ __device__ constexpr size_t sub_lds_bytes(int N, int L, int vb)
 {
     return sub_img_bytes(N, L, vb) + (size_t)2 * 16 * vb + (size_t)sub_region_vals(L) * vb + (size_t)16 * vb +
-           (TSPGPU_SUB_OVERLAP ? (size_t)(sub_l2_vals(L) + L * (N - L)) * vb : 0);
+           (TSPGPU_SUB_OVERLAP ? (size_t)(sub_l2_vals(L) + L * (N - L)) * vb : 0) +
+           (TSPGPU_SUB_OVERLAP >= 2 ? (size_t)((L + 1) * (N - L) + (N - L)) * vb : 0);
 }
 
 template <typename V, int N, int L>
@@ -102,6 +103,9 @@ struct SubCtx {
     V *layer2;         // layer 2 (passes 0/1 write it, middle pass 2 reads it): the region's
                        // bottom, or its own area when the edge passes overlap (TSPGPU_SUB_OVERLAP)
     V *pst;            // pass L-1's push values staged in LDS (TSPGPU_SUB_OVERLAP): [row][i]
+    V *fst;            // passes 0/1's push values (TSPGPU_SUB_OVERLAP >= 2): [i] row 0, [H + a*H + i] row {a}
+    V *lst;            // pass L's push values (TSPGPU_SUB_OVERLAP >= 2): [i]
+    int ov;            // the overlap level this kernel runs (TSPGPU_SUB_OVERLAP; 0 below 256 threads)
     Rsrc<V> push;      // this block's push area
     Rsrc<uint64_t> par;  // this block's parent words
 };
@@ -439,6 +443,16 @@ __device__ __forceinline__ uint32_t sub_clock()
 {
     return (uint32_t)__builtin_amdgcn_s_memtime();
 }
+// Wave roles rotated (TSPGPU_SUB_ROT): the rows of a pass go to the threads
+// in wave order, so wave 0 of every workgroup works in every pass and wave 3
+// in three of seven; with the workgroups of a CU placing wave w on SIMD w, one
+// SIMD would carry all the heaviest waves.  1: the roles rotate by the
+// workgroup's index, 2: by workgroup and sub-cube (every wave gets every role
+// in turn).  Any bijection is valid: passes hand over only through LDS and
+// memory behind barriers.
+#ifndef TSPGPU_SUB_ROT
+#define TSPGPU_SUB_ROT 0
+#endif
 // one |h| dispatch per sub-cube around all middle passes (instead of one per pass)
 #ifndef TSPGPU_SUB_MIDSWITCH
 #define TSPGPU_SUB_MIDSWITCH 0
@@ -706,7 +720,8 @@ __device__ __forceinline__ void sub_first(const SubCtx<V, N, L> &c, uint32_t h, 
     const uint32_t nh = ~h & ((1u << H) - 1u);
     V g0[C > 0 ? C : 1];  // G[h][hm_i]: row 0 of sub-cube h (wave-uniform)
 #pragma unroll
-    for (int i = 0; i < C; ++i) g0[i] = c.push.load(0, sub_col<H>(h, hm[i]) * (uint32_t)(NL * VB));
+    for (int i = 0; i < C; ++i)
+        g0[i] = c.ov >= 2 ? c.fst[i] : c.push.load(0, sub_col<H>(h, hm[i]) * (uint32_t)(NL * VB));
     if (tid < (uint32_t)(L * Q1)) {
         const uint32_t a = tid / Q1, q = tid % Q1;
         const uint32_t kk = q < (uint32_t)(L - 1) ? q + (q >= a ? 1u : 0u) : L + nth_bit(nh, q - (L - 1));
@@ -723,7 +738,8 @@ __device__ __forceinline__ void sub_first(const SubCtx<V, N, L> &c, uint32_t h, 
         const uint32_t voff = (1u + a) * VB;  // row {a}: index 1 + a in the mask list
 #pragma unroll
         for (int i = 0; i < C; ++i) {
-            const V g1 = c.push.load(voff, sub_col<H>(h, hm[i]) * (uint32_t)(NL * VB));
+            const V g1 = c.ov >= 2 ? c.fst[H + a * H + i]
+                                                 : c.push.load(voff, sub_col<H>(h, hm[i]) * (uint32_t)(NL * VB));
             relax_min(acc, g1, lds_val<V>(c.img, (L + hm[i]) * DSB + kk * VB));
         }
         if (kk < (uint32_t)L) {
@@ -776,7 +792,7 @@ __device__ __forceinline__ void sub_last(const SubCtx<V, N, L> &c, uint32_t h, u
     for (int m = 0; m < L; ++m) relax_any<ARG>(m == 0, acc, arg, c.layerL[m], lds_val<V>(c.img, m * DSB + kk * VB), (uint32_t)m);
 #pragma unroll
     for (int i = 0; i < C; ++i) {
-        const V g = c.push.load((NL - 1) * VB, sub_col<H>(h, hm[i]) * (uint32_t)(NL * VB));
+        const V g = c.ov >= 2 ? c.lst[i] : c.push.load((NL - 1) * VB, sub_col<H>(h, hm[i]) * (uint32_t)(NL * VB));
         relax_any<ARG>(false, acc, arg, g, lds_val<V>(c.img, (L + hm[i]) * DSB + kk * VB), L + hm[i]);
     }
     if (act) c.push.store((NL - 1) * VB, sub_col<H>(h | (1u << x), x) * (uint32_t)(NL * VB), acc);
@@ -825,7 +841,7 @@ __device__ __forceinline__ void sub_penult(const SubCtx<V, N, L> &c, uint32_t h,
     }
 #pragma unroll
     for (int i = 0; i < C; ++i) {
-        const V g = TSPGPU_SUB_OVERLAP ? c.pst[r * H + i] : c.push.load(voff, sub_col<H>(h, hm[i]) * (uint32_t)(NL * VB));
+        const V g = c.ov ? c.pst[r * H + i] : c.push.load(voff, sub_col<H>(h, hm[i]) * (uint32_t)(NL * VB));
         relax_any<ARG>(false, acc, arg, g, lds_val<V>(c.img, (L + hm[i]) * DSB + kk * VB), L + hm[i]);
     }
     if (act) {
@@ -856,6 +872,33 @@ __device__ __forceinline__ void sub_stage_penult(const SubCtx<V, N, L> &c, uint3
         const uint32_t r = lane / C, i = lane % C;
         const uint32_t x = nth_bit(h, i);
         c.pst[r * H + i] = c.push.load((BASE + r) * VB, sub_col<H>(h, x) * (uint32_t)(NL * VB));
+    }
+}
+
+// Passes 0/1's push values of sub-cube h (|h| = C) into LDS (TSPGPU_SUB_OVERLAP
+// >= 2): lanes e < C row 0 of column (h, hm_e); lanes C + a*C + i row {a} of
+// column (h, hm_i), a < L.
+template <typename V, int N, int L, int C>
+__device__ __forceinline__ void sub_stage_first(const SubCtx<V, N, L> &c, uint32_t h, uint32_t lane)
+{
+    constexpr int H = N - L, NL = 1 << L, VB = sizeof(V);
+    if constexpr (C > 0) {
+        if (lane < (uint32_t)C) {
+            c.fst[lane] = c.push.load(0, sub_col<H>(h, nth_bit(h, lane)) * (uint32_t)(NL * VB));
+        } else if (lane < (uint32_t)(C + L * C)) {
+            const uint32_t e = lane - C, a = e / C, i = e % C;
+            c.fst[H + a * H + i] = c.push.load((1u + a) * VB, sub_col<H>(h, nth_bit(h, i)) * (uint32_t)(NL * VB));
+        }
+    }
+}
+// Pass L's push values of sub-cube h (|h| = C): lane i < C, row NL - 1 of column (h, hm_i).
+template <typename V, int N, int L, int C>
+__device__ __forceinline__ void sub_stage_last(const SubCtx<V, N, L> &c, uint32_t h, uint32_t lane)
+{
+    constexpr int H = N - L, NL = 1 << L, VB = sizeof(V);
+    if constexpr (C > 0 && C < H) {
+        if (lane < (uint32_t)C)
+            c.lst[lane] = c.push.load((NL - 1) * VB, sub_col<H>(h, nth_bit(h, lane)) * (uint32_t)(NL * VB));
     }
 }
 
@@ -936,6 +979,18 @@ __device__ __forceinline__ void sub_dispatch_stage(const SubCtx<V, N, L> &c, uin
     TSPGPU_SUB_SWITCH_C(hc, sub_stage_penult, c, h, lane)
 }
 template <typename V, int N, int L>
+__device__ __forceinline__ void sub_dispatch_stage_first(const SubCtx<V, N, L> &c, uint32_t h, int hc, uint32_t lane)
+{
+    constexpr int H = N - L;
+    TSPGPU_SUB_SWITCH_C(hc, sub_stage_first, c, h, lane)
+}
+template <typename V, int N, int L>
+__device__ __forceinline__ void sub_dispatch_stage_last(const SubCtx<V, N, L> &c, uint32_t h, int hc, uint32_t lane)
+{
+    constexpr int H = N - L;
+    TSPGPU_SUB_SWITCH_C(hc, sub_stage_last, c, h, lane)
+}
+template <typename V, int N, int L>
 __device__ __forceinline__ void sub_dispatch_last(const SubCtx<V, N, L> &c, uint32_t h, int hc, uint32_t lane)
 {
     constexpr int H = N - L;
@@ -977,6 +1032,7 @@ __global__ __launch_bounds__(THREADS, tiled_waves(THREADS, sub_wg(WG))) void hk_
     // their virtual lanes (pass 0/1 lanes 0..191, pass L 192..; pass L-1
     // lanes 0..127, the next sub-cube's image rows 128..) over the workgroup
     static_assert(THREADS % 64 == 0 && THREADS >= cbinom(L, L / 2), "one row per thread in a middle pass");
+    static_assert(!TSPGPU_SUB_ROT || (THREADS & (THREADS - 1)) == 0, "rotated roles: a power-of-two workgroup");
     static_assert(L * (N - 1) + H <= 192 && L * 8 <= 128, "edge intervals: virtual lane layout");
     // static LDS: image/region offsets fold into immediates (A/B against
     // dynamic LDS: equal within noise, profiles/r03/k1_ab_table.log)
@@ -988,8 +1044,13 @@ __global__ __launch_bounds__(THREADS, tiled_waves(THREADS, sub_wg(WG))) void hk_
     c.d0 = d0;
     c.region = dc + 16;
     c.layerL = c.region + sub_region_vals(L);
-    c.layer2 = TSPGPU_SUB_OVERLAP ? c.layerL + 16 : c.region + sub_layer_off(L, 2);
+    // (the overlapped edge passes need the idle waves of a 256-thread workgroup)
+    constexpr int OV = THREADS == 256 ? TSPGPU_SUB_OVERLAP : 0;
+    c.ov = OV;
+    c.layer2 = OV ? c.layerL + 16 : c.region + sub_layer_off(L, 2);
     c.pst = c.layerL + 16 + sub_l2_vals(L);
+    c.fst = c.pst + L * H;
+    c.lst = c.fst + (L + 1) * H;
     const uint32_t tid = threadIdx.x;
     const uint4 *rowtab = reinterpret_cast<const uint4 *>(rows);
 
@@ -1024,14 +1085,17 @@ __global__ __launch_bounds__(THREADS, tiled_waves(THREADS, sub_wg(WG))) void hk_
         for (uint32_t h = 0; h < (uint32_t)NH; ++h) {
             const int hc = __builtin_popcount(h);
             if (TSPGPU_SUB_STAMP) st_a = sub_clock();
+            // this sub-cube's thread -> role map (TSPGPU_SUB_ROT; whole waves)
+            const uint32_t rot = TSPGPU_SUB_ROT == 2 ? (uint32_t)blockIdx.x + h : (TSPGPU_SUB_ROT == 1 ? (uint32_t)blockIdx.x : 0u);
+            const uint32_t vtid = TSPGPU_SUB_ROT ? (tid + 64u * rot) & (uint32_t)(THREADS - 1) : tid;
             // interval A(h): passes 0/1 of h (lanes < 192) beside pass L of h - 1 (lanes 192..)
             // (TSPGPU_SUB_OVERLAP: at h = 0 only; later they run inside the middle passes)
-            uint32_t t = opaque_u32(tid);
+            uint32_t t = opaque_u32(vtid);
             {
                 constexpr int M2 = tiled_moff(L, 2), C2 = cbinom(L, 2);
                 ent = rowtab[M2 + (t < (uint32_t)C2 ? t : 0u)];
             }
-            if (!TSPGPU_SUB_OVERLAP || h == 0) {
+            if (!OV || h == 0) {
 #pragma unroll
                 for (uint32_t v0 = 0; v0 < 256u; v0 += THREADS) {  // (one iteration at 256 threads)
                     const uint32_t v = t + v0;
@@ -1058,7 +1122,7 @@ __global__ __launch_bounds__(THREADS, tiled_waves(THREADS, sub_wg(WG))) void hk_
                     static_for<L - 3>([&](auto jj) {
                         constexpr int j = 2 + decltype(jj)::value;
                         const uint4 cur = ent;
-                        const uint32_t tj = opaque_u32(tid);
+                        const uint32_t tj = opaque_u32(vtid);
                         if constexpr (j + 1 <= L - 2) {
                             constexpr int MN = tiled_moff(L, j + 1), CN = cbinom(L, j + 1);
                             ent = rowtab[MN + (tj < (uint32_t)CN ? tj : 0u)];
@@ -1081,20 +1145,40 @@ __global__ __launch_bounds__(THREADS, tiled_waves(THREADS, sub_wg(WG))) void hk_
                 static_for<L - 3>([&](auto jj) {
                     constexpr int j = 2 + decltype(jj)::value;
                     const uint4 cur = ent;
-                    const uint32_t tj = opaque_u32(tid);
+                    const uint32_t tj = opaque_u32(vtid);
                     if constexpr (j + 1 <= L - 2) {
                         constexpr int MN = tiled_moff(L, j + 1), CN = cbinom(L, j + 1);
                         ent = rowtab[MN + (tj < (uint32_t)CN ? tj : 0u)];
                     }
                     sub_dispatch_mid_j<V, N, L, j>(c, h, hc, tj, cur, pend, pre);
-                    if constexpr (TSPGPU_SUB_OVERLAP) {
+                    if constexpr (OV) {
                         // edge passes on the waves this middle pass leaves idle
-                        static_assert(cbinom(L, 2) <= 64 && cbinom(L, L - 3) <= 128, "overlap: idle waves");
-                        if constexpr (j == 2) {  // pass L of h - 1 (its layerL is still in LDS)
-                            if (h > 0 && tj >= 64u) sub_dispatch_last<V, N, L>(c, h - 1, __builtin_popcount(h - 1), tj - 64u);
-                        }
-                        if constexpr (j == L - 3) {  // pass L - 1's push values into LDS
-                            if (tj >= 128u) sub_dispatch_stage<V, N, L>(c, h, hc, tj - 128u);
+                        static_assert(cbinom(L, 2) <= 64 && cbinom(L, 3) <= 128 && cbinom(L, L - 3) <= 128, "overlap: idle waves");
+                        if constexpr (OV >= 2) {
+                            // pass 2: the edge passes' push values into LDS (waves 1-3);
+                            // pass 3: pass L of h - 1 from them (wave 3)
+                            if constexpr (j == 2) {
+                                if (tj >= 192u) {
+                                    if (h + 1 < (uint32_t)NH)
+                                        sub_dispatch_stage_first<V, N, L>(c, h + 1, __builtin_popcount(h + 1), tj - 192u);
+                                } else if (tj >= 128u) {
+                                    sub_dispatch_stage<V, N, L>(c, h, hc, tj - 128u);
+                                } else if (tj >= 64u && h > 0) {
+                                    sub_dispatch_stage_last<V, N, L>(c, h - 1, __builtin_popcount(h - 1), tj - 64u);
+                                }
+                            }
+                            if constexpr (j == 3) {
+                                if (h > 0 && tj >= 192u)
+                                    sub_dispatch_last<V, N, L>(c, h - 1, __builtin_popcount(h - 1), tj - 192u);
+                            }
+                        } else {
+                            if constexpr (j == 2) {  // pass L of h - 1 (its layerL is still in LDS)
+                                if (h > 0 && tj >= 64u)
+                                    sub_dispatch_last<V, N, L>(c, h - 1, __builtin_popcount(h - 1), tj - 64u);
+                            }
+                            if constexpr (j == L - 3) {  // pass L - 1's push values into LDS
+                                if (tj >= 128u) sub_dispatch_stage<V, N, L>(c, h, hc, tj - 128u);
+                            }
                         }
                         if constexpr (j == L - 2) {  // passes 0/1 of h + 1 (layer 2 in its own area)
                             if (h + 1 < (uint32_t)NH && tj >= 64u)
@@ -1114,7 +1198,7 @@ __global__ __launch_bounds__(THREADS, tiled_waves(THREADS, sub_wg(WG))) void hk_
                 });
             }
             // pass L - 1 (lanes < 128) beside the next sub-cube's high image rows/columns (lanes 128..)
-            t = opaque_u32(tid);
+            t = opaque_u32(vtid);
 #pragma unroll
             for (uint32_t v0 = 0; v0 < 256u; v0 += THREADS) {
                 const uint32_t v = t + v0;

@@ -93,9 +93,9 @@ __host__ __device__ __forceinline__ double key_value(unsigned long long k)
 struct Stage {
     double x[kChunk + 1], y[kChunk + 1], e[kChunk];
 };
-__device__ __forceinline__ int stage_chunk(Stage &sm, const tspgpu_city *c2, int L2, int j0)
+__device__ __forceinline__ int stage_chunk(Stage &sm, const tspgpu_city *c2, int L2, int j0, int cw = kChunk)
 {
-    const int J = min(kChunk, L2 - j0);
+    const int J = min(cw, L2 - j0);
     for (int t = threadIdx.x; t <= J; t += kMergeThreads) {
         const int j = j0 + t;
         const tspgpu_city c = c2[j < L2 ? j : j - L2];
@@ -125,7 +125,7 @@ __device__ __forceinline__ void sweep_row(const Stage &sm, int J, const tspgpu_c
 // Pass 1: min swap key over all L1 x L2 pairs; blockIdx.y = path-2 chunk.
 // Also resets this merge's first-occurrence words for find_kernel.
 __global__ __launch_bounds__(kMergeThreads) void argmin_kernel(const tspgpu_city *c1, int L1, const tspgpu_city *c2,
-                                                               int L2, Ctl *ctl, unsigned long long *blockmin)
+                                                               int L2, int cw, Ctl *ctl, unsigned long long *blockmin)
 {
     if (ctl->stall) return;
     __shared__ Stage sm;
@@ -135,8 +135,8 @@ __global__ __launch_bounds__(kMergeThreads) void argmin_kernel(const tspgpu_city
         ctl->fw[1] = ~0ull;
     }
     unsigned long long best = ~0ull;
-    for (int j0 = blockIdx.y * kChunk; j0 < L2; j0 += gridDim.y * kChunk) {
-        const int J = stage_chunk(sm, c2, L2, j0);
+    for (int j0 = blockIdx.y * cw; j0 < L2; j0 += gridDim.y * cw) {
+        const int J = stage_chunk(sm, c2, L2, j0, cw);
         for (int i = blockIdx.x * kMergeThreads + threadIdx.x; i < L1; i += gridDim.x * kMergeThreads)
             sweep_row(sm, J, c1, L1, i, [&](int, double sc) {
                 const unsigned long long k = order_key(sc);
@@ -249,15 +249,15 @@ __global__ __launch_bounds__(kMergeThreads) void fold_pick_kernel(const tspgpu_c
 // Pass 2: every pair within eps2 of the minimum is a candidate (only blocks
 // whose own minimum is that close rescan; the others return at once).
 __global__ __launch_bounds__(kMergeThreads) void cand_kernel(const tspgpu_city *c1, int L1, const tspgpu_city *c2,
-                                                             int L2, double eps2, Ctl *ctl,
+                                                             int L2, int cw, double eps2, Ctl *ctl,
                                                              const unsigned long long *blockmin, Cand *cand)
 {
     if (ctl->stall) return;
     __shared__ Stage sm;
     const double thr = key_value(ctl->minkey) + eps2;
     if (!(key_value(blockmin[blockIdx.y * gridDim.x + blockIdx.x]) <= thr)) return;
-    for (int j0 = blockIdx.y * kChunk; j0 < L2; j0 += gridDim.y * kChunk) {
-        const int J = stage_chunk(sm, c2, L2, j0);
+    for (int j0 = blockIdx.y * cw; j0 < L2; j0 += gridDim.y * cw) {
+        const int J = stage_chunk(sm, c2, L2, j0, cw);
         for (int i = blockIdx.x * kMergeThreads + threadIdx.x; i < L1; i += gridDim.x * kMergeThreads)
             sweep_row(sm, J, c1, L1, i, [&](int t, double sc) {
                 if (sc <= thr) {
@@ -671,12 +671,19 @@ struct Merger {
         const unsigned long long b = (work + kMergeThreads - 1) / kMergeThreads;
         return (int)std::max<unsigned long long>(1, std::min<unsigned long long>(b, (unsigned long long)cus * 8));
     }
-    // blockIdx.x strides path-1 edges, blockIdx.y path-2 chunks; gx * gy <= kMaxBlocks
-    dim3 pair_grid(int L1, int L2) const
+    // blockIdx.x strides path-1 edges, blockIdx.y path-2 chunks of *cw cities;
+    // gx * gy <= kMaxBlocks.  The chunks narrow (down to 8 cities) until the
+    // grid has about two blocks per CU: a tree merge of two ~1000-city paths
+    // was 4 blocks on 4 CUs (argmin + candidates ~380 us, profiles/r05)
+    dim3 pair_grid(int L1, int L2, int *cw) const
     {
         const int cap = std::min(cus * 8, kMaxBlocks);
-        const int gy = std::min((L2 + kChunk - 1) / kChunk, cap);
-        const int gx = std::max(1, std::min((L1 + kMergeThreads - 1) / kMergeThreads, cap / gy));
+        const int gx0 = std::max(1, std::min((L1 + kMergeThreads - 1) / kMergeThreads, cap));
+        int w = kChunk;
+        while (w > 8 && (long long)gx0 * ((L2 + w - 1) / w) < 2LL * cus) w /= 2;
+        const int gy = std::min((L2 + w - 1) / w, cap);
+        const int gx = std::max(1, std::min(gx0, cap / gy));
+        *cw = w;
         return dim3(gx, gy);
     }
     void enqueue(const Op &o, int idx)
@@ -690,9 +697,10 @@ struct Merger {
                                dim3(kMergeThreads), 0, st, o.src, o.L1, o.c2, M, ctl, o.dst, idx, 0);
             return;
         }
-        const dim3 g = pair_grid(o.L1, o.L2);
-        hipLaunchKernelGGL(argmin_kernel, g, dim3(kMergeThreads), 0, st, o.src, o.L1, o.c2, o.L2, ctl, blockmin);
-        hipLaunchKernelGGL(cand_kernel, g, dim3(kMergeThreads), 0, st, o.src, o.L1, o.c2, o.L2, eps2, ctl, blockmin,
+        int cw = kChunk;
+        const dim3 g = pair_grid(o.L1, o.L2, &cw);
+        hipLaunchKernelGGL(argmin_kernel, g, dim3(kMergeThreads), 0, st, o.src, o.L1, o.c2, o.L2, cw, ctl, blockmin);
+        hipLaunchKernelGGL(cand_kernel, g, dim3(kMergeThreads), 0, st, o.src, o.L1, o.c2, o.L2, cw, eps2, ctl, blockmin,
                            cand);
         hipLaunchKernelGGL(find_kernel, dim3(grid_for((unsigned long long)std::max(o.L1, M))), dim3(kMergeThreads), 0,
                            st, o.src, o.L1, o.c2, M, ctl, cand, picks, idx, 0, 0, 0, 0);
