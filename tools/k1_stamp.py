@@ -23,13 +23,16 @@ dd, dc, dt = ctx.upload(d), ctx.alloc(B * 8), ctx.alloc(B * (n + 1) * 4)
 for _ in range(3):
     ctx.solve_device(dd, n, B, dc, dt, ctx.stream)
 ctx.synchronize()
-t = ctx.download(dt, (B, n + 1), np.int32)[:, :16].astype(np.uint32).astype(np.float64).reshape(B, 4, 4)
+raw = ctx.download(dt, (B, n + 1), np.int32)
+t = raw[:, :16].astype(np.uint32).astype(np.float64).reshape(B, 4, 4)
+rt = raw[:, 16].astype(np.uint32).astype(np.float64)
 body, bar, edge, tot = (t[:, :, k] for k in range(4))
 out = {"lib": os.path.basename(os.environ.get("TSPGPU_LIB", "libtspgpu.so")), "B": B,
        "median_cycles_per_block_wave": {"body": float(np.median(body)), "barrier": float(np.median(bar)),
                                         "edge": float(np.median(edge)), "total": float(np.median(tot))},
        "frac_of_total": {"body": float(np.median(body / tot)), "barrier": float(np.median(bar / tot)),
                          "edge": float(np.median(edge / tot))},
+       "in_kernel_clock_ghz": float(np.median(tot[:, 0] / rt) * 0.1),
        "per_wave_body_median": [float(np.median(body[:, w])) for w in range(4)],
        "per_wave_barrier_median": [float(np.median(bar[:, w])) for w in range(4)]}
 print(json.dumps(out))

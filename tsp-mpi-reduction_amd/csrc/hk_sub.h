@@ -106,6 +106,7 @@ struct SubCtx {
     V *fst;            // passes 0/1's push values (TSPGPU_SUB_OVERLAP >= 2): [i] row 0, [H + a*H + i] row {a}
     V *lst;            // pass L's push values (TSPGPU_SUB_OVERLAP >= 2): [i]
     int ov;            // the overlap level this kernel runs (TSPGPU_SUB_OVERLAP; 0 below 256 threads)
+    const V *dg;       // this block's distance matrix in global memory (n x n; TSPGPU_SUB_SHH)
     Rsrc<V> push;      // this block's push area
     Rsrc<uint64_t> par;  // this block's parent words
 };
@@ -350,7 +351,8 @@ __host__ __device__ constexpr int sub_lds_role(int k)
 // stores in the middle passes, 16 = the sub-cube barriers wait for LDS only,
 // 32 = the middle passes' push loads all read one L2-resident row (the loads
 // stay, their memory traffic goes), 64 = the middle passes' push stores all
-// write one L2-resident row (likewise)
+// write one L2-resident row (likewise), 128 = both, for the lowest high city's
+// columns only (a fifth of the traffic)
 #ifndef TSPGPU_SUB_ABL
 #define TSPGPU_SUB_ABL 0
 #endif
@@ -453,6 +455,9 @@ __device__ __forceinline__ uint32_t sub_clock()
 #ifndef TSPGPU_SUB_ROT
 #define TSPGPU_SUB_ROT 0
 #endif
+#ifndef TSPGPU_SUB_SHH
+#define TSPGPU_SUB_SHH 0
+#endif
 // one |h| dispatch per sub-cube around all middle passes (instead of one per pass)
 #ifndef TSPGPU_SUB_MIDSWITCH
 #define TSPGPU_SUB_MIDSWITCH 0
@@ -494,12 +499,16 @@ __device__ __forceinline__ void sub_mid(const SubCtx<V, N, L> &c, uint32_t h, ui
             nb &= nb - 1u;
         }
     }
-    // high-high distances of this sub-cube: wave-uniform
+    // high-high distances of this sub-cube: wave-uniform (TSPGPU_SUB_SHH:
+    // scalar loads from the block's matrix in memory, no LDS read and no
+    // v_readfirstlane; else from the LDS image)
     V hh[HC * QH > 0 ? HC * QH : 1];
 #pragma unroll
     for (int i = 0; i < HC; ++i)
 #pragma unroll
-        for (int u = 0; u < QH; ++u) hh[i * QH + u] = uniform_val<V>(c.img, HR0 + i * DSB + HC0 + u * VB);
+        for (int u = 0; u < QH; ++u)
+            hh[i * QH + u] = TSPGPU_SUB_SHH ? c.dg[(L + 1 + hm[i]) * (N + 1) + (L + 1 + hn[u])]
+                                            : uniform_val<V>(c.img, HR0 + i * DSB + HC0 + u * VB);
     const uint32_t r = tid;
     const bool act = r < (uint32_t)ROWS;
     V g[T];
@@ -518,6 +527,7 @@ __device__ __forceinline__ void sub_mid(const SubCtx<V, N, L> &c, uint32_t h, ui
         for (int i = 0; i < HC; ++i)
             g[J + i] = (TSPGPU_SUB_ABL & 1)    ? c.region[CUR + (i % J) * ROWS + r]
                        : (TSPGPU_SUB_ABL & 32) ? c.push.load(r * VB, 0)
+                       : ((TSPGPU_SUB_ABL & 128) && hm[i] == 0) ? c.push.load(r * VB, 0)
                        : PRE_IN                ? pre[i]
                                                : c.push.load(voff, sub_col<H>(h, hm[i]) * (uint32_t)(NL * VB));
     }
@@ -671,7 +681,7 @@ __device__ __forceinline__ void sub_mid(const SubCtx<V, N, L> &c, uint32_t h, ui
             } else {
                 // high k -> push column (h | k, k) of sub-cube h | k, same row index
                 const uint32_t cb = hn[q - QL];
-                if (TSPGPU_SUB_ABL & 64)
+                if ((TSPGPU_SUB_ABL & 64) || ((TSPGPU_SUB_ABL & 128) && cb == 0))
                     c.push.store(r * VB, 8192u, acc[qq]);
                 else if (DEFER_OUT)
                     pend[q - QL] = acc[qq];  // (stored by the next pass, after its loads)
@@ -1059,6 +1069,7 @@ __global__ __launch_bounds__(THREADS, tiled_waves(THREADS, sub_wg(WG))) void hk_
         c.push.rs = uniform_rsrc(slot, (uint32_t)tiled_push_bytes(N, L, VB));
         c.par.rs = uniform_rsrc(slot + tiled_push_bytes(N, L, VB), (uint32_t)tiled_parent_bytes(N, L));
         const V *dsrc = dist + (size_t)blk * n * n;
+        c.dg = dsrc;
         // natural image (inner distances) and, for sub-cube 0 (no high
         // member), the high columns in order
         for (int i = tid; i < N * N; i += THREADS) {
@@ -1081,7 +1092,11 @@ __global__ __launch_bounds__(THREADS, tiled_waves(THREADS, sub_wg(WG))) void hk_
 #pragma unroll
         for (int u = 0; u < kSubPend; ++u) pend[u] = pre[u] = V(0);
         uint32_t st_body = 0, st_bar = 0, st_edge = 0, st_t0 = 0, st_a = 0;
-        if (TSPGPU_SUB_STAMP) st_t0 = sub_clock();
+        uint64_t st_rt0 = 0;
+        if (TSPGPU_SUB_STAMP) {
+            st_t0 = sub_clock();
+            st_rt0 = __builtin_amdgcn_s_memrealtime();
+        }
         for (uint32_t h = 0; h < (uint32_t)NH; ++h) {
             const int hc = __builtin_popcount(h);
             if (TSPGPU_SUB_STAMP) st_a = sub_clock();
@@ -1212,10 +1227,12 @@ __global__ __launch_bounds__(THREADS, tiled_waves(THREADS, sub_wg(WG))) void hk_
         }
         if (TSPGPU_SUB_STAMP) {
             const uint32_t tot = sub_clock() - st_t0;
+            const uint64_t rt = __builtin_amdgcn_s_memrealtime() - st_rt0;  // 100 MHz constant clock
             if ((tid & 63u) == 0) {
                 int32_t *w = tour_out + (size_t)blk * (n + 1) + 4 * (tid >> 6);
                 w[0] = (int32_t)st_body, w[1] = (int32_t)st_bar, w[2] = (int32_t)st_edge, w[3] = (int32_t)tot;
             }
+            if (tid == 0) tour_out[(size_t)blk * (n + 1) + 16] = (int32_t)rt;  // (in-kernel clock = tot / rt x 100 MHz)
             __syncthreads();
             continue;
         }
