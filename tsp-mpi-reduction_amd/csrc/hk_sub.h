@@ -1401,6 +1401,248 @@ __global__ __launch_bounds__(64 * kSubBtWaves) void hk_sub_backtrack(int nblocks
         wave_sync();  // dr is reloaded for the next block
     }
 }
+
+// ---------------------------------------------------------------------------
+// Backtracking of variant 6, workgroup form (TSPGPU_SUB_BT = 1).
+// The walk is hk_sub_backtrack's — (1) parent words while the set has
+// >= N - TSPGPU_TILED_TA_OFF members, (2) the prefix set T0 (K = N - 5 cities)
+// solved by its own Held-Karp, then the first strict minimum over T0's
+// members ascending (tsp.cpp:457-470) — but laid out for latency:
+//   * (1) runs one LANE per block, for every block the workgroup owns, before
+//     any prefix DP (its four dependent parent-word loads are paid once per
+//     workgroup, not once per block);
+//   * (2) runs the whole workgroup on one block with the table in LDS, compact
+//     (row M keeps its |M| member values: K * 2^(K-1) values, 40 KB at f64
+//     K = 10), one barrier per layer.  Thread t owns destination kk = t / TPK
+//     for the whole DP, so the K distances into kk sit in registers.
+// Round 4's hk_tiled_backtrack recomputed whole sub-cube rows from the pushes
+// through the slot's global recompute area, one wave per block (a chain of
+// global round trips per layer: 1.75 ms per 65536 16-city blocks, 6.7% of the
+// step).  Values are the forward pass's bits (same candidates, IEEE min is
+// order-free), ties as the reference's.
+// ---------------------------------------------------------------------------
+#ifndef TSPGPU_SUB_BT
+#define TSPGPU_SUB_BT 0  // (measured no faster than hk_tiled_backtrack yet: off)
+#endif
+#ifndef TSPGPU_SUB_BT_ABL
+#define TSPGPU_SUB_BT_ABL 0  // timing ablations (results wrong): 1 no prefix DP, 2 no walk, 4 no DP barriers, 8 no input loads
+#endif
+constexpr int kSubBtThreads = 256;
+// workgroups per CU: the LDS table decides (f64 K = 10: 46 KB)
+__host__ __device__ constexpr int sub_bt_wg(int vb) { return vb == 8 ? 3 : 6; }
+
+// one layer J of the prefix DP: thread (kk, sub) computes G[P | kk][kk] for the
+// (J-1)-subsets P of T0 \ {kk} numbered sub, sub + TPK, ...  (all items of a
+// thread unrolled: the table lookups of every item issue before the first row
+// read, so a layer costs a few LDS round trips, not one per item).  Layer j is
+// stored member-major: G[M][m] at layer_off(K, j) + (m's place in M) x C(K, j)
+// + colex rank of M, so lanes reading neighbouring rows hit neighbouring banks.
+template <typename V, int K, int J, int TPK>
+__device__ __forceinline__ void sub_bt_layer(V *g, const uint16_t *sub9, const uint16_t *rk, const V (&dcol)[K],
+                                             int kk, int sub)
+{
+    constexpr int CNT = cbinom(K - 1, J - 1), IT = (CNT + TPK - 1) / TPK;
+    constexpr int BOFF = mask_off(K - 1, J - 1);  // first (J-1)-subset in sub9
+    constexpr int RIN = layer_off(K, J - 1), CIN = cbinom(K, J - 1);
+    constexpr int ROUT = layer_off(K, J), COUT = cbinom(K, J);
+    const uint32_t below = (1u << kk) - 1u;
+    uint32_t P[IT];
+    int ro[IT], wo[IT];
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+        const int p = sub + it * TPK;
+        const uint32_t p9 = p < CNT ? sub9[BOFF + p] : 0u;
+        P[it] = (p9 & below) | ((p9 & ~below) << 1);  // kk's bit left out
+    }
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+        const uint32_t M = P[it] | (1u << kk);
+        ro[it] = RIN + rk[P[it]];
+        wo[it] = ROUT + __builtin_popcount(M & below) * COUT + rk[M];
+    }
+    // branch-free: every lane loads K values, so an item's loads issue back to
+    // back and wait once (an exec-masked load per member waits once per member)
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+        V v[K];
+#pragma unroll
+        for (int m = 0; m < K; ++m)  // (a non-member reads g[0]: one broadcast address, no extra bank traffic)
+            v[m] = g[((P[it] >> m) & 1u) ? ro[it] + __builtin_popcount(P[it] & ((1u << m) - 1u)) * CIN : 0];
+        V acc = ValT<V>::inf;
+#pragma unroll
+        for (int m = 0; m < K; ++m) acc = ValT<V>::vmin(acc, ((P[it] >> m) & 1u) ? v[m] + dcol[m] : ValT<V>::inf);
+        if (sub + it * TPK < CNT) g[wo[it]] = acc;
+    }
+}
+template <typename V, int K, int J, int TPK>
+__device__ __forceinline__ void sub_bt_layers(V *g, const uint16_t *sub9, const uint16_t *rk, const V (&dcol)[K],
+                                              int kk, int sub)
+{
+    if constexpr (J <= K) {
+        if (kk < K) sub_bt_layer<V, K, J, TPK>(g, sub9, rk, dcol, kk, sub);
+        if (!(TSPGPU_SUB_BT_ABL & 4)) __syncthreads();
+        sub_bt_layers<V, K, J + 1, TPK>(g, sub9, rk, dcol, kk, sub);
+    }
+}
+
+template <typename V, int N, int L>
+__global__ __launch_bounds__(kSubBtThreads) void hk_sub_bt_wg(int nblocks, int blk0, const char *__restrict__ slots,
+                                                              uint32_t slot_bytes, const TiledInfo *__restrict__ info,
+                                                              const V *__restrict__ dist, V *__restrict__ cost_out,
+                                                              int32_t *__restrict__ tour_out)
+{
+    constexpr int NL = 1 << L, n = N + 1, VB = sizeof(V), K = sub_bt_k(N), NK = 1 << K;
+    constexpr int T = kSubBtThreads, TPK = T / K, DLV = K * K + K;
+    static_assert(K >= 2 && K <= 10 && DLV + K <= T, "prefix DP size");
+    __shared__ V g[K << (K - 1)];          // layer j member-major (sub_bt_layer)
+    __shared__ V dl[DLV];                  // d[city m][city kk] at m * K + kk; d[city m][k0] at K * K + m
+    __shared__ uint16_t rk[NK];            // colex rank of a subset among the subsets of its size
+    __shared__ int lo[K + 1], cn[K + 1];   // layer_off(K, j), C(K, j)
+    __shared__ uint16_t sub9[NK / 2];      // (K-1)-bit subsets by size, then colex rank
+    __shared__ uint16_t wT0[T];            // (1)'s result per owned block: T0, k0 (-1: nothing left)
+    __shared__ int8_t wk0[T];
+    __shared__ int8_t city[K];
+    const uint32_t tid = threadIdx.x;
+
+    __shared__ uint16_t bn[K + 1][K + 1];  // binomials (setup only)
+    if (tid == 0)
+        for (int a = 0; a <= K; ++a)
+            for (int b = 0; b <= K; ++b) bn[a][b] = b == 0 ? 1 : (a == 0 ? 0 : bn[a - 1][b - 1] + bn[a - 1][b]);
+    __syncthreads();
+    for (uint32_t M = tid; M < (uint32_t)NK; M += T) {
+        int r = 0, i = 0;
+        for (int b = 0; b < K; ++b)
+            if ((M >> b) & 1u) r += bn[b][++i];
+        const int j = __builtin_popcount(M);
+        int lof = 0, mo = 0;  // layer_off(K, j), mask_off(K - 1, j)
+        for (int u = 0; u < j; ++u) {
+            lof += bn[K][u] * u;
+            mo += bn[K - 1][u];
+        }
+        rk[M] = (uint16_t)r;
+        if (M < (uint32_t)NK / 2) sub9[mo + r] = (uint16_t)M;
+        if (M == (1u << j) - 1u) {  // one thread per layer
+            lo[j] = lof;
+            cn[j] = bn[K][j];
+        }
+    }
+
+    const int kk = (int)tid / TPK, sub = (int)tid % TPK;  // this thread's destination (kk >= K: idle in the DP)
+    for (int base = blk0 + (int)blockIdx.x; base < nblocks; base += T * (int)gridDim.x) {
+        // (1) parent words, one lane per block
+        {
+            const int blk = base + (int)tid * (int)gridDim.x;
+            uint32_t T0 = 0;
+            int k0 = -1;
+            if (blk < nblocks) {
+                int32_t *tour = tour_out + (size_t)blk * (n + 1);
+                const int bestM = tour[n - 1];
+                if (bestM >= 1) {
+                    const uint64_t *pw = reinterpret_cast<const uint64_t *>(slots + (size_t)(blk - blk0) * slot_bytes +
+                                                                            tiled_push_bytes(N, L, VB));
+                    uint32_t S = (1u << N) - 1u;
+                    int k = bestM - 1, pos = n - 2;
+                    bool ok = bestM <= N;
+                    for (; ok && pos >= 1 && __builtin_popcount(S) - 1 >= N - TSPGPU_TILED_TA_OFF; --pos) {
+                        const uint32_t Tm = S & ~(1u << k);
+                        const uint32_t hT = Tm >> L, lT = Tm & (uint32_t)(NL - 1);
+                        const uint32_t idx = (uint32_t)info->moff[__builtin_popcount(lT)] + info->rank[lT];
+                        const uint64_t w = pw[(size_t)hT * NL + idx];
+                        const int q = k - __builtin_popcount(Tm & ((1u << k) - 1u));  // k's place among the non-members
+                        const int pm = (int)((w >> (4 * q)) & 15u);
+                        ok = pm < N && ((Tm >> pm) & 1u);
+                        tour[pos] = ok ? pm + 1 : 0;
+                        S = Tm;
+                        k = pm;
+                    }
+                    if (ok && pos >= 1) {
+                        T0 = S & ~(1u << k);
+                        ok = pos == K && __builtin_popcount(T0) == K;
+                        k0 = k;
+                    }
+                    if (!ok) {
+                        cost_out[blk] = V(-1);
+                        k0 = -1;
+                    }
+                }
+            }
+            wT0[tid] = (uint16_t)T0;
+            wk0[tid] = (int8_t)k0;
+        }
+        __syncthreads();
+        const int owned = (nblocks - base + (int)gridDim.x - 1) / (int)gridDim.x;
+        const int cntw = owned < T ? owned : T;
+        // this thread's staged input of owned block i: a distance of dl, or
+        // (K*K+K <= tid < K*K+2K) layer 1's G[{m}][m] = d[0][city m] (tsp.cpp:435)
+        auto stage = [&](int i, int *cm) -> V {
+            *cm = 0;
+            if ((TSPGPU_SUB_BT_ABL & 8) || i >= cntw || wk0[i] < 0 || tid >= (uint32_t)(DLV + K)) return V(0);
+            const uint32_t T0 = wT0[i];
+            const int k0 = wk0[i];
+            auto nth = [T0](int m) {  // the m-th member of T0 ascending
+                uint32_t b = T0;
+                for (int r = 0; r < m; ++r) b &= b - 1u;
+                return __builtin_ctz(b);
+            };
+            const V *dsrc = dist + (size_t)(base + i * (int)gridDim.x) * n * n;
+            if (tid < (uint32_t)(K * K)) return dsrc[(nth((int)tid / K) + 1) * n + nth((int)tid % K) + 1];
+            if (tid < (uint32_t)DLV) return dsrc[(nth((int)tid - K * K) + 1) * n + k0 + 1];
+            *cm = nth((int)tid - DLV);
+            return dsrc[*cm + 1];
+        };
+        auto place = [&](V v, int cm) {
+            if (tid < (uint32_t)DLV) {
+                dl[tid] = v;
+            } else if (tid < (uint32_t)(DLV + K)) {
+                g[tid - DLV] = v;  // G[{m}][m] at layer_off(K, 1) + rank m
+                city[tid - DLV] = (int8_t)cm;
+            }
+        };
+        int cm = 0;
+        V pf = stage(0, &cm);
+        place(pf, cm);
+        __syncthreads();
+        // (2) one block at a time: prefix DP over T0, then the walk; the next
+        // block's inputs are loaded meanwhile
+        for (int i = 0; i < cntw; ++i) {
+            const bool live = wk0[i] >= 0;  // (uniform)
+            pf = stage(i + 1, &cm);
+            if (live) {
+                V dcol[K];
+#pragma unroll
+                for (int m = 0; m < K; ++m) dcol[m] = dl[m * K + (kk < K ? kk : 0)];
+                if (!(TSPGPU_SUB_BT_ABL & 1)) sub_bt_layers<V, K, 2, TPK>(g, sub9, rk, dcol, kk, sub);
+                if (tid < 64 && !(TSPGPU_SUB_BT_ABL & 2)) {
+                    const int blk = base + i * (int)gridDim.x;
+                    int32_t *tour = tour_out + (size_t)blk * (n + 1);
+                    const uint32_t lane = tid;
+                    uint32_t Mloc = (uint32_t)NK - 1u;
+                    int kl = -1;  // the current city's local index (-1: k0, outside T0)
+                    bool ok = true;
+                    for (int pos = K; ok && pos >= 1; --pos) {
+                        const int jm = __builtin_popcount(Mloc);
+                        const bool mem = lane < (uint32_t)K && ((Mloc >> lane) & 1u);
+                        V cand = ValT<V>::invalid;
+                        if (mem)
+                            cand = g[lo[jm] + __builtin_popcount(Mloc & ((1u << lane) - 1u)) * cn[jm] + rk[Mloc]] +
+                                   (kl < 0 ? dl[K * K + lane] : dl[lane * K + kl]);
+                        const V best = wave_min(cand);
+                        const unsigned long long hit = __ballot(mem && cand == best);
+                        const int li = hit ? __ffsll(hit) - 1 : K;
+                        ok = li < K;
+                        if (lane == 0) tour[pos] = ok ? city[li] + 1 : 0;
+                        if (ok) Mloc &= ~(1u << li);
+                        kl = li;
+                    }
+                    if (!ok && lane == 0) cost_out[blk] = V(-1);
+                }
+            }
+            __syncthreads();  // g, dl and city are the next block's
+            place(pf, cm);
+            __syncthreads();
+        }
+    }
+}
 }  // namespace
 
 struct SubArgs {
@@ -1413,6 +1655,7 @@ struct SubArgs {
     void *cost;
     int32_t *tour;
     int grid, bt_grid;
+    int cus;                  // compute units (the workgroup-form backtracking's grid)
     hipStream_t stream;
     hipEvent_t ev_mid;
 };
@@ -1427,7 +1670,13 @@ hipError_t launch_sub_n(const SubArgs &a)
     if (e == hipSuccess && a.ev_mid) e = hipEventRecord(a.ev_mid, a.stream);
     if (e != hipSuccess) return e;
     if constexpr (TSPGPU_SUB_STAMP) return hipSuccess;  // (diagnostic build: the tour words hold the stamps)
-    if constexpr (TSPGPU_SUB_RECYCLE)
+    if constexpr (TSPGPU_SUB_BT && !TSPGPU_SUB_RECYCLE) {
+        const int nb = a.blk1 - a.blk0, cap = a.cus * sub_bt_wg(sizeof(V));
+        const int g = nb < cap ? nb : cap;
+        hipLaunchKernelGGL((hk_sub_bt_wg<V, N, L>), dim3(g), dim3(kSubBtThreads), 0, a.stream, a.blk1, a.blk0,
+                           a.slots, a.slot_bytes, a.info, static_cast<const V *>(a.dist), static_cast<V *>(a.cost),
+                           a.tour);
+    } else if constexpr (TSPGPU_SUB_RECYCLE)
         hipLaunchKernelGGL((hk_sub_backtrack<V, N, L>), dim3(a.bt_grid), dim3(64 * kSubBtWaves), 0, a.stream, a.blk1,
                            a.blk0, a.slots, a.slot_bytes, a.info, static_cast<const V *>(a.dist),
                            static_cast<V *>(a.cost), a.tour);
