@@ -24,9 +24,12 @@
 #include <vector>
 
 #include "ctx.h"
+#include "xfer.h"
 #include "wave.h"
 #include "tspgpu.h"
 #include "tuning.h"
+
+using tspgpu::xcopy_async;
 
 namespace {
 
@@ -357,7 +360,7 @@ int tspgpu_solve_instance(tspgpu_ctx *c, const double *dist, int n, double *cost
         if (e == hipSuccess) e = hipMalloc((void **)&w->info, sizeof(WideInfo));
         if (e == hipSuccess) e = hipMalloc((void **)&w->cost, sizeof(double));
         if (e == hipSuccess) e = hipMalloc((void **)&w->tour, sizeof(int32_t) * (n + 1));
-        if (e == hipSuccess) e = hipMemcpyAsync(w->info, &h, sizeof h, hipMemcpyHostToDevice, st);
+        if (e == hipSuccess) e = xcopy_async(w->info, &h, sizeof h, hipMemcpyHostToDevice, st);
         if (e == hipSuccess) e = hipEventCreate(&w->e0);
         if (e == hipSuccess) e = hipEventCreate(&w->e1);
         if (e == hipSuccess) e = hipStreamSynchronize(st);
@@ -371,15 +374,15 @@ int tspgpu_solve_instance(tspgpu_ctx *c, const double *dist, int n, double *cost
             c->wide_free = wide_state_free;
         }
     }
-    hipError_t e = hipMemcpyAsync(w->dist, dist, sizeof(double) * n * n, hipMemcpyHostToDevice, st);
+    hipError_t e = xcopy_async(w->dist, dist, sizeof(double) * n * n, hipMemcpyHostToDevice, st);
     if (e == hipSuccess) {
         (void)hipEventRecord(w->e0, st);
         enqueue_wide(w, h, n, c->cu_count, st);
         (void)hipEventRecord(w->e1, st);
         if (e == hipSuccess) e = hipGetLastError();
     }
-    if (e == hipSuccess) e = hipMemcpyAsync(cost_out, w->cost, sizeof(double), hipMemcpyDeviceToHost, st);
-    if (e == hipSuccess) e = hipMemcpyAsync(tour_out, w->tour, sizeof(int32_t) * (n + 1), hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = xcopy_async(cost_out, w->cost, sizeof(double), hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = xcopy_async(tour_out, w->tour, sizeof(int32_t) * (n + 1), hipMemcpyDeviceToHost, st);
     if (e == hipSuccess) e = hipStreamSynchronize(st);
     if (e == hipSuccess && kernel_ms) {
         float ms = 0.f;

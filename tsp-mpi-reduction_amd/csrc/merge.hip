@@ -35,9 +35,12 @@
 #include <vector>
 
 #include "ctx.h"
+#include "xfer.h"
 #include "tuning.h"
 #include "wave.h"
 #include "tspgpu.h"
+
+using tspgpu::xcopy_async;
 
 namespace {
 
@@ -593,7 +596,7 @@ struct DVec {
         tspgpu_city *q = nullptr;
         hipError_t e = hipMalloc((void **)&q, c * sizeof(tspgpu_city));
         if (e != hipSuccess) return herr(e);
-        if (len) e = hipMemcpyAsync(q, p, len * sizeof(tspgpu_city), hipMemcpyDeviceToDevice, st);
+        if (len) e = xcopy_async(q, p, len * sizeof(tspgpu_city), hipMemcpyDeviceToDevice, st);
         if (e == hipSuccess) e = hipStreamSynchronize(st);
         if (p) (void)hipFree(p);
         p = q;
@@ -652,7 +655,7 @@ struct Merger {
         if (e == hipSuccess) {
             Ctl z{};
             z.minkey = ~0ull;
-            e = hipMemcpyAsync(ctl, &z, sizeof z, hipMemcpyHostToDevice, st);
+            e = xcopy_async(ctl, &z, sizeof z, hipMemcpyHostToDevice, st);
         }
         ops.reserve(kBatch);
         return herr(e);
@@ -741,7 +744,7 @@ struct Merger {
         bool found = false;
         if (nc > 0 && nc <= kCandCap) {
             std::vector<Cand> hc(nc);
-            e = hipMemcpyAsync(hc.data(), cand, nc * sizeof(Cand), hipMemcpyDeviceToHost, st);
+            e = xcopy_async(hc.data(), cand, nc * sizeof(Cand), hipMemcpyDeviceToHost, st);
             if (e == hipSuccess) e = hipStreamSynchronize(st);
             if (e != hipSuccess) return herr(e);
             std::sort(hc.begin(), hc.end(),
@@ -757,9 +760,9 @@ struct Merger {
         } else {
             // too many near-ties for the buffer: exact scan on the host
             std::vector<tspgpu_city> h1(o.L1), h2(o.L2);
-            e = hipMemcpyAsync(h1.data(), o.src, o.L1 * sizeof(tspgpu_city), hipMemcpyDeviceToHost, st);
+            e = xcopy_async(h1.data(), o.src, o.L1 * sizeof(tspgpu_city), hipMemcpyDeviceToHost, st);
             if (e == hipSuccess)
-                e = hipMemcpyAsync(h2.data(), o.c2, o.L2 * sizeof(tspgpu_city), hipMemcpyDeviceToHost, st);
+                e = xcopy_async(h2.data(), o.c2, o.L2 * sizeof(tspgpu_city), hipMemcpyDeviceToHost, st);
             if (e == hipSuccess) e = hipStreamSynchronize(st);
             if (e != hipSuccess) return herr(e);
             for (int i = 0; i < o.L1; ++i)
@@ -781,12 +784,13 @@ struct Merger {
     {
         size_t first = 0;  // ops[first..] not yet folded
         for (;;) {
-            hipError_t e = hipMemcpyAsync(hctl, ctl, sizeof(Ctl), hipMemcpyDeviceToHost, st);
+            hipError_t e = xcopy_async(hctl, ctl, sizeof(Ctl), hipMemcpyDeviceToHost, st);
             if (e == hipSuccess) e = hipStreamSynchronize(st);
             if (e != hipSuccess) return herr(e);
             const size_t upto = hctl->stall ? (size_t)hctl->stall_at : ops.size();
             if (upto > first) {
-                e = hipMemcpy(hpicks + first, picks + first, (upto - first) * sizeof(Pick), hipMemcpyDeviceToHost);
+                e = xcopy_async(hpicks + first, picks + first, (upto - first) * sizeof(Pick), hipMemcpyDeviceToHost, st);
+                if (e == hipSuccess) e = hipStreamSynchronize(st);
                 if (e != hipSuccess) return herr(e);
                 for (size_t m = first; m < upto; ++m) {
                     const Cand &k = hpicks[m].c;
@@ -806,14 +810,14 @@ struct Merger {
             const int M = o.L2 - 1;
             Ctl reset = *hctl;
             reset.fw[0] = reset.fw[1] = ~0ull;
-            e = hipMemcpyAsync(ctl, &reset, sizeof reset, hipMemcpyHostToDevice, st);
+            e = xcopy_async(ctl, &reset, sizeof reset, hipMemcpyHostToDevice, st);
             if (e != hipSuccess) return herr(e);
             hipLaunchKernelGGL(find_kernel, dim3(grid_for((unsigned long long)std::max(o.L1, M))),
                                dim3(kMergeThreads), 0, st, o.src, o.L1, o.c2, M, ctl, cand, picks, (int)first,
                                pk.a.id, pk.b.id, pk.c.id, 1);
             hipLaunchKernelGGL(splice_kernel, dim3(grid_for(3ull * ((unsigned long long)o.L1 + M))),
                                dim3(kMergeThreads), 0, st, o.src, o.L1, o.c2, M, ctl, o.dst, (int)first, 1);
-            e = hipMemcpyAsync(hctl, ctl, sizeof(Ctl), hipMemcpyDeviceToHost, st);
+            e = xcopy_async(hctl, ctl, sizeof(Ctl), hipMemcpyDeviceToHost, st);
             if (e == hipSuccess) e = hipStreamSynchronize(st);
             if (e != hipSuccess) return herr(e);
             if (hctl->stall == 2) return -EDEADLK;
@@ -913,12 +917,12 @@ int persist_folds(Merger &m, const tspgpu_city *blocks, int L, const double *cos
     while (!rc && !active.empty()) {
         std::vector<FoldJob> aj;
         for (int r : active) aj.push_back(jobs[r]);
-        e = hipMemcpyAsync(djobs, aj.data(), aj.size() * sizeof(FoldJob), hipMemcpyHostToDevice, m.st);
+        e = xcopy_async(djobs, aj.data(), aj.size() * sizeof(FoldJob), hipMemcpyHostToDevice, m.st);
         if (e == hipSuccess)
             hipLaunchKernelGGL(fold_persist_kernel, dim3((unsigned)aj.size()), dim3(kFoldThreads), 0, m.st, blocks, L,
                                m.eps2, djobs, douts);
         if (e == hipSuccess) e = hipGetLastError();
-        if (e == hipSuccess) e = hipMemcpyAsync(outs.data(), douts, aj.size() * sizeof(FoldOut), hipMemcpyDeviceToHost, m.st);
+        if (e == hipSuccess) e = xcopy_async(outs.data(), douts, aj.size() * sizeof(FoldOut), hipMemcpyDeviceToHost, m.st);
         if (e == hipSuccess) e = hipStreamSynchronize(m.st);
         if (e != hipSuccess) {
             rc = herr(e);
@@ -936,9 +940,9 @@ int persist_folds(Merger &m, const tspgpu_city *blocks, int L, const double *cos
             }
             // several candidates: merge o.at exactly on the host, then relaunch
             std::vector<tspgpu_city> path((size_t)o.len), blk((size_t)L);
-            e = hipMemcpyAsync(path.data(), rank[r].p, path.size() * sizeof(tspgpu_city), hipMemcpyDeviceToHost, m.st);
+            e = xcopy_async(path.data(), rank[r].p, path.size() * sizeof(tspgpu_city), hipMemcpyDeviceToHost, m.st);
             if (e == hipSuccess)
-                e = hipMemcpyAsync(blk.data(), blocks + (size_t)(firstb[r] + 1 + o.at) * L, L * sizeof(tspgpu_city),
+                e = xcopy_async(blk.data(), blocks + (size_t)(firstb[r] + 1 + o.at) * L, L * sizeof(tspgpu_city),
                                    hipMemcpyDeviceToHost, m.st);
             if (e == hipSuccess) e = hipStreamSynchronize(m.st);
             if (e != hipSuccess) {
@@ -950,7 +954,7 @@ int persist_folds(Merger &m, const tspgpu_city *blocks, int L, const double *cos
             if (rc) break;
             hpick[(size_t)firstb[r] + o.at].c = pk;
             host_picked[(size_t)firstb[r] + o.at] = 1;
-            e = hipMemcpyAsync(rank[r].p, path.data(), path.size() * sizeof(tspgpu_city), hipMemcpyHostToDevice, m.st);
+            e = xcopy_async(rank[r].p, path.data(), path.size() * sizeof(tspgpu_city), hipMemcpyHostToDevice, m.st);
             if (e != hipSuccess) {
                 rc = herr(e);
                 break;
@@ -965,7 +969,7 @@ int persist_folds(Merger &m, const tspgpu_city *blocks, int L, const double *cos
     if (!rc) {
         // the logged picks -> exact costs in merge order (tsp.cpp:263)
         std::vector<Pick> dp((size_t)nb);
-        e = hipMemcpyAsync(dp.data(), dpicks, dp.size() * sizeof(Pick), hipMemcpyDeviceToHost, m.st);
+        e = xcopy_async(dp.data(), dpicks, dp.size() * sizeof(Pick), hipMemcpyDeviceToHost, m.st);
         if (e == hipSuccess) e = hipStreamSynchronize(m.st);
         rc = herr(e);
         for (int r = 0; r < P && !rc; ++r) {
@@ -1030,14 +1034,14 @@ int tspgpu_merge(tspgpu_ctx *ctx, const tspgpu_city *p1, int L1, double c1, cons
     if (!rc) rc = t.reserve((size_t)L1 + L2, m.st);
     if (!rc) rc = b.reserve(L2, m.st);
     hipError_t e = hipSuccess;
-    if (!rc) e = hipMemcpyAsync(s.p, p1, L1 * sizeof(tspgpu_city), hipMemcpyHostToDevice, m.st);
-    if (!rc && e == hipSuccess) e = hipMemcpyAsync(b.p, p2, L2 * sizeof(tspgpu_city), hipMemcpyHostToDevice, m.st);
+    if (!rc) e = xcopy_async(s.p, p1, L1 * sizeof(tspgpu_city), hipMemcpyHostToDevice, m.st);
+    if (!rc && e == hipSuccess) e = xcopy_async(b.p, p2, L2 * sizeof(tspgpu_city), hipMemcpyHostToDevice, m.st);
     if (!rc) rc = herr(e);
     s.len = L1;
     double cost = c1;
     if (!rc) rc = m.merge(s, t, &cost, b.p, L2, &c2);
     if (!rc) rc = m.sync();
-    if (!rc) rc = herr(hipMemcpyAsync(out, s.p, s.len * sizeof(tspgpu_city), hipMemcpyDeviceToHost, m.st));
+    if (!rc) rc = herr(xcopy_async(out, s.p, s.len * sizeof(tspgpu_city), hipMemcpyDeviceToHost, m.st));
     if (!rc) rc = herr(hipStreamSynchronize(m.st));
     const int len = (int)s.len;
     s.release();
@@ -1063,7 +1067,8 @@ int tspgpu_reduce(tspgpu_ctx *ctx, const tspgpu_city *paths, int L, const double
     if (rc) return rc;
     DVec blocks;
     rc = blocks.reserve(ncity, m.st);
-    if (!rc) rc = herr(hipMemcpy(blocks.p, paths, ncity * sizeof(tspgpu_city), hipMemcpyHostToDevice));
+    if (!rc) rc = herr(xcopy_async(blocks.p, paths, ncity * sizeof(tspgpu_city), hipMemcpyHostToDevice, m.st));
+    if (!rc) rc = herr(hipStreamSynchronize(m.st));
     blocks.len = ncity;
     // distributeBlocks' counts (tsp.cpp:167-192): rank r gets #{b in [1,B] : b mod P == r}
     std::vector<int> cnt(nprocs, 0);
@@ -1100,7 +1105,7 @@ int tspgpu_reduce(tspgpu_ctx *ctx, const tspgpu_city *paths, int L, const double
     for (int r = 0; r < nprocs && !rc && next < nblocks; ++r) {
         rc = rank[r].reserve(ncity, m.st);
         if (rc) break;
-        rc = herr(hipMemcpyAsync(rank[r].p, blocks.p + (size_t)next * L, L * sizeof(tspgpu_city),
+        rc = herr(xcopy_async(rank[r].p, blocks.p + (size_t)next * L, L * sizeof(tspgpu_city),
                                  hipMemcpyDeviceToDevice, m.st));
         rank[r].len = L;
         rcost[r] = costs[next];
@@ -1122,7 +1127,7 @@ int tspgpu_reduce(tspgpu_ctx *ctx, const tspgpu_city *paths, int L, const double
         const size_t add = rank[from].len;
         r2 = acc.reserve(std::max(acc.len + add, ncity), m.st);
         if (r2) return r2;
-        r2 = herr(hipMemcpyAsync(acc.p + acc.len, rank[from].p, add * sizeof(tspgpu_city), hipMemcpyDeviceToDevice,
+        r2 = herr(xcopy_async(acc.p + acc.len, rank[from].p, add * sizeof(tspgpu_city), hipMemcpyDeviceToDevice,
                                  m.st));
         if (r2) return r2;
         acc.len += add;

@@ -25,6 +25,7 @@
 #include "ctx.h"
 #include "heldkarp.h"
 #include "k1_cfg.h"
+#include "xfer.h"
 
 namespace tspgpu {
 
@@ -109,6 +110,14 @@ int ensure(T **p, size_t *have, size_t need)
     return 0;
 }
 
+// a one-time table upload on the context's stream (xfer.h: small tables skip
+// the runtime's copy path and its first-use cost)
+hipError_t upload_sync(tspgpu_ctx *c, void *d, const void *h, size_t bytes)
+{
+    hipError_t e = xcopy_async(d, h, bytes, hipMemcpyHostToDevice, c->stream);
+    return e == hipSuccess ? hipStreamSynchronize(c->stream) : e;
+}
+
 int ensure_tables(tspgpu_ctx *c, int N)
 {
     if (c->d_info[N]) return 0;
@@ -121,9 +130,9 @@ int ensure_tables(tspgpu_ctx *c, int N)
             if (__builtin_popcount(m) == t) masks.push_back(m);
     hipError_t e = hipMalloc((void **)&c->d_info[N], sizeof(LayerInfo));
     if (e == hipSuccess) e = hipMalloc((void **)&c->d_masks[N], masks.size() * sizeof(uint32_t));
-    if (e == hipSuccess) e = hipMemcpy(c->d_info[N], &info, sizeof(info), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = upload_sync(c, c->d_info[N], &info, sizeof(info));
     if (e == hipSuccess)
-        e = hipMemcpy(c->d_masks[N], masks.data(), masks.size() * sizeof(uint32_t), hipMemcpyHostToDevice);
+        e = upload_sync(c, c->d_masks[N], masks.data(), masks.size() * sizeof(uint32_t));
     if (e != hipSuccess) {
         if (c->d_info[N]) (void)hipFree(c->d_info[N]);
         if (c->d_masks[N]) (void)hipFree(c->d_masks[N]);
@@ -155,7 +164,7 @@ int ensure_tiled_info(tspgpu_ctx *c, int L)
     info->moff[L + 1] = k;
     void *d = nullptr;
     hipError_t e = hipMalloc(&d, sizeof(TiledInfo));
-    if (e == hipSuccess) e = hipMemcpy(d, info.get(), sizeof(TiledInfo), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = upload_sync(c, d, info.get(), sizeof(TiledInfo));
     if (e != hipSuccess) {
         if (d) (void)hipFree(d);
         return hip_err(e);
@@ -258,7 +267,7 @@ int ensure_sub_rows(tspgpu_ctx *c, int L)
     }
     void *d = nullptr;
     hipError_t e = hipMalloc(&d, rows.size() * sizeof(SubRow));
-    if (e == hipSuccess) e = hipMemcpy(d, rows.data(), rows.size() * sizeof(SubRow), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = upload_sync(c, d, rows.data(), rows.size() * sizeof(SubRow));
     if (e != hipSuccess) {
         if (d) (void)hipFree(d);
         return hip_err(e);
@@ -767,13 +776,13 @@ int solve_host_copy(tspgpu_ctx *c, const V *dist, int n, int nblocks, V *cost_ou
     if ((rc = ensure(&c->d_dist, &c->dist_bytes, db))) return rc;
     if ((rc = ensure(&c->d_cost, &c->cost_bytes, cb))) return rc;
     if ((rc = ensure(&c->d_tour, &c->tour_bytes, tb))) return rc;
-    hipError_t e = hipMemcpyAsync(c->d_dist, dist, db, hipMemcpyHostToDevice, c->stream);
-    if (e == hipSuccess) e = hipMemsetAsync(c->d_tour, 0xff, tb, c->stream);
+    hipError_t e = xcopy_async(c->d_dist, dist, db, hipMemcpyHostToDevice, c->stream);
+    if (e == hipSuccess) e = xset_async(c->d_tour, 0xff, tb, c->stream);
     if (e != hipSuccess) return hip_err(e);
     rc = solve_device_locked(c, c->d_dist, n, nblocks, c->d_cost, c->d_tour, c->stream, (int)sizeof(V));
     if (rc) return rc;
-    e = hipMemcpyAsync(cost_out, c->d_cost, cb, hipMemcpyDeviceToHost, c->stream);
-    if (e == hipSuccess) e = hipMemcpyAsync(tour_out, c->d_tour, tb, hipMemcpyDeviceToHost, c->stream);
+    e = xcopy_async(cost_out, c->d_cost, cb, hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = xcopy_async(tour_out, c->d_tour, tb, hipMemcpyDeviceToHost, c->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
     if (e != hipSuccess) return hip_err(e);
     for (int b = 0; b < nblocks; ++b)
@@ -872,7 +881,7 @@ static int copy_sync(tspgpu_ctx *c, void *dst, const void *src, size_t bytes, hi
     if (!bytes) return 0;
     std::lock_guard<std::mutex> g(c->mu);
     if (hipSetDevice(c->device) != hipSuccess) return -ENODEV;
-    hipError_t e = hipMemcpyAsync(dst, src, bytes, kind, c->stream);
+    hipError_t e = xcopy_async(dst, src, bytes, kind, c->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
     return hip_err(e);
 }
