@@ -1060,6 +1060,10 @@ int tspgpu_reduce(tspgpu_ctx *ctx, const tspgpu_city *paths, int L, const double
     if (nblocks < 1 || nprocs < 1 || nblocks < nprocs || L < 2) return -EINVAL;
     const size_t ncity = (size_t)nblocks * L;
     if (!finite_cities(paths, ncity)) return -EINVAL;
+    if (nblocks == 1) {  // one rank, one block: no fold, no tree (nothing to launch or load)
+        *final_cost = costs[0];
+        return 0;
+    }
     std::lock_guard<std::mutex> g(ctx->mu);
     if (hipSetDevice(ctx->device) != hipSuccess) return -ENODEV;
     Merger m;

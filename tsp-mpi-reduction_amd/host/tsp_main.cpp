@@ -329,6 +329,11 @@ int main(int argc, char **argv)
     timespec ts_solve0, ts_solve1, ts_merge1;
     tspgpu_ctx *kept = nullptr;  // the block search's context on TSP_GPU, reused by the merges
     clock_gettime(CLOCK_MONOTONIC_RAW, &ts_solve0);
+    // (the HIP runtime's own start-up, the analogue of the reference's
+    // MPI_Init inside its clock: reported apart by TSP_STATS)
+    timespec ts_rt;
+    (void)tspgpu_device_count();
+    clock_gettime(CLOCK_MONOTONIC_RAW, &ts_rt);
     if (multi) {
         // rank 0's own share here, the other ranks' shares from their files
         std::vector<int> cnt(P), off(P, 0);
@@ -375,11 +380,8 @@ int main(int argc, char **argv)
         tspgpu_opts o;
         std::memset(&o, 0, sizeof o);
         o.device = env_int("TSP_GPU", 0);
-        tspgpu_ctx *ctx = kept;
-        kept = nullptr;
-        red = ctx ? 0 : tspgpu_ctx_create(&o, &ctx);
-        if (!red) red = tspgpu_reduce(ctx, paths.data(), L, cost.data(), B, P, &final_cost, log.data(), (int)log.size());
-        if (ctx) tspgpu_ctx_destroy(ctx);
+        red = kept ? 0 : tspgpu_ctx_create(&o, &kept);
+        if (!red) red = tspgpu_reduce(kept, paths.data(), L, cost.data(), B, P, &final_cost, log.data(), (int)log.size());
     }
     if (red) {
         std::fflush(stdout);
@@ -396,6 +398,11 @@ int main(int argc, char **argv)
     const uint64_t ms = (uint64_t)((1000000000L * (end.tv_sec - start.tv_sec) + end.tv_nsec - start.tv_nsec) / 1e6);
     std::printf("TSP ran in %llu ms for %lu cities and the trip cost %f\n", (unsigned long long)ms,
                 (unsigned long)(unsigned int)(B * n), final_cost);
+    // the device context is torn down after the clock, like the reference's
+    // MPI_Finalize after its end time (tsp.cpp:358-366)
+    std::fflush(stdout);
+    if (kept) tspgpu_ctx_destroy(kept);
+    kept = nullptr;
     // opt-in statistics on stderr (SURVEY.md §5 "Metrics": stdout stays the
     // reference's byte for byte): phase times and the block search's rate
     if (env_int("TSP_STATS", 0)) {
@@ -405,9 +412,9 @@ int main(int argc, char **argv)
         const double solve_s = sec(ts_solve0, ts_solve1);
         const double relax = tspgpu_relaxations_per_block(n) * (multi ? 0.0 : (double)B);
         std::fprintf(stderr,
-                     "tsp stats: n %d blocks %d ranks %d | setup %.3f ms, block search %.3f ms (%s), merge %.3f ms, "
-                     "total %.3f ms | %.4g DP relaxations/s\n",
-                     n, B, P, 1e3 * sec(start, ts_solve0), 1e3 * solve_s,
+                     "tsp stats: n %d blocks %d ranks %d | setup %.3f ms, block search %.3f ms (HIP runtime start-up "
+                     "%.3f ms of it; %s), merge %.3f ms, total %.3f ms | %.4g DP relaxations/s\n",
+                     n, B, P, 1e3 * sec(start, ts_solve0), 1e3 * solve_s, 1e3 * sec(ts_solve0, ts_rt),
                      multi ? "rank 0's share + the rank files" : "all blocks, one process",
                      1e3 * sec(ts_solve1, ts_merge1), 1e3 * sec(start, end),
                      solve_s > 0 && relax > 0 ? relax / solve_s : 0.0);
