@@ -387,10 +387,21 @@ __device__ __forceinline__ void tail_one(const SearchArgs &a, const V *dl, const
             ocp = __longlong_as_double(__shfl((long long)__double_as_longlong(cp), o));
         else
             ocp = (V)__shfl((int)cp, o);
-        // the incumbent read once per owner (a tour is still recorded iff its
-        // atomicMin finds it within the incumbent: a stale read only costs
-        // attempts), then lowered by every attempt's answer
-        V cur = ENum<V>::val(__hip_atomic_load(a.inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        // ONE atomicMin per owner, with its best completion (round 5): the
+        // incumbent it returns, lowered by that best, is the bound every order
+        // below is recorded against — the optimal tours still all pass (a
+        // lane's best is never below the optimum), and no order waits on an
+        // atomicMin of its own (before: one dependent atomicMin per improving
+        // order, the tail's critical path)
+        V obest;
+        if constexpr (sizeof(V) == 8)
+            obest = __longlong_as_double(__shfl((long long)__double_as_longlong(best), o));
+        else
+            obest = (V)__shfl((int)best, o);
+        unsigned long long oinc = 0;
+        if (__lane_id() == 0) oinc = atomicMin(a.inc, (unsigned long long)ENum<V>::bits(obest));
+        oinc = (unsigned long long)__shfl((long long)oinc, 0);
+        const V cur = ENum<V>::vmin(ENum<V>::val(oinc), obest);
         for (uint32_t gg = ogm; gg; gg &= gg - 1u) {
             const int g = __builtin_ctz(gg);
             for (int p = g * kGroup + __lane_id(); p < (g + 1) * kGroup; p += 64) {
@@ -420,14 +431,11 @@ __device__ __forceinline__ void tail_one(const SearchArgs &a, const V *dl, const
                 }
                 const V total = c + dl[k * kTRow];
                 if (total <= cur) {
+                    // (total <= cur <= the incumbent the atomicMin returned: a
+                    // record slot only for such tours — rec_count decides the
+                    // -EOVERFLOW / second-phase fallback)
                     const uint64_t tb = ENum<V>::bits(total);
-                    // a record slot only for a tour still within the incumbent
-                    // the atomicMin returns (a stale read must not fill the
-                    // record buffer with tours above the optimum: rec_count
-                    // decides the -EOVERFLOW / second-phase fallback)
-                    const unsigned long long old = atomicMin(a.inc, (unsigned long long)tb);
-                    const unsigned int slot = tb <= old ? atomicAdd(a.rec_count, 1u) : ~0u;
-                    cur = ENum<V>::vmin(ENum<V>::val(old), total);
+                    const unsigned int slot = atomicAdd(a.rec_count, 1u);
                     if (slot < a.rec_cap) {
                         SearchRecord *R = a.rec + slot;
                         R->cost = tb;
@@ -435,13 +443,12 @@ __device__ __forceinline__ void tail_one(const SearchArgs &a, const V *dl, const
 #pragma unroll
                         for (int l = 0; l < TL; ++l) R->city[olen - 1 + l] = (uint8_t)ord[l];
                     }
-                    if (tb <= old)
-                        tie_offer(a, tcache, tb, [&](int q) {
-                            int v = 0;
+                    tie_offer(a, tcache, tb, [&](int q) {
+                        int v = 0;
 #pragma unroll
-                            for (int l = 0; l < TL; ++l) v = q == olen + l ? ord[l] : v;
-                            return q < olen ? path_byte(ow, q) : v;
-                        });
+                        for (int l = 0; l < TL; ++l) v = q == olen + l ? ord[l] : v;
+                        return q < olen ? path_byte(ow, q) : v;
+                    });
                 }
             }
         }
@@ -572,7 +579,10 @@ __device__ __forceinline__ void tail_wide(const SearchArgs &a, const V *dl, cons
             },
             std::make_integer_sequence<int, 4>{});
         // rare: this lane's orders within the incumbent, recorded one by one
+        // after ONE atomicMin with the lane's best (as tail_one)
         if (!(on && best <= cur)) continue;
+        const unsigned long long linc = atomicMin(a.inc, (unsigned long long)ENum<V>::bits(best));
+        cur = ENum<V>::vmin(ENum<V>::val(linc), best);
 #pragma unroll 1
         for (int pi = 0; pi < 24; ++pi) {
             const uint32_t pm = g_perm4.p[pi];
@@ -584,9 +594,7 @@ __device__ __forceinline__ void tail_wide(const SearchArgs &a, const V *dl, cons
             const V total = c + sel4(d04, a3);
             if (!(total <= cur)) continue;
             const uint64_t tb = ENum<V>::bits(total);
-            const unsigned long long old = atomicMin(a.inc, (unsigned long long)tb);
-            const unsigned int slot = tb <= old ? atomicAdd(a.rec_count, 1u) : ~0u;  // (as tail_one)
-            cur = ENum<V>::vmin(ENum<V>::val(old), total);
+            const unsigned int slot = atomicAdd(a.rec_count, 1u);  // (as tail_one)
             const int ord[TL] = {ti, tj, sel4(r, a0), sel4(r, a1), sel4(r, a2), sel4(r, a3)};
             if (slot < a.rec_cap) {
                 SearchRecord *R = a.rec + slot;
@@ -595,13 +603,12 @@ __device__ __forceinline__ void tail_wide(const SearchArgs &a, const V *dl, cons
 #pragma unroll
                 for (int l = 0; l < TL; ++l) R->city[olen - 1 + l] = (uint8_t)ord[l];
             }
-            if (tb <= old)
-                tie_offer(a, tcache, tb, [&](int q) {
-                    int v = 0;
+            tie_offer(a, tcache, tb, [&](int q) {
+                int v = 0;
 #pragma unroll
-                    for (int l = 0; l < TL; ++l) v = q == olen + l ? ord[l] : v;
-                    return q < olen ? path_byte(ow, q) : v;
-                });
+                for (int l = 0; l < TL; ++l) v = q == olen + l ? ord[l] : v;
+                return q < olen ? path_byte(ow, q) : v;
+            });
         }
     }
 }

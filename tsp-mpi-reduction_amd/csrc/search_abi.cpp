@@ -1187,6 +1187,9 @@ static int run_chain(tspgpu_search *s, bool *done, int every = 0, tspgpu_level_h
     int chain_grid = 2;
     chain_fpb = (uint32_t)tuned_int("CHAIN_FPB", (int)chain_fpb);  // (sweeps)
     chain_grid = std::max(1, tuned_int("CHAIN_GRID", chain_grid));
+    // the tail's count is only known on the device, so its grid is sized for
+    // the buffer and the blocks beyond the count leave at once
+    const int tail_grid = std::max(1, tuned_int("CHAIN_TAIL_GRID", 8));
     // the levels expanded block-locally (expand_local_kernel; knob
     // CHAIN_LOCAL), runs of 64 input paths per block
     // (from 20 cities: 7-11% fewer kernel-us at 20-32 cities; at 14-16 cities
@@ -1268,7 +1271,7 @@ static int run_chain(tspgpu_search *s, bool *done, int every = 0, tspgpu_level_h
     if (e == hipSuccess) {
         SearchArgs a = args_of(s);
         a.overflow = reinterpret_cast<unsigned int *>(s->d_words + 13);  // (an abandoned chain folds no tails)
-        e = launch_tail(a, f64, s->ctx->cu_count * 8);
+        e = launch_tail(a, f64, s->ctx->cu_count * tail_grid);
     }
     if (!fetch) (void)hipEventRecord(s->e1, st);
     unsigned long long local[8] = {};

@@ -51,6 +51,7 @@ Knob g_knobs[] = {
     {"SEARCH_CHAIN_POISON", false, 0},    // 1: fill the chain's level buffers with 0xFF first (tests)
     {"CHAIN_FPB", false, 0},
     {"CHAIN_GRID", false, 0},
+    {"CHAIN_TAIL_GRID", false, 0},  // chained tail_kernel workgroups per CU
     {"CHAIN_LOCAL", false, 0},      // 0: a launch per chained level (no block-local levels)
     {"CHAIN_LOCAL_FPB", false, 0},
     {"SEARCH_DEBUG", false, 0},    // host phase times on stderr
