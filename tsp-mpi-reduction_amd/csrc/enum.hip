@@ -315,6 +315,10 @@ __device__ __forceinline__ int path_byte(const uint32_t (&w)[8], int l)
 // One handed-over prefix (slot idx of a.ftail): refold, bound test, all
 // TL! completions; `act` false = a lane with nothing to do (wave-uniform code).
 // (A wave with only a few prefixes takes tail_wide below instead.)
+#ifndef TSPGPU_TAIL_ABL
+#define TSPGPU_TAIL_ABL 0  // timing ablations of tail_kernel (results wrong): 1 leave at entry, 2 after staging,
+                           // 4 no folding, 8 no recording (tail_wide), 16 no tie offer, 32 no record (tail_wide)
+#endif
 template <typename V, int TL>
 __device__ __forceinline__ void tail_one(const SearchArgs &a, const V *dl, const V *am, uint32_t full, uint32_t idx,
                                          bool act, unsigned long long &lanes, TieCache &tcache)
@@ -470,17 +474,6 @@ __host__ __device__ constexpr int perm4(int idx, int pos)
     }
     return res;
 }
-struct Perm4Table {
-    uint8_t p[24];  // 2 bits per position
-};
-constexpr Perm4Table make_perm4()
-{
-    Perm4Table t{};
-    for (int i = 0; i < 24; ++i)
-        t.p[i] = (uint8_t)(perm4(i, 0) | perm4(i, 1) << 2 | perm4(i, 2) << 4 | perm4(i, 3) << 6);
-    return t;
-}
-__constant__ Perm4Table g_perm4 = make_perm4();
 // v[i] / m[i][j] for a runtime i, j by selects (no dynamically indexed registers)
 template <typename T>
 __device__ __forceinline__ T sel4(const T (&v)[4], int i)
@@ -578,32 +571,101 @@ __device__ __forceinline__ void tail_wide(const SearchArgs &a, const V *dl, cons
                 complete<V, 4, (15 & ~(1 << Q)), Q>(s4, d04, pj + dk4[Q], best);
             },
             std::make_integer_sequence<int, 4>{});
-        // rare: this lane's orders within the incumbent, recorded one by one
-        // after ONE atomicMin with the lane's best (as tail_one)
+        // rare: this lane's orders within the incumbent.  ONE atomicMin with
+        // the lane's best, ONE record-slot range for the orders within the
+        // bound it returns (all at the lane's best) and ONE tie offer, of the
+        // least key among them (the slot keeps the least key anyway): the
+        // 24-step loop below only stores.  Per-order atomics in that loop,
+        // taken by a different lane at every step, cost ~21 us of the 16-city
+        // chain's ~98 (round-5 ablation, TSPGPU_TAIL_ABL).
         if (!(on && best <= cur)) continue;
+        if constexpr (TSPGPU_TAIL_ABL & 8) continue;
         const unsigned long long linc = atomicMin(a.inc, (unsigned long long)ENum<V>::bits(best));
         cur = ENum<V>::vmin(ENum<V>::val(linc), best);
+        if constexpr (TSPGPU_TAIL_ABL & 64) {
+            stat_line(a)[8] = (unsigned long long)ENum<V>::bits(cur);  // (keeps the ablated value alive; padding word)
+            continue;
+        }
+        // order pi of the four: lexicographic permutation pi of {0,1,2,3},
+        // decoded arithmetically (a __constant__ table read per step was a
+        // dependent memory round trip per order: ~18 us of the 16-city chain)
+        auto total_of = [&](int pi, int (&ax)[4]) {
+            uint32_t lst = 0x3210u;  // indices not used yet, one per nibble
+            int q = pi;
+#pragma unroll
+            for (int l = 0; l < 4; ++l) {
+                const int fact = l == 0 ? 6 : (l == 1 ? 2 : 1);
+                const int dgt = q / fact;
+                q -= dgt * fact;
+                const int sh = 4 * dgt;
+                ax[l] = (int)((lst >> sh) & 15u);
+                lst = (lst & ((1u << sh) - 1u)) | ((lst >> (sh + 4)) << sh);
+            }
+            V c = pj + sel4(dk4, ax[0]);
+            c = c + sel44(s4, ax[0], ax[1]);
+            c = c + sel44(s4, ax[1], ax[2]);
+            c = c + sel44(s4, ax[2], ax[3]);
+            return c + sel4(d04, ax[3]);
+        };
+        // the mask pass: the 24 orders at compile time (constant indices, no selects)
+        uint32_t pass = 0;
+        static_for(
+            [&](auto i) {
+                constexpr int PI = decltype(i)::value;
+                constexpr int A0 = perm4(PI, 0), A1 = perm4(PI, 1), A2 = perm4(PI, 2), A3 = perm4(PI, 3);
+                V c = pj + dk4[A0];
+                c = c + s4[A0][A1];
+                c = c + s4[A1][A2];
+                c = c + s4[A2][A3];
+                if (c + d04[A3] <= cur) pass |= 1u << PI;
+            },
+            std::make_integer_sequence<int, 24>{});
+        if constexpr (TSPGPU_TAIL_ABL & 32) {
+            stat_line(a)[8] = pass;
+            continue;
+        }
+        if (!pass) continue;
+        unsigned int slot = atomicAdd(a.rec_count, (unsigned int)__builtin_popcount(pass));  // (as tail_one)
+        if constexpr (TSPGPU_TAIL_ABL & 128) {
+            stat_line(a)[8] = slot;
+            continue;
+        }
+        const int N = a.n - 1;
+        int kpi = -1;
+        unsigned long long kw0 = ~0ull, kw1 = ~0ull;
 #pragma unroll 1
-        for (int pi = 0; pi < 24; ++pi) {
-            const uint32_t pm = g_perm4.p[pi];
-            const int a0 = (int)(pm & 3u), a1 = (int)((pm >> 2) & 3u), a2 = (int)((pm >> 4) & 3u), a3 = (int)(pm >> 6);
-            V c = pj + sel4(dk4, a0);
-            c = c + sel44(s4, a0, a1);
-            c = c + sel44(s4, a1, a2);
-            c = c + sel44(s4, a2, a3);
-            const V total = c + sel4(d04, a3);
-            if (!(total <= cur)) continue;
-            const uint64_t tb = ENum<V>::bits(total);
-            const unsigned int slot = atomicAdd(a.rec_count, 1u);  // (as tail_one)
-            const int ord[TL] = {ti, tj, sel4(r, a0), sel4(r, a1), sel4(r, a2), sel4(r, a3)};
+        for (uint32_t pp = pass; pp; pp &= pp - 1u, ++slot) {
+            const int pi = __builtin_ctz(pp);
+            int ax[4];
+            const V total = total_of(pi, ax);
+            const int ord[TL] = {ti, tj, sel4(r, ax[0]), sel4(r, ax[1]), sel4(r, ax[2]), sel4(r, ax[3])};
             if (slot < a.rec_cap) {
                 SearchRecord *R = a.rec + slot;
-                R->cost = tb;
+                R->cost = ENum<V>::bits(total);
                 for (int l = 1; l < olen; ++l) R->city[l - 1] = (uint8_t)path_byte(ow, l);
 #pragma unroll
                 for (int l = 0; l < TL; ++l) R->city[olen - 1 + l] = (uint8_t)ord[l];
             }
-            tie_offer(a, tcache, tb, [&](int q) {
+            if (a.tie) {
+                unsigned long long w0, w1;
+                tie_key(N, [&](int q) {
+                    int v = 0;
+#pragma unroll
+                    for (int l = 0; l < TL; ++l) v = q == olen + l ? ord[l] : v;
+                    return q < olen ? path_byte(ow, q) : v;
+                }, w0, w1);
+                if (w0 < kw0 || (w0 == kw0 && w1 < kw1)) {
+                    kw0 = w0;
+                    kw1 = w1;
+                    kpi = pi;
+                }
+            }
+        }
+        if (kpi >= 0 && !(TSPGPU_TAIL_ABL & 16)) {
+            int ax[4];
+            const V total = total_of(kpi, ax);
+            const int ord[TL] = {ti, tj, sel4(r, ax[0]), sel4(r, ax[1]), sel4(r, ax[2]), sel4(r, ax[3])};
+            tie_offer(a, tcache, ENum<V>::bits(total), [&](int q) {
                 int v = 0;
 #pragma unroll
                 for (int l = 0; l < TL; ++l) v = q == olen + l ? ord[l] : v;
@@ -621,6 +683,7 @@ constexpr uint32_t kTailWide = 4;
 template <typename V, int TL>
 __global__ __launch_bounds__(256) void tail_kernel(SearchArgs a)
 {
+    if constexpr (TSPGPU_TAIL_ABL & 1) return;
     __shared__ V dl[kSearchMaxN * kTRow];
     __shared__ V am[kSearchMaxN];
     __shared__ uint32_t wq[4][128];
@@ -639,6 +702,7 @@ __global__ __launch_bounds__(256) void tail_kernel(SearchArgs a)
     for (int i = threadIdx.x; i < n * n; i += blockDim.x) dl[(i / n) * kTRow + i % n] = gd[i];
     for (int i = threadIdx.x; i < n; i += blockDim.x) am[i] = ga[i];
     __syncthreads();
+    if constexpr (TSPGPU_TAIL_ABL & 2) return;
 
     const uint32_t full = (uint32_t)((1ull << n) - 1ull) & ~1u;
     const int lane = __lane_id();
@@ -665,6 +729,7 @@ __global__ __launch_bounds__(256) void tail_kernel(SearchArgs a)
             const uint32_t idx = act ? q[qn - take + lane] : 0u;
             __builtin_amdgcn_wave_barrier();
             qn -= take;
+            if constexpr (TSPGPU_TAIL_ABL & 4) continue;
             if constexpr (TL == 6) {
                 if (take <= kTailWide) {
                     tail_wide<V, TL>(a, dl, am, full, idx, act, lanes, tcache);
