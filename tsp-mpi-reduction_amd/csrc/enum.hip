@@ -625,28 +625,19 @@ __device__ __forceinline__ void tail_wide(const SearchArgs &a, const V *dl, cons
             continue;
         }
         if (!pass) continue;
-        unsigned int slot = atomicAdd(a.rec_count, (unsigned int)__builtin_popcount(pass));  // (as tail_one)
-        if constexpr (TSPGPU_TAIL_ABL & 128) {
-            stat_line(a)[8] = slot;
-            continue;
-        }
+        // keys first (VALU only), then the slot range and the tie offer issued
+        // back to back (the offer's wait covers both round trips), then the
+        // record stores (no later wait on them)
         const int N = a.n - 1;
         int kpi = -1;
         unsigned long long kw0 = ~0ull, kw1 = ~0ull;
+        if (a.tie) {
 #pragma unroll 1
-        for (uint32_t pp = pass; pp; pp &= pp - 1u, ++slot) {
-            const int pi = __builtin_ctz(pp);
-            int ax[4];
-            const V total = total_of(pi, ax);
-            const int ord[TL] = {ti, tj, sel4(r, ax[0]), sel4(r, ax[1]), sel4(r, ax[2]), sel4(r, ax[3])};
-            if (slot < a.rec_cap) {
-                SearchRecord *R = a.rec + slot;
-                R->cost = ENum<V>::bits(total);
-                for (int l = 1; l < olen; ++l) R->city[l - 1] = (uint8_t)path_byte(ow, l);
-#pragma unroll
-                for (int l = 0; l < TL; ++l) R->city[olen - 1 + l] = (uint8_t)ord[l];
-            }
-            if (a.tie) {
+            for (uint32_t pp = pass; pp; pp &= pp - 1u) {
+                const int pi = __builtin_ctz(pp);
+                int ax[4];
+                (void)total_of(pi, ax);
+                const int ord[TL] = {ti, tj, sel4(r, ax[0]), sel4(r, ax[1]), sel4(r, ax[2]), sel4(r, ax[3])};
                 unsigned long long w0, w1;
                 tie_key(N, [&](int q) {
                     int v = 0;
@@ -661,6 +652,11 @@ __device__ __forceinline__ void tail_wide(const SearchArgs &a, const V *dl, cons
                 }
             }
         }
+        unsigned int slot = atomicAdd(a.rec_count, (unsigned int)__builtin_popcount(pass));  // (as tail_one)
+        if constexpr (TSPGPU_TAIL_ABL & 128) {
+            stat_line(a)[8] = slot;
+            continue;
+        }
         if (kpi >= 0 && !(TSPGPU_TAIL_ABL & 16)) {
             int ax[4];
             const V total = total_of(kpi, ax);
@@ -671,6 +667,19 @@ __device__ __forceinline__ void tail_wide(const SearchArgs &a, const V *dl, cons
                 for (int l = 0; l < TL; ++l) v = q == olen + l ? ord[l] : v;
                 return q < olen ? path_byte(ow, q) : v;
             });
+        }
+#pragma unroll 1
+        for (uint32_t pp = pass; pp; pp &= pp - 1u, ++slot) {
+            if (slot >= a.rec_cap) break;
+            const int pi = __builtin_ctz(pp);
+            int ax[4];
+            const V total = total_of(pi, ax);
+            const int ord[TL] = {ti, tj, sel4(r, ax[0]), sel4(r, ax[1]), sel4(r, ax[2]), sel4(r, ax[3])};
+            SearchRecord *R = a.rec + slot;
+            R->cost = ENum<V>::bits(total);
+            for (int l = 1; l < olen; ++l) R->city[l - 1] = (uint8_t)path_byte(ow, l);
+#pragma unroll
+            for (int l = 0; l < TL; ++l) R->city[olen - 1 + l] = (uint8_t)ord[l];
         }
     }
 }
