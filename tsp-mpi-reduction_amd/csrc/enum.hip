@@ -315,10 +315,6 @@ __device__ __forceinline__ int path_byte(const uint32_t (&w)[8], int l)
 // One handed-over prefix (slot idx of a.ftail): refold, bound test, all
 // TL! completions; `act` false = a lane with nothing to do (wave-uniform code).
 // (A wave with only a few prefixes takes tail_wide below instead.)
-#ifndef TSPGPU_TAIL_ABL
-#define TSPGPU_TAIL_ABL 0  // timing ablations of tail_kernel (results wrong): 1 leave at entry, 2 after staging,
-                           // 4 no folding, 8 no recording (tail_wide), 16 no tie offer, 32 no record (tail_wide)
-#endif
 template <typename V, int TL>
 __device__ __forceinline__ void tail_one(const SearchArgs &a, const V *dl, const V *am, uint32_t full, uint32_t idx,
                                          bool act, unsigned long long &lanes, TieCache &tcache)
@@ -577,15 +573,10 @@ __device__ __forceinline__ void tail_wide(const SearchArgs &a, const V *dl, cons
         // least key among them (the slot keeps the least key anyway): the
         // 24-step loop below only stores.  Per-order atomics in that loop,
         // taken by a different lane at every step, cost ~21 us of the 16-city
-        // chain's ~98 (round-5 ablation, TSPGPU_TAIL_ABL).
+        // chain's ~98 (round-5 ablation builds, profiles/r05/k2_tail_ablation.txt).
         if (!(on && best <= cur)) continue;
-        if constexpr (TSPGPU_TAIL_ABL & 8) continue;
         const unsigned long long linc = atomicMin(a.inc, (unsigned long long)ENum<V>::bits(best));
         cur = ENum<V>::vmin(ENum<V>::val(linc), best);
-        if constexpr (TSPGPU_TAIL_ABL & 64) {
-            stat_line(a)[8] = (unsigned long long)ENum<V>::bits(cur);  // (keeps the ablated value alive; padding word)
-            continue;
-        }
         // order pi of the four: lexicographic permutation pi of {0,1,2,3},
         // decoded arithmetically (a __constant__ table read per step was a
         // dependent memory round trip per order: ~18 us of the 16-city chain)
@@ -620,10 +611,6 @@ __device__ __forceinline__ void tail_wide(const SearchArgs &a, const V *dl, cons
                 if (c + d04[A3] <= cur) pass |= 1u << PI;
             },
             std::make_integer_sequence<int, 24>{});
-        if constexpr (TSPGPU_TAIL_ABL & 32) {
-            stat_line(a)[8] = pass;
-            continue;
-        }
         if (!pass) continue;
         // keys first (VALU only), then the slot range and the tie offer issued
         // back to back (the offer's wait covers both round trips), then the
@@ -653,11 +640,7 @@ __device__ __forceinline__ void tail_wide(const SearchArgs &a, const V *dl, cons
             }
         }
         unsigned int slot = atomicAdd(a.rec_count, (unsigned int)__builtin_popcount(pass));  // (as tail_one)
-        if constexpr (TSPGPU_TAIL_ABL & 128) {
-            stat_line(a)[8] = slot;
-            continue;
-        }
-        if (kpi >= 0 && !(TSPGPU_TAIL_ABL & 16)) {
+        if (kpi >= 0) {
             int ax[4];
             const V total = total_of(kpi, ax);
             const int ord[TL] = {ti, tj, sel4(r, ax[0]), sel4(r, ax[1]), sel4(r, ax[2]), sel4(r, ax[3])};
@@ -692,7 +675,6 @@ constexpr uint32_t kTailWide = 4;
 template <typename V, int TL>
 __global__ __launch_bounds__(256) void tail_kernel(SearchArgs a)
 {
-    if constexpr (TSPGPU_TAIL_ABL & 1) return;
     __shared__ V dl[kSearchMaxN * kTRow];
     __shared__ V am[kSearchMaxN];
     __shared__ uint32_t wq[4][128];
@@ -711,7 +693,6 @@ __global__ __launch_bounds__(256) void tail_kernel(SearchArgs a)
     for (int i = threadIdx.x; i < n * n; i += blockDim.x) dl[(i / n) * kTRow + i % n] = gd[i];
     for (int i = threadIdx.x; i < n; i += blockDim.x) am[i] = ga[i];
     __syncthreads();
-    if constexpr (TSPGPU_TAIL_ABL & 2) return;
 
     const uint32_t full = (uint32_t)((1ull << n) - 1ull) & ~1u;
     const int lane = __lane_id();
@@ -738,7 +719,6 @@ __global__ __launch_bounds__(256) void tail_kernel(SearchArgs a)
             const uint32_t idx = act ? q[qn - take + lane] : 0u;
             __builtin_amdgcn_wave_barrier();
             qn -= take;
-            if constexpr (TSPGPU_TAIL_ABL & 4) continue;
             if constexpr (TL == 6) {
                 if (take <= kTailWide) {
                     tail_wide<V, TL>(a, dl, am, full, idx, act, lanes, tcache);

@@ -54,44 +54,25 @@ __host__ __device__ constexpr size_t sub_img_bytes(int N, int L, int vb)
 {
     return (size_t)(N + (N - L)) * sub_ds(L) * vb;
 }
-// One low layer in LDS at a time (TSPGPU_SUB_ONE_LAYER): a middle pass loads
-// its rows' values into registers, the workgroup passes a barrier, and the
-// next layer is written over the one just read — the region is the largest
-// layer, C(10,5) x 5 = 1260 values (10 KB), instead of two adjacent layers
-// (20 KB), so the block's LDS drops from 24.5 to 14.5 KB and occupancy is set
-// by registers alone.
-#ifndef TSPGPU_SUB_ONE_LAYER
-#define TSPGPU_SUB_ONE_LAYER 0  // measured 5% slower (the extra barrier), profiles/r03/k1_ab_table.log run 8
-#endif
-__host__ __device__ constexpr int sub_region_vals(int L)
-{
-    if (!TSPGPU_SUB_ONE_LAYER) return tiled_region_vals(L);
-    int m = 0;
-    for (int j = 0; j <= L; ++j) m = tiled_layer_vals(L, j) > m ? tiled_layer_vals(L, j) : m;
-    return m;
-}
-// where layer j starts in the region
+// the region holds the two live low layers (tiled_region_vals): layer j at
+// the bottom when j is even, at the top when odd
+__host__ __device__ constexpr int sub_region_vals(int L) { return tiled_region_vals(L); }
 __host__ __device__ constexpr int sub_layer_off(int L, int j)
 {
-    return (!TSPGPU_SUB_ONE_LAYER && (j & 1)) ? tiled_region_vals(L) - tiled_layer_vals(L, j) : 0;
+    return (j & 1) ? tiled_region_vals(L) - tiled_layer_vals(L, j) : 0;
 }
-// Overlapped edge passes (TSPGPU_SUB_OVERLAP): passes 0/1 of sub-cube h + 1
+// Overlapped edge passes (256-thread workgroups): passes 0/1 of sub-cube h + 1
 // run during the last middle pass of h and pass L of h during the first middle
-// pass of h + 1, on the waves those passes leave idle, and pass L - 1's push
-// values are staged into LDS during middle pass L - 3 — the separate edge
-// interval A(h) and its exposed memory round trips go away (diagnostic stamps:
-// the two edge intervals took 33% of a block's time for 13% of its
-// relaxations).  Needs layer 2 of the next sub-cube outside the region
-// (C(L,2) x 2 values) and the staged values (L rows x H).
-#ifndef TSPGPU_SUB_OVERLAP
-#define TSPGPU_SUB_OVERLAP 2  // 2: with the edge passes' push values staged in LDS (-3% forward, profiles/r05)
-#endif
+// pass of h + 1, on the waves those passes leave idle; the push values of
+// passes 0/1, L - 1 and L are staged into LDS one pass earlier — the separate
+// edge interval and its exposed memory round trips go away (round 5: -3%
+// forward, profiles/r05).  Needs layer 2 of the next sub-cube outside the
+// region (C(L,2) x 2 values) and the staged values.
 __host__ __device__ constexpr int sub_l2_vals(int L) { return cbinom(L, 2) * 2; }
 __host__ __device__ constexpr size_t sub_lds_bytes(int N, int L, int vb)
 {
     return sub_img_bytes(N, L, vb) + (size_t)2 * 16 * vb + (size_t)sub_region_vals(L) * vb + (size_t)16 * vb +
-           (TSPGPU_SUB_OVERLAP ? (size_t)(sub_l2_vals(L) + L * (N - L)) * vb : 0) +
-           (TSPGPU_SUB_OVERLAP >= 2 ? (size_t)((L + 1) * (N - L) + (N - L)) * vb : 0);
+           (size_t)(sub_l2_vals(L) + L * (N - L)) * vb + (size_t)((L + 1) * (N - L) + (N - L)) * vb;
 }
 
 template <typename V, int N, int L>
@@ -101,12 +82,11 @@ struct SubCtx {
     V *region;         // live low layers (as variant 5)
     V *layerL;         // G[h | full low][m], m low: written by pass L-1, read by pass L
     V *layer2;         // layer 2 (passes 0/1 write it, middle pass 2 reads it): the region's
-                       // bottom, or its own area when the edge passes overlap (TSPGPU_SUB_OVERLAP)
-    V *pst;            // pass L-1's push values staged in LDS (TSPGPU_SUB_OVERLAP): [row][i]
-    V *fst;            // passes 0/1's push values (TSPGPU_SUB_OVERLAP >= 2): [i] row 0, [H + a*H + i] row {a}
-    V *lst;            // pass L's push values (TSPGPU_SUB_OVERLAP >= 2): [i]
-    int ov;            // the overlap level this kernel runs (TSPGPU_SUB_OVERLAP; 0 below 256 threads)
-    const V *dg;       // this block's distance matrix in global memory (n x n; TSPGPU_SUB_SHH)
+                       // bottom, or its own area when the edge passes overlap
+    V *pst;            // pass L-1's push values staged in LDS (overlapped edge passes): [row][i]
+    V *fst;            // passes 0/1's push values: [i] row 0, [H + a*H + i] row {a}
+    V *lst;            // pass L's push values: [i]
+    int ov;            // 2: overlapped edge passes (256-thread workgroups), 0: separate edge intervals
     Rsrc<V> push;      // this block's push area
     Rsrc<uint64_t> par;  // this block's parent words
 };
@@ -196,9 +176,6 @@ __device__ __forceinline__ void relax_min3(int32_t &a, int32_t g0, int32_t d0, i
         : [a] "+v"(a), [t0] "=&v"(t0), [t1] "=&v"(t1)
         : [g0] "v"(g0), [d0] "v"(d0), [g1] "v"(g1), [d1] "v"(d1));
 }
-#ifndef TSPGPU_SUB_MIN3
-#define TSPGPU_SUB_MIN3 1  // i32 middle passes: member pairs per destination through v_min3_i32
-#endif
 __device__ __forceinline__ void relax_min2(int32_t &a0, int32_t g0, int32_t d0, int32_t &a1, int32_t g1, int32_t d1)
 {
     int32_t t0, t1;
@@ -210,12 +187,6 @@ __device__ __forceinline__ void relax_min2(int32_t &a0, int32_t g0, int32_t d0, 
         : [a0] "+v"(a0), [a1] "+v"(a1), [t0] "=&v"(t0), [t1] "=&v"(t1)
         : [g0] "v"(g0), [d0] "v"(d0), [g1] "v"(g1), [d1] "v"(d1));
 }
-#ifndef TSPGPU_SUB_PAIR
-#define TSPGPU_SUB_PAIR 1  // middle passes: min-only relaxations two at a time (relax_min2)
-#endif
-#ifndef TSPGPU_SUB_SB
-#define TSPGPU_SUB_SB 1  // middle passes: a scheduling barrier after every SB relaxation pairs
-#endif
 
 // generic relaxation with a first-member initialisation (edge passes)
 template <bool ARG, typename V>
@@ -344,128 +315,42 @@ __host__ __device__ constexpr int sub_lds_role(int k)
     return -1;
 }
 
-// Timing-only ablations (measurement builds, tools/ab_build.sh; the results
-// are WRONG): 1 = the middle passes take their high members' values from the
-// LDS region instead of the push loads, 2 = no LDS distance gathers (one
-// register value), 4 = no barrier between the middle passes, 8 = no push
-// stores in the middle passes, 16 = the sub-cube barriers wait for LDS only,
-// 32 = the middle passes' push loads all read one L2-resident row (the loads
-// stay, their memory traffic goes), 64 = the middle passes' push stores all
-// write one L2-resident row (likewise), 128 = both, for the lowest high city's
-// columns only (a fifth of the traffic)
-#ifndef TSPGPU_SUB_ABL
-#define TSPGPU_SUB_ABL 0
-#endif
+constexpr int kSubQC = 7;     // destinations relaxed together (register budget)
+constexpr int kSubAhead = 6;  // distance loads in flight per lane
 
-#ifndef TSPGPU_SUB_QC
-#define TSPGPU_SUB_QC 7  // destinations relaxed together (register budget)
-#endif
-#ifndef TSPGPU_SUB_AHEAD
-#define TSPGPU_SUB_AHEAD 6  // distance loads in flight per lane
-#endif
-
-// Push columns recycled (TSPGPU_SUB_RECYCLE).  Column (h', x) is written by
-// sub-cube h' \ x and read by sub-cube h' only, so in the numeric sub-cube
-// order it is live over [h' \ x, h']; first-fit over those intervals gives
-// 23 columns at H = 5 instead of 80 (184 KB per block instead of 640 KB), and
-// the six resident blocks of a CU then touch ~280 MB of pushes instead of ~1
-// GB — close to the 256 MB Infinity Cache.  (Ablations, profiles/r04: push
-// loads and stores redirected to one L2-resident row -18% forward time.)
-#ifndef TSPGPU_SUB_RECYCLE
-#define TSPGPU_SUB_RECYCLE 0
-#endif
-template <int H>
-struct SubColMap {
-    uint32_t slot[(1 << H) * H];
-    int count;
-};
-template <int H>
-constexpr SubColMap<H> sub_col_map()
-{
-    SubColMap<H> m{};
-    int until[(1 << H) * H] = {};  // per column slot: the consumer sub-cube of its current column
-    int n = 0;
-    for (int p = 0; p < (1 << H); ++p)  // producers in the forward order
-        for (int x = 0; x < H; ++x) {
-            if ((p >> x) & 1) continue;
-            const int hp = p | (1 << x);
-            int s = -1;
-            for (int k = 0; k < n && s < 0; ++k)
-                if (until[k] < p) s = k;  // (its consumer has finished)
-            if (s < 0) s = n++;
-            until[s] = hp;
-            m.slot[hp * H + x] = (uint32_t)s;
-        }
-    m.count = n;
-    return m;
-}
-template <int H>
-__constant__ SubColMap<H> g_sub_cols = sub_col_map<H>();
-// the push column of (sub-cube hp, high city x)
+// the push column of (sub-cube hp, high city x): [hp][x] in the slot's push area
 template <int H>
 __device__ __forceinline__ uint32_t sub_col(uint32_t hp, uint32_t x)
 {
-    // (wave-uniform: a scalar load from the constant table)
-    if constexpr (TSPGPU_SUB_RECYCLE) return g_sub_cols<H>.slot[__builtin_amdgcn_readfirstlane(hp * H + x)];
     return hp * H + x;
 }
 
-// Deferred push stores (TSPGPU_SUB_DEFER).  Vector-memory operations retire
-// in issue order (one vmcnt per wave), so a pass's push loads, issued after
-// the previous pass's push stores, could only be used once those stores had
-// completed: every pass waited for the last one's write acknowledgements.  A
-// middle pass now keeps its high-destination results in registers (at most
-// H - |h| values per thread), issues the NEXT pass's push loads first and only
-// then these stores — the loads no longer queue behind them.  (Ablations,
-// profiles/r04: no middle push stores -18% forward time, no push loads -11%.)
-#ifndef TSPGPU_SUB_DEFER
-#define TSPGPU_SUB_DEFER 0  // measured slower: +14% forward time (62 VGPR spills), profiles/r04/k1_defer_ab.log
-#endif
-constexpr int kSubPend = 6;  // >= H - |h|
+// Measured and not kept (A/B logs under profiles/r03-r05; the switches were
+// removed from this header in round 6): one low layer in LDS (+5%), push
+// columns recycled into 23 slots with a prefix-set backtracking (+6%), push
+// stores deferred behind the next pass's loads (+14%, spills), the next pass's
+// push loads issued early (+18%: they wait behind older stores in the in-order
+// vmcnt), rotated wave roles, scalar loads of the high-high distances (+60%),
+// one |h| dispatch per sub-cube, a workgroup-form backtracking (no faster).
 
-// Early push loads (TSPGPU_SUB_EARLY).  A middle pass's high members' values
-// (push loads, memory latency) were issued at its start and needed after the
-// first J x QC relaxations: every pass exposed most of a memory round trip.
-// Thread r owns row r in every pass of a sub-cube and the high members of
-// pass J + 1 are pass J's (same h), so pass J issues pass J + 1's push loads
-// itself, AFTER its own relaxations and stores (registers are free there),
-// and they land during the barrier and the next pass's LDS reads.
-#ifndef TSPGPU_SUB_EARLY
-#define TSPGPU_SUB_EARLY 0
+// Next pass's push values loaded ahead (TSPGPU_SUB_PF, A/B): vector-memory
+// operations retire in issue order (one vmcnt per wave), so a pass's push
+// loads, issued at its start, also waited for the previous pass's push
+// stores' acknowledgements.  Thread r owns row r in every middle pass of a
+// sub-cube and the high members of pass J + 1 are pass J's, so pass J issues
+// pass J + 1's push loads itself — BEFORE its own push stores (1: between its
+// last chunk's relaxations and the global stores; 2: before the last chunk's
+// relaxations), which puts its stores behind the loads in the vmcnt order.
+// (Round 5's early loads were issued after the stores and lost.)  The last
+// chunk holds every high destination (chunks [0, Q - QC) and [Q - QC, Q)).
+#ifndef TSPGPU_SUB_PF
+#define TSPGPU_SUB_PF 0
 #endif
-// Diagnostic build (TSPGPU_SUB_STAMP): per wave, the shader clock spent in the
-// middle-pass bodies, at their barriers, in the edge intervals and in the whole
-// block, written over the block's tour words (tour_out[blk*(n+1) + 4*wave + k],
-// k = body, barrier, edge, total; the backtracking kernel is skipped).  The
-// results are not tours in such a build.
-#ifndef TSPGPU_SUB_STAMP
-#define TSPGPU_SUB_STAMP 0
-#endif
-__device__ __forceinline__ uint32_t sub_clock()
-{
-    return (uint32_t)__builtin_amdgcn_s_memtime();
-}
-// Wave roles rotated (TSPGPU_SUB_ROT): the rows of a pass go to the threads
-// in wave order, so wave 0 of every workgroup works in every pass and wave 3
-// in three of seven; with the workgroups of a CU placing wave w on SIMD w, one
-// SIMD would carry all the heaviest waves.  1: the roles rotate by the
-// workgroup's index, 2: by workgroup and sub-cube (every wave gets every role
-// in turn).  Any bijection is valid: passes hand over only through LDS and
-// memory behind barriers.
-#ifndef TSPGPU_SUB_ROT
-#define TSPGPU_SUB_ROT 0
-#endif
-#ifndef TSPGPU_SUB_SHH
-#define TSPGPU_SUB_SHH 0
-#endif
-// one |h| dispatch per sub-cube around all middle passes (instead of one per pass)
-#ifndef TSPGPU_SUB_MIDSWITCH
-#define TSPGPU_SUB_MIDSWITCH 0
-#endif
+constexpr int kSubPre = 6;  // >= H
 
 template <typename V, int N, int L, int T, int J>
 __device__ __forceinline__ void sub_mid(const SubCtx<V, N, L> &c, uint32_t h, uint32_t tid, const uint4 &ent,
-                                        V (&pend)[kSubPend], V (&pre)[kSubPend])
+                                        V (&pre)[kSubPre])
 {
     constexpr int H = N - L;
     constexpr int Q = N - T;
@@ -499,16 +384,12 @@ __device__ __forceinline__ void sub_mid(const SubCtx<V, N, L> &c, uint32_t h, ui
             nb &= nb - 1u;
         }
     }
-    // high-high distances of this sub-cube: wave-uniform (TSPGPU_SUB_SHH:
-    // scalar loads from the block's matrix in memory, no LDS read and no
-    // v_readfirstlane; else from the LDS image)
+    // high-high distances of this sub-cube: wave-uniform, from the LDS image
     V hh[HC * QH > 0 ? HC * QH : 1];
 #pragma unroll
     for (int i = 0; i < HC; ++i)
 #pragma unroll
-        for (int u = 0; u < QH; ++u)
-            hh[i * QH + u] = TSPGPU_SUB_SHH ? c.dg[(L + 1 + hm[i]) * (N + 1) + (L + 1 + hn[u])]
-                                            : uniform_val<V>(c.img, HR0 + i * DSB + HC0 + u * VB);
+        for (int u = 0; u < QH; ++u) hh[i * QH + u] = uniform_val<V>(c.img, HR0 + i * DSB + HC0 + u * VB);
     const uint32_t r = tid;
     const bool act = r < (uint32_t)ROWS;
     V g[T];
@@ -517,24 +398,16 @@ __device__ __forceinline__ void sub_mid(const SubCtx<V, N, L> &c, uint32_t h, ui
 #pragma unroll
         for (int p = 0; p < J; ++p) g[p] = act ? src[p * ROWS + r] : V(0);
     }
-    // (one layer in LDS: every wave has its row's values before any of the
-    // next layer overwrites them)
-    if (TSPGPU_SUB_ONE_LAYER) lds_barrier();
     const uint32_t voff = (BASE + r) * VB;  // the row's offset in a push column
-    constexpr bool PRE_IN = TSPGPU_SUB_EARLY && J > 2, PRE_OUT = TSPGPU_SUB_EARLY && J < L - 2;
+    constexpr bool PF_IN = TSPGPU_SUB_PF && J > 2, PF_OUT = TSPGPU_SUB_PF && J < L - 2;
     if (act) {
 #pragma unroll
         for (int i = 0; i < HC; ++i)
-            g[J + i] = (TSPGPU_SUB_ABL & 1)    ? c.region[CUR + (i % J) * ROWS + r]
-                       : (TSPGPU_SUB_ABL & 32) ? c.push.load(r * VB, 0)
-                       : ((TSPGPU_SUB_ABL & 128) && hm[i] == 0) ? c.push.load(r * VB, 0)
-                       : PRE_IN                ? pre[i]
-                                               : c.push.load(voff, sub_col<H>(h, hm[i]) * (uint32_t)(NL * VB));
+            g[J + i] = PF_IN ? pre[i] : c.push.load(voff, sub_col<H>(h, hm[i]) * (uint32_t)(NL * VB));
     }
-    // pass J + 1's push loads (TSPGPU_SUB_EARLY): by this thread, which owns
-    // row r there too; after everything else of this pass
+    // pass J + 1's push values (this thread owns row r there too)
     auto prefetch = [&] {
-        if constexpr (PRE_OUT && HC > 0) {
+        if constexpr (PF_OUT && HC > 0) {
             constexpr int ROWS_X = cbinom(L, J + 1), BASE_X = tiled_moff(L, J + 1);
             __builtin_amdgcn_sched_barrier(0);
             if (r < (uint32_t)ROWS_X) {
@@ -542,21 +415,9 @@ __device__ __forceinline__ void sub_mid(const SubCtx<V, N, L> &c, uint32_t h, ui
                 for (int i = 0; i < HC; ++i)
                     pre[i] = c.push.load((BASE_X + r) * VB, sub_col<H>(h, hm[i]) * (uint32_t)(NL * VB));
             }
+            __builtin_amdgcn_sched_barrier(0);
         }
-        // (every entry redefined here: none stays live through a pass)
-#pragma unroll
-        for (int i = PRE_OUT ? HC : kSubPend; i < kSubPend; ++i) pre[i] = V(0);
     };
-    // the previous middle pass's pushes, behind this pass's loads
-    constexpr bool DEFER_IN = TSPGPU_SUB_DEFER && J > 2, DEFER_OUT = TSPGPU_SUB_DEFER && J < L - 2;
-    if constexpr (DEFER_IN) {
-        constexpr int ROWS_P = cbinom(L, J - 1), BASE_P = tiled_moff(L, J - 1);
-        if (r < (uint32_t)ROWS_P) {
-#pragma unroll
-            for (int u = 0; u < QH; ++u)
-                c.push.store((BASE_P + r) * VB, sub_col<H>(h | (1u << hn[u]), hn[u]) * (uint32_t)(NL * VB), pend[u]);
-        }
-    }
     if (!act) {
         prefetch();
         return;
@@ -571,23 +432,27 @@ __device__ __forceinline__ void sub_mid(const SubCtx<V, N, L> &c, uint32_t h, ui
 #pragma unroll
     for (int i = 0; i < HC; ++i) hrow[i] = (L + hm[i]) * DSB;
     uint32_t wlo = 0, whi = 0;
-    constexpr int QC = TSPGPU_SUB_QC;
-    static_for<(Q + QC - 1) / QC>([&](auto ci) {
-        constexpr int C0 = decltype(ci)::value * QC;
-        constexpr int QN = Q - C0 < QC ? Q - C0 : QC;
+    constexpr int QC = kSubQC;
+    constexpr int NC = (Q + QC - 1) / QC;
+    static_assert(NC <= 2 && QH <= QC, "chunks");
+    static_for<NC>([&](auto ci) {
+        constexpr int CI = decltype(ci)::value;
+        // (TSPGPU_SUB_PF: the last chunk holds every high destination)
+        constexpr int C0 = TSPGPU_SUB_PF ? (CI == 0 ? 0 : Q - QC) : CI * QC;
+        constexpr int QN = TSPGPU_SUB_PF ? (NC == 1 ? Q : (CI == 0 ? Q - QC : QC)) : (Q - C0 < QC ? Q - C0 : QC);
+        constexpr bool LAST = CI == NC - 1;
+        if constexpr (LAST && TSPGPU_SUB_PF == 2) prefetch();
         constexpr int CNT = sub_lds_count<T, J, QL, C0, QN>();
-        constexpr int AH = TSPGPU_SUB_AHEAD < CNT ? TSPGPU_SUB_AHEAD : CNT;
+        constexpr int AH = kSubAhead < CNT ? kSubAhead : CNT;
         // integer min-only rows: member pairs per destination (v_min3_i32)
-        constexpr bool QP = TSPGPU_SUB_MIN3 && !ARG && std::is_same<V, int32_t>::value;
+        constexpr bool QP = !ARG && std::is_same<V, int32_t>::value;
         V acc[QN];
         uint32_t arg[ARG ? QN : 1];
         // distance of LDS relaxation k (compile-time pair)
         auto dload = [&](auto kk) -> V {
             constexpr int pq = sub_lds_pair<T, J, QL, C0, QN, QP>(decltype(kk)::value);
             constexpr int p = pq / 64, q = C0 + pq % 64;
-            if constexpr (TSPGPU_SUB_ABL & 2)
-                return g[p] + g[0];  // (ablation: no gather)
-            else if constexpr (p < J && q < QL)
+            if constexpr (p < J && q < QL)
                 return lds_val<V>(c.img, mrow[p] + kof[q]);
             else if constexpr (p < J)
                 return lds_val<V>(c.img, mrow[p] + HC0 + (q - QL) * VB);
@@ -633,7 +498,7 @@ __device__ __forceinline__ void sub_mid(const SubCtx<V, N, L> &c, uint32_t h, ui
                     __builtin_amdgcn_sched_barrier(0);
                 }
             });
-        } else if constexpr (TSPGPU_SUB_PAIR && !ARG) {
+        } else if constexpr (!ARG) {
             static_for<(CNT + 1) / 2>([&](auto kk2) {
                 constexpr int k0 = 2 * decltype(kk2)::value, k1 = k0 + 1;
                 constexpr int pq0 = sub_lds_pair<T, J, QL, C0, QN, QP>(k0);
@@ -649,7 +514,7 @@ __device__ __forceinline__ void sub_mid(const SubCtx<V, N, L> &c, uint32_t h, ui
                     relax_one(std::integral_constant<int, k0>{});
                     if constexpr (k1 < CNT) relax_one(std::integral_constant<int, k1>{});
                 }
-                if constexpr ((decltype(kk2)::value + 1) % TSPGPU_SUB_SB == 0) __builtin_amdgcn_sched_barrier(0);
+                __builtin_amdgcn_sched_barrier(0);
             });
         } else {
             static_for<CNT>([&](auto kk) {
@@ -670,6 +535,36 @@ __device__ __forceinline__ void sub_mid(const SubCtx<V, N, L> &c, uint32_t h, ui
                         relax_min_s(acc[qq], g[J + i], hh[i * QH + (q - QL)]);
                 }
             }
+        if constexpr (TSPGPU_SUB_PF) {
+            // low destinations (LDS), the next pass's push loads, then the
+            // high destinations (push stores) and the parent word
+#pragma unroll
+            for (int qq = 0; qq < QN; ++qq) {
+                const int q = C0 + qq;
+                if (q < QL) {
+                    const uint32_t k = kof[q] / VB;
+                    const uint32_t slot = (k - (uint32_t)q) * (uint32_t)ROWS_N + sub_rank(ent, q);
+                    c.region[NXT + slot] = acc[qq];
+                }
+                if constexpr (ARG) {
+                    const uint32_t pos = arg[qq] / DSB;
+                    if (q < 8)
+                        wlo |= pos << (4 * q);
+                    else
+                        whi |= pos << (4 * (q - 8));
+                }
+            }
+            if constexpr (LAST && TSPGPU_SUB_PF == 1) prefetch();
+#pragma unroll
+            for (int qq = 0; qq < QN; ++qq) {
+                const int q = C0 + qq;
+                if (q >= QL) {
+                    const uint32_t cb = hn[q - QL];
+                    c.push.store(voff, sub_col<H>(h | (1u << cb), cb) * (uint32_t)(NL * VB), acc[qq]);
+                }
+            }
+            return;
+        }
 #pragma unroll
         for (int qq = 0; qq < QN; ++qq) {
             const int q = C0 + qq;
@@ -681,12 +576,7 @@ __device__ __forceinline__ void sub_mid(const SubCtx<V, N, L> &c, uint32_t h, ui
             } else {
                 // high k -> push column (h | k, k) of sub-cube h | k, same row index
                 const uint32_t cb = hn[q - QL];
-                if ((TSPGPU_SUB_ABL & 64) || ((TSPGPU_SUB_ABL & 128) && cb == 0))
-                    c.push.store(r * VB, 8192u, acc[qq]);
-                else if (DEFER_OUT)
-                    pend[q - QL] = acc[qq];  // (stored by the next pass, after its loads)
-                else if (!(TSPGPU_SUB_ABL & 8))
-                    c.push.store(voff, sub_col<H>(h | (1u << cb), cb) * (uint32_t)(NL * VB), acc[qq]);
+                c.push.store(voff, sub_col<H>(h | (1u << cb), cb) * (uint32_t)(NL * VB), acc[qq]);
             }
             if constexpr (ARG) {
                 const uint32_t pos = arg[qq] / DSB;  // image row of the argmin member = its city bit
@@ -698,7 +588,6 @@ __device__ __forceinline__ void sub_mid(const SubCtx<V, N, L> &c, uint32_t h, ui
         }
     });
     if constexpr (ARG) c.par.store((BASE + r) * 8u, h * (uint32_t)(NL * 8), ((uint64_t)whi << 32) | wlo);
-    prefetch();
 }
 
 // ---------------------------------------------------------------------------
@@ -867,7 +756,7 @@ __device__ __forceinline__ void sub_penult(const SubCtx<V, N, L> &c, uint32_t h,
 }
 
 // ---------------------------------------------------------------------------
-// Pass L-1's push values of sub-cube h (|h| = C) into LDS (TSPGPU_SUB_OVERLAP):
+// Pass L-1's push values of sub-cube h (|h| = C) into LDS (overlapped edge passes):
 // lane e < L * C loads row r = e / C (layer L-1, rank r) of push column
 // (h, hm_i), i = e % C, into pst[r * H + i] — by a wave that is idle in the
 // middle pass it runs beside, so the load's round trip is off the critical path.
@@ -885,8 +774,8 @@ __device__ __forceinline__ void sub_stage_penult(const SubCtx<V, N, L> &c, uint3
     }
 }
 
-// Passes 0/1's push values of sub-cube h (|h| = C) into LDS (TSPGPU_SUB_OVERLAP
-// >= 2): lanes e < C row 0 of column (h, hm_e); lanes C + a*C + i row {a} of
+// Passes 0/1's push values of sub-cube h (|h| = C) into LDS (overlapped edge
+// passes): lanes e < C row 0 of column (h, hm_e); lanes C + a*C + i row {a} of
 // column (h, hm_i), a < L.
 template <typename V, int N, int L, int C>
 __device__ __forceinline__ void sub_stage_first(const SubCtx<V, N, L> &c, uint32_t h, uint32_t lane)
@@ -944,12 +833,12 @@ __device__ __forceinline__ void sub_build_high(const SubCtx<V, N, L> &c, uint32_
 
 template <typename V, int N, int L, int J>
 __device__ __forceinline__ void sub_dispatch_mid_j(const SubCtx<V, N, L> &c, uint32_t h, int hc, uint32_t tid,
-                                                   const uint4 &ent, V (&pend)[kSubPend], V (&pre)[kSubPend])
+                                                   const uint4 &ent, V (&pre)[kSubPre])
 {
     constexpr int H = N - L;
 #define TSPGPU_SM(HC)                                                                                  \
     case HC:                                                                                           \
-        if constexpr (HC <= H) sub_mid<V, N, L, J + (HC <= H ? HC : 0), J>(c, h, tid, ent, pend, pre);  \
+        if constexpr (HC <= H) sub_mid<V, N, L, J + (HC <= H ? HC : 0), J>(c, h, tid, ent, pre);  \
         break;
     switch (hc) {
         TSPGPU_SM(0) TSPGPU_SM(1) TSPGPU_SM(2) TSPGPU_SM(3) TSPGPU_SM(4) TSPGPU_SM(5) TSPGPU_SM(6) TSPGPU_SM(7)
@@ -1019,14 +908,8 @@ __device__ __forceinline__ void sub_dispatch_last(const SubCtx<V, N, L> &c, uint
 // Forward pass + closing min of blocks blk0 + blockIdx.x, +gridDim.x, ...;
 // writes cost_out[blk] and the tour's last inner city (tour[n-1]) like
 // hk_tiled_kernel; hk_tiled_backtrack completes the tour from the slot.
-// (TSPGPU_SUB_WG_OVERRIDE: a measurement build's occupancy for every
-// configuration; the host then sizes the grid from TSPGPU_WG_PER_CU)
-#ifndef TSPGPU_SUB_WG_OVERRIDE
-#define TSPGPU_SUB_WG_OVERRIDE 0
-#endif
-__host__ __device__ constexpr int sub_wg(int wg) { return TSPGPU_SUB_WG_OVERRIDE > 0 ? TSPGPU_SUB_WG_OVERRIDE : wg; }
 template <typename V, int N, int L, int THREADS, int WG>
-__global__ __launch_bounds__(THREADS, tiled_waves(THREADS, sub_wg(WG))) void hk_sub_kernel(
+__global__ __launch_bounds__(THREADS, tiled_waves(THREADS, WG)) void hk_sub_kernel(
     const V *__restrict__ dist, int nblocks, int blk0, char *__restrict__ slots, uint32_t slot_bytes,
     const SubRow *__restrict__ rows, V *__restrict__ cost_out, int32_t *__restrict__ tour_out)
 {
@@ -1042,7 +925,6 @@ __global__ __launch_bounds__(THREADS, tiled_waves(THREADS, sub_wg(WG))) void hk_
     // their virtual lanes (pass 0/1 lanes 0..191, pass L 192..; pass L-1
     // lanes 0..127, the next sub-cube's image rows 128..) over the workgroup
     static_assert(THREADS % 64 == 0 && THREADS >= cbinom(L, L / 2), "one row per thread in a middle pass");
-    static_assert(!TSPGPU_SUB_ROT || (THREADS & (THREADS - 1)) == 0, "rotated roles: a power-of-two workgroup");
     static_assert(L * (N - 1) + H <= 192 && L * 8 <= 128, "edge intervals: virtual lane layout");
     // static LDS: image/region offsets fold into immediates (A/B against
     // dynamic LDS: equal within noise, profiles/r03/k1_ab_table.log)
@@ -1055,7 +937,7 @@ __global__ __launch_bounds__(THREADS, tiled_waves(THREADS, sub_wg(WG))) void hk_
     c.region = dc + 16;
     c.layerL = c.region + sub_region_vals(L);
     // (the overlapped edge passes need the idle waves of a 256-thread workgroup)
-    constexpr int OV = THREADS == 256 ? TSPGPU_SUB_OVERLAP : 0;
+    constexpr int OV = THREADS == 256 ? 2 : 0;
     c.ov = OV;
     c.layer2 = OV ? c.layerL + 16 : c.region + sub_layer_off(L, 2);
     c.pst = c.layerL + 16 + sub_l2_vals(L);
@@ -1069,7 +951,6 @@ __global__ __launch_bounds__(THREADS, tiled_waves(THREADS, sub_wg(WG))) void hk_
         c.push.rs = uniform_rsrc(slot, (uint32_t)tiled_push_bytes(N, L, VB));
         c.par.rs = uniform_rsrc(slot + tiled_push_bytes(N, L, VB), (uint32_t)tiled_parent_bytes(N, L));
         const V *dsrc = dist + (size_t)blk * n * n;
-        c.dg = dsrc;
         // natural image (inner distances) and, for sub-cube 0 (no high
         // member), the high columns in order
         for (int i = tid; i < N * N; i += THREADS) {
@@ -1087,25 +968,14 @@ __global__ __launch_bounds__(THREADS, tiled_waves(THREADS, sub_wg(WG))) void hk_
         __syncthreads();
 
         uint4 ent = make_uint4(0, 0, 0, 0);
-        V pend[kSubPend];  // deferred push stores of the last middle pass (TSPGPU_SUB_DEFER)
-        V pre[kSubPend];   // the next middle pass's push values (TSPGPU_SUB_EARLY)
+        V pre[kSubPre];  // the next middle pass's push values (TSPGPU_SUB_PF)
 #pragma unroll
-        for (int u = 0; u < kSubPend; ++u) pend[u] = pre[u] = V(0);
-        uint32_t st_body = 0, st_bar = 0, st_edge = 0, st_t0 = 0, st_a = 0;
-        uint64_t st_rt0 = 0;
-        if (TSPGPU_SUB_STAMP) {
-            st_t0 = sub_clock();
-            st_rt0 = __builtin_amdgcn_s_memrealtime();
-        }
+        for (int i = 0; i < kSubPre; ++i) pre[i] = V(0);
         for (uint32_t h = 0; h < (uint32_t)NH; ++h) {
             const int hc = __builtin_popcount(h);
-            if (TSPGPU_SUB_STAMP) st_a = sub_clock();
-            // this sub-cube's thread -> role map (TSPGPU_SUB_ROT; whole waves)
-            const uint32_t rot = TSPGPU_SUB_ROT == 2 ? (uint32_t)blockIdx.x + h : (TSPGPU_SUB_ROT == 1 ? (uint32_t)blockIdx.x : 0u);
-            const uint32_t vtid = TSPGPU_SUB_ROT ? (tid + 64u * rot) & (uint32_t)(THREADS - 1) : tid;
             // interval A(h): passes 0/1 of h (lanes < 192) beside pass L of h - 1 (lanes 192..)
-            // (TSPGPU_SUB_OVERLAP: at h = 0 only; later they run inside the middle passes)
-            uint32_t t = opaque_u32(vtid);
+            // (overlapped: at h = 0 only; later they run inside the middle passes)
+            uint32_t t = opaque_u32(tid);
             {
                 constexpr int M2 = tiled_moff(L, 2), C2 = cbinom(L, 2);
                 ent = rowtab[M2 + (t < (uint32_t)C2 ? t : 0u)];
@@ -1119,101 +989,47 @@ __global__ __launch_bounds__(THREADS, tiled_waves(THREADS, sub_wg(WG))) void hk_
                     else if (h > 0)
                         sub_dispatch_last<V, N, L>(c, h - 1, __builtin_popcount(h - 1), v - 192u);
                 }
-                if (TSPGPU_SUB_ABL & 16) lds_barrier(); else __syncthreads();
-            }
-            if (TSPGPU_SUB_STAMP) {
-                const uint32_t tb = sub_clock();
-                st_edge += tb - st_a;
-                st_a = tb;
+                __syncthreads();
             }
             // middle passes j = 2..L-2, unrolled (every offset a compile-time
             // constant); the next pass's row entry is loaded one pass ahead
-            if constexpr (TSPGPU_SUB_MIDSWITCH) {
-                // one dispatch on |h| per sub-cube around all middle passes:
-                // each case is one straight-line sequence (the compiler's
-                // wait counters and register lifetimes see across passes)
-                auto mids = [&](auto hcc) {
-                    constexpr int HC = decltype(hcc)::value;
-                    static_for<L - 3>([&](auto jj) {
-                        constexpr int j = 2 + decltype(jj)::value;
-                        const uint4 cur = ent;
-                        const uint32_t tj = opaque_u32(vtid);
-                        if constexpr (j + 1 <= L - 2) {
-                            constexpr int MN = tiled_moff(L, j + 1), CN = cbinom(L, j + 1);
-                            ent = rowtab[MN + (tj < (uint32_t)CN ? tj : 0u)];
-                        }
-                        sub_mid<V, N, L, j + HC, j>(c, h, tj, cur, pend, pre);
-                        if (!(TSPGPU_SUB_ABL & 4)) lds_barrier();
-                    });
-                };
-                switch (hc) {
-                case 0: mids(std::integral_constant<int, 0>{}); break;
-                case 1: if constexpr (H >= 1) mids(std::integral_constant<int, (H >= 1 ? 1 : 0)>{}); break;
-                case 2: if constexpr (H >= 2) mids(std::integral_constant<int, (H >= 2 ? 2 : 0)>{}); break;
-                case 3: if constexpr (H >= 3) mids(std::integral_constant<int, (H >= 3 ? 3 : 0)>{}); break;
-                case 4: if constexpr (H >= 4) mids(std::integral_constant<int, (H >= 4 ? 4 : 0)>{}); break;
-                case 5: if constexpr (H >= 5) mids(std::integral_constant<int, (H >= 5 ? 5 : 0)>{}); break;
-                case 6: if constexpr (H >= 6) mids(std::integral_constant<int, (H >= 6 ? 6 : 0)>{}); break;
-                default: break;
+            static_for<L - 3>([&](auto jj) {
+                constexpr int j = 2 + decltype(jj)::value;
+                const uint4 cur = ent;
+                const uint32_t tj = opaque_u32(tid);
+                if constexpr (j + 1 <= L - 2) {
+                    constexpr int MN = tiled_moff(L, j + 1), CN = cbinom(L, j + 1);
+                    ent = rowtab[MN + (tj < (uint32_t)CN ? tj : 0u)];
                 }
-            } else {
-                static_for<L - 3>([&](auto jj) {
-                    constexpr int j = 2 + decltype(jj)::value;
-                    const uint4 cur = ent;
-                    const uint32_t tj = opaque_u32(vtid);
-                    if constexpr (j + 1 <= L - 2) {
-                        constexpr int MN = tiled_moff(L, j + 1), CN = cbinom(L, j + 1);
-                        ent = rowtab[MN + (tj < (uint32_t)CN ? tj : 0u)];
-                    }
-                    sub_dispatch_mid_j<V, N, L, j>(c, h, hc, tj, cur, pend, pre);
-                    if constexpr (OV) {
-                        // edge passes on the waves this middle pass leaves idle
-                        static_assert(cbinom(L, 2) <= 64 && cbinom(L, 3) <= 128 && cbinom(L, L - 3) <= 128, "overlap: idle waves");
-                        if constexpr (OV >= 2) {
-                            // pass 2: the edge passes' push values into LDS (waves 1-3);
-                            // pass 3: pass L of h - 1 from them (wave 3)
-                            if constexpr (j == 2) {
-                                if (tj >= 192u) {
-                                    if (h + 1 < (uint32_t)NH)
-                                        sub_dispatch_stage_first<V, N, L>(c, h + 1, __builtin_popcount(h + 1), tj - 192u);
-                                } else if (tj >= 128u) {
-                                    sub_dispatch_stage<V, N, L>(c, h, hc, tj - 128u);
-                                } else if (tj >= 64u && h > 0) {
-                                    sub_dispatch_stage_last<V, N, L>(c, h - 1, __builtin_popcount(h - 1), tj - 64u);
-                                }
-                            }
-                            if constexpr (j == 3) {
-                                if (h > 0 && tj >= 192u)
-                                    sub_dispatch_last<V, N, L>(c, h - 1, __builtin_popcount(h - 1), tj - 192u);
-                            }
-                        } else {
-                            if constexpr (j == 2) {  // pass L of h - 1 (its layerL is still in LDS)
-                                if (h > 0 && tj >= 64u)
-                                    sub_dispatch_last<V, N, L>(c, h - 1, __builtin_popcount(h - 1), tj - 64u);
-                            }
-                            if constexpr (j == L - 3) {  // pass L - 1's push values into LDS
-                                if (tj >= 128u) sub_dispatch_stage<V, N, L>(c, h, hc, tj - 128u);
-                            }
-                        }
-                        if constexpr (j == L - 2) {  // passes 0/1 of h + 1 (layer 2 in its own area)
-                            if (h + 1 < (uint32_t)NH && tj >= 64u)
-                                sub_dispatch_first<V, N, L>(c, h + 1, __builtin_popcount(h + 1), tj - 64u);
+                sub_dispatch_mid_j<V, N, L, j>(c, h, hc, tj, cur, pre);
+                if constexpr (OV) {
+                    // edge passes on the waves this middle pass leaves idle
+                    static_assert(cbinom(L, 2) <= 64 && cbinom(L, 3) <= 128 && cbinom(L, L - 3) <= 128, "overlap: idle waves");
+                    // pass 2: the edge passes' push values into LDS (waves 1-3);
+                    // pass 3: pass L of h - 1 from them (wave 3)
+                    if constexpr (j == 2) {
+                        if (tj >= 192u) {
+                            if (h + 1 < (uint32_t)NH)
+                                sub_dispatch_stage_first<V, N, L>(c, h + 1, __builtin_popcount(h + 1), tj - 192u);
+                        } else if (tj >= 128u) {
+                            sub_dispatch_stage<V, N, L>(c, h, hc, tj - 128u);
+                        } else if (tj >= 64u && h > 0) {
+                            sub_dispatch_stage_last<V, N, L>(c, h - 1, __builtin_popcount(h - 1), tj - 64u);
                         }
                     }
-                    uint32_t tm = 0;
-                    if (TSPGPU_SUB_STAMP) {
-                        tm = sub_clock();
-                        st_body += tm - st_a;
+                    if constexpr (j == 3) {
+                        if (h > 0 && tj >= 192u)
+                            sub_dispatch_last<V, N, L>(c, h - 1, __builtin_popcount(h - 1), tj - 192u);
                     }
-                    if (!(TSPGPU_SUB_ABL & 4)) lds_barrier();
-                    if (TSPGPU_SUB_STAMP) {
-                        st_a = sub_clock();
-                        st_bar += st_a - tm;
+                    if constexpr (j == L - 2) {  // passes 0/1 of h + 1 (layer 2 in its own area)
+                        if (h + 1 < (uint32_t)NH && tj >= 64u)
+                            sub_dispatch_first<V, N, L>(c, h + 1, __builtin_popcount(h + 1), tj - 64u);
                     }
-                });
-            }
+                }
+                lds_barrier();
+            });
             // pass L - 1 (lanes < 128) beside the next sub-cube's high image rows/columns (lanes 128..)
-            t = opaque_u32(vtid);
+            t = opaque_u32(tid);
 #pragma unroll
             for (uint32_t v0 = 0; v0 < 256u; v0 += THREADS) {
                 const uint32_t v = t + v0;
@@ -1222,19 +1038,7 @@ __global__ __launch_bounds__(THREADS, tiled_waves(THREADS, sub_wg(WG))) void hk_
                 else if (h + 1 < (uint32_t)NH)
                     sub_build_high<V, N, L>(c, h + 1, v - 128u);
             }
-            if (TSPGPU_SUB_ABL & 16) lds_barrier(); else __syncthreads();
-            if (TSPGPU_SUB_STAMP) st_edge += sub_clock() - st_a;
-        }
-        if (TSPGPU_SUB_STAMP) {
-            const uint32_t tot = sub_clock() - st_t0;
-            const uint64_t rt = __builtin_amdgcn_s_memrealtime() - st_rt0;  // 100 MHz constant clock
-            if ((tid & 63u) == 0) {
-                int32_t *w = tour_out + (size_t)blk * (n + 1) + 4 * (tid >> 6);
-                w[0] = (int32_t)st_body, w[1] = (int32_t)st_bar, w[2] = (int32_t)st_edge, w[3] = (int32_t)tot;
-            }
-            if (tid == 0) tour_out[(size_t)blk * (n + 1) + 16] = (int32_t)rt;  // (in-kernel clock = tot / rt x 100 MHz)
             __syncthreads();
-            continue;
         }
 
         // closing min (tsp.cpp:483-499): G[full][m] + d[m][0], first strict min
@@ -1264,386 +1068,9 @@ __global__ __launch_bounds__(THREADS, tiled_waves(THREADS, sub_wg(WG))) void hk_
     }
 }
 
-// ---------------------------------------------------------------------------
-// Backtracking of variant 6 with recycled push columns (TSPGPU_SUB_RECYCLE:
-// the forward pass no longer keeps every pushed value, so the rows below the
-// parent words cannot be recomputed from them).  One wave per block:
-// (1) the rows with >= N - TSPGPU_TILED_TA_OFF members: their parent words,
-//     as hk_tiled_backtrack;
-// (2) below: the first prefix set T0 = {t1..tK} (K = N - TA_OFF - 1 cities)
-//     gets its own Held-Karp, G[S][m] for every S within T0, in the slot's
-//     recompute area (2^K x K values) — the same recurrence over the same
-//     IEEE adds and mins, so the forward pass's bits (G[S][m] depends on S
-//     and m only; min is order-free) — and the walk continues with the first
-//     strict minimum over the members ascending (tsp.cpp:457-470), cities of
-//     T0 ascending = local indices ascending.
-// 10 * 9 * 2^8 = 23 K relaxations per 16-city block (1.3% of the forward
-// pass), against a recompute of whole sub-cube rows before.
-// ---------------------------------------------------------------------------
-constexpr int kSubBtWaves = 4;
-__host__ __device__ constexpr int sub_bt_k(int N) { return N - TSPGPU_TILED_TA_OFF - 1; }
-__host__ __device__ constexpr size_t sub_rec_bytes(int N, int vb) { return ((size_t)vb * sub_bt_k(N)) << sub_bt_k(N); }
-// one block's global slot for variant 6: push area, parent words and the
-// recompute area of either backtracking kernel
-__host__ __device__ constexpr size_t sub_slot_bytes(int N, int L, int vb)
-{
-    const size_t rec = tiled_recomp_bytes(L, vb) > sub_rec_bytes(N, vb) ? tiled_recomp_bytes(L, vb) : sub_rec_bytes(N, vb);
-    return tiled_push_bytes(N, L, vb) + tiled_parent_bytes(N, L) + ((rec + 255) & ~(size_t)255);
-}
-
-namespace {  // (internal linkage, like hk_tiled_backtrack)
-template <typename V, int N, int L>
-__global__ __launch_bounds__(64 * kSubBtWaves) void hk_sub_backtrack(int nblocks, int blk0,
-                                                                     const char *__restrict__ slots, uint32_t slot_bytes,
-                                                                     const TiledInfo *__restrict__ info,
-                                                                     const V *__restrict__ dist,
-                                                                     V *__restrict__ cost_out,
-                                                                     int32_t *__restrict__ tour_out)
-{
-    constexpr int NL = 1 << L, n = N + 1, VB = sizeof(V), K = sub_bt_k(N), NK = 1 << K;
-    static_assert(K >= 1 && K <= 12 && K < N, "prefix DP size");
-    __shared__ uint16_t lrank[NL];
-    __shared__ int smoff[L + 2];
-    __shared__ V drs[kSubBtWaves][N * N + N];  // per wave: d[m][k] (inner cities), then d[0][k]
-    for (int i = threadIdx.x; i < NL; i += 64 * kSubBtWaves) lrank[i] = info->rank[i];
-    if (threadIdx.x < (uint32_t)(L + 2)) smoff[threadIdx.x] = info->moff[threadIdx.x];
-    __syncthreads();
-    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
-    V *dr = drs[wave];
-    const V *d0 = dr + N * N;
-    auto wave_sync = [] {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-    };
-    for (int blk = blk0 + (int)(blockIdx.x * kSubBtWaves + wave); blk < nblocks;
-         blk += (int)(gridDim.x * kSubBtWaves)) {
-        const V *dsrc = dist + (size_t)blk * n * n;
-        for (int i = lane; i < N * N; i += 64) dr[i] = dsrc[(i / N + 1) * n + (i % N + 1)];
-        if (lane < (uint32_t)N) dr[N * N + lane] = dsrc[lane + 1];
-        wave_sync();
-        int32_t *tour = tour_out + (size_t)blk * (n + 1);
-        const int bestM = tour[n - 1];
-        if (bestM < 1) continue;  // no tour (cost already -1)
-        char *slot = const_cast<char *>(slots) + (size_t)(blk - blk0) * slot_bytes;
-        Rsrc<uint64_t> par;
-        par.rs = uniform_rsrc(slot + tiled_push_bytes(N, L, VB), (uint32_t)tiled_parent_bytes(N, L));
-        Rsrc<V> rec;
-        rec.rs = uniform_rsrc(slot + tiled_push_bytes(N, L, VB) + tiled_parent_bytes(N, L),
-                              (uint32_t)sub_rec_bytes(N, VB));
-        uint32_t S = (1u << N) - 1u;
-        int k = bestM - 1;
-        bool ok = bestM >= 1 && bestM <= N;
-        int pos = n - 2;
-        // (1) parent words
-        for (; ok && pos >= 1 && __builtin_popcount(S) - 1 >= N - TSPGPU_TILED_TA_OFF; --pos) {
-            const uint32_t T = S & ~(1u << k);
-            const uint32_t hT = T >> L, lT = T & (uint32_t)(NL - 1);
-            const uint32_t idx = (uint32_t)smoff[__builtin_popcount(lT)] + lrank[lT];
-            const uint64_t w = par.load(idx * 8u, hT * (uint32_t)(NL * 8));
-            const int q = k - __builtin_popcount(T & ((1u << k) - 1u));  // k's place among T's non-members
-            const int pm = (int)((w >> (4 * q)) & 15u);
-            ok = pm < N && ((T >> pm) & 1u);
-            if (lane == 0) tour[pos] = ok ? pm + 1 : 0;
-            S = T;
-            k = pm;
-        }
-        if (ok && pos >= 1) {
-            // (2) the prefix set's own DP, local city i = the i-th member of T0 ascending
-            const uint32_t T0 = S & ~(1u << k);
-            ok = __builtin_popcount(T0) == K;
-            int city[K];
-            {
-                uint32_t b = T0;
-#pragma unroll
-                for (int i = 0; i < K; ++i) {
-                    city[i] = b ? __builtin_ctz(b) : 0;
-                    b &= b - 1u;
-                }
-            }
-            // layer 1: G[{i}][i] = d[0][city i] (tsp.cpp:435)
-            if (ok && lane < (uint32_t)K) rec.store(((1u << lane) * K + lane) * VB, 0, d0[city[lane]]);
-            for (int j = 2; ok && j <= K; ++j) {
-                wave_sync();
-                for (uint32_t M = lane; M < (uint32_t)NK; M += 64) {
-                    if (__builtin_popcount(M) != j) continue;
-#pragma unroll
-                    for (int kk = 0; kk < K; ++kk) {
-                        if (!((M >> kk) & 1u)) continue;
-                        const uint32_t P = M & ~(1u << kk);
-                        V acc = ValT<V>::inf;
-#pragma unroll
-                        for (int m = 0; m < K; ++m)
-                            if ((P >> m) & 1u)
-                                acc = ValT<V>::vmin(acc, rec.load((P * K + m) * VB, 0) + dr[city[m] * N + city[kk]]);
-                        rec.store((M * K + kk) * VB, 0, acc);
-                    }
-                }
-            }
-            wave_sync();
-            // the walk below T0: first strict minimum over the members ascending
-            uint32_t Mloc = (uint32_t)NK - 1u;
-            for (; ok && pos >= 1; --pos) {
-                const bool mem = lane < (uint32_t)K && ((Mloc >> lane) & 1u);
-                V cand = ValT<V>::invalid;
-                if (mem) cand = rec.load((Mloc * K + lane) * VB, 0) + dr[city[lane < (uint32_t)K ? lane : 0] * N + k];
-                const V best = wave_min(cand);
-                const unsigned long long hit = __ballot(mem && cand == best);
-                const int li = hit ? __ffsll(hit) - 1 : K;
-                ok = li < K;
-                const int pm = ok ? city[li < K ? li : 0] : N;
-                if (lane == 0) tour[pos] = ok ? pm + 1 : 0;
-                if (ok) Mloc &= ~(1u << li);
-                k = pm;
-            }
-        }
-        if (!ok && lane == 0) cost_out[blk] = V(-1);
-        wave_sync();  // dr is reloaded for the next block
-    }
-}
-
-// ---------------------------------------------------------------------------
-// Backtracking of variant 6, workgroup form (TSPGPU_SUB_BT = 1).
-// The walk is hk_sub_backtrack's — (1) parent words while the set has
-// >= N - TSPGPU_TILED_TA_OFF members, (2) the prefix set T0 (K = N - 5 cities)
-// solved by its own Held-Karp, then the first strict minimum over T0's
-// members ascending (tsp.cpp:457-470) — but laid out for latency:
-//   * (1) runs one LANE per block, for every block the workgroup owns, before
-//     any prefix DP (its four dependent parent-word loads are paid once per
-//     workgroup, not once per block);
-//   * (2) runs the whole workgroup on one block with the table in LDS, compact
-//     (row M keeps its |M| member values: K * 2^(K-1) values, 40 KB at f64
-//     K = 10), one barrier per layer.  Thread t owns destination kk = t / TPK
-//     for the whole DP, so the K distances into kk sit in registers.
-// Round 4's hk_tiled_backtrack recomputed whole sub-cube rows from the pushes
-// through the slot's global recompute area, one wave per block (a chain of
-// global round trips per layer: 1.75 ms per 65536 16-city blocks, 6.7% of the
-// step).  Values are the forward pass's bits (same candidates, IEEE min is
-// order-free), ties as the reference's.
-// ---------------------------------------------------------------------------
-#ifndef TSPGPU_SUB_BT
-#define TSPGPU_SUB_BT 0  // (measured no faster than hk_tiled_backtrack yet: off)
-#endif
-#ifndef TSPGPU_SUB_BT_ABL
-#define TSPGPU_SUB_BT_ABL 0  // timing ablations (results wrong): 1 no prefix DP, 2 no walk, 4 no DP barriers, 8 no input loads
-#endif
-constexpr int kSubBtThreads = 256;
-// workgroups per CU: the LDS table decides (f64 K = 10: 46 KB)
-__host__ __device__ constexpr int sub_bt_wg(int vb) { return vb == 8 ? 3 : 6; }
-
-// one layer J of the prefix DP: thread (kk, sub) computes G[P | kk][kk] for the
-// (J-1)-subsets P of T0 \ {kk} numbered sub, sub + TPK, ...  (all items of a
-// thread unrolled: the table lookups of every item issue before the first row
-// read, so a layer costs a few LDS round trips, not one per item).  Layer j is
-// stored member-major: G[M][m] at layer_off(K, j) + (m's place in M) x C(K, j)
-// + colex rank of M, so lanes reading neighbouring rows hit neighbouring banks.
-template <typename V, int K, int J, int TPK>
-__device__ __forceinline__ void sub_bt_layer(V *g, const uint16_t *sub9, const uint16_t *rk, const V (&dcol)[K],
-                                             int kk, int sub)
-{
-    constexpr int CNT = cbinom(K - 1, J - 1), IT = (CNT + TPK - 1) / TPK;
-    constexpr int BOFF = mask_off(K - 1, J - 1);  // first (J-1)-subset in sub9
-    constexpr int RIN = layer_off(K, J - 1), CIN = cbinom(K, J - 1);
-    constexpr int ROUT = layer_off(K, J), COUT = cbinom(K, J);
-    const uint32_t below = (1u << kk) - 1u;
-    uint32_t P[IT];
-    int ro[IT], wo[IT];
-#pragma unroll
-    for (int it = 0; it < IT; ++it) {
-        const int p = sub + it * TPK;
-        const uint32_t p9 = p < CNT ? sub9[BOFF + p] : 0u;
-        P[it] = (p9 & below) | ((p9 & ~below) << 1);  // kk's bit left out
-    }
-#pragma unroll
-    for (int it = 0; it < IT; ++it) {
-        const uint32_t M = P[it] | (1u << kk);
-        ro[it] = RIN + rk[P[it]];
-        wo[it] = ROUT + __builtin_popcount(M & below) * COUT + rk[M];
-    }
-    // branch-free: every lane loads K values, so an item's loads issue back to
-    // back and wait once (an exec-masked load per member waits once per member)
-#pragma unroll
-    for (int it = 0; it < IT; ++it) {
-        V v[K];
-#pragma unroll
-        for (int m = 0; m < K; ++m)  // (a non-member reads g[0]: one broadcast address, no extra bank traffic)
-            v[m] = g[((P[it] >> m) & 1u) ? ro[it] + __builtin_popcount(P[it] & ((1u << m) - 1u)) * CIN : 0];
-        V acc = ValT<V>::inf;
-#pragma unroll
-        for (int m = 0; m < K; ++m) acc = ValT<V>::vmin(acc, ((P[it] >> m) & 1u) ? v[m] + dcol[m] : ValT<V>::inf);
-        if (sub + it * TPK < CNT) g[wo[it]] = acc;
-    }
-}
-template <typename V, int K, int J, int TPK>
-__device__ __forceinline__ void sub_bt_layers(V *g, const uint16_t *sub9, const uint16_t *rk, const V (&dcol)[K],
-                                              int kk, int sub)
-{
-    if constexpr (J <= K) {
-        if (kk < K) sub_bt_layer<V, K, J, TPK>(g, sub9, rk, dcol, kk, sub);
-        if (!(TSPGPU_SUB_BT_ABL & 4)) __syncthreads();
-        sub_bt_layers<V, K, J + 1, TPK>(g, sub9, rk, dcol, kk, sub);
-    }
-}
-
-template <typename V, int N, int L>
-__global__ __launch_bounds__(kSubBtThreads) void hk_sub_bt_wg(int nblocks, int blk0, const char *__restrict__ slots,
-                                                              uint32_t slot_bytes, const TiledInfo *__restrict__ info,
-                                                              const V *__restrict__ dist, V *__restrict__ cost_out,
-                                                              int32_t *__restrict__ tour_out)
-{
-    constexpr int NL = 1 << L, n = N + 1, VB = sizeof(V), K = sub_bt_k(N), NK = 1 << K;
-    constexpr int T = kSubBtThreads, TPK = T / K, DLV = K * K + K;
-    static_assert(K >= 2 && K <= 10 && DLV + K <= T, "prefix DP size");
-    __shared__ V g[K << (K - 1)];          // layer j member-major (sub_bt_layer)
-    __shared__ V dl[DLV];                  // d[city m][city kk] at m * K + kk; d[city m][k0] at K * K + m
-    __shared__ uint16_t rk[NK];            // colex rank of a subset among the subsets of its size
-    __shared__ int lo[K + 1], cn[K + 1];   // layer_off(K, j), C(K, j)
-    __shared__ uint16_t sub9[NK / 2];      // (K-1)-bit subsets by size, then colex rank
-    __shared__ uint16_t wT0[T];            // (1)'s result per owned block: T0, k0 (-1: nothing left)
-    __shared__ int8_t wk0[T];
-    __shared__ int8_t city[K];
-    const uint32_t tid = threadIdx.x;
-
-    __shared__ uint16_t bn[K + 1][K + 1];  // binomials (setup only)
-    if (tid == 0)
-        for (int a = 0; a <= K; ++a)
-            for (int b = 0; b <= K; ++b) bn[a][b] = b == 0 ? 1 : (a == 0 ? 0 : bn[a - 1][b - 1] + bn[a - 1][b]);
-    __syncthreads();
-    for (uint32_t M = tid; M < (uint32_t)NK; M += T) {
-        int r = 0, i = 0;
-        for (int b = 0; b < K; ++b)
-            if ((M >> b) & 1u) r += bn[b][++i];
-        const int j = __builtin_popcount(M);
-        int lof = 0, mo = 0;  // layer_off(K, j), mask_off(K - 1, j)
-        for (int u = 0; u < j; ++u) {
-            lof += bn[K][u] * u;
-            mo += bn[K - 1][u];
-        }
-        rk[M] = (uint16_t)r;
-        if (M < (uint32_t)NK / 2) sub9[mo + r] = (uint16_t)M;
-        if (M == (1u << j) - 1u) {  // one thread per layer
-            lo[j] = lof;
-            cn[j] = bn[K][j];
-        }
-    }
-
-    const int kk = (int)tid / TPK, sub = (int)tid % TPK;  // this thread's destination (kk >= K: idle in the DP)
-    for (int base = blk0 + (int)blockIdx.x; base < nblocks; base += T * (int)gridDim.x) {
-        // (1) parent words, one lane per block
-        {
-            const int blk = base + (int)tid * (int)gridDim.x;
-            uint32_t T0 = 0;
-            int k0 = -1;
-            if (blk < nblocks) {
-                int32_t *tour = tour_out + (size_t)blk * (n + 1);
-                const int bestM = tour[n - 1];
-                if (bestM >= 1) {
-                    const uint64_t *pw = reinterpret_cast<const uint64_t *>(slots + (size_t)(blk - blk0) * slot_bytes +
-                                                                            tiled_push_bytes(N, L, VB));
-                    uint32_t S = (1u << N) - 1u;
-                    int k = bestM - 1, pos = n - 2;
-                    bool ok = bestM <= N;
-                    for (; ok && pos >= 1 && __builtin_popcount(S) - 1 >= N - TSPGPU_TILED_TA_OFF; --pos) {
-                        const uint32_t Tm = S & ~(1u << k);
-                        const uint32_t hT = Tm >> L, lT = Tm & (uint32_t)(NL - 1);
-                        const uint32_t idx = (uint32_t)info->moff[__builtin_popcount(lT)] + info->rank[lT];
-                        const uint64_t w = pw[(size_t)hT * NL + idx];
-                        const int q = k - __builtin_popcount(Tm & ((1u << k) - 1u));  // k's place among the non-members
-                        const int pm = (int)((w >> (4 * q)) & 15u);
-                        ok = pm < N && ((Tm >> pm) & 1u);
-                        tour[pos] = ok ? pm + 1 : 0;
-                        S = Tm;
-                        k = pm;
-                    }
-                    if (ok && pos >= 1) {
-                        T0 = S & ~(1u << k);
-                        ok = pos == K && __builtin_popcount(T0) == K;
-                        k0 = k;
-                    }
-                    if (!ok) {
-                        cost_out[blk] = V(-1);
-                        k0 = -1;
-                    }
-                }
-            }
-            wT0[tid] = (uint16_t)T0;
-            wk0[tid] = (int8_t)k0;
-        }
-        __syncthreads();
-        const int owned = (nblocks - base + (int)gridDim.x - 1) / (int)gridDim.x;
-        const int cntw = owned < T ? owned : T;
-        // this thread's staged input of owned block i: a distance of dl, or
-        // (K*K+K <= tid < K*K+2K) layer 1's G[{m}][m] = d[0][city m] (tsp.cpp:435)
-        auto stage = [&](int i, int *cm) -> V {
-            *cm = 0;
-            if ((TSPGPU_SUB_BT_ABL & 8) || i >= cntw || wk0[i] < 0 || tid >= (uint32_t)(DLV + K)) return V(0);
-            const uint32_t T0 = wT0[i];
-            const int k0 = wk0[i];
-            auto nth = [T0](int m) {  // the m-th member of T0 ascending
-                uint32_t b = T0;
-                for (int r = 0; r < m; ++r) b &= b - 1u;
-                return __builtin_ctz(b);
-            };
-            const V *dsrc = dist + (size_t)(base + i * (int)gridDim.x) * n * n;
-            if (tid < (uint32_t)(K * K)) return dsrc[(nth((int)tid / K) + 1) * n + nth((int)tid % K) + 1];
-            if (tid < (uint32_t)DLV) return dsrc[(nth((int)tid - K * K) + 1) * n + k0 + 1];
-            *cm = nth((int)tid - DLV);
-            return dsrc[*cm + 1];
-        };
-        auto place = [&](V v, int cm) {
-            if (tid < (uint32_t)DLV) {
-                dl[tid] = v;
-            } else if (tid < (uint32_t)(DLV + K)) {
-                g[tid - DLV] = v;  // G[{m}][m] at layer_off(K, 1) + rank m
-                city[tid - DLV] = (int8_t)cm;
-            }
-        };
-        int cm = 0;
-        V pf = stage(0, &cm);
-        place(pf, cm);
-        __syncthreads();
-        // (2) one block at a time: prefix DP over T0, then the walk; the next
-        // block's inputs are loaded meanwhile
-        for (int i = 0; i < cntw; ++i) {
-            const bool live = wk0[i] >= 0;  // (uniform)
-            pf = stage(i + 1, &cm);
-            if (live) {
-                V dcol[K];
-#pragma unroll
-                for (int m = 0; m < K; ++m) dcol[m] = dl[m * K + (kk < K ? kk : 0)];
-                if (!(TSPGPU_SUB_BT_ABL & 1)) sub_bt_layers<V, K, 2, TPK>(g, sub9, rk, dcol, kk, sub);
-                if (tid < 64 && !(TSPGPU_SUB_BT_ABL & 2)) {
-                    const int blk = base + i * (int)gridDim.x;
-                    int32_t *tour = tour_out + (size_t)blk * (n + 1);
-                    const uint32_t lane = tid;
-                    uint32_t Mloc = (uint32_t)NK - 1u;
-                    int kl = -1;  // the current city's local index (-1: k0, outside T0)
-                    bool ok = true;
-                    for (int pos = K; ok && pos >= 1; --pos) {
-                        const int jm = __builtin_popcount(Mloc);
-                        const bool mem = lane < (uint32_t)K && ((Mloc >> lane) & 1u);
-                        V cand = ValT<V>::invalid;
-                        if (mem)
-                            cand = g[lo[jm] + __builtin_popcount(Mloc & ((1u << lane) - 1u)) * cn[jm] + rk[Mloc]] +
-                                   (kl < 0 ? dl[K * K + lane] : dl[lane * K + kl]);
-                        const V best = wave_min(cand);
-                        const unsigned long long hit = __ballot(mem && cand == best);
-                        const int li = hit ? __ffsll(hit) - 1 : K;
-                        ok = li < K;
-                        if (lane == 0) tour[pos] = ok ? city[li] + 1 : 0;
-                        if (ok) Mloc &= ~(1u << li);
-                        kl = li;
-                    }
-                    if (!ok && lane == 0) cost_out[blk] = V(-1);
-                }
-            }
-            __syncthreads();  // g, dl and city are the next block's
-            place(pf, cm);
-            __syncthreads();
-        }
-    }
-}
-}  // namespace
+// one block's global slot for variant 6: variant 5's layout (push area, parent
+// words, recompute area), so hk_tiled_backtrack completes the tours
+__host__ __device__ constexpr size_t sub_slot_bytes(int N, int L, int vb) { return tiled_slot_bytes(N, L, vb); }
 
 struct SubArgs {
     const void *dist;
@@ -1655,7 +1082,6 @@ struct SubArgs {
     void *cost;
     int32_t *tour;
     int grid, bt_grid;
-    int cus;                  // compute units (the workgroup-form backtracking's grid)
     hipStream_t stream;
     hipEvent_t ev_mid;
 };
@@ -1669,21 +1095,9 @@ hipError_t launch_sub_n(const SubArgs &a)
     hipError_t e = hipGetLastError();
     if (e == hipSuccess && a.ev_mid) e = hipEventRecord(a.ev_mid, a.stream);
     if (e != hipSuccess) return e;
-    if constexpr (TSPGPU_SUB_STAMP) return hipSuccess;  // (diagnostic build: the tour words hold the stamps)
-    if constexpr (TSPGPU_SUB_BT && !TSPGPU_SUB_RECYCLE) {
-        const int nb = a.blk1 - a.blk0, cap = a.cus * sub_bt_wg(sizeof(V));
-        const int g = nb < cap ? nb : cap;
-        hipLaunchKernelGGL((hk_sub_bt_wg<V, N, L>), dim3(g), dim3(kSubBtThreads), 0, a.stream, a.blk1, a.blk0,
-                           a.slots, a.slot_bytes, a.info, static_cast<const V *>(a.dist), static_cast<V *>(a.cost),
-                           a.tour);
-    } else if constexpr (TSPGPU_SUB_RECYCLE)
-        hipLaunchKernelGGL((hk_sub_backtrack<V, N, L>), dim3(a.bt_grid), dim3(64 * kSubBtWaves), 0, a.stream, a.blk1,
-                           a.blk0, a.slots, a.slot_bytes, a.info, static_cast<const V *>(a.dist),
-                           static_cast<V *>(a.cost), a.tour);
-    else
-        hipLaunchKernelGGL((hk_tiled_backtrack<V, N, L>), dim3(a.bt_grid), dim3(64 * kTiledBtWaves), 0, a.stream,
-                           a.blk1, a.blk0, a.slots, a.slot_bytes, a.info, static_cast<const V *>(a.dist),
-                           static_cast<V *>(a.cost), a.tour);
+    hipLaunchKernelGGL((hk_tiled_backtrack<V, N, L>), dim3(a.bt_grid), dim3(64 * kTiledBtWaves), 0, a.stream, a.blk1,
+                       a.blk0, a.slots, a.slot_bytes, a.info, static_cast<const V *>(a.dist), static_cast<V *>(a.cost),
+                       a.tour);
     return hipGetLastError();
 }
 

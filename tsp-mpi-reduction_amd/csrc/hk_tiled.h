@@ -65,18 +65,6 @@ constexpr int kTiledMaxL = 12;
 #define TSPGPU_TILED_DS 19
 #endif
 constexpr int kTiledDS = TSPGPU_TILED_DS;
-// Ablation knobs for timing experiments only (results are WRONG when set):
-//   1 high-member values from LDS, 2 d values from a register, 4 no barrier
-//   between the passes of a sub-cube, 8 plain minimum (no argmin), 32 no
-//   backtracking, 64 backtracking kernel stops after staging, 128 no recompute,
-//   1024 no sub-cube reordering of the distance table (TSPGPU_TILED_PERM),
-//   2048 / 4096 skip the passes with j <= 1 or >= L-1 / j <= 2 or >= L-2
-#ifndef TSPGPU_TILED_ABL
-#define TSPGPU_TILED_ABL 0
-#endif
-#if TSPGPU_TILED_ABL != 0 && !defined(TSPGPU_K1_SWEEP)
-#error "TSPGPU_TILED_ABL gives wrong results: measurement builds only (make K1_SWEEP=1)"
-#endif
 // Rows with at least N - TSPGPU_TILED_TA_OFF members keep the argmin (a
 // 64-bit parent word each); every smaller row is relaxed without it and the
 // backtracking recomputes the few rows it needs (see tiled_backtrack).
@@ -89,34 +77,12 @@ constexpr int kTiledDS = TSPGPU_TILED_DS;
 #ifndef TSPGPU_TILED_AHEAD
 #define TSPGPU_TILED_AHEAD 6  // d loads in flight per lane in the relaxation loop
 #endif
-// High cities in sub-cube order: the forward kernel keeps the high rows and
-// columns of its LDS distance table in the order sigma_h = (members of h
-// ascending, then non-members ascending), so a pass (whose member/non-member
-// split of the high cities is static) addresses them with immediate offsets:
-// no VALU address add for a relaxation with a high member or destination, and
-// the high-high distances are wave-uniform reads.  Wave 0 permutes the table
-// from sigma_h to sigma_{h+1} after the last pass of sub-cube h (that pass has
-// one row, so wave 0 is the only reader left).  Measured at n = 16 (cfg 14,
-// 16384 blocks, profiles/r02/k1_tiled_v16_perm.log): the passes get 3% faster
-// (7.37 ms with the reordering skipped, results wrong) but the reordering on
-// wave 0's path costs more (7.79-7.81 ms vs 7.58-7.61 without): off.
-#ifndef TSPGPU_TILED_PERM
-#define TSPGPU_TILED_PERM 0
-#endif
-// Destination-parallel passes: a pass whose (row, destination) pairs fit the
-// workgroup's threads at once (j <= 1 and j >= L - 1 at L = 10: 1-10 rows)
-// gives every pair its own lane — T relaxations per lane instead of a T x Q
-// chain on one lane while the other waves wait at the barrier.  Those four
-// passes hold 13% of the relaxations but took 20% of the kernel time
-// (skipping them: 7.57 -> 6.04 ms, profiles/r02/k1_tiled_small_pass_ablation.log).
-// Measured slower, so off: parity holds but cfg 14 goes 7.61 -> 9.02 ms (bit 1,
-// passes j <= 1), 10.31 (bit 2, j >= L - 1), 11.41 ms (both), because the
-// extra pass bodies push the whole fused kernel's register allocation into
-// spills (VGPR spills 19 -> 28 / 54 / 61, scratch ops 47 -> 125 / 186;
-// profiles/r02/k1_tiled_dp_sweep.log).
-#ifndef TSPGPU_TILED_DP
-#define TSPGPU_TILED_DP 0
-#endif
+// Measured and not kept (profiles/r02; the switches were removed in round
+// 6): the high distance rows/columns permuted into sub-cube order between
+// sub-cubes (the passes 3% faster, the permutation on wave 0's path 6% slower
+// — variant 6 does it on idle threads instead, hk_sub.h) and
+// destination-parallel edge passes (spills; variant 6 has them in a form that
+// does not spill).
 
 // host-built tables of one L (device copy, staged into LDS per workgroup)
 struct TiledInfo {
@@ -332,8 +298,8 @@ __device__ __forceinline__ void tiled_pass(const TiledCtx<V, N, L, R> &c, uint32
     constexpr int CUR = (J & 1) ? REGV - ROWS * J : 0;
     constexpr int NXT = ((J + 1) & 1) ? REGV - ROWS_N * (J + 1) : 0;
     // argmin and parent word only for the top rows (tiled_backtrack recomputes
-    // the rest); ablation 8 drops it everywhere (timing only)
-    constexpr bool ARG = T >= N - TSPGPU_TILED_TA_OFF && !(TSPGPU_TILED_ABL & 8);
+    // the rest)
+    constexpr bool ARG = T >= N - TSPGPU_TILED_TA_OFF;
     // distance rows of kTiledDS entries (R copies each): a member's row
     // offset is bit * DROW, a non-member's column offset bit << SK; the argmin
     // is kept as the member's row offset (one register less per member) and
@@ -357,15 +323,6 @@ __device__ __forceinline__ void tiled_pass(const TiledCtx<V, N, L, R> &c, uint32
             nb &= nb - 1u;
         }
     }
-    // table row -> city of every member row (argmin rows, sub-cube order):
-    // nibble p = p for the low rows, L + hm[i] for high row L + i
-    uint64_t pmap = 0;
-    if constexpr (ARG && TSPGPU_TILED_PERM) {
-#pragma unroll
-        for (int p = 0; p < L; ++p) pmap |= (uint64_t)p << (4 * p);
-#pragma unroll
-        for (int i = 0; i < HC; ++i) pmap |= (uint64_t)(L + hm[i]) << (4 * (L + i));
-    }
     const uint32_t lane_off = (tid & (uint32_t)(R - 1)) * VB;
     const char *drb = reinterpret_cast<const char *>(c.dr);
     char *lds_nxt = reinterpret_cast<char *>(c.region + NXT);
@@ -377,12 +334,7 @@ __device__ __forceinline__ void tiled_pass(const TiledCtx<V, N, L, R> &c, uint32
 #pragma unroll
         for (int p = 0; p < J; ++p) g[p] = c.region[CUR + p * ROWS + r];
 #pragma unroll
-        for (int i = 0; i < HC; ++i) {
-            if constexpr (TSPGPU_TILED_ABL & 1)
-                g[J + i] = c.region[(CUR + i * 7 + r) % REGV];
-            else
-                g[J + i] = c.push.load(voff, (h * H + hm[i]) * (uint32_t)(NL * VB));
-        }
+        for (int i = 0; i < HC; ++i) g[J + i] = c.push.load(voff, (h * H + hm[i]) * (uint32_t)(NL * VB));
         // members ascending (low bits of l, then the high members of h)
         uint32_t mrow[T];
         uint32_t lb = l;
@@ -392,8 +344,7 @@ __device__ __forceinline__ void tiled_pass(const TiledCtx<V, N, L, R> &c, uint32
             lb &= lb - 1u;
         }
 #pragma unroll
-        for (int i = 0; i < HC; ++i)  // high member i: table row L + i in sub-cube order
-            mrow[J + i] = (TSPGPU_TILED_PERM ? (uint32_t)(L + i) : (L + hm[i])) * DROW + lane_off;
+        for (int i = 0; i < HC; ++i) mrow[J + i] = (L + hm[i]) * DROW + lane_off;
         // Destinations in chunks of at most TSPGPU_TILED_QC (registers: acc,
         // arg and the column offsets of one chunk only); the non-members come
         // ascending (low non-members of l, then those of h).  Per chunk: the
@@ -417,8 +368,8 @@ __device__ __forceinline__ void tiled_pass(const TiledCtx<V, N, L, R> &c, uint32
                 if (q < QL) {
                     kof[qq] = (uint32_t)__builtin_ctz(nb) << SK;
                     nb &= nb - 1u;
-                } else {  // high non-member q - QL: table column L + HC + (q - QL) in sub-cube order
-                    kof[qq] = (TSPGPU_TILED_PERM ? (uint32_t)(L + HC + (q - QL)) : (L + hn[q - QL])) << SK;
+                } else {  // high non-member q - QL
+                    kof[qq] = (L + hn[q - QL]) << SK;
                 }
             }
             V acc[QN];
@@ -431,8 +382,7 @@ __device__ __forceinline__ void tiled_pass(const TiledCtx<V, N, L, R> &c, uint32
                 for (int i = 0; i < AH; ++i) dv[i] = *reinterpret_cast<const V *>(drb + mrow[i / QN] + kof[i % QN]);
 #pragma unroll
                 for (int i = 0; i < TQ; ++i) {
-                    V d = dv[i % AH];
-                    if constexpr (TSPGPU_TILED_ABL & 2) d = g[(i + 1) % T];
+                    const V d = dv[i % AH];
                     if (i + AH < TQ)
                         dv[i % AH] = *reinterpret_cast<const V *>(drb + mrow[(i + AH) / QN] + kof[(i + AH) % QN]);
                     if (i < QN) {
@@ -462,9 +412,7 @@ __device__ __forceinline__ void tiled_pass(const TiledCtx<V, N, L, R> &c, uint32
                 }
                 // the row's parent word: nibble q = bit index of the argmin member
                 if constexpr (ARG) {
-                    uint32_t pos = arg[qq] / DROW;  // table row of the argmin member
-                    if constexpr (TSPGPU_TILED_PERM && HC > 0)
-                        pos = (uint32_t)(pmap >> (4 * pos)) & 15u;  // -> its city
+                    const uint32_t pos = arg[qq] / DROW;  // table row of the argmin member = its city bit
                     if (q < 8)
                         wlo |= pos << (4 * q);
                     else
@@ -483,130 +431,6 @@ __host__ __device__ constexpr int pow2_at_least(int q)
     return p;
 }
 
-// Destination-parallel form of tiled_pass (TSPGPU_TILED_DP): thread t owns the
-// pair (row r = t / QP, destination q = t % QP), QP = Q rounded up to a power
-// of two so that a row's lanes never straddle a wave.  The lane loads its
-// row's values, finds its destination k (the q-th non-member: low ones
-// ascending, then the high ones) and takes the same T relaxations, in the
-// same member order (the first strict minimum), as the row-owner pass does
-// for k; stores go to the same places.  In the top rows (the argmin kept)
-// the row's parent word is OR-reduced over its QP lanes and stored by lane 0.
-template <typename V, int N, int L, int T, int J, int THREADS, int R>
-__device__ __forceinline__ void tiled_pass_dp(const TiledCtx<V, N, L, R> &c, uint32_t h, uint32_t tid)
-{
-    constexpr int H = N - L;
-    constexpr int Q = N - T;
-    constexpr int HC = T - J;
-    constexpr int QL = L - J;
-    constexpr int QH = Q - QL;
-    constexpr int QP = pow2_at_least(Q);
-    constexpr int NL = 1 << L;
-    constexpr int VB = sizeof(V);
-    constexpr int ROWS = cbinom(L, J);
-    constexpr int BASE = tiled_moff(L, J);
-    constexpr int ROWS_N = J < L ? cbinom(L, J + 1) : 0;
-    constexpr int REGV = tiled_region_vals(L);
-    constexpr int CUR = (J & 1) ? REGV - ROWS * J : 0;
-    constexpr int NXT = ((J + 1) & 1) ? REGV - ROWS_N * (J + 1) : 0;
-    constexpr bool ARG = T >= N - TSPGPU_TILED_TA_OFF && !(TSPGPU_TILED_ABL & 8);
-    constexpr int SK = __builtin_ctz((unsigned)(R * VB));
-    constexpr uint32_t DROW = (uint32_t)(kTiledDS * R * VB);
-    static_assert(QP <= 64 && ROWS * QP <= THREADS, "destination-parallel pass: one pair per thread");
-    const uint32_t lane_off = (tid & (uint32_t)(R - 1)) * VB;
-    const char *drb = reinterpret_cast<const char *>(c.dr);
-    char *lds_nxt = reinterpret_cast<char *>(c.region + NXT);
-    const uint32_t r = tid / QP, q = tid % QP;
-    if (r >= (uint32_t)ROWS) return;  // (whole groups of QP lanes: the reduction below stays inside active lanes)
-    const bool act = q < (uint32_t)Q;
-    const uint32_t l = c.lmask[BASE + r];
-    const uint32_t voff = (BASE + r) * VB;
-    // this lane's destination: the q-th non-member of the row (low ones first)
-    uint32_t k = 0, cb = 0;
-    {
-        uint32_t nb = ~l & (uint32_t)(NL - 1);
-#pragma unroll
-        for (int i = 0; i < QL; ++i) {
-            if ((uint32_t)i == q) k = (uint32_t)__builtin_ctz(nb);
-            nb &= nb - 1u;
-        }
-        uint32_t hb = ~h & ((1u << H) - 1u);
-#pragma unroll
-        for (int i = 0; i < QH; ++i) {
-            if ((uint32_t)(QL + i) == q) cb = (uint32_t)__builtin_ctz(hb), k = L + cb;
-            hb &= hb - 1u;
-        }
-    }
-    const char *dk = drb + lane_off + (k << SK);
-    // members streamed in the row-owner pass's order (low ascending, then the
-    // high ones), each value and distance used once: no per-row arrays
-    V acc = V(0);
-    uint32_t arg = 0;
-    if (act) {
-        uint32_t lb = l;
-#pragma unroll
-        for (int p = 0; p < J; ++p) {
-            const uint32_t m = (uint32_t)__builtin_ctz(lb) * DROW;
-            lb &= lb - 1u;
-            const V g = c.region[CUR + p * ROWS + r];
-            const V d = *reinterpret_cast<const V *>(dk + m);
-            if (p == 0) {
-                acc = g + d;
-                arg = m;
-            } else if constexpr (ARG) {
-                relax_argmin(acc, arg, g, d, m);
-            } else {
-                relax_min(acc, g, d);
-            }
-            __builtin_amdgcn_sched_barrier(0);  // (as in tiled_pass: no hoisting of every load)
-        }
-        uint32_t hb = h;
-#pragma unroll
-        for (int i = 0; i < HC; ++i) {
-            const uint32_t hm = (uint32_t)__builtin_ctz(hb);
-            hb &= hb - 1u;
-            const uint32_t m = (L + hm) * DROW;
-            const V g = c.push.load(voff, (h * H + hm) * (uint32_t)(NL * VB));
-            const V d = *reinterpret_cast<const V *>(dk + m);
-            if (J == 0 && i == 0) {
-                acc = g + d;
-                arg = m;
-            } else if constexpr (ARG) {
-                relax_argmin(acc, arg, g, d, m);
-            } else {
-                relax_min(acc, g, d);
-            }
-            __builtin_amdgcn_sched_barrier(0);  // (as in tiled_pass: no hoisting of every load)
-        }
-        if (q < (uint32_t)QL) {  // low k -> the next LDS layer (position k - q)
-            const uint32_t rb = c.lrankb[l | (1u << k)];
-            *reinterpret_cast<V *>(lds_nxt + (k - q) * (uint32_t)(ROWS_N * VB) + rb) = acc;
-        } else {  // high k -> the push column of sub-cube h | k
-            c.push.store(voff, ((h | (1u << cb)) * H + cb) * (uint32_t)(NL * VB), acc);
-        }
-    }
-    if constexpr (ARG) {
-        uint64_t w = act ? (uint64_t)(arg / DROW) << (4 * q) : 0ull;
-#pragma unroll
-        for (int off = 1; off < QP; off *= 2) {
-            const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)w, off);
-            const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(w >> 32), off);
-            w |= ((uint64_t)hi << 32) | lo;
-        }
-        if (q == 0) c.par.store((BASE + r) * 8u, h * (uint32_t)(NL * 8), w);
-    }
-}
-
-template <typename V, int N, int L, int T, int J, int THREADS, int R>
-__device__ __forceinline__ void tiled_pass_any(const TiledCtx<V, N, L, R> &c, uint32_t h, uint32_t tid)
-{
-    constexpr int Q = N - T;
-    constexpr int DPB = J <= 1 ? 1 : 2;  // TSPGPU_TILED_DP bit 1: the first passes, bit 2: the last ones
-    if constexpr ((TSPGPU_TILED_DP & DPB) && !TSPGPU_TILED_PERM && Q >= 2 && cbinom(L, J) * pow2_at_least(Q) <= THREADS)
-        tiled_pass_dp<V, N, L, T, J, THREADS, R>(c, h, tid);
-    else
-        tiled_pass<V, N, L, T, J, THREADS, R>(c, h, tid);
-}
-
 // Parallel bit deposit: the i-th set bit of m receives bit i of x.
 __device__ __forceinline__ uint32_t pdep_u32(uint32_t x, uint32_t m)
 {
@@ -617,63 +441,6 @@ __device__ __forceinline__ uint32_t pdep_u32(uint32_t x, uint32_t m)
         m ^= low;
     }
     return r;
-}
-
-// TSPGPU_TILED_PERM: one wave rewrites the high rows and columns of the
-// forward kernel's LDS distance table from sub-cube order sigma_hf to
-// sigma_ht (sigma_h: members of h ascending, then non-members ascending; h = 0
-// is the natural order).  Every lane loads its entries first, then stores.
-template <typename V, int N, int L, int R>
-__device__ __forceinline__ void tiled_perm_high(V *dr, uint32_t hf, uint32_t ht, uint32_t lane)
-{
-    constexpr int H = N - L, E = H * N + L * H, PER = (E * R + 63) / 64;
-    // uniform: sig = the city at each position under ht, inv = the position of
-    // each city under hf (nibbles; members ascending, then non-members)
-    uint32_t sig = 0, inv = 0;
-    {
-        int ps = 0, pi = 0;
-#pragma unroll
-        for (int x = 0; x < H; ++x)
-            if ((ht >> x) & 1u) sig |= (uint32_t)x << (4 * ps++);
-#pragma unroll
-        for (int x = 0; x < H; ++x)
-            if (!((ht >> x) & 1u)) sig |= (uint32_t)x << (4 * ps++);
-#pragma unroll
-        for (int x = 0; x < H; ++x)
-            if ((hf >> x) & 1u) inv |= (uint32_t)(pi++) << (4 * x);
-#pragma unroll
-        for (int x = 0; x < H; ++x)
-            if (!((hf >> x) & 1u)) inv |= (uint32_t)(pi++) << (4 * x);
-    }
-    auto src_pos = [&](int t) -> int {  // table position under hf of the city at position t under ht
-        if (t < L) return t;
-        const uint32_t x = (sig >> (4 * (t - L))) & 15u;
-        return L + (int)((inv >> (4 * x)) & 15u);
-    };
-    V v[PER];
-    int dst[PER];
-#pragma unroll
-    for (int k = 0; k < PER; ++k) {
-        const int e = (int)lane + 64 * k;
-        dst[k] = -1;
-        v[k] = V(0);
-        if (e < E * R) {
-            const int c = e % R, ee = e / R;
-            int a, b;
-            if (ee < H * N) {
-                a = L + ee / N;
-                b = ee % N;
-            } else {
-                a = (ee - H * N) / H;
-                b = L + (ee - H * N) % H;
-            }
-            dst[k] = (a * kTiledDS + b) * R + c;
-            v[k] = dr[(src_pos(a) * kTiledDS + src_pos(b)) * R + c];
-        }
-    }
-#pragma unroll
-    for (int k = 0; k < PER; ++k)
-        if (dst[k] >= 0) dr[dst[k]] = v[k];
 }
 
 // G[h<<L | l][m] after the forward pass: a high m from the push area, a low m
@@ -765,13 +532,13 @@ __device__ bool tiled_backtrack(const TiledCtx<V, N, L, R> &c, const V *d0, int 
         const uint32_t T = S & ~(1u << k);
         const uint32_t hT = T >> L, lT = T & (uint32_t)(NL - 1);
         int pm;
-        if (__builtin_popcount(T) >= N - TSPGPU_TILED_TA_OFF && !(TSPGPU_TILED_ABL & 8)) {
+        if (__builtin_popcount(T) >= N - TSPGPU_TILED_TA_OFF) {
             const uint32_t idx = (uint32_t)c.moff[__builtin_popcount(lT)] + c.lrankb[lT] / VB;
             const uint64_t w = c.par.load(idx * 8u, hT * (uint32_t)(NL * 8));
             const int q = k - __builtin_popcount(T & ((1u << k) - 1u));  // k's place among T's non-members
             pm = (int)((w >> (4 * q)) & 15u);
         } else {
-            if (!(TSPGPU_TILED_ABL & 128) && (hT != hcur || (lT & ~lcur))) {
+            if (hT != hcur || (lT & ~lcur)) {
                 tiled_recompute(c, d0, hT, lT, lane);
                 hcur = hT;
                 lcur = lT;
@@ -799,7 +566,7 @@ __device__ __forceinline__ void tiled_dispatch_h(const TiledCtx<V, N, L, R> &c, 
 #define TSPGPU_TP(HC)                                                                      \
     case HC:                                                                               \
         if constexpr (HC <= H && J + HC >= 1 && J + HC < N)                                \
-            tiled_pass_any<V, N, L, J + HC, J, THREADS, R>(c, h, tid);                     \
+            tiled_pass<V, N, L, J + HC, J, THREADS, R>(c, h, tid);                         \
         break;
     switch (hc) {
         TSPGPU_TP(0) TSPGPU_TP(1) TSPGPU_TP(2) TSPGPU_TP(3) TSPGPU_TP(4) TSPGPU_TP(5) TSPGPU_TP(6)
@@ -890,15 +657,9 @@ __global__ __launch_bounds__(THREADS, tiled_waves(THREADS, WG)) void hk_tiled_ke
             const int j0 = h == 0 ? 1 : 0;
             const int j1 = h == (uint32_t)(NH - 1) ? L - 1 : L;
             for (int j = j0; j <= j1; ++j) {
-                if ((TSPGPU_TILED_ABL & 2048) && (j <= 1 || j >= L - 1)) continue;
-                if ((TSPGPU_TILED_ABL & 4096) && (j <= 2 || j >= L - 2)) continue;
                 tiled_dispatch<V, N, L, THREADS, R>(c, h, hc, j, tid);
-                if (!(TSPGPU_TILED_ABL & 4) && j < j1) lds_barrier();
+                if (j < j1) lds_barrier();
             }
-            // the last pass (j = L, one row: thread 0) leaves wave 0 the only
-            // reader of the distance table: it reorders the high cities for h + 1
-            if (TSPGPU_TILED_PERM && !(TSPGPU_TILED_ABL & 1024) && h + 1 < (uint32_t)NH && tid < 64u)
-                tiled_perm_high<V, N, L, R>(dr, h, h + 1, tid);
             // pushes of this sub-cube are read by later ones: full barrier
             __syncthreads();
         }
@@ -965,7 +726,6 @@ __global__ __launch_bounds__(64 * kTiledBtWaves, TSPGPU_TILED_BTWG) void hk_tile
     for (int blk = blk0 + (int)(blockIdx.x * kTiledBtWaves + wave); blk < nblocks;
          blk += (int)(gridDim.x * kTiledBtWaves)) {
         const V *dsrc = dist + (size_t)blk * n * n;
-        if (TSPGPU_TILED_ABL & 256) continue;
         for (int i = lane; i < N * kTiledDS; i += 64) {
             const int m = i / kTiledDS, k = i % kTiledDS;
             dr[i] = k < N ? dsrc[(m + 1) * n + (k + 1)] : V(0);
@@ -974,7 +734,6 @@ __global__ __launch_bounds__(64 * kTiledBtWaves, TSPGPU_TILED_BTWG) void hk_tile
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-        if (TSPGPU_TILED_ABL & 64) continue;
         int32_t *tour = tour_out + (size_t)blk * (n + 1);
         const int bestM = tour[n - 1];
         if (bestM < 1) continue;  // no tour (cost already -1)
@@ -1019,14 +778,10 @@ hipError_t launch_tiled_n(const TiledArgs &a)
                        static_cast<V *>(a.cost), a.tour);
     hipError_t e = hipGetLastError();
     if (e == hipSuccess && a.ev_mid) e = hipEventRecord(a.ev_mid, a.stream);
-    if (e != hipSuccess || (TSPGPU_TILED_ABL & 32)) return e;
+    if (e != hipSuccess) return e;
     hipLaunchKernelGGL((hk_tiled_backtrack<V, N, L>), dim3(a.bt_grid), dim3(64 * kTiledBtWaves), 0, a.stream, a.blk1, a.blk0,
                        a.slots, a.slot_bytes, a.info, static_cast<const V *>(a.dist), static_cast<V *>(a.cost),
                        a.tour);
-    if (TSPGPU_TILED_ABL & 512)
-        hipLaunchKernelGGL((hk_tiled_backtrack<V, N, L>), dim3(a.bt_grid), dim3(64 * kTiledBtWaves), 0, a.stream, a.blk1,
-                           a.blk0, a.slots, a.slot_bytes, a.info, static_cast<const V *>(a.dist),
-                           static_cast<V *>(a.cost), a.tour);
     return hipGetLastError();
 }
 

@@ -323,7 +323,6 @@ int solve_sub(tspgpu_ctx *c, const SubCfg *cfg, const void *d_dist, int n, int n
         a.tour = d_tour;
         a.grid = std::min(grid, a.blk1 - a.blk0);
         a.bt_grid = std::min((a.blk1 - a.blk0 + kTiledBtWaves - 1) / kTiledBtWaves, c->cu_count * TSPGPU_TILED_BTWG);
-        a.cus = c->cu_count;
         a.stream = stream;
         hipError_t e = cfg->launch(a);
         if (e != hipSuccess) return hip_err(e);

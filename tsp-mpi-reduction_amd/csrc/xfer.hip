@@ -1,5 +1,6 @@
 // Small transfers through mapped pinned slots and our own copy kernel (xfer.h).
 #include "xfer.h"
+#include "xfer_pool.h"
 
 #include <cstdint>
 #include <cstring>
@@ -24,73 +25,60 @@ __global__ __launch_bounds__(256) void xset_kernel(W *__restrict__ dst, W v, siz
 
 int grid_for(size_t n) { return (int)(n / 256 + 1 < 1024 ? n / 256 + 1 : 1024); }
 
+// hipLaunchKernel returns THIS launch's status (hipGetLastError after a
+// triple-chevron launch would also return, and clear, an error some earlier
+// call left on the thread)
+template <typename W>
+hipError_t launch_copy_w(const void *src, void *dst, size_t n, hipStream_t st)
+{
+    const W *s = static_cast<const W *>(src);
+    W *d = static_cast<W *>(dst);
+    void *args[] = {&s, &d, &n};
+    return hipLaunchKernel(reinterpret_cast<const void *>(&xcopy_kernel<W>), dim3(grid_for(n)), dim3(256), args, 0, st);
+}
 hipError_t launch_copy(const void *src, void *dst, size_t bytes, hipStream_t st)
 {
     const uintptr_t a = (uintptr_t)src | (uintptr_t)dst | (uintptr_t)bytes;
-    if (!(a & 15)) {
-        hipLaunchKernelGGL(xcopy_kernel<uint4>, dim3(grid_for(bytes / 16)), dim3(256), 0, st,
-                           static_cast<const uint4 *>(src), static_cast<uint4 *>(dst), bytes / 16);
-    } else if (!(a & 7)) {
-        hipLaunchKernelGGL(xcopy_kernel<uint64_t>, dim3(grid_for(bytes / 8)), dim3(256), 0, st,
-                           static_cast<const uint64_t *>(src), static_cast<uint64_t *>(dst), bytes / 8);
-    } else if (!(a & 3)) {
-        hipLaunchKernelGGL(xcopy_kernel<uint32_t>, dim3(grid_for(bytes / 4)), dim3(256), 0, st,
-                           static_cast<const uint32_t *>(src), static_cast<uint32_t *>(dst), bytes / 4);
-    } else {
-        hipLaunchKernelGGL(xcopy_kernel<uint8_t>, dim3(grid_for(bytes)), dim3(256), 0, st,
-                           static_cast<const uint8_t *>(src), static_cast<uint8_t *>(dst), bytes);
-    }
-    return hipGetLastError();
+    if (!(a & 15)) return launch_copy_w<uint4>(src, dst, bytes / 16, st);
+    if (!(a & 7)) return launch_copy_w<uint64_t>(src, dst, bytes / 8, st);
+    if (!(a & 3)) return launch_copy_w<uint32_t>(src, dst, bytes / 4, st);
+    return launch_copy_w<uint8_t>(src, dst, bytes, st);
+}
+template <typename W>
+hipError_t launch_set_w(void *dst, W v, size_t n, hipStream_t st)
+{
+    W *d = static_cast<W *>(dst);
+    void *args[] = {&d, &v, &n};
+    return hipLaunchKernel(reinterpret_cast<const void *>(&xset_kernel<W>), dim3(grid_for(n)), dim3(256), args, 0, st);
 }
 
-// the slot pool: process-wide, any device (portable mapped pinned memory)
-constexpr int kSlots = 8;
-struct Slot {
-    char *h = nullptr;
-    hipEvent_t ev = nullptr;  // behind the last kernel that read or wrote the slot
-    int dev = -1;             // device of ev
-    bool pending = false;
-};
-struct Pool {
-    std::mutex mu;
-    Slot s[kSlots];
-    int next = 0;
-    bool broken = false;  // pinned allocation failed once: always the runtime path
-};
-Pool &pool()
-{
-    static Pool p;
-    return p;
-}
-
-// a free slot (waiting for its last user if all are busy), or null
-Slot *take(Pool &p, int dev)
-{
-    if (p.broken) return nullptr;
-    Slot &s = p.s[p.next];
-    p.next = (p.next + 1) % kSlots;
-    if (!s.h) {
+// the pinned slots (xfer_pool.h): one pool per device, events of that device
+struct HipSlots {
+    using Event = hipEvent_t;
+    using Stream = hipStream_t;
+    template <typename S>
+    bool alloc(S &s)
+    {
         if (hipHostMalloc((void **)&s.h, kXferSlotBytes, hipHostMallocMapped | hipHostMallocPortable) != hipSuccess) {
             s.h = nullptr;
-            p.broken = true;
-            return nullptr;
+            return false;
         }
-    }
-    if (s.pending) {
-        if (hipEventSynchronize(s.ev) != hipSuccess) return nullptr;
-        s.pending = false;
-    }
-    if (s.dev != dev) {
-        if (s.ev) (void)hipEventDestroy(s.ev);
-        s.ev = nullptr;
         if (hipEventCreateWithFlags(&s.ev, hipEventDisableTiming) != hipSuccess) {
+            (void)hipHostFree(s.h);
+            s.h = nullptr;
             s.ev = nullptr;
-            s.dev = -1;
-            return nullptr;
+            return false;
         }
-        s.dev = dev;
+        return true;
     }
-    return &s;
+    bool done(hipEvent_t e) { return hipEventQuery(e) == hipSuccess; }
+};
+constexpr int kMaxPoolDevs = 64;
+using Pool = XferPool<HipSlots>;
+Pool *pool(int dev)
+{
+    static Pool pools[kMaxPoolDevs];
+    return dev >= 0 && dev < kMaxPoolDevs ? &pools[dev] : nullptr;
 }
 
 }  // namespace
@@ -104,20 +92,27 @@ hipError_t xcopy_async(void *dst, const void *src, size_t bytes, hipMemcpyKind k
     int dev = 0;
     hipError_t e = hipGetDevice(&dev);
     if (e != hipSuccess) return e;
-    Pool &p = pool();
-    std::lock_guard<std::mutex> g(p.mu);
-    Slot *s = take(p, dev);
+    Pool *p = pool(dev);
+    bool wait = false;
+    Pool::Slot *s = p ? p->claim(st, &wait) : nullptr;
     if (!s) return hipMemcpyAsync(dst, src, bytes, kind, st);
+    // (outside the pool's lock: the slot is this thread's until release)
+    if (wait) e = hipEventSynchronize(s->ev);  // the last copy through it, on this same stream
+    if (e != hipSuccess) {
+        p->release(s, st, true);
+        return e;
+    }
     if (kind == hipMemcpyHostToDevice) {
         std::memcpy(s->h, src, bytes);
         e = launch_copy(s->h, dst, bytes, st);
         if (e == hipSuccess) e = hipEventRecord(s->ev, st);
-        s->pending = e == hipSuccess;
+        p->release(s, st, e == hipSuccess);
         return e;
     }
     e = launch_copy(src, s->h, bytes, st);
     if (e == hipSuccess) e = hipStreamSynchronize(st);
     if (e == hipSuccess) std::memcpy(dst, s->h, bytes);
+    p->release(s, st, false);
     return e;
 }
 
@@ -125,14 +120,8 @@ hipError_t xset_async(void *dst, int value, size_t bytes, hipStream_t st)
 {
     if (!bytes) return hipSuccess;
     const uint32_t b = (uint32_t)value & 0xffu;
-    if (!(((uintptr_t)dst | bytes) & 3)) {
-        hipLaunchKernelGGL(xset_kernel<uint32_t>, dim3(grid_for(bytes / 4)), dim3(256), 0, st,
-                           static_cast<uint32_t *>(dst), b * 0x01010101u, bytes / 4);
-    } else {
-        hipLaunchKernelGGL(xset_kernel<uint8_t>, dim3(grid_for(bytes)), dim3(256), 0, st,
-                           static_cast<uint8_t *>(dst), (uint8_t)b, bytes);
-    }
-    return hipGetLastError();
+    if (!(((uintptr_t)dst | bytes) & 3)) return launch_set_w<uint32_t>(dst, b * 0x01010101u, bytes / 4, st);
+    return launch_set_w<uint8_t>(dst, (uint8_t)b, bytes, st);
 }
 
 }  // namespace tspgpu

@@ -22,6 +22,7 @@ min and its tie rule, across shards).
 """
 from __future__ import annotations
 
+import atexit
 import errno
 import os
 import threading
@@ -105,13 +106,44 @@ class RcclComm:
 _COMMS = {}
 
 
+def _group_ranks(group):
+    """The group's members as global ranks (its identity for the cache: id()
+    of a freed subgroup can be reused by a new group with other members)."""
+    import torch.distributed as tdist
+
+    if group is None:
+        return tuple(range(tdist.get_world_size()))
+    return tuple(tdist.get_global_rank(group, r) for r in range(tdist.get_world_size(group)))
+
+
 def rccl_comm(group, rank: int, world: int, device_index: int) -> RcclComm:
     """The process's communicator for this group and device (created once:
-    ncclCommInitRank costs far more than a search)."""
-    key = (id(group), rank, world, device_index)
-    if key not in _COMMS:
-        _COMMS[key] = RcclComm(group, rank, world, device_index)
-    return _COMMS[key]
+    ncclCommInitRank costs far more than a search).  Keyed on the group's
+    global rank list and the process-group object, which the cache keeps
+    alive (so its id is never reused: a re-initialised torch.distributed or a
+    new subgroup gets its own communicator), and the device."""
+    import torch.distributed as tdist
+
+    pg = group if group is not None else tdist.group.WORLD
+    key = (_group_ranks(group), id(pg), rank, world, device_index)
+    ent = _COMMS.get(key)
+    if ent is None or not ent[1].handle:
+        ent = _COMMS[key] = (pg, RcclComm(group, rank, world, device_index))
+    return ent[1]
+
+
+def close_comms():
+    """Destroy every cached RCCL communicator (ncclCommDestroy); called at
+    exit, and safe to call before torch.distributed.destroy_process_group."""
+    while _COMMS:
+        _, (_, c) = _COMMS.popitem()
+        try:
+            c.close()
+        except Exception:  # (at interpreter exit the library may be gone)
+            pass
+
+
+atexit.register(close_comms)
 
 
 _I64_MAX = (1 << 63) - 1
@@ -152,8 +184,10 @@ def solve_sharded(ctx, dist, group=None, depth: int = 0, device=None, exchange_e
        all-reduce MIN of (incumbent, -busy) every `exchange_every` steps
        (default 4; the same count on every rank, so the collectives pair up)
        followed by all-reduce MIN of w0 (ranks without one send the maximum)
-       and of w1 among its holders.  Every rank certifies the winning key once
-       (tspgpu_tie_tour_gpu): tsp()'s tour with no record leaving any rank.
+       and of w1 among its holders.  Rank 0 certifies the winning key
+       (tspgpu_tie_tour_gpu) and broadcasts the result — one more collective
+       in stats["collectives"] — so every rank takes the same branch:
+       tsp()'s tour with no record leaving any rank.
        Only when a tie table overflowed or the certificate fails do the ranks
        gather their optimal records for the host tie rule (a second search
        first if records were lost).
@@ -236,19 +270,33 @@ def solve_sharded(ctx, dist, group=None, depth: int = 0, device=None, exchange_e
             if herr:
                 raise tspgpu.TspGpuError(-errno.EIO, f"{herr} in-stream RCCL exchanges failed to enqueue")
         elif collective:
-            nh = [0]
+            nh, herr = [0], []
 
             def host_exchange(_stream, _word):
                 # (gloo: the word through the host at the level boundary —
-                # counters synchronises the stream up to here)
+                # counters synchronises the stream up to here).  ctypes drops
+                # an exception raised in a callback, so a failing rank would
+                # skip its all-reduce while the others block in theirs: every
+                # call joins the collective (with the neutral maximum when
+                # its own word is unavailable) and the error is raised after
+                # the chain returns.
                 nh[0] += 1
-                cur = S.counters()[0]
+                try:
+                    cur = S.counters()[0] if not herr else _I64_MAX
+                except Exception as e:  # noqa: BLE001 (re-raised below)
+                    herr.append(e)
+                    cur = _I64_MAX
                 best = allmin([cur])[0]
-                if best < cur:
-                    S.set_bound(tspgpu.bits_cost(best, S.dtype))
+                if not herr and best < cur:
+                    try:
+                        S.set_bound(tspgpu.bits_cost(best, S.dtype))
+                    except Exception as e:  # noqa: BLE001
+                        herr.append(e)
 
             chained = S.chain(exchange_levels, hook=host_exchange)
             hooks = nh[0]
+            if herr:
+                raise herr[0]
         else:
             chained = S.chain()
         inc, nodes, recs = S.counters()  # (a finished chain: from its own readback)
