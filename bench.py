@@ -660,6 +660,7 @@ def k2_strong_scaling(ctx, n, seed, group, backend, world, rank, reps=2):
             "bb_nodes_expanded": st["nodes"], "rounds": st.get("rounds"), "exchanges": st["exchanges"],
             "in_chain_exchanges": st.get("hooks", 0), "exchange_levels": st.get("exchange_levels"),
             "chained": st.get("chained"), "optimal_tours": st["optimal_tours"],
+            "host_phases_ms": st.get("host_phases_ms"),
             "exchange": "RCCL all-reduce MIN of the device incumbent inside the chain every "
                         f"{st.get('exchange_levels')} levels (libtspcomm), then one all-gather" if backend == "nccl"
                         else ("host all-reduce MIN at level boundaries (gloo)" if world > 1 else "none (one rank)")}

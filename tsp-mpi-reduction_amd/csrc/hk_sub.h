@@ -333,24 +333,8 @@ __device__ __forceinline__ uint32_t sub_col(uint32_t hp, uint32_t x)
 // vmcnt), rotated wave roles, scalar loads of the high-high distances (+60%),
 // one |h| dispatch per sub-cube, a workgroup-form backtracking (no faster).
 
-// Next pass's push values loaded ahead (TSPGPU_SUB_PF, A/B): vector-memory
-// operations retire in issue order (one vmcnt per wave), so a pass's push
-// loads, issued at its start, also waited for the previous pass's push
-// stores' acknowledgements.  Thread r owns row r in every middle pass of a
-// sub-cube and the high members of pass J + 1 are pass J's, so pass J issues
-// pass J + 1's push loads itself — BEFORE its own push stores (1: between its
-// last chunk's relaxations and the global stores; 2: before the last chunk's
-// relaxations), which puts its stores behind the loads in the vmcnt order.
-// (Round 5's early loads were issued after the stores and lost.)  The last
-// chunk holds every high destination (chunks [0, Q - QC) and [Q - QC, Q)).
-#ifndef TSPGPU_SUB_PF
-#define TSPGPU_SUB_PF 0
-#endif
-constexpr int kSubPre = 6;  // >= H
-
 template <typename V, int N, int L, int T, int J>
-__device__ __forceinline__ void sub_mid(const SubCtx<V, N, L> &c, uint32_t h, uint32_t tid, const uint4 &ent,
-                                        V (&pre)[kSubPre])
+__device__ __forceinline__ void sub_mid(const SubCtx<V, N, L> &c, uint32_t h, uint32_t tid, const uint4 &ent)
 {
     constexpr int H = N - L;
     constexpr int Q = N - T;
@@ -399,29 +383,11 @@ __device__ __forceinline__ void sub_mid(const SubCtx<V, N, L> &c, uint32_t h, ui
         for (int p = 0; p < J; ++p) g[p] = act ? src[p * ROWS + r] : V(0);
     }
     const uint32_t voff = (BASE + r) * VB;  // the row's offset in a push column
-    constexpr bool PF_IN = TSPGPU_SUB_PF && J > 2, PF_OUT = TSPGPU_SUB_PF && J < L - 2;
     if (act) {
 #pragma unroll
-        for (int i = 0; i < HC; ++i)
-            g[J + i] = PF_IN ? pre[i] : c.push.load(voff, sub_col<H>(h, hm[i]) * (uint32_t)(NL * VB));
+        for (int i = 0; i < HC; ++i) g[J + i] = c.push.load(voff, sub_col<H>(h, hm[i]) * (uint32_t)(NL * VB));
     }
-    // pass J + 1's push values (this thread owns row r there too)
-    auto prefetch = [&] {
-        if constexpr (PF_OUT && HC > 0) {
-            constexpr int ROWS_X = cbinom(L, J + 1), BASE_X = tiled_moff(L, J + 1);
-            __builtin_amdgcn_sched_barrier(0);
-            if (r < (uint32_t)ROWS_X) {
-#pragma unroll
-                for (int i = 0; i < HC; ++i)
-                    pre[i] = c.push.load((BASE_X + r) * VB, sub_col<H>(h, hm[i]) * (uint32_t)(NL * VB));
-            }
-            __builtin_amdgcn_sched_barrier(0);
-        }
-    };
-    if (!act) {
-        prefetch();
-        return;
-    }
+    if (!act) return;
     uint32_t mrow[J], kof[QL];
 #pragma unroll
     for (int p = 0; p < J; ++p) mrow[p] = sub_nib(ent, p) * DSB;
@@ -433,15 +399,9 @@ __device__ __forceinline__ void sub_mid(const SubCtx<V, N, L> &c, uint32_t h, ui
     for (int i = 0; i < HC; ++i) hrow[i] = (L + hm[i]) * DSB;
     uint32_t wlo = 0, whi = 0;
     constexpr int QC = kSubQC;
-    constexpr int NC = (Q + QC - 1) / QC;
-    static_assert(NC <= 2 && QH <= QC, "chunks");
-    static_for<NC>([&](auto ci) {
-        constexpr int CI = decltype(ci)::value;
-        // (TSPGPU_SUB_PF: the last chunk holds every high destination)
-        constexpr int C0 = TSPGPU_SUB_PF ? (CI == 0 ? 0 : Q - QC) : CI * QC;
-        constexpr int QN = TSPGPU_SUB_PF ? (NC == 1 ? Q : (CI == 0 ? Q - QC : QC)) : (Q - C0 < QC ? Q - C0 : QC);
-        constexpr bool LAST = CI == NC - 1;
-        if constexpr (LAST && TSPGPU_SUB_PF == 2) prefetch();
+    static_for<(Q + QC - 1) / QC>([&](auto ci) {
+        constexpr int C0 = decltype(ci)::value * QC;
+        constexpr int QN = Q - C0 < QC ? Q - C0 : QC;
         constexpr int CNT = sub_lds_count<T, J, QL, C0, QN>();
         constexpr int AH = kSubAhead < CNT ? kSubAhead : CNT;
         // integer min-only rows: member pairs per destination (v_min3_i32)
@@ -535,36 +495,6 @@ __device__ __forceinline__ void sub_mid(const SubCtx<V, N, L> &c, uint32_t h, ui
                         relax_min_s(acc[qq], g[J + i], hh[i * QH + (q - QL)]);
                 }
             }
-        if constexpr (TSPGPU_SUB_PF) {
-            // low destinations (LDS), the next pass's push loads, then the
-            // high destinations (push stores) and the parent word
-#pragma unroll
-            for (int qq = 0; qq < QN; ++qq) {
-                const int q = C0 + qq;
-                if (q < QL) {
-                    const uint32_t k = kof[q] / VB;
-                    const uint32_t slot = (k - (uint32_t)q) * (uint32_t)ROWS_N + sub_rank(ent, q);
-                    c.region[NXT + slot] = acc[qq];
-                }
-                if constexpr (ARG) {
-                    const uint32_t pos = arg[qq] / DSB;
-                    if (q < 8)
-                        wlo |= pos << (4 * q);
-                    else
-                        whi |= pos << (4 * (q - 8));
-                }
-            }
-            if constexpr (LAST && TSPGPU_SUB_PF == 1) prefetch();
-#pragma unroll
-            for (int qq = 0; qq < QN; ++qq) {
-                const int q = C0 + qq;
-                if (q >= QL) {
-                    const uint32_t cb = hn[q - QL];
-                    c.push.store(voff, sub_col<H>(h | (1u << cb), cb) * (uint32_t)(NL * VB), acc[qq]);
-                }
-            }
-            return;
-        }
 #pragma unroll
         for (int qq = 0; qq < QN; ++qq) {
             const int q = C0 + qq;
@@ -833,12 +763,12 @@ __device__ __forceinline__ void sub_build_high(const SubCtx<V, N, L> &c, uint32_
 
 template <typename V, int N, int L, int J>
 __device__ __forceinline__ void sub_dispatch_mid_j(const SubCtx<V, N, L> &c, uint32_t h, int hc, uint32_t tid,
-                                                   const uint4 &ent, V (&pre)[kSubPre])
+                                                   const uint4 &ent)
 {
     constexpr int H = N - L;
 #define TSPGPU_SM(HC)                                                                                  \
     case HC:                                                                                           \
-        if constexpr (HC <= H) sub_mid<V, N, L, J + (HC <= H ? HC : 0), J>(c, h, tid, ent, pre);  \
+        if constexpr (HC <= H) sub_mid<V, N, L, J + (HC <= H ? HC : 0), J>(c, h, tid, ent);  \
         break;
     switch (hc) {
         TSPGPU_SM(0) TSPGPU_SM(1) TSPGPU_SM(2) TSPGPU_SM(3) TSPGPU_SM(4) TSPGPU_SM(5) TSPGPU_SM(6) TSPGPU_SM(7)
@@ -968,9 +898,6 @@ __global__ __launch_bounds__(THREADS, tiled_waves(THREADS, WG)) void hk_sub_kern
         __syncthreads();
 
         uint4 ent = make_uint4(0, 0, 0, 0);
-        V pre[kSubPre];  // the next middle pass's push values (TSPGPU_SUB_PF)
-#pragma unroll
-        for (int i = 0; i < kSubPre; ++i) pre[i] = V(0);
         for (uint32_t h = 0; h < (uint32_t)NH; ++h) {
             const int hc = __builtin_popcount(h);
             // interval A(h): passes 0/1 of h (lanes < 192) beside pass L of h - 1 (lanes 192..)
@@ -1001,7 +928,7 @@ __global__ __launch_bounds__(THREADS, tiled_waves(THREADS, WG)) void hk_sub_kern
                     constexpr int MN = tiled_moff(L, j + 1), CN = cbinom(L, j + 1);
                     ent = rowtab[MN + (tj < (uint32_t)CN ? tj : 0u)];
                 }
-                sub_dispatch_mid_j<V, N, L, j>(c, h, hc, tj, cur, pre);
+                sub_dispatch_mid_j<V, N, L, j>(c, h, hc, tj, cur);
                 if constexpr (OV) {
                     // edge passes on the waves this middle pass leaves idle
                     static_assert(cbinom(L, 2) <= 64 && cbinom(L, 3) <= 128 && cbinom(L, L - 3) <= 128, "overlap: idle waves");

@@ -47,10 +47,15 @@ void local_search(const V *d, int n, std::vector<int> &t)
     // tolerance (asymmetric matrices: the local deltas assume symmetry), and
     // the number of moves is capped: the loop always ends
     double cur = len_of(t);
-    auto accept = [&](std::vector<int> &cand) {
-        const double c = len_of(cand);
-        if (c < cur - 1e-9 * (1.0 + std::fabs(cur))) {
-            t.swap(cand);
+    auto better = [&](double c) { return c < cur - 1e-9 * (1.0 + std::fabs(cur)); };
+    // (scratch buffers reused by every candidate: no allocation per move)
+    std::vector<int> cand, seg;
+    cand.reserve(n);
+    seg.reserve(4);
+    auto accept = [&](std::vector<int> &cd) {
+        const double c = len_of(cd);
+        if (better(c)) {
+            t.swap(cd);
             cur = c;
             return true;
         }
@@ -62,9 +67,15 @@ void local_search(const V *d, int n, std::vector<int> &t)
             for (int j = i + 1; j < n && !improved; ++j) {
                 const int a = t[i - 1], b = t[i], c = t[j], e = t[(j + 1) % n];
                 if ((D(a, c) + D(b, e)) - (D(a, b) + D(c, e)) < 0) {
-                    std::vector<int> cand(t);
-                    std::reverse(cand.begin() + i, cand.begin() + j + 1);
-                    improved = accept(cand);
+                    // the 2-opt candidate in place, undone when it does not pay
+                    std::reverse(t.begin() + i, t.begin() + j + 1);
+                    const double cl = len_of(t);
+                    if (better(cl)) {
+                        cur = cl;
+                        improved = 1;
+                    } else {
+                        std::reverse(t.begin() + i, t.begin() + j + 1);
+                    }
                 }
             }
         for (int len = 1; len <= 3 && !improved && n > len + 2; ++len)
@@ -83,7 +94,8 @@ void local_search(const V *d, int n, std::vector<int> &t)
                     const double rev = D(u, s1) + D(s0, v) - D(u, v);
                     const bool r = rev < fwd;
                     if ((r ? rev : fwd) - gain >= 0) continue;
-                    std::vector<int> seg, cand;
+                    seg.clear();
+                    cand.clear();
                     for (int z = 0; z < len; ++z) seg.push_back(t[(i + z) % n]);
                     if (r) std::reverse(seg.begin(), seg.end());
                     for (int z = 0; z < n - len; ++z) {
@@ -192,37 +204,59 @@ void held_karp_pi(const std::vector<double> &D, int n, std::vector<double> &best
         ub += D[(size_t)k * n];
     }
     std::vector<double> pi(n, 0.0), key(n);
-    std::vector<int> deg(n), par(n);
-    std::vector<char> in(n);
+    std::vector<int> deg(n), par(n), out(n);
     double best = -INFINITY, lam = 2.0;
     int stall = 0;
     best_pi.assign(n, 0.0);
-    auto dp = [&](int x, int y) { return D[(size_t)x * n + y] + pi[x] + pi[y]; };
+    const double *Dp = D.data();
     for (int it = 0; it < 300 && n >= 3; ++it) {
         std::fill(deg.begin(), deg.end(), 0);
-        std::fill(in.begin(), in.end(), 0);
         double lb = 0.0;
-        for (int v = 1; v < n; ++v) key[v] = dp(1, v), par[v] = 1;
-        in[1] = 1;
-        for (int step = 2; step < n; ++step) {
-            int u = -1;
-            for (int v = 2; v < n; ++v)
-                if (!in[v] && (u < 0 || key[v] < key[u])) u = v;
-            in[u] = 1;
-            lb += key[u];
+        // Prim from city 1 over cities 1..n-1 on d' = (d + pi_x) + pi_y: the
+        // cities not in the tree kept in a compact list, ascending, so every
+        // scan touches only them and the first minimum is the lowest index
+        // (the same tree, the same sums as the scan over all cities with an
+        // in-tree flag it replaces: round 6, 32 cities ~1.3 ms)
+        int m = 0;
+        {
+            const double *D1 = Dp + n;
+            const double p1 = pi[1];
+            for (int v = 2; v < n; ++v) {
+                key[v] = (D1[v] + p1) + pi[v];
+                par[v] = 1;
+                out[m++] = v;
+            }
+        }
+        while (m > 0) {
+            int bi = 0;
+            double bk = key[out[0]];
+            for (int i = 1; i < m; ++i) {
+                const double k = key[out[i]];
+                if (k < bk) bk = k, bi = i;
+            }
+            const int u = out[bi];
+            for (int i = bi + 1; i < m; ++i) out[i - 1] = out[i];
+            --m;
+            lb += bk;
             ++deg[u];
             ++deg[par[u]];
-            for (int v = 2; v < n; ++v)
-                if (!in[v] && dp(u, v) < key[v]) key[v] = dp(u, v), par[v] = u;
+            const double *Du = Dp + (size_t)u * n;
+            const double pu = pi[u];
+            for (int i = 0; i < m; ++i) {
+                const int v = out[i];
+                const double w = (Du[v] + pu) + pi[v];
+                if (w < key[v]) key[v] = w, par[v] = u;
+            }
         }
+        auto dp0 = [&](int v) { return (Dp[v] + pi[0]) + pi[v]; };
         int a = -1, b = -1;
         for (int v = 1; v < n; ++v) {
-            if (a < 0 || dp(0, v) < dp(0, a))
+            if (a < 0 || dp0(v) < dp0(a))
                 b = a, a = v;
-            else if (b < 0 || dp(0, v) < dp(0, b))
+            else if (b < 0 || dp0(v) < dp0(b))
                 b = v;
         }
-        lb += dp(0, a) + dp(0, b);
+        lb += dp0(a) + dp0(b);
         deg[0] = 2;
         ++deg[a];
         ++deg[b];

@@ -238,6 +238,14 @@ def solve_sharded(ctx, dist, group=None, depth: int = 0, device=None, exchange_e
     def _heuristic():
         heur["v"] = tspgpu.heuristic_tour(dist, first=rank, step=world) if split else tspgpu.heuristic_tour(dist)
 
+    # host phase clock (stats["host_phases_ms"]): where a rank's wall time goes
+    ph, ph_t = {}, [time.perf_counter()]
+
+    def mark(name):
+        t = time.perf_counter()
+        ph[name] = ph.get(name, 0.0) + (t - ph_t[0]) * 1e3
+        ph_t[0] = t
+
     th = threading.Thread(target=_heuristic) if len(dist) >= 20 else None  # (smaller: not worth a thread)
     if th is not None:
         th.start()
@@ -248,6 +256,7 @@ def solve_sharded(ctx, dist, group=None, depth: int = 0, device=None, exchange_e
             th.join()
     if "v" not in heur:
         _heuristic()  # (no thread, or it raised: here, so an error surfaces)
+    mark("create_and_heuristic")
     try:
         if split:
             ub_r, _ = heur["v"]
@@ -256,6 +265,7 @@ def solve_sharded(ctx, dist, group=None, depth: int = 0, device=None, exchange_e
         else:
             ub, _ = heur["v"]
         S.set_bound(ub)
+        mark("bound")
         t0 = time.perf_counter()
         two = S.n - 1 > 20
         exchanges = 0
@@ -299,6 +309,7 @@ def solve_sharded(ctx, dist, group=None, depth: int = 0, device=None, exchange_e
                 raise herr[0]
         else:
             chained = S.chain()
+        mark("chain")
         inc, nodes, recs = S.counters()  # (a finished chain: from its own readback)
         # Fast path, every rank one finished chain: ONE collective.  Each rank
         # contributes (incumbent, chained, its tie slot at that incumbent,
@@ -349,6 +360,7 @@ def solve_sharded(ctx, dist, group=None, depth: int = 0, device=None, exchange_e
             if two:
                 (K1,) = allmin([_key_i64(w1) if found and k0 == K0 else _I64_MAX])
         cost = tspgpu.bits_cost(opt, S.dtype)
+        mark("winner")
         tie, tour = 0, None
         if nov == 0 and K0 != _I64_MAX:
             # certified ONCE, on rank 0, and broadcast: every rank then takes
@@ -368,6 +380,7 @@ def solve_sharded(ctx, dist, group=None, depth: int = 0, device=None, exchange_e
                 rc, t = (0 if vals[0] else -errno.EAGAIN), np.asarray(vals[1:], dtype=np.int32)
             if rc == 0:
                 tie, tour = 1, t
+        mark("certificate")
         phases, fallback, gathered, n_opt = 1, 0, 0, 0
         if not tie:
             tour, phases, fallback, nodes, n_opt = _records_winner(S, ctx, dist, opt, recs, nodes, allmin,
@@ -385,13 +398,14 @@ def solve_sharded(ctx, dist, group=None, depth: int = 0, device=None, exchange_e
                 total_nodes = int(nodes)
         wall = time.perf_counter() - t0
         kernel_ms, rounds = S.timing()
+        mark("records_and_stats")
         stats = {"nodes": total_nodes, "rank_nodes": int(S.counters()[1]),
                  "optimal_tours": n_opt, "depth": S.depth,
                  "items": S.items, "phases": phases, "fallback": fallback, "kernel_ms": kernel_ms, "rounds": rounds,
                  "wall_s": wall, "tie": tie, "record_gather": gathered, "chained": int(chained),
                  "collectives": ncoll[0], "exchanges": exchanges, "hooks": hooks, "exchange_levels": exchange_levels,
                  "exchange_every": exchange_every, "world": world,
-                 "backend": backend}
+                 "backend": backend, "host_phases_ms": ph}
         return cost, tour, stats
     finally:
         S.close()
