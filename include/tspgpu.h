@@ -263,6 +263,14 @@ int tspgpu_search_enumerate(tspgpu_ctx *ctx, const void *dist, int dtype, int n,
  * from every shard and calls tspgpu_select_tour.  depth 0 = automatic. */
 int tspgpu_search_create(tspgpu_ctx *ctx, const void *dist, int dtype, int n, int shard, int nshards, int depth,
                          tspgpu_search **out);
+/* tspgpu_search_create with flags.  TSPGPU_SEARCH_DEVICE_BOUND: the create
+ * launch also computes the initial incumbent on the device (nearest neighbour
+ * from spread start cities + 2-opt, the cheaper left fold of either
+ * direction; every shard of an instance gets the same bound), so a driver
+ * needs no host heuristic and no tspgpu_search_set_bound before the search. */
+#define TSPGPU_SEARCH_DEVICE_BOUND 1
+int tspgpu_search_create_ex(tspgpu_ctx *ctx, const void *dist, int dtype, int n, int shard, int nshards, int depth,
+                            int flags, tspgpu_search **out);
 int tspgpu_search_destroy(tspgpu_search *s);
 int tspgpu_search_info(const tspgpu_search *s, int *depth, uint64_t *items, uint64_t *local_items);
 /* initial incumbent (a real tour's cost, e.g. tspgpu_heuristic_tour) */

@@ -35,7 +35,7 @@ class FakeSearch:
     chainable = True  # chain(): the whole shard in one call (False: the stepwise path)
     tie_on = True     # tie_slot(): the least key at a cost (False: "overflow", the records decide)
 
-    def __init__(self, ctx, dist, shard=0, nshards=1, depth=0):
+    def __init__(self, ctx, dist, shard=0, nshards=1, depth=0, device_bound=False):
         import tspgpu
 
         self.dist, self.dtype = tspgpu._search_dist(dist)
@@ -49,6 +49,8 @@ class FakeSearch:
         self.claimed = 0
         self.rounds = 0
         self.keys = {}  # cost bits -> least tie key (w0, w1) of the tours found at that cost
+        if device_bound:  # (the create launch's bound: a real tour's cost, the same on every shard)
+            self.set_bound(tspgpu.heuristic_tour(self.dist)[0])
 
     def _fold(self, t):
         c = self.dist.dtype.type(0)

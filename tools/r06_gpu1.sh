@@ -21,3 +21,6 @@ echo "bench rc=$?"; tail -c 600 $OUT/bench.json
 # K1 A/B: next pass's push loads issued before this pass's push stores (TSPGPU_SUB_PF=1)
 OUT=gpurun_out/r06/ab_pf ROUNDS=2 timeout -k 10 600 bash tools/ab_time.sh
 echo "ab rc=$?"
+# K2: host/device split of the sharded solve at N = 1 (32-city seed 35, 16-city golden)
+timeout -k 10 300 python3 tools/k2_sharded_phases.py > gpurun_out/r06/gpu1/k2_phases.json 2> gpurun_out/r06/gpu1/k2_phases.err
+echo "k2 phases rc=$?"; cat gpurun_out/r06/gpu1/k2_phases.json

@@ -13,3 +13,5 @@ timeout -k 10 300 python3 -u tools/k1_time.py 16 65536 4 6 > $OUT/k1_time_65536_
 echo "k1 i32 time rc=$?"; tail -1 $OUT/k1_time_65536_i32.log
 timeout -k 10 300 python3 tools/k2_sharded_phases.py > $OUT/k2_phases.json 2> $OUT/k2_phases.err
 echo "k2 phases rc=$?"; cat $OUT/k2_phases.json
+timeout -k 10 600 python3 tools/startup_split_probe.py > $OUT/startup_split_probe.json 2>&1
+echo "startup probe rc=$?"; cat $OUT/startup_split_probe.json

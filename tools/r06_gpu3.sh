@@ -1,0 +1,14 @@
+#!/bin/bash
+# Round-6 check 3: K2 with the device initial bound up to 32 cities (sharded
+# and native, against the host multi-start), the K2 GPU tests, and the
+# backtracking A/B (members-only relaxations, lib_ab/btm.so).
+set -u
+cd "$(dirname "$0")/.."
+OUT=gpurun_out/r06/gpu3
+mkdir -p $OUT
+timeout -k 10 600 python -u -m pytest tests/test_search_gpu.py tests/test_rccl_gpu.py tests/test_search_dist.py tests/test_search_cli.py -x -q --timeout 240 --timeout-method thread > $OUT/k2_tests.log 2>&1
+rc=$?; echo "k2 tests rc=$rc"; tail -3 $OUT/k2_tests.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 400 python3 tools/k2_sharded_phases.py > $OUT/k2_phases.json 2> $OUT/k2_phases.err
+echo "k2 phases rc=$?"; cat $OUT/k2_phases.json
+OUT=gpurun_out/r06/ab_bt ROUNDS=2 timeout -k 10 600 bash tools/ab_time.sh
+echo "ab rc=$?"

@@ -465,12 +465,20 @@ __device__ __forceinline__ uint32_t tiled_pidx(const TiledCtx<V, N, L, R> &c, ui
 // every low member m, layer by layer from the pushed high-member values — the
 // forward pass's own relaxations restricted to those rows, the minimum only
 // (IEEE min is order-free, so the values are the forward pass's bits).
+// Round 6: a lane per (row, destination) pair — a layer of C(nl, j) rows has
+// (nl - j) destinations per row, so a wave's lanes are busy where the
+// row-per-lane form left most idle in the small layers, and each lane relaxes
+// only its own destination over the row's members only (not N predicated
+// relaxations per possible destination): hk_tiled_backtrack per 65536 16-city
+// blocks 1.76 ms (row per lane) -> 1.44 ms (pairs) -> ~1.33 ms (members
+// only; profiles/r06/bt_ab.txt).
 template <typename V, int N, int L, int R>
 __device__ void tiled_recompute(const TiledCtx<V, N, L, R> &c, const V *d0, uint32_t h, uint32_t lT,
                                 uint32_t lane)
 {
     constexpr int VB = sizeof(V);
     const int nl = __builtin_popcount(lT);
+    const int hcnt = __builtin_popcount(h);
     int j0 = 0;
     if (h == 0) {  // no high member: layer 1 is G[{k}][k] = d[0][k] (tsp.cpp:435)
         if (lane < (uint32_t)L && ((lT >> lane) & 1u)) c.rec.store(((1u << lane) * L + lane) * VB, 0, d0[lane]);
@@ -480,32 +488,38 @@ __device__ void tiled_recompute(const TiledCtx<V, N, L, R> &c, const V *d0, uint
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-        const int cnt = cbinom(nl, j), mo = c.moff[j];
-        for (int r = (int)lane; r < cnt; r += 64) {
+        const int q = nl - j, pairs = cbinom(nl, j) * q, mo = c.moff[j];
+        for (int e = (int)lane; e < pairs; e += 64) {
+            const int r = e / q, qi = e - r * q;
             // the r-th j-subset of lT in colex order = the r-th j-subset of
-            // the low bits, deposited on lT's cities
+            // the low bits, deposited on lT's cities; its qi-th destination
             const uint32_t lp = pdep_u32(c.lmask[mo + r], lT);
-            const uint32_t dst = lT & ~lp;
+            const uint32_t s = (uint32_t)__builtin_ctz(pdep_u32(1u << qi, lT & ~lp));
             const uint32_t Tm = (h << L) | lp;
             const uint32_t pidx = tiled_pidx(c, lp);
-            V gv[N];  // the row's values (all loads in flight at once; non-members unused)
+            // members only: the row's T = j + |h| members (T wave-uniform, so
+            // every "q < T" is a scalar branch), their loads all in flight
+            // (round 6: -7.5% against N predicated relaxations per pair)
+            const int T = j + hcnt;
+            V acc = ValT<V>::inf;
+            // (every value in flight at once: 9 VGPRs of spills at six
+            // workgroups per CU, and still faster than loading the member
+            // list in two halves without spills, 0.41 vs 0.51 ms per 16384
+            // blocks: profiles/r06/bt_ab.txt)
+            V gv[N - 1];
+            uint32_t x = Tm;
 #pragma unroll
-            for (int m = 0; m < N; ++m) gv[m] = tiled_g(c, h, lp, pidx, m);
-            // every destination s of lT \ lp, every member m: predicated, the
-            // distance reads are wave-uniform LDS broadcasts
-#pragma unroll
-            for (int s = 0; s < L; ++s) {
-                if ((dst >> s) & 1u) {
-                    V acc = ValT<V>::inf;
-#pragma unroll
-                    for (int m = 0; m < N; ++m) {
-                        const V t = ValT<V>::vmin(acc, gv[m] + c.dr[(m * kTiledDS + s) * R]);
-                        acc = ((Tm >> m) & 1u) ? t : acc;
-                    }
-                    c.rec.store(((lp | (1u << s)) * L + (uint32_t)s) * VB, 0, acc);
-                }
-                __builtin_amdgcn_sched_barrier(0);
+            for (int q = 0; q < N - 1; ++q) {
+                if (q < T) gv[q] = tiled_g(c, h, lp, pidx, __builtin_ctz(x));
+                x &= x - 1u;
             }
+            x = Tm;
+#pragma unroll
+            for (int q = 0; q < N - 1; ++q) {
+                if (q < T) acc = ValT<V>::vmin(acc, gv[q] + c.dr[((uint32_t)__builtin_ctz(x) * kTiledDS + s) * R]);
+                x &= x - 1u;
+            }
+            c.rec.store(((lp | (1u << s)) * L + s) * VB, 0, acc);
         }
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");

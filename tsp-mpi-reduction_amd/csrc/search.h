@@ -300,7 +300,7 @@ struct SearchInit {
     unsigned long long *inc_word[2];
     unsigned long long inc_init;  // f64 bits or a non-negative int32 cost
     const void *heur_dist;        // heur_n x heur_n, f64 or i32 (host staging, read by the kernel)
-    int heur_n;                   // 0: no device heuristic; else 4 <= heur_n <= 20
+    int heur_n;                   // 0: no device heuristic; else 4 <= heur_n <= kSearchMaxN
     int heur_f64;
     int heur_sym;                 // the matrix is symmetric (2-opt deltas are then exact)
     int heur_starts;              // start cities, spread over 0..n-1 (at most 16)

@@ -1204,7 +1204,8 @@ __device__ __forceinline__ double wave_sum(double x)
 
 __device__ __forceinline__ void init_heuristic(const SearchInit &in)
 {
-    constexpr int kWaves = 16, kPairs = 3;  // 1024 threads (heur_starts of them work); heur_n <= 20: <= 171 pairs
+    // 1024 threads (heur_starts of them work); heur_n <= kSearchMaxN: <= 465 pairs (8 per lane)
+    constexpr int kWaves = 16, kPairs = ((kSearchMaxN - 1) * (kSearchMaxN - 2) / 2 + 63) / 64;
     __shared__ double hd[kSearchMaxN * kSearchMaxN];
     __shared__ int ht[kWaves][kSearchMaxN];
     __shared__ double hbest[kWaves];
@@ -1343,7 +1344,7 @@ __global__ __launch_bounds__(1024) void init_kernel(SearchInit in)
 
 hipError_t launch_init(const SearchInit &init, hipStream_t stream)
 {
-    if (init.ncopy < 0 || init.ncopy > 8 || init.heur_n < 0 || init.heur_n > 20 ||
+    if (init.ncopy < 0 || init.ncopy > 8 || init.heur_n < 0 || init.heur_n > kSearchMaxN ||
         (init.heur_n && (init.heur_n < 4 || init.heur_starts < 1 || init.heur_starts > 16)))
         return hipErrorInvalidValue;
     // 16 blocks of 1024 (block 0's sixteen waves: the heuristic's start cities)

@@ -598,7 +598,7 @@ static int search_create(tspgpu_ctx *c, const void *dist, int dtype, int n, int 
         in.inc_word[0] = s->d_words + 1;
         in.inc_word[1] = s->d_words + 14;
         in.inc_init = w[1];
-        if (dev_bound && n >= 4 && n <= 20) {
+        if (dev_bound && n >= 4 && n <= kSearchMaxN) {
             bool msym = true;
             for (int i = 0; i < n && msym; ++i)
                 for (int j = 0; j < i && msym; ++j)
@@ -610,8 +610,9 @@ static int search_create(tspgpu_ctx *c, const void *dist, int dtype, int n, int 
             in.heur_sym = msym ? 1 : 0;
             // four spread starts, as the host's (search_host.cpp heuristic): at
             // 14/16/19 cities the same bound and nodes as 8 or 16 starts, and
-            // each wave has a SIMD to itself (profiles/r04/k2_device_bound.log)
-            in.heur_starts = 4;
+            // each wave has a SIMD to itself (profiles/r04/k2_device_bound.log);
+            // from 20 cities sixteen (the host multi-start takes ~2 ms there)
+            in.heur_starts = n >= 20 ? 16 : 4;
         }
         in.fill_ff = reinterpret_cast<uint32_t *>(s->d_tie);
         in.n_ff = (uint32_t)(kTieBytes / 4);
@@ -647,6 +648,24 @@ int tspgpu_search_create(tspgpu_ctx *c, const void *dist, int dtype, int n, int 
                          tspgpu_search **out)
 {
     return search_create(c, dist, dtype, n, shard, nshards, depth, nullptr, out);
+}
+
+int tspgpu_search_create_ex(tspgpu_ctx *c, const void *dist, int dtype, int n, int shard, int nshards, int depth,
+                            int flags, tspgpu_search **out)
+{
+    if (flags & ~TSPGPU_SEARCH_DEVICE_BOUND) return -EINVAL;
+    const bool dev = (flags & TSPGPU_SEARCH_DEVICE_BOUND) != 0;
+    int rc = search_create(c, dist, dtype, n, shard, nshards, depth, nullptr, out, dev);
+    if (rc || !dev || (*out)->dev_heur) return rc;
+    // (pageable staging knob: no create launch, so the host's bound)
+    double ub = 0.0;
+    rc = tspgpu_heuristic_tour(dist, dtype, n, &ub, nullptr);
+    if (!rc) rc = tspgpu_search_set_bound(*out, ub);
+    if (rc) {
+        tspgpu_search_destroy(*out);
+        *out = nullptr;
+    }
+    return rc;
 }
 
 int tspgpu_search_destroy(tspgpu_search *s)
@@ -1604,7 +1623,8 @@ static int search_solve(tspgpu_ctx *c, const void *dist, int dtype, int n, doubl
     // launch (search.hip init_heuristic, one wave per start city) instead of
     // by the host before the search (~35 us of the ~0.2 ms at 16 cities);
     // knob SEARCH_DEVICE_BOUND=0: the host
-    const bool dev_bound = !noprune && n >= 13 && n < 20 && tuned_or("SEARCH_DEVICE_BOUND", 1) != 0;
+    const bool dev_bound = !noprune && n >= 13 && n < tuned_int("SEARCH_DEVICE_BOUND_MAXN", 20) &&
+                           tuned_or("SEARCH_DEVICE_BOUND", 1) != 0;
     if (n >= 20) {  // (smaller: a thread costs more than it saves)
         try {
             ht = std::thread([&] { hrc = tspgpu_heuristic_tour(dist, dtype, n, &ub, nullptr); });

@@ -160,12 +160,17 @@ def _key_u64(v: int) -> int:
 
 
 def solve_sharded(ctx, dist, group=None, depth: int = 0, device=None, exchange_every: int | None = None,
-                  exchange_levels: int = 2):
+                  exchange_levels: int = 2, bound: str | None = None):
     """Search one instance over the ranks of `group` (None: the default group,
     or a single process when torch.distributed is not initialised).
 
-    1. The multi-start bound: from 20 cities each rank runs 1/W of the starts
-       and the ranks all-reduce MIN; below, every rank computes the same
+    1. The initial bound.  bound="device" (the default): the search's create
+       launch computes it on the GPU (nearest neighbour + 2-opt from spread
+       start cities, TSPGPU_SEARCH_DEVICE_BOUND) — the same on every rank, no
+       host heuristic and no collective; round 6: the host multi-start took
+       0.6-0.8 ms of a 1.7-1.9 ms 32-city solve.  bound="host": the host
+       multi-start tour; from 20 cities each rank runs 1/W of the starts and
+       the ranks all-reduce MIN, below every rank computes the same
        four-start bound itself.
     2. Each rank runs its shard as ONE device chain (tspgpu_search_chain: the
        seeds, every frontier level and the tail fold back to back, one
@@ -232,7 +237,11 @@ def solve_sharded(ctx, dist, group=None, depth: int = 0, device=None, exchange_e
     # cities r, r+W, ...; all-reduce MIN of the costs) and computed on a thread
     # while the search is created (ctypes releases the GIL); below, every rank
     # computes the same four-start bound itself (microseconds; no collective)
-    split = collective and world > 1 and len(dist) >= 20
+    bound = bound or os.environ.get("TSPGPU_SHARDED_BOUND", "device")
+    if bound not in ("device", "host"):
+        raise ValueError(f"bound must be 'device' or 'host', not {bound!r}")
+    dev_bound = bound == "device"
+    split = not dev_bound and collective and world > 1 and len(dist) >= 20
     heur = {}
 
     def _heuristic():
@@ -246,15 +255,15 @@ def solve_sharded(ctx, dist, group=None, depth: int = 0, device=None, exchange_e
         ph[name] = ph.get(name, 0.0) + (t - ph_t[0]) * 1e3
         ph_t[0] = t
 
-    th = threading.Thread(target=_heuristic) if len(dist) >= 20 else None  # (smaller: not worth a thread)
+    th = threading.Thread(target=_heuristic) if not dev_bound and len(dist) >= 20 else None  # (smaller: no thread)
     if th is not None:
         th.start()
     try:
-        S = tspgpu.Search(ctx, dist, shard=rank, nshards=world, depth=depth)
+        S = tspgpu.Search(ctx, dist, shard=rank, nshards=world, depth=depth, device_bound=dev_bound)
     finally:
         if th is not None:
             th.join()
-    if "v" not in heur:
+    if not dev_bound and "v" not in heur:
         _heuristic()  # (no thread, or it raised: here, so an error surfaces)
     mark("create_and_heuristic")
     try:
@@ -262,9 +271,10 @@ def solve_sharded(ctx, dist, group=None, depth: int = 0, device=None, exchange_e
             ub_r, _ = heur["v"]
             word = tspgpu.cost_bits(ub_r, S.dtype) if ub_r is not None else _I64_MAX
             ub = tspgpu.bits_cost(allmin([word])[0], S.dtype)
-        else:
+            S.set_bound(ub)
+        elif not dev_bound:
             ub, _ = heur["v"]
-        S.set_bound(ub)
+            S.set_bound(ub)
         mark("bound")
         t0 = time.perf_counter()
         two = S.n - 1 > 20
@@ -405,7 +415,7 @@ def solve_sharded(ctx, dist, group=None, depth: int = 0, device=None, exchange_e
                  "wall_s": wall, "tie": tie, "record_gather": gathered, "chained": int(chained),
                  "collectives": ncoll[0], "exchanges": exchanges, "hooks": hooks, "exchange_levels": exchange_levels,
                  "exchange_every": exchange_every, "world": world,
-                 "backend": backend, "host_phases_ms": ph}
+                 "backend": backend, "host_phases_ms": ph, "bound": bound}
         return cost, tour, stats
     finally:
         S.close()

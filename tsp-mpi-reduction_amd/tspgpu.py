@@ -27,7 +27,8 @@ EXPORTED_SYMBOLS = (
     "tspgpu_device_info", "tspgpu_last_variant", "tspgpu_k1_split_timing", "tspgpu_k1_last_split_ms", "tspgpu_device_count", "tspgpu_stream_create",
     "tspgpu_stream_destroy", "tspgpu_stream_synchronize",
     # K2
-    "tspgpu_search_solve", "tspgpu_search_enumerate", "tspgpu_search_create", "tspgpu_search_destroy", "tspgpu_search_info",
+    "tspgpu_search_solve", "tspgpu_search_enumerate", "tspgpu_search_create", "tspgpu_search_create_ex",
+    "tspgpu_search_destroy", "tspgpu_search_info",
     "tspgpu_search_set_bound", "tspgpu_search_start", "tspgpu_search_step", "tspgpu_search_run_all",
     "tspgpu_search_timing", "tspgpu_search_incumbent_device", "tspgpu_search_chain", "tspgpu_search_tie_slot",
     "tspgpu_search_counters", "tspgpu_search_reset_records", "tspgpu_search_records", "tspgpu_heuristic_tour",
@@ -143,6 +144,8 @@ def lib():
         L.tspgpu_search_enumerate.argtypes = [vp, vp, ctypes.c_int, ctypes.c_int, dp, ip, ctypes.POINTER(SearchStats)]
         L.tspgpu_search_create.argtypes = [vp, vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                            ctypes.c_int, ctypes.POINTER(vp)]
+        L.tspgpu_search_create_ex.argtypes = [vp, vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                              ctypes.c_int, ctypes.c_int, ctypes.POINTER(vp)]
         L.tspgpu_search_destroy.argtypes = [vp]
         L.tspgpu_search_info.argtypes = [vp, ctypes.POINTER(ctypes.c_int), u64p, u64p]
         L.tspgpu_search_set_bound.argtypes = [vp, ctypes.c_double]
@@ -623,14 +626,17 @@ def tie_tour_gpu(ctx: "Context", dist, w0: int, w1: int, cost):
 class Search:
     """One instance (or shard `shard` of `nshards`) of the K2 search on a Context."""
 
-    def __init__(self, ctx: "Context", dist, shard: int = 0, nshards: int = 1, depth: int = 0):
+    def __init__(self, ctx: "Context", dist, shard: int = 0, nshards: int = 1, depth: int = 0,
+                 device_bound: bool = False):
+        """device_bound: the initial incumbent from the create launch's device
+        heuristic (TSPGPU_SEARCH_DEVICE_BOUND) instead of set_bound."""
         self.dist, self.dtype = _search_dist(dist)
         self.n = self.dist.shape[0]
         h = ctypes.c_void_p()
-        rc = lib().tspgpu_search_create(ctx.handle, self.dist.ctypes.data, self.dtype, self.n, shard, nshards,
-                                        depth, ctypes.byref(h))
+        rc = lib().tspgpu_search_create_ex(ctx.handle, self.dist.ctypes.data, self.dtype, self.n, shard, nshards,
+                                           depth, 1 if device_bound else 0, ctypes.byref(h))
         if rc:
-            raise TspGpuError(rc, "tspgpu_search_create")
+            raise TspGpuError(rc, "tspgpu_search_create_ex")
         self.handle = h
         dep, items, local = ctypes.c_int(), ctypes.c_uint64(), ctypes.c_uint64()
         lib().tspgpu_search_info(h, ctypes.byref(dep), ctypes.byref(items), ctypes.byref(local))
