@@ -1,14 +1,18 @@
-// K1 dispatch: picks the per-N instantiation (hk_n*.hip) and the n == 2 kernel.
-// Kernel design and the bit-exactness argument: heldkarp_impl.h.
+// K1 dispatch: picks the layer kernel (heldkarp_impl.h launch_threads) and the
+// n == 2 kernel.  Every layer kernel is compiled in its own unit under k1l/
+// (tools/gen_hk_units.py; declared extern here), so a process loads only the
+// code objects of the kernels it launches.  Kernel design and the
+// bit-exactness argument: heldkarp_impl.h.
 #include "heldkarp_impl.h"
+#include "k1l/hkl_units.h"
 
 namespace tspgpu {
 
-#define TSPGPU_EXTERN(NN) extern template hipError_t launch_threads<NN>(const LaunchArgs &, int);
-TSPGPU_EXTERN(2) TSPGPU_EXTERN(3) TSPGPU_EXTERN(4) TSPGPU_EXTERN(5) TSPGPU_EXTERN(6) TSPGPU_EXTERN(7)
-TSPGPU_EXTERN(8) TSPGPU_EXTERN(9) TSPGPU_EXTERN(10) TSPGPU_EXTERN(11) TSPGPU_EXTERN(12) TSPGPU_EXTERN(13)
-TSPGPU_EXTERN(14) TSPGPU_EXTERN(15) TSPGPU_EXTERN(16) TSPGPU_EXTERN(17) TSPGPU_EXTERN(18) TSPGPU_EXTERN(19)
-#undef TSPGPU_EXTERN
+#define TSPGPU_INST(NN) template hipError_t launch_threads<NN>(const LaunchArgs &, int);
+TSPGPU_INST(2) TSPGPU_INST(3) TSPGPU_INST(4) TSPGPU_INST(5) TSPGPU_INST(6) TSPGPU_INST(7)
+TSPGPU_INST(8) TSPGPU_INST(9) TSPGPU_INST(10) TSPGPU_INST(11) TSPGPU_INST(12) TSPGPU_INST(13)
+TSPGPU_INST(14) TSPGPU_INST(15) TSPGPU_INST(16) TSPGPU_INST(17) TSPGPU_INST(18) TSPGPU_INST(19)
+#undef TSPGPU_INST
 
 // n == 2: tsp.cpp:483-502 with cityNums = {1}: key(empty,1) is default-inserted
 // with cost 0, so cost = 0 + d[1][0] and the path is [1, 0].

@@ -825,12 +825,13 @@ hipError_t launch_threads_v(const LaunchArgs &a, int grid)
     if constexpr (VAR == 4 && (N < 11 || N > 15)) {
         // ping-pong + parent words: 12..16 cities (4-bit parents, <= 14 per row)
         return launch_n<V, N, false, 256, 2>(a, grid);
+    } else {  // (else: no unreachable variant-4 kernel is instantiated)
+        if constexpr (N >= 12 && N <= 15) {
+            if (a.threads == 512) return launch_n<V, N, false, 512, VAR>(a, grid);
+            if (a.threads == 1024) return launch_n<V, N, false, 1024, VAR>(a, grid);
+        }
+        return launch_n<V, N, false, 256, VAR>(a, grid);
     }
-    if constexpr (N >= 12 && N <= 15) {
-        if (a.threads == 512) return launch_n<V, N, false, 512, VAR>(a, grid);
-        if (a.threads == 1024) return launch_n<V, N, false, 1024, VAR>(a, grid);
-    }
-    return launch_n<V, N, false, 256, VAR>(a, grid);
 }
 
 template <int N>

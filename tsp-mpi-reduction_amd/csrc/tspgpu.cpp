@@ -123,11 +123,17 @@ int ensure_tables(tspgpu_ctx *c, int N)
     if (c->d_info[N]) return 0;
     LayerInfo info;
     host_layer_info(N, &info);
+    // every N-bit mask by (popcount, value): each popcount class in ascending
+    // order by Gosper's next-combination step (O(2^N), not (N+1) 2^N scans)
     std::vector<uint32_t> masks;
     masks.reserve((size_t)1 << N);
-    for (int t = 0; t <= N; ++t)
-        for (uint32_t m = 0; m < (1u << N); ++m)
-            if (__builtin_popcount(m) == t) masks.push_back(m);
+    masks.push_back(0u);
+    for (int t = 1; t <= N; ++t)
+        for (uint32_t m = (1u << t) - 1u; m < (1u << N);) {
+            masks.push_back(m);
+            const uint32_t c = m & (0u - m), r = m + c;
+            m = (((r ^ m) >> 2) / c) | r;
+        }
     hipError_t e = hipMalloc((void **)&c->d_info[N], sizeof(LayerInfo));
     if (e == hipSuccess) e = hipMalloc((void **)&c->d_masks[N], masks.size() * sizeof(uint32_t));
     if (e == hipSuccess) e = upload_sync(c, c->d_info[N], &info, sizeof(info));
