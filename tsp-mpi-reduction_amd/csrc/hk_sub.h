@@ -315,8 +315,14 @@ __host__ __device__ constexpr int sub_lds_role(int k)
     return -1;
 }
 
-constexpr int kSubQC = 7;     // destinations relaxed together (register budget)
-constexpr int kSubAhead = 6;  // distance loads in flight per lane
+#ifndef TSPGPU_SUB_QC
+#define TSPGPU_SUB_QC 7
+#endif
+#ifndef TSPGPU_SUB_AHEAD
+#define TSPGPU_SUB_AHEAD 6
+#endif
+constexpr int kSubQC = TSPGPU_SUB_QC;        // destinations relaxed together (register budget)
+constexpr int kSubAhead = TSPGPU_SUB_AHEAD;  // distance loads in flight per lane
 
 // the push column of (sub-cube hp, high city x): [hp][x] in the slot's push area
 template <int H>
