@@ -229,6 +229,14 @@ int tspgpu_tie_tour(const void *dist, int dtype, int n, uint64_t w0, uint64_t w1
  * so binade crossings late in long tours are proven too. */
 int tspgpu_tie_tour_gpu(tspgpu_ctx *ctx, const void *dist, int dtype, int n, uint64_t w0, uint64_t w1,
                         uint64_t cost_bits, int32_t *tour_out);
+/* tspgpu_tie_tour with the certificate's prefix minima taken from the
+ * search's optimal records instead of a Held-Karp DP: records[0..count) must
+ * be EVERY tour the search recorded (tspgpu_search_records with no overflow,
+ * all shards), so that they hold the whole optimal set O; a prefix the records
+ * cannot decide falls back to the DP on ctx's GPU (ctx may be NULL: then not
+ * certified, -EAGAIN). */
+int tspgpu_tie_tour_records(tspgpu_ctx *ctx, const void *dist, int dtype, int n, uint64_t w0, uint64_t w1,
+                            uint64_t cost_bits, const tspgpu_tour_record *records, int count, int32_t *tour_out);
 /* the key of a tour (tour[0] = 0, tour[1..n-1] = t1..tN): test helper */
 int tspgpu_tie_key(int n, const int32_t *tour, uint64_t *w0, uint64_t *w1);
 

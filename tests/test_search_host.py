@@ -237,3 +237,49 @@ def test_tie_tour_rejects_wrong_cost_and_bad_keys():
     assert tspgpu.tie_tour(d, 10 ** 9, 0, opt)[0] == -22      # digits out of range
     with pytest.raises(tspgpu.TspGpuError):
         tspgpu.tie_key([0, 1, 1, 2, 0])                       # not a permutation
+
+
+def _needs_prefix_check(d, t):
+    """Levels j at which the certificate's one-ulp test fails (a fold one ulp
+    below F[j] could round to the same F[j+1]): there it needs G[{t1..tj}][tj]."""
+    n = d.shape[0]
+    N = n - 1
+    F, acc, prev = [0.0] * (N + 2), 0.0, 0
+    for j in range(1, N + 1):
+        acc = acc + d[prev, t[j]]
+        F[j], prev = acc, t[j]
+    F[N + 1] = acc + d[prev, 0]
+    out = []
+    for j in range(2, N + 1):
+        dj = d[t[j], t[j + 1]] if j < N else d[t[N], 0]
+        if not (np.nextafter(F[j], -np.inf) + dj < F[j + 1]):
+            out.append(j)
+    return out
+
+
+@pytest.mark.parametrize("n", [6, 7, 8, 9])
+def test_tie_certificate_from_the_optimal_records(n):
+    """tspgpu_tie_tour_records (round 6): the certificate's prefix minima from
+    the complete optimal set O instead of a Held-Karp DP — with no DP to fall
+    back on (ctx None), it must certify exactly what the DP certifies, with
+    tsp()'s tour; and a record set missing the winner must not certify where a
+    prefix check is needed."""
+    rng = np.random.default_rng(4400 + n)
+    checked = 0
+    for k, d in enumerate(instances(rng, n, 40 if n <= 8 else 12)):
+        if k % 4 == 0:  # costs in the thousands: binade crossings along the tour
+            d = d * 4.0
+        opt, oset = optimal_set(d)
+        best = min(oset, key=rev_lex)
+        w0, w1 = tspgpu.tie_key([0, *best, 0])
+        rc_dp, tour_dp = tspgpu.tie_tour(d, w0, w1, opt)
+        recs = records(oset, opt, tspgpu.F64)
+        rc, tour = tspgpu.tie_tour_records(None, d, w0, w1, opt, recs)
+        assert rc == rc_dp == 0, (n, k, rc, rc_dp)
+        assert tour.tolist() == tour_dp.tolist() == O.solve_block(d)[1]
+        # (lattice and collinear instances fold exactly: nothing to prove)
+        if k % 4 in (0, 3) and _needs_prefix_check(d, [0, *best, 0]):
+            checked += 1
+            others = [r for r, p in zip(recs, oset) if p != best]
+            assert tspgpu.tie_tour_records(None, d, w0, w1, opt, others)[0] == -11  # not the whole O
+    assert checked > 0  # (the record path was exercised)

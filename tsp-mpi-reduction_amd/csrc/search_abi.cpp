@@ -1180,6 +1180,16 @@ int tspgpu_tie_tour_gpu(tspgpu_ctx *ctx, const void *dist, int dtype, int n, uin
     return tspgpu::host::tie_tour(dist, dtype, n, w0, w1, cost_bits, tour_out, true, gpu_prefix, ctx, kTieHostMax);
 }
 
+int tspgpu_tie_tour_records(tspgpu_ctx *ctx, const void *dist, int dtype, int n, uint64_t w0, uint64_t w1,
+                            uint64_t cost_bits, const tspgpu_tour_record *records, int count, int32_t *tour_out)
+{
+    if (count < 0 || (count > 0 && !records)) return -EINVAL;
+    tspgpu::host::RecordsPrefix rp{records, count, cost_bits, ctx ? gpu_prefix : nullptr, ctx};
+    // (host_max 0: every prefix check from the records first)
+    return tspgpu::host::tie_tour(dist, dtype, n, w0, w1, cost_bits, tour_out, true, tspgpu::host::records_prefix,
+                                  &rp, 0);
+}
+
 static bool chainable(const tspgpu_search *s)
 {
     // above 18 cities only with the tree bound (its frontiers are small; without
@@ -1715,9 +1725,17 @@ static int search_solve(tspgpu_ctx *c, const void *dist, int dtype, int n, doubl
     std::vector<int32_t> tie_tour(n + 1, 0);
     if (!rc && s->tie_on && tie_h[0] == 1 && tie_h[4] == 0) {
         const bool two = n - 1 > 20;
+        // every record on the host already (the fetch's speculative read):
+        // the certificate's prefix minima come from the optimal set itself
+        // (search_host.h records_prefix), no prefix DP on the GPU
+        tspgpu::host::RecordsPrefix rp{specp, (int)recs, inc, gpu_prefix, c};
         if (!two || tie_h[2] == tie_h[1])
-            tie_done = tspgpu::host::tie_tour(dist, dtype, n, two ? tie_h[2] : tie_h[1], two ? tie_h[3] : 0ull, inc,
-                                              tie_tour.data(), recs > s->rec_cap, gpu_prefix, c, kTieHostMax) == 0;
+            tie_done = (spec_ok ? tspgpu::host::tie_tour(dist, dtype, n, two ? tie_h[2] : tie_h[1],
+                                                         two ? tie_h[3] : 0ull, inc, tie_tour.data(), true,
+                                                         tspgpu::host::records_prefix, &rp, 0)
+                                : tspgpu::host::tie_tour(dist, dtype, n, two ? tie_h[2] : tie_h[1],
+                                                         two ? tie_h[3] : 0ull, inc, tie_tour.data(),
+                                                         recs > s->rec_cap, gpu_prefix, c, kTieHostMax)) == 0;
     }
     // the record buffer overflowed: search again with the optimum as the bound,
     // so only optimal tours are recorded, into a buffer of the size now known

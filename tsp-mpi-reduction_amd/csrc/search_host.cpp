@@ -477,6 +477,38 @@ double prefix_min(const double *d, int n, const int32_t *t, int j)
     return G[(size_t)full * J + (J - 1)];
 }
 
+int records_prefix(void *user, const double *d, int n, const int32_t *t, int j, double *g)
+{
+    const auto *rp = static_cast<const RecordsPrefix *>(user);
+    const auto *recs = static_cast<const tspgpu_tour_record *>(rp->recs);
+    const int N = n - 1;
+    double best = INFINITY;
+    bool have_t = false;  // t itself among the optimal records (else they are not all of O)
+    for (int r = 0; r < rp->count; ++r) {
+        const tspgpu_tour_record &R = recs[r];
+        if (R.cost != rp->opt_bits) continue;
+        bool same_tail = true;  // positions j..N: the same prefix set and the same end t_j
+        for (int i = j; i <= N && same_tail; ++i) same_tail = R.city[i - 1] == t[i];
+        if (!same_tail) continue;
+        double f = 0.0;  // the left fold of the prefix, as tsp()'s DP folds it
+        int prev = 0;
+        bool same = true;
+        for (int i = 1; i <= j; ++i) {
+            f = f + d[prev * n + R.city[i - 1]];
+            prev = R.city[i - 1];
+            same = same && R.city[i - 1] == t[i];
+        }
+        have_t = have_t || same;
+        best = f < best ? f : best;
+    }
+    if (have_t) {
+        *g = best;
+        return 0;
+    }
+    if (rp->next) return rp->next(rp->next_user, d, n, t, j, g);
+    return -EAGAIN;
+}
+
 // 0: t (t[0] = 0, t[1..N]) folds to opt and every prefix fold is minimal
 // (no value one ulp lower could round to the same next fold); -EAGAIN: the
 // fold matches but that is not proven; -EINVAL: not a tour of cost opt

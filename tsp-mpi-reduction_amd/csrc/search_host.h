@@ -27,5 +27,23 @@ typedef int (*PrefixDp)(void *user, const double *d, int n, const int32_t *t, in
 // host_max cities by Held-Karp on the host, longer ones through dp (if any)
 int tie_tour(const void *dist, int dtype, int n, uint64_t w0, uint64_t w1, uint64_t cost_bits, int32_t *tour_out,
              bool allow_dp, PrefixDp dp = nullptr, void *user = nullptr, int host_max = 16);
+// G[{t1..tj}][tj] from the COMPLETE set O of the search's optimal tours
+// instead of a DP (round 6): an ordering P' of the prefix set {t1..tj} ending
+// at tj with fold(P') <= F[j] makes P' + (t_{j+1}..t_N) a tour of cost <= OPT
+// (rounding is monotone), i.e. a member of O; so the least prefix fold over
+// the tours of O that share positions j..N with t is min(G, F[j]) = G.
+// Every tour of cost <= the incumbent at the time is recorded and no tour of
+// cost OPT is ever pruned, so O is complete whenever the records did not
+// overflow — the caller's guarantee (count = every record of the search).
+// user = RecordsPrefix; when t itself is not among the records (they are not
+// the whole set after all) it defers to next (or fails: -EAGAIN).
+struct RecordsPrefix {
+    const void *recs;  // tspgpu_tour_record[count]: cost word, then cities t1..tN
+    int count;
+    uint64_t opt_bits;
+    PrefixDp next;     // fallback DP (may be null)
+    void *next_user;
+};
+int records_prefix(void *user, const double *d, int n, const int32_t *t, int j, double *g);
 }  // namespace host
 }  // namespace tspgpu

@@ -380,7 +380,20 @@ def solve_sharded(ctx, dist, group=None, depth: int = 0, device=None, exchange_e
             rc, t = -errno.EAGAIN, np.zeros(S.n + 1, dtype=np.int32)
             if rank == 0:
                 w = (_key_u64(K0), _key_u64(K1) if two else 0, cost)
-                rc, t = tspgpu.tie_tour_gpu(ctx, dist, *w) if ctx is not None else tspgpu.tie_tour(dist, *w)
+                # one rank holds every record: the certificate's prefix minima
+                # come from its optimal records (tspgpu_tie_tour_records), no
+                # prefix DP; several ranks (records spread) or lost records:
+                # the DP on this rank's GPU
+                recs_opt = None
+                if world == 1 and fast:
+                    try:
+                        recs_opt = S.records(opt)
+                    except tspgpu.TspGpuError:
+                        recs_opt = None
+                if recs_opt:
+                    rc, t = tspgpu.tie_tour_records(ctx, dist, *w, recs_opt)
+                else:
+                    rc, t = tspgpu.tie_tour_gpu(ctx, dist, *w) if ctx is not None else tspgpu.tie_tour(dist, *w)
             if collective:
                 buf = torch.tensor([1 if rc == 0 else 0, *[int(x) for x in t]], dtype=torch.int64, device=device)
                 src = tdist.get_global_rank(group, 0) if group is not None else 0

@@ -33,7 +33,7 @@ EXPORTED_SYMBOLS = (
     "tspgpu_search_timing", "tspgpu_search_incumbent_device", "tspgpu_search_chain", "tspgpu_search_tie_slot",
     "tspgpu_search_counters", "tspgpu_search_reset_records", "tspgpu_search_records", "tspgpu_heuristic_tour",
     "tspgpu_heuristic_tour_starts",
-    "tspgpu_select_tour", "tspgpu_tie_tour", "tspgpu_tie_tour_gpu", "tspgpu_tie_key",
+    "tspgpu_select_tour", "tspgpu_tie_tour", "tspgpu_tie_tour_gpu", "tspgpu_tie_tour_records", "tspgpu_tie_key",
     # K3
     "tspgpu_merge", "tspgpu_reduce",
     # K1-wide
@@ -171,6 +171,8 @@ def lib():
         L.tspgpu_tuning_clear.argtypes = [ctypes.c_char_p]
         L.tspgpu_tie_tour_gpu.argtypes = [vp, vp, ctypes.c_int, ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64,
                                           ctypes.c_uint64, ip]
+        L.tspgpu_tie_tour_records.argtypes = [vp, vp, ctypes.c_int, ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64,
+                                              ctypes.c_uint64, ctypes.POINTER(TourRecord), ctypes.c_int, ip]
         L.tspgpu_tie_key.argtypes = [ctypes.c_int, ip, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]
         cp = ctypes.POINTER(City)
         L.tspgpu_solve_instance.argtypes = [vp, dp, ctypes.c_int, dp, ip, dp]
@@ -620,6 +622,21 @@ def tie_tour_gpu(ctx: "Context", dist, w0: int, w1: int, cost):
     n = d.shape[0]
     tour = np.zeros(n + 1, dtype=np.int32)
     rc = lib().tspgpu_tie_tour_gpu(ctx.handle, d.ctypes.data, dt, n, w0, w1, cost_bits(cost, dt), _ip(tour))
+    return rc, tour
+
+
+def tie_tour_records(ctx, dist, w0: int, w1: int, cost, records):
+    """tie_tour with the certificate's prefix minima from the search's records
+    (tspgpu_tie_tour_records): `records` must be every tour the search
+    recorded at the optimum (Search.records(opt) without overflow, all
+    shards).  ctx: the GPU DP for a prefix the records cannot decide (None:
+    not certified).  -> (rc, tour)."""
+    d, dt = _search_dist(dist)
+    n = d.shape[0]
+    tour = np.zeros(n + 1, dtype=np.int32)
+    arr = (TourRecord * max(1, len(records)))(*records)
+    rc = lib().tspgpu_tie_tour_records(ctx.handle if ctx is not None else None, d.ctypes.data, dt, n, w0, w1,
+                                       cost_bits(cost, dt), arr, len(records), _ip(tour))
     return rc, tour
 
 
