@@ -1015,6 +1015,10 @@ def main():
         try:
             k2s = k2_strong_scaling(ctx, args.k2_n, args.k2_seed, kgroup, backend, world, rank)
             walls = group.gather(k2s["rank_wall_ms"])
+            # every rank's host/device split (its wall by host phase, its kernels)
+            k2s["rank_split"] = group.gather({"rank": rank, "wall_ms": k2s["rank_wall_ms"],
+                                              "kernel_ms": k2s["rank_kernel_ms"],
+                                              "host_phases_ms": k2s.get("host_phases_ms")})
             k2s["time_to_optimal_ms"] = max(walls)
             k2s["bb_nodes_per_s"] = k2s["bb_nodes_expanded"] / (k2s["time_to_optimal_ms"] * 1e-3)
             k2s["rank_walls_ms"] = walls
