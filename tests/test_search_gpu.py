@@ -648,3 +648,37 @@ def test_chain_overflow_reads_no_unwritten_slot(knobs, n, cap):
     assert c1 == c0 and t1.tolist() == t0.tolist(), s1
     if n == 16:
         assert c1 == 3871.1947567096445 and t1.tolist() == [0, 14, 2, 13, 10, 12, 6, 4, 9, 11, 3, 5, 15, 8, 1, 7, 0]
+
+
+@pytest.mark.parametrize("n,seed", [(16, 0), (20, 4), (24, 5), (32, 35), (32, 14)])
+def test_device_bound_and_record_certificate(gpu_ctx, knobs, n, seed):
+    """Round 6: the create launch's device bound up to 32 cities
+    (tspgpu_search_create_ex TSPGPU_SEARCH_DEVICE_BOUND, solve_sharded's
+    default) and the certificate from the optimal records
+    (tspgpu_tie_tour_records) give exactly the answer of the host-bound search
+    and of the native solve with and without the device bound extended."""
+    from bench import Shard, k2_instance
+
+    d = Shard(16, 1, 0, 1).distances()[0] if n == 16 else np.asarray(k2_instance(n, seed))
+    want = tspgpu.search_solve(gpu_ctx, d)
+    knobs.set("SEARCH_DEVICE_BOUND_MAXN", "33")
+    native_dev = tspgpu.search_solve(gpu_ctx, d)
+    knobs.clear("SEARCH_DEVICE_BOUND_MAXN")
+    dev = search_dist.solve_sharded(gpu_ctx, d, bound="device")
+    host = search_dist.solve_sharded(gpu_ctx, d, bound="host")
+    for cost, tour, st in (native_dev, dev, host):
+        assert cost == want[0] and tour.tolist() == want[1].tolist(), (n, seed, st)
+    assert dev[2]["bound"] == "device" and dev[2]["tie"] == 1 and dev[2]["record_gather"] == 0
+    # the record certificate agrees with the GPU prefix-DP certificate
+    S = tspgpu.Search(gpu_ctx, d, device_bound=True)
+    try:
+        assert S.chain()
+        inc, _, _ = S.counters()
+        found, w0, w1, ovf = S.tie_slot(inc)
+        assert found and not ovf
+        recs = S.records(inc)
+        rc_r, t_r = tspgpu.tie_tour_records(gpu_ctx, d, w0, w1 if n - 1 > 20 else 0, want[0], recs)
+        rc_g, t_g = tspgpu.tie_tour_gpu(gpu_ctx, d, w0, w1 if n - 1 > 20 else 0, want[0])
+        assert rc_r == rc_g == 0 and t_r.tolist() == t_g.tolist() == want[1].tolist()
+    finally:
+        S.close()

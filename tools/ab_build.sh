@@ -12,6 +12,6 @@ mkdir -p lib_ab/obj
 make -s lib/libtspgpu.so
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -fPIC -Wall -I../include -Iinclude -Icsrc \
     -fno-honor-nans -mno-amdgpu-ieee $FLAGS -c csrc/k1/$CFG.hip -o lib_ab/obj/$NAME.o
-objs=$(ls lib/*.o lib/k1/*.o | grep -v "k1/$CFG.o")
+objs=$(ls lib/*.o lib/k1/*.o lib/k1l/*.o | grep -v "k1/$CFG.o")
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o lib_ab/$NAME.so $objs lib_ab/obj/$NAME.o
 echo "built lib_ab/$NAME.so ($FLAGS)"
