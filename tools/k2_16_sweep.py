@@ -18,7 +18,7 @@ reps = int(sys.argv[1]) if len(sys.argv) > 1 else 30
 ctx = tspgpu.Context(device=0)
 d = Shard(16, 1, 0, 1).distances()[0]
 c0, t0, _ = tspgpu.search_solve(ctx, d)
-SETS = [{}, {"SEARCH_DEPTH": 5}, {"SEARCH_DEPTH": 6}, {"SEARCH_DEPTH": 3}, {"SEARCH_TAIL": 5},
+SETS = [{}] if os.environ.get("DEFAULT_ONLY") else [{}, {"SEARCH_DEPTH": 5}, {"SEARCH_DEPTH": 6}, {"SEARCH_DEPTH": 3}, {"SEARCH_TAIL": 5},
         {"SEARCH_DEPTH": 5, "SEARCH_TAIL": 5}, {"CHAIN_LOCAL": 1, "CHAIN_LOCAL_FPB": 32},
         {"CHAIN_GRID": 1}, {"CHAIN_GRID": 4}, {"CHAIN_FPB": 128}]
 for knobs in SETS:
@@ -32,7 +32,8 @@ for knobs in SETS:
             nodes = st["nodes"]
             same = same and c == c0 and list(t) == list(t0)
         ks.sort()
-        print(json.dumps({"knobs": knobs, "kernel_ms_median": round(ks[len(ks) // 2], 4),
+        print(json.dumps({"knobs": knobs, "lib": os.path.basename(tspgpu.LIB_PATH) if hasattr(tspgpu, "LIB_PATH") else None,
+                          "cost": c0, "kernel_ms_median": round(ks[len(ks) // 2], 4),
                           "kernel_ms_best": round(ks[0], 4), "nodes": nodes, "depth": st.get("depth"),
                           "same_answer": same}), flush=True)
     except tspgpu.TspGpuError as e:
