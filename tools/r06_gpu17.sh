@@ -1,0 +1,24 @@
+#!/bin/bash
+# Round-6 check 17: expand_kernel blocks without a run leave before staging
+# their tables (tables read into registers, count checked, then LDS) against
+# the previous build: 16-city chain time (3 alternating rounds of 60
+# searches) and the K2 SQ counters (VALU instructions per node, bench.py's
+# K2 PMC child: 4 searches).
+set -u
+cd "$(dirname "$0")/.."
+OUT=gpurun_out/r06/early
+mkdir -p $OUT
+export TMPDIR=/tmp
+for r in 1 2 3; do
+  for so in tsp-mpi-reduction_amd/lib_ab/base.so tsp-mpi-reduction_amd/lib_ab/early.so; do
+    name=$(basename $so .so)
+    DEFAULT_ONLY=1 TSPGPU_LIB=$PWD/$so timeout -k 10 120 python3 -u tools/k2_16_sweep.py 60 > $OUT/$name.r$r.log 2>&1
+    echo "$name r$r rc=$? $(tail -1 $OUT/$name.r$r.log)"
+  done
+done
+for so in tsp-mpi-reduction_amd/lib_ab/base.so tsp-mpi-reduction_amd/lib_ab/early.so; do
+  name=$(basename $so .so)
+  TSPGPU_LIB=$PWD/$so timeout -s KILL 90 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT GRBM_GUI_ACTIVE --output-format csv -d $OUT/pmc_$name -o pmc -- python3 bench.py --pmc-child-k2 > $OUT/pmc_$name.log 2>&1
+  echo "pmc $name rc=$?"
+  python3 tools/k2_pmc_split.py $(ls $OUT/pmc_$name/*counter_collection.csv $OUT/pmc_$name/*/*counter_collection.csv 2>/dev/null | head -1) 2479117 4 > $OUT/split_$name.json && tail -2 $OUT/split_$name.json
+done

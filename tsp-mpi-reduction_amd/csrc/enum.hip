@@ -1122,12 +1122,10 @@ __global__ __launch_bounds__(256) void expand_kernel(SearchArgs a)
     // chained levels: once a level has overflowed, the later ones return at
     // once — the input slots an overflowing block reserved were never written
     // (they hold stale or uninitialised paths) and must not be read
-    __shared__ uint32_t dead;
     // every device read of the launch's set-up in flight together (the
     // level's count, the overflow flag, the incumbent, the tables): one
     // memory round trip and one barrier before the work, not three of each —
     // a chained level is a latency chain of such round trips (~2 us each)
-    if (threadIdx.x == 0) dead = a.overflow ? __hip_atomic_load(a.overflow, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
     // the next step counts its children into the other counter word (no host memset per step)
     if (a.out_next && blockIdx.x == 0 && threadIdx.x == 0) *a.out_next = 0u;
     uint32_t fin_count = a.fin_count;
@@ -1136,22 +1134,43 @@ __global__ __launch_bounds__(256) void expand_kernel(SearchArgs a)
         fin_count = c < a.fout_cap ? c : a.fout_cap;
     }
     const V thr = EThr<V>::of(ENum<V>::val(__hip_atomic_load(a.inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)));
-    // (a block without a run of this level stages its tables all the same: it
-    // leaves at the barrier, and the tables are a few hundred bytes of L2)
-    for (int i = threadIdx.x; i < n * n; i += blockDim.x) dl[(i / n) * kTRow + i % n] = gd[i];
-    for (int i = threadIdx.x; i < n; i += blockDim.x) am[i] = ga[i];
-    if (a.sym)
-        for (int i = threadIdx.x; i < 2 * n; i += blockDim.x) b2[i] = static_cast<const V *>(a.bnd2)[i];
-    load_binom(bn);
-    // the tree bound's d' (kTRow rows), pi and margin
+    // the tables into registers first (a thread per (row, column) with
+    // column = lane & 31: no division), the count and overflow checked while
+    // they are in flight, and only a block with a run of this level writes
+    // them to LDS — at 16 cities most of the grid has no run (24-157 runs of
+    // 512 blocks per level) and leaves before doing any of it
     __shared__ double dm[kSearchMaxN * kTRow + kSearchMaxN + 1];
-    if (a.mst) {
-        for (int i = threadIdx.x; i < n * n; i += blockDim.x) dm[(i / n) * kTRow + i % n] = a.mst[i];
-        for (int i = threadIdx.x; i < n; i += blockDim.x) dm[kSearchMaxN * kTRow + i] = a.mst[n * n + i];
-        if (threadIdx.x == 0) dm[kSearchMaxN * kTRow + kSearchMaxN] = a.mst[n * n + n];
+    const int tcol = (int)(threadIdx.x & 31u), trow = (int)(threadIdx.x >> 5);
+    constexpr int kRowsPer = 256 / 32;
+    V dv[kSearchMaxN / kRowsPer];
+    double mv[kSearchMaxN / kRowsPer];
+#pragma unroll
+    for (int k = 0; k < kSearchMaxN / kRowsPer; ++k) {
+        const int row = trow + kRowsPer * k;
+        const bool in = row < n && tcol < n;
+        dv[k] = in ? gd[row * n + tcol] : V(0);
+        mv[k] = in && a.mst ? a.mst[row * n + tcol] : 0.0;
     }
+    const int t = (int)threadIdx.x;
+    const V av = t < n ? ga[t] : V(0);
+    const V bv = a.sym && t < 2 * n ? static_cast<const V *>(a.bnd2)[t] : V(0);
+    const double pv = a.mst && t <= n ? a.mst[n * n + t] : 0.0;
+    const uint32_t ovf = a.overflow ? __hip_atomic_load(a.overflow, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+    if (ovf || blockIdx.x * a.fin_per_block >= fin_count) return;  // (block-uniform)
+#pragma unroll
+    for (int k = 0; k < kSearchMaxN / kRowsPer; ++k) {
+        const int row = trow + kRowsPer * k;
+        if (row < n && tcol < n) {
+            dl[row * kTRow + tcol] = dv[k];
+            if (a.mst) dm[row * kTRow + tcol] = mv[k];
+        }
+    }
+    if (t < n) am[t] = av;
+    if (a.sym && t < 2 * n) b2[t] = bv;
+    if (a.mst && t < n) dm[kSearchMaxN * kTRow + t] = pv;
+    if (a.mst && t == n) dm[kSearchMaxN * kTRow + kSearchMaxN] = pv;
+    load_binom(bn);
     __syncthreads();
-    if (dead || blockIdx.x * a.fin_per_block >= fin_count) return;  // (block-uniform)
 
     const uint32_t full = (uint32_t)((1ull << n) - 1ull) & ~1u;
     const int lane = __lane_id(), wv = threadIdx.x >> 6;

@@ -1213,7 +1213,9 @@ static int run_chain(tspgpu_search *s, bool *done, int every = 0, tspgpu_level_h
     // the reference's 16-city instance 0.30 -> 0.22 ms in process against
     // 1024-path runs on one block per CU (profiles/r03/k2_chain_sweep.log)
     uint32_t chain_fpb = 256;
-    int chain_grid = 2;
+    // (at <= 16 cities a level has at most ~160 runs of 256 paths: one block
+    // per CU covers them, and the blocks without a run cost VALU for nothing)
+    int chain_grid = s->n <= 16 ? 1 : 2;
     chain_fpb = (uint32_t)tuned_int("CHAIN_FPB", (int)chain_fpb);  // (sweeps)
     chain_grid = std::max(1, tuned_int("CHAIN_GRID", chain_grid));
     // the tail's count is only known on the device, so its grid is sized for
