@@ -859,6 +859,60 @@ __global__ __launch_bounds__(kSearchThreads) void seed_kernel(SearchArgs a)
     seed_body<V>(a, blockIdx.x, gridDim.x);
 }
 
+// The cheapest completion from tail city I over the other TL - 1 (straight
+// through them, then to city 0) as a left-fold DP over subsets, layer by
+// layer: f[S][y] = the cheapest path from I over S ending at y, each path's
+// cost summed from I forward like `complete` does.  fl(a + d) is monotone in
+// a, so fl(min_P fl(P) + d) = min_P fl(fl(P) + d): every f[S][y] — and the
+// result — is bit-identical to the minimum over all (TL-1)! orders that
+// `complete` folds, at 165 adds instead of 445 for TL = 6.
+template <typename V, int TL, int I>
+__device__ __forceinline__ V suffix_dp(const V (&s)[TL][TL], const V (&d0)[TL])
+{
+    constexpr int R = ((1 << TL) - 1) & ~(1 << I);
+    V f[1 << TL][TL];
+    static_for(
+        [&](auto kk) {
+            constexpr int K = decltype(kk)::value + 1;  // |S|
+            static_for(
+                [&](auto ss) {
+                    constexpr int S = decltype(ss)::value;
+                    if constexpr ((S & ~R) == 0 && __builtin_popcount(S) == K) {
+                        static_for(
+                            [&](auto yy) {
+                                constexpr int Y = decltype(yy)::value;
+                                if constexpr ((S >> Y) & 1) {
+                                    if constexpr (K == 1) {
+                                        f[S][Y] = V(0) + s[I][Y];
+                                    } else {
+                                        constexpr int P = S & ~(1 << Y), Z0 = __builtin_ctz(P);
+                                        V m = f[P][Z0] + s[Z0][Y];
+                                        static_for(
+                                            [&](auto zz) {
+                                                constexpr int Z = decltype(zz)::value;
+                                                if constexpr (Z > Z0 && ((P >> Z) & 1)) m = ENum<V>::vmin(m, f[P][Z] + s[Z][Y]);
+                                            },
+                                            std::make_integer_sequence<int, TL>{});
+                                        f[S][Y] = m;
+                                    }
+                                }
+                            },
+                            std::make_integer_sequence<int, TL>{});
+                    }
+                },
+                std::make_integer_sequence<int, 1 << TL>{});
+        },
+        std::make_integer_sequence<int, TL - 1>{});
+    V best = ENum<V>::big();
+    static_for(
+        [&](auto yy) {
+            constexpr int Y = decltype(yy)::value;
+            if constexpr ((R >> Y) & 1) best = ENum<V>::vmin(best, f[R][Y] + d0[Y]);
+        },
+        std::make_integer_sequence<int, TL>{});
+    return best;
+}
+
 template <typename V, int TL>
 __device__ __forceinline__ void suffix_body(const SearchArgs &a, uint32_t sets, uint32_t block, uint32_t nblocks)
 {
@@ -903,9 +957,7 @@ __device__ __forceinline__ void suffix_body(const SearchArgs &a, uint32_t sets, 
             [&](auto i) {
                 constexpr int J = decltype(i)::value;
                 if (J != I) return;
-                double best = ENum<double>::big();
-                complete<double, TL, (((1 << TL) - 1) & ~(1 << J)), J>(sm, d0, 0.0, best);
-                H[(size_t)r0 * TL + J] = best;
+                H[(size_t)r0 * TL + J] = suffix_dp<double, TL, J>(sm, d0);
             },
             std::make_integer_sequence<int, TL>{});
     }
