@@ -9,8 +9,10 @@ both order like signed int64 for the non-negative costs the ABI accepts)
 every few steps, so every GPU prunes with the best tour found anywhere.  At
 the end: all-reduce(MIN) of the incumbent = the optimum, then all-reduce(MIN)
 of each rank's device tie key at that cost (the reverse-lex least optimal
-tour it found; w0, then w1 among its holders), certified once on every rank
-(tspgpu_tie_tour) — the same tour as tsp() / K1 on one GPU, SURVEY.md §8(e).
+tour it found; w0, then w1 among its holders), certified once, on rank 0
+(tspgpu_tie_tour_records from its own optimal records at world 1, else
+tspgpu_tie_tour), and broadcast — one more collective, counted in the stats'
+`collectives` — the same tour as tsp() / K1 on one GPU, SURVEY.md §8(e).
 Records are gathered only when the certificate cannot be given.
 
 With the "nccl" backend (RCCL on ROCm) the exchanges are device all-reduces
