@@ -10,7 +10,7 @@ rows = list(csv.DictReader(open(sys.argv[1])))
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
 dur = defaultdict(list)
 for r in rows:
-    name = r["Kernel_Name"].split("(")[0].replace("void ", "")
+    name = r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0].replace("void ", "")
     dur[name].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
 for name, v in sorted(dur.items(), key=lambda kv: -sum(kv[1])):
     v2 = sorted(v)
