@@ -304,6 +304,7 @@ struct SearchInit {
     int heur_f64;
     int heur_sym;                 // the matrix is symmetric (2-opt deltas are then exact)
     int heur_starts;              // start cities, spread over 0..n-1 (at most 16)
+    int heur_iters;               // 2-opt moves at most per start (0: nearest neighbour only)
 };
 hipError_t launch_init(const SearchInit &init, hipStream_t stream);
 // suffix table (enum.hip): size a.hs_len of a.hsuf, one thread per set

@@ -1252,7 +1252,7 @@ __device__ __forceinline__ void init_heuristic(const SearchInit &in)
             cur = j;
         }
         double total = wave_sum(lane < n ? hd[t[lane] * n + t[lane + 1 < n ? lane + 1 : 0]] : 0.0);
-        for (int it = 0; it < 8 * n; ++it) {
+        for (int it = 0; it < in.heur_iters; ++it) {
             double best = 0.0;
             int bi = 0, bj = 0;
 #pragma unroll

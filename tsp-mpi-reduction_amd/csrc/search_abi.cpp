@@ -613,6 +613,7 @@ static int search_create(tspgpu_ctx *c, const void *dist, int dtype, int n, int 
             // each wave has a SIMD to itself (profiles/r04/k2_device_bound.log);
             // from 20 cities sixteen (the host multi-start takes ~2 ms there)
             in.heur_starts = n >= 20 ? 16 : 4;
+            in.heur_iters = tuned_int("SEARCH_HEUR_ITERS", 8 * n);
         }
         in.fill_ff = reinterpret_cast<uint32_t *>(s->d_tie);
         in.n_ff = (uint32_t)(kTieBytes / 4);

@@ -47,6 +47,7 @@ Knob g_knobs[] = {
     {"SEARCH_PAGEABLE", false, 0}, // 1: pageable instead of pinned host words
     {"SEARCH_DEVICE_BOUND", false, 0},  // 0: search_solve below 20 cities takes the host heuristic's bound
     {"SEARCH_DEVICE_BOUND_MAXN", false, 0},  // search_solve takes the device bound from 13 cities up to below this (20)
+    {"SEARCH_HEUR_ITERS", false, 0},         // device heuristic: 2-opt moves at most per start (default 8 n)
     {"SEARCH_TAILS", false, 0},
     {"SEARCH_CHAIN_CAP_LOG2", false, 0},  // chained level buffers (tests force the overflow rerun)
     {"SEARCH_CHAIN_POISON", false, 0},    // 1: fill the chain's level buffers with 0xFF first (tests)
