@@ -1335,6 +1335,149 @@ __global__ __launch_bounds__(256) void expand_kernel(SearchArgs a)
     }  // runs
 }
 
+// The chain's first level fused into the prologue's seed blocks (chained
+// searches with at least two levels: the seeds' children are not tail paths
+// and take no suffix test, so the suffix table the other blocks of the same
+// launch are building is not read).  A seed block builds 256 seeds at a time
+// in registers — the same prefixes and the same B0 pruning as seed_body — and
+// expands the survivors at once with expand_kernel's bounds, writing the
+// children at block-scanned offsets of a.fout (a.out_count): one launch and
+// one round of set-up reads fewer than seeds + level 0.  Same children, same
+// node counts.
+// children of one evaluated path at slots [slot, slot + |live|) of out
+template <typename V>
+__device__ __forceinline__ void seed_emit(PathItem *out, uint32_t slot, const Expand<V> &e)
+{
+    const int cb = e.len >> 2, cs = 8 * (e.len & 3);
+    uint32_t cw[8];
+#pragma unroll
+    for (int b = 0; b < 8; ++b) cw[b] = b == 0 ? ((e.w[0] & ~255u) | (uint32_t)(e.len + 1)) : e.w[b];
+    for (uint32_t x = e.live; x; x &= x - 1u, ++slot) {
+        const uint32_t j = (uint32_t)__builtin_ctz(x);
+        uint32_t o[8];
+#pragma unroll
+        for (int b = 0; b < 8; ++b) o[b] = b == cb ? ((cw[b] & ~(255u << cs)) | (j << cs)) : cw[b];
+        uint4 *dst = reinterpret_cast<uint4 *>(out + slot);
+        dst[0] = make_uint4(o[0], o[1], o[2], o[3]);
+        dst[1] = make_uint4(o[4], o[5], o[6], o[7]);
+    }
+}
+
+template <typename V, int TL>
+__device__ __forceinline__ void seed_expand_body(const SearchArgs &a, uint32_t block, uint32_t nblocks)
+{
+    using W = typename SeedNum<V>::Wide;
+    __shared__ V dl[kSearchMaxN * kTRow];
+    __shared__ V am[kSearchMaxN];
+    __shared__ V b2[2 * kSearchMaxN];
+    __shared__ uint32_t bn[32][8];
+    __shared__ double dm[kSearchMaxN * kTRow + kSearchMaxN + 1];
+    __shared__ uint32_t pv[33];
+    __shared__ uint32_t wtot[4];
+    __shared__ uint32_t bbase, bskip;
+    const int n = a.n, N = n - 1, D = a.depth;
+    const V *gd = static_cast<const V *>(a.dist);
+    const V *ga = static_cast<const V *>(a.amin);
+    const int t = (int)threadIdx.x, tcol = t & 31;
+    for (int row = t >> 5; row < n; row += 8)
+        if (tcol < n) {
+            dl[row * kTRow + tcol] = gd[row * n + tcol];
+            if (a.mst) dm[row * kTRow + tcol] = a.mst[row * n + tcol];
+        }
+    if (t < n) am[t] = ga[t];
+    if (a.sym && t < 2 * n) b2[t] = static_cast<const V *>(a.bnd2)[t];
+    if (a.mst && t < n) dm[kSearchMaxN * kTRow + t] = a.mst[n * n + t];
+    if (a.mst && t == n) dm[kSearchMaxN * kTRow + kSearchMaxN] = a.mst[n * n + n];
+    load_binom(bn);
+    if (t == 0) {
+        uint32_t p = 1;
+        pv[D] = 1;
+        for (int l = D; l >= 2; --l) {
+            p *= (uint32_t)(N - l + 1);
+            pv[l - 1] = p;
+        }
+    }
+    __syncthreads();
+    const uint64_t incw = __hip_atomic_load(a.inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const V inc = SeedNum<V>::val(incw);
+    const V thr = EThr<V>::of(ENum<V>::val(incw));
+    const uint32_t full = (uint32_t)((1ull << n) - 1ull) & ~1u;
+    W aall = 0;
+    for (int x = 0; x < n; ++x) aall += (W)am[x];
+    const uint32_t local = a.items / a.nshards + (a.items % a.nshards > a.shard ? 1u : 0u);
+    const int lane = __lane_id(), wv = t >> 6;
+    unsigned long long nodes = 0;
+    for (uint32_t base = block * 256u; base < local; base += nblocks * 256u) {  // (block-uniform)
+        // the seed of this thread (seed_body's prefix order and bound)
+        const uint32_t i = base + (uint32_t)t;
+        uint32_t p = i * a.nshards + a.shard;
+        uint32_t rr = full;
+        W ra = aall;
+        V c = 0;
+        int prev = 0;
+        bool live = i < local;
+        uint32_t w[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        for (int l = 1; l <= D && live; ++l) {
+            const uint32_t q = p / pv[l];
+            p -= q * pv[l];
+            uint32_t x = rr;
+            for (uint32_t u = 0; u < q; ++u) x &= x - 1u;
+            const int tc = __builtin_ctz(x);
+            c = c + dl[prev * kTRow + tc];
+            rr &= ~(1u << tc);
+            ra -= (W)am[tc];
+#pragma unroll
+            for (int b = 0; b < 8; ++b)
+                if ((l >> 2) == b) w[b] |= (uint32_t)tc << (8 * (l & 3));
+            prev = tc;
+            if (!a.noprune && SeedNum<V>::pruned((W)c + ra, inc)) live = false;
+        }
+        w[0] |= (uint32_t)(D + 1);
+        // its children (expand_kernel's bounds; no tail children at this level)
+        const Expand<V> e = expand_eval<V, TL>(a, dl, am, b2, bn, dm, full, live ? 0u : 1u, 1u, thr, w);
+        nodes += (unsigned long long)__builtin_popcount(e.rem) + e.hnodes;
+        const uint32_t cnt = (uint32_t)__builtin_popcount(e.live);
+        uint32_t incl = cnt;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const uint32_t y = __shfl_up(incl, off);
+            if (lane >= off) incl += y;
+        }
+        if (lane == 63) wtot[wv] = incl;
+        __syncthreads();
+        uint32_t wofs = 0, tot = 0;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            wofs += u < wv ? wtot[u] : 0u;
+            tot += wtot[u];
+        }
+        if (t == 0) {
+            bbase = tot ? atomicAdd(a.out_count, tot) : 0u;
+            bskip = 0u;
+            if (a.overflow && tot && (uint64_t)bbase + tot > a.fout_cap) {
+                *a.overflow = 1u;  // the chained search is abandoned (the host reruns it step by step)
+                bskip = 1u;
+            }
+        }
+        __syncthreads();
+        if (!bskip) seed_emit(a.fout, bbase + wofs + incl - cnt, e);
+        __syncthreads();  // (wtot, bbase and bskip are rewritten by the next round)
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) nodes += __shfl_xor(nodes, off);
+    if (lane == 0 && nodes) atomicAdd(stat_line(a), nodes);
+}
+
+template <typename V, int TL>
+__global__ __launch_bounds__(256) void prologue1_kernel(SearchArgs a, uint32_t sets, uint32_t seed_blocks)
+{
+    if (a.t_start && blockIdx.x == 0 && threadIdx.x == 0) *a.t_start = wall_clock64();
+    if (blockIdx.x < seed_blocks)
+        seed_expand_body<V, TL>(a, blockIdx.x, seed_blocks);
+    else
+        suffix_body<V, TL>(a, sets, blockIdx.x - seed_blocks, gridDim.x - seed_blocks);
+}
+
 // Chained frontier levels, block-local (SearchArgs::local_levels): a block
 // takes a run of fin_per_block input paths and expands its subtree level after
 // level inside the launch — the paths between two levels stay in an LDS queue
@@ -1575,6 +1718,21 @@ hipError_t launch_seed(const SearchArgs &a, bool f64, int grid)
         hipLaunchKernelGGL(seed_kernel<double>, dim3(grid), dim3(kSearchThreads), 0, a.stream, a);
     else
         hipLaunchKernelGGL(seed_kernel<int32_t>, dim3(grid), dim3(kSearchThreads), 0, a.stream, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_prologue1(const SearchArgs &a, bool f64, int seed_grid, uint32_t sets)
+{
+    if (a.n > kSearchMaxN || !a.hsuf || (a.hs_len != 5 && a.hs_len != 6) || !a.fout) return hipErrorInvalidValue;
+    const int grid = seed_grid + (int)std::min<uint32_t>((sets * (uint32_t)a.hs_len + 255u) / 256u, 4096u);
+    const uint32_t sb = (uint32_t)seed_grid;
+#define TSPGPU_PRO(VT, TLV) hipLaunchKernelGGL((prologue1_kernel<VT, TLV>), dim3(grid), dim3(256), 0, a.stream, a, sets, sb)
+    if (a.hs_len == 5) {
+        if (f64) TSPGPU_PRO(double, 5); else TSPGPU_PRO(int32_t, 5);
+    } else {
+        if (f64) TSPGPU_PRO(double, 6); else TSPGPU_PRO(int32_t, 6);
+    }
+#undef TSPGPU_PRO
     return hipGetLastError();
 }
 

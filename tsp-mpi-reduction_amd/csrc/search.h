@@ -311,6 +311,8 @@ hipError_t launch_init(const SearchInit &init, hipStream_t stream);
 hipError_t launch_suffix(const SearchArgs &a, bool f64, uint32_t sets);
 // seeds (seed_grid blocks) and the suffix table in one launch (enum.hip)
 hipError_t launch_prologue(const SearchArgs &a, bool f64, int seed_grid, uint32_t sets);
+// the same with the chain's first level fused into the seed blocks (children to a.fout / a.out_count)
+hipError_t launch_prologue1(const SearchArgs &a, bool f64, int seed_grid, uint32_t sets);
 // colex rank helpers shared by host and device: C(n, k) for n < 32, k <= 7
 __host__ __device__ constexpr uint32_t search_binom(int nn, int k)
 {

@@ -982,6 +982,70 @@ static int search_start(tspgpu_search *s, bool sync)
     return rc;
 }
 
+// Chained searches of at least two levels: the seeds and the first level in
+// one launch (launch_prologue1): the seed segment is allocated as in
+// search_start (unused), then the chain's two level buffers ob[0..1]; the
+// first level's children go to ob[0] and their count to word 11 (the word the
+// chain's level 1 reads).
+static bool fusable(const tspgpu_search *s)
+{
+    // build_suffix's conditions for a frontier table, and a size prologue1 has
+    const int N = s->n - 1, L = s->tail_len;
+    return s->frontier && !s->noprune && s->suffix_len != 0 && (L == 5 || L == 6) && N >= L + 2 && s->kernel != 1 &&
+           s->kernel != 3;
+}
+static int search_start_fused(tspgpu_search *s, uint64_t cap, int ob[2])
+{
+    (void)hipSetDevice(s->ctx->device);
+    s->fresh = false;
+    if (int rc = ensure_items(s, 0, s->local_items + 1)) return rc;
+    s->cur = 0;
+    s->rounds = 0;
+    s->tails = 0;
+    hipStream_t st = s->ctx->stream;
+    hipError_t e = s->pristine ? hipSuccess : hipMemsetAsync(s->d_words + 8, 0, 16, st);
+    if (e != hipSuccess) return herr(e);
+    s->expand_steps = 0;
+    uint32_t sets = 0;
+    if (int rc = build_suffix(s, false, &sets)) return rc;
+    if (!sets) return -EIO;  // (run_chain fuses only when the table is built: fusable())
+    s->seg_buf.clear();
+    s->seg_n.clear();
+    int rc = 0;
+    const int seed_buf = front_spare(s, (size_t)s->local_items + 1, &rc);
+    if (seed_buf < 0) return rc;
+    s->seg_buf.push_back(seed_buf);
+    s->seg_n.push_back(0);
+    for (int k = 0; k < 2; ++k) {
+        ob[k] = front_spare(s, (size_t)cap, &rc);
+        if (ob[k] < 0) return rc;
+        s->seg_buf.push_back(ob[k]);  // (marked used so the second front_spare picks another)
+        s->seg_n.push_back(0);
+    }
+    if (tuned_or("SEARCH_CHAIN_POISON", 0) != 0) {  // tests: no slot may be read that was not written
+        for (int k = 0; k < 2 && e == hipSuccess; ++k)
+            e = hipMemsetAsync(s->fb[ob[k]], 0xFF, sizeof(PathItem) * cap, st);
+        if (e == hipSuccess) e = hipMemsetAsync(s->d_tail, 0xFF, sizeof(PathItem) * s->tail_cap, st);
+    }
+    if (!s->pristine && e == hipSuccess) {
+        e = hipMemsetAsync(s->d_words, 0, 8, st);  // queue
+        if (e == hipSuccess) e = hipMemsetAsync(s->d_words + 4, 0, 8, st);  // items out
+    }
+    s->pristine = false;
+    if (e != hipSuccess) return herr(e);
+    SearchArgs a = args_of(s);
+    a.fout = s->fb[ob[0]];
+    a.fout_cap = (uint32_t)cap;
+    a.out_count = reinterpret_cast<unsigned int *>(s->d_words + 11);
+    a.overflow = reinterpret_cast<unsigned int *>(s->d_words + 13);
+    const uint64_t blocks = (s->local_items + kSearchThreads - 1) / kSearchThreads;
+    const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>(blocks, (uint64_t)s->ctx->cu_count * 8));
+    e = launch_prologue1(a, s->dtype == TSPGPU_F64, grid, sets);
+    if (e != hipSuccess) return herr(e);
+    s->pending = s->local_items;
+    return 0;
+}
+
 // Frontier search, one step: either fold the waiting tails, or expand the
 // last T frontier items (LIFO keeps the frontier small) by one level.
 static int frontier_step(tspgpu_search *s, uint64_t *pending)
@@ -1258,17 +1322,24 @@ static int run_chain(tspgpu_search *s, bool *done, int every = 0, tspgpu_level_h
     const bool fetch = s->fetch && s->h_stage;
     if (!fetch) (void)hipEventRecord(s->e2, st);
     s->stamp = fetch;
-    int rc = search_start(s, false);  // the seeds, enqueued: their count stays in word 4
+    // the first level fused into the seeds' launch (knob CHAIN_FUSE_SEEDS, on
+    // with per-level launches and >= 2 levels: then no seed's child is a
+    // tail; 16 cities: 0.081 -> 0.072 ms, profiles/r06/k2_16/fuse/; a second
+    // fused level inside the seed blocks took as long as its own launch)
+    const bool fuse = !chain_local && levels >= 2 && fusable(s) && tuned_or("CHAIN_FUSE_SEEDS", 1) != 0;
+    int ob[2] = {-1, -1};
+    int rc = fuse ? search_start_fused(s, kChainCap, ob) : search_start(s, false);  // (unfused: the seeds' count stays in word 4)
     s->stamp = false;
     if (rc) return rc;
-    int ob[2];
-    for (int k = 0; k < 2; ++k) {
-        ob[k] = front_spare(s, (size_t)kChainCap, &rc);
-        if (ob[k] < 0) return rc;
-        s->seg_buf.push_back(ob[k]);  // (marked used so the second front_spare picks another)
-        s->seg_n.push_back(0);
+    if (!fuse) {
+        for (int k = 0; k < 2; ++k) {
+            ob[k] = front_spare(s, (size_t)kChainCap, &rc);
+            if (ob[k] < 0) return rc;
+            s->seg_buf.push_back(ob[k]);  // (marked used so the second front_spare picks another)
+            s->seg_n.push_back(0);
+        }
     }
-    if (tuned_or("SEARCH_CHAIN_POISON", 0) != 0) {  // tests: no slot may be read that was not written
+    if (!fuse && tuned_or("SEARCH_CHAIN_POISON", 0) != 0) {  // tests: no slot may be read that was not written
         for (int k = 0; k < 2 && e == hipSuccess; ++k)
             e = hipMemsetAsync(s->fb[ob[k]], 0xFF, sizeof(PathItem) * kChainCap, st);
         if (e == hipSuccess) e = hipMemsetAsync(s->d_tail, 0xFF, sizeof(PathItem) * s->tail_cap, st);
@@ -1276,7 +1347,11 @@ static int run_chain(tspgpu_search *s, bool *done, int every = 0, tspgpu_level_h
     }
     // level l reads its input count from word 4 (the seeds, l = 0) or
     // 10 + l%3, writes 10 + (l+1)%3 and zeroes 10 + (l+2)%3
-    for (int l = 0; l < levels && e == hipSuccess; ++l) {
+    if (fuse && hooks && 1 % every == 0) {  // (level 0 ran in the seeds' launch)
+        hook(user, st, s->d_words + 1);
+        ++guard.done;
+    }
+    for (int l = fuse ? 1 : 0; l < levels && e == hipSuccess; ++l) {
         SearchArgs a = args_of(s);
         a.fseg[0] = l == 0 ? s->fb[s->seg_buf[0]] : s->fb[ob[(l - 1) & 1]];
         a.fseg_start[0] = 0;

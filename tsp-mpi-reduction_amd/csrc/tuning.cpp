@@ -54,6 +54,7 @@ Knob g_knobs[] = {
     {"CHAIN_FPB", false, 0},
     {"CHAIN_GRID", false, 0},
     {"CHAIN_TAIL_GRID", false, 0},  // chained tail_kernel workgroups per CU
+    {"CHAIN_FUSE_SEEDS", false, 0}, // 0: the chain's first level in its own launch (not in the seeds')
     {"CHAIN_LOCAL", false, 0},      // 0: a launch per chained level (no block-local levels)
     {"CHAIN_LOCAL_FPB", false, 0},
     {"SEARCH_DEBUG", false, 0},    // host phase times on stderr
