@@ -717,7 +717,7 @@ def _rocprof_pass(counters, n, blocks, kernel, tag, timeout=90, child=None, redu
     return {k: agg(v) for k, v in vals.items()}, None
 
 
-K2_KERNELS = ("prologue_kernel", "expand_kernel", "tail_kernel")
+K2_KERNELS = ("prologue_kernel", "prologue1_kernel", "expand_kernel", "tail_kernel")
 K2_PMC_SEARCHES = 4  # searches the K2 PMC child runs (counters are summed over them)
 
 

@@ -1375,6 +1375,7 @@ __device__ __forceinline__ void seed_expand_body(const SearchArgs &a, uint32_t b
     __shared__ uint32_t pv[33];
     __shared__ uint32_t wtot[4];
     __shared__ uint32_t bbase, bskip;
+    __shared__ typename SeedNum<V>::Wide aall_s;
     const int n = a.n, N = n - 1, D = a.depth;
     const V *gd = static_cast<const V *>(a.dist);
     const V *ga = static_cast<const V *>(a.amin);
@@ -1396,14 +1397,17 @@ __device__ __forceinline__ void seed_expand_body(const SearchArgs &a, uint32_t b
             p *= (uint32_t)(N - l + 1);
             pv[l - 1] = p;
         }
+        // seed_body's sum, in its order, once per block
+        W s0 = 0;
+        for (int x = 0; x < n; ++x) s0 += (W)ga[x];
+        aall_s = s0;
     }
     __syncthreads();
     const uint64_t incw = __hip_atomic_load(a.inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const V inc = SeedNum<V>::val(incw);
     const V thr = EThr<V>::of(ENum<V>::val(incw));
     const uint32_t full = (uint32_t)((1ull << n) - 1ull) & ~1u;
-    W aall = 0;
-    for (int x = 0; x < n; ++x) aall += (W)am[x];
+    const W aall = aall_s;
     const uint32_t local = a.items / a.nshards + (a.items % a.nshards > a.shard ? 1u : 0u);
     const int lane = __lane_id(), wv = t >> 6;
     unsigned long long nodes = 0;

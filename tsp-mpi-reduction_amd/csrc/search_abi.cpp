@@ -1285,7 +1285,9 @@ static int run_chain(tspgpu_search *s, bool *done, int every = 0, tspgpu_level_h
     chain_grid = std::max(1, tuned_int("CHAIN_GRID", chain_grid));
     // the tail's count is only known on the device, so its grid is sized for
     // the buffer and the blocks beyond the count leave at once
-    const int tail_grid = std::max(1, tuned_int("CHAIN_TAIL_GRID", 8));
+    // (<= 16 cities: one block per CU — the waves beyond the count only read
+    // it and leave, 4 VALU lane-instructions per node at 8 per CU)
+    const int tail_grid = std::max(1, tuned_int("CHAIN_TAIL_GRID", s->n <= 16 ? 1 : 8));
     // the levels expanded block-locally (expand_local_kernel; knob
     // CHAIN_LOCAL), runs of 64 input paths per block
     // (from 20 cities: 7-11% fewer kernel-us at 20-32 cities; at 14-16 cities
