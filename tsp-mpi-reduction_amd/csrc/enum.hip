@@ -286,21 +286,36 @@ __device__ __forceinline__ void load_path(const PathItem *p, bool act, uint32_t 
 
 // The left fold ((d[0][t1] + d[t1][t2]) + ...) of the path in w (len cities),
 // its end city and its members, from the matrix in LDS.
+// The distances of eight positions are read before any of them is added (the
+// addresses come from the path bytes alone, and every byte indexes inside the
+// 32 x 32 table): one LDS round trip per eight cities instead of one per city;
+// the adds stay in path order.
 template <typename V>
 __device__ __forceinline__ void fold_path(const V *dl, const uint32_t (&w)[8], int len, V &c, int &k, uint32_t &mem)
 {
 #pragma unroll
-    for (int b = 0; b < 8; ++b)
+    for (int g = 0; g < 4; ++g) {
+        if (8 * g >= len) break;
+        V v[8];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int lv = 4 * b + q;
+        for (int q = 0; q < 8; ++q) {
+            const int lv = 8 * g + q;
+            const int t = (int)((w[lv >> 2] >> (8 * (lv & 3))) & 31u);
+            const int pl = lv - 1;
+            const int p = pl <= 0 ? 0 : (int)((w[pl >> 2] >> (8 * (pl & 3))) & 31u);
+            v[q] = lv >= 1 ? dl[p * kTRow + t] : V(0);
+        }
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const int lv = 8 * g + q;
             if (lv >= 1 && lv < len) {
-                const int t = (int)((w[b] >> (8 * q)) & 255u);
-                c = c + dl[k * kTRow + t];
+                const int t = (int)((w[lv >> 2] >> (8 * (lv & 3))) & 255u);
+                c = c + v[q];
                 mem |= 1u << t;
                 k = t;
             }
         }
+    }
 }
 
 // byte l of a path's words (a select chain: no dynamically indexed registers)
