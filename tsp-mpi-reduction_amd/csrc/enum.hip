@@ -1128,10 +1128,25 @@ __device__ __forceinline__ Expand<V> expand_eval(const SearchArgs &a, const V *d
     e.rem = act ? (full & ~mem) : 0u;
     V remA = am[0];  // every city still to be entered: its cheapest incoming edge (exact sums)
     V remB = 0;      // B1: the rem cities' half sums (exact sums)
-    for (uint32_t x = e.rem; x; x &= x - 1u) {
-        const int t = __builtin_ctz(x);
-        remA += am[t];
-        if (a.sym) remB += b2[2 * t];
+    // eight cities' table reads in flight before their adds (ascending order kept)
+    for (uint32_t x = e.rem; x;) {
+        V va[8], vb[8];
+        uint32_t y = x;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const int t = __builtin_ctz(y | 0x80000000u) & 31;
+            va[q] = am[t];
+            vb[q] = a.sym ? b2[2 * t] : V(0);
+            y &= y - 1u;
+        }
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            if (x) {
+                remA += va[q];
+                if (a.sym) remB += vb[q];
+                x &= x - 1u;
+            }
+        }
     }
     const bool htest = a.hs_len == TL && a.tail_len == TL && e.len == a.tail_level && !a.noprune;
     e.live = 0;
@@ -1142,12 +1157,31 @@ __device__ __forceinline__ Expand<V> expand_eval(const SearchArgs &a, const V *d
         e.hnodes = act ? (uint32_t)((TL + 1) * TL) : 0u;
         return e;
     }
-    for (uint32_t x = e.rem; x; x &= x - 1u) {
-        const int j = __builtin_ctz(x);
-        const V cj = c + dl[k * kTRow + j];
-        bool ok = a.noprune || !(cj + (remA - am[j]) > thr);
-        if (ok && a.sym && !a.noprune) ok = !(cj + (((remB - b2[2 * j]) + b2[2 * j + 1]) + b2[1]) > thr);
-        if (ok) e.live |= 1u << j;
+    // children four at a time, their table reads in flight together
+    for (uint32_t x = e.rem; x;) {
+        V vd[4], va[4], vb0[4], vb1[4];
+        int jj[4];
+        uint32_t y = x;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int j = __builtin_ctz(y | 0x80000000u) & 31;
+            jj[q] = j;
+            vd[q] = dl[k * kTRow + j];
+            va[q] = am[j];
+            vb0[q] = a.sym ? b2[2 * j] : V(0);
+            vb1[q] = a.sym ? b2[2 * j + 1] : V(0);
+            y &= y - 1u;
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            if (x) {
+                const V cj = c + vd[q];
+                bool ok = a.noprune || !(cj + (remA - va[q]) > thr);
+                if (ok && a.sym && !a.noprune) ok = !(cj + (((remB - vb0[q]) + vb1[q]) + b2[1]) > thr);
+                if (ok) e.live |= 1u << jj[q];
+                x &= x - 1u;
+            }
+        }
     }
     // the tree bound of the whole rest (all children at once), only for paths
     // the cheaper bounds left children of; its margin
