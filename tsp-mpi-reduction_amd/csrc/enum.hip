@@ -1288,12 +1288,17 @@ __global__ __launch_bounds__(256) void expand_kernel(SearchArgs a)
     uint32_t cT = 0, cF = 0;
     unsigned long long nodes = 0;
     uint32_t lv[kExpandTiles];
+    uint32_t w0[8];  // the first tile's path, kept for pass 2 (no reload)
 #pragma unroll
     for (int t = 0; t < kExpandTiles; ++t) {
         const uint32_t base = b0 + 256u * t;
         lv[t] = 0;
         if (base >= b1) continue;
         const Expand<V> e = expand_eval<V, TL>(a, dl, am, b2, bn, dm, full, base + threadIdx.x, b1, thr);
+        if (t == 0) {
+#pragma unroll
+            for (int b = 0; b < 8; ++b) w0[b] = e.w[b];
+        }
         lv[t] = e.live;
         const uint32_t cnt = (uint32_t)__builtin_popcount(e.live);
         if (e.len == a.tail_level) cT += cnt; else cF += cnt;  // children have len inner cities
@@ -1334,7 +1339,12 @@ __global__ __launch_bounds__(256) void expand_kernel(SearchArgs a)
         if (base >= b1) break;  // block-uniform
         Expand<V> e;
         const bool act = base + threadIdx.x < b1;
-        load_path(fin_at(a, base + threadIdx.x), act, e.w);
+        if (t == 0) {
+#pragma unroll
+            for (int b = 0; b < 8; ++b) e.w[b] = act ? w0[b] : 0u;
+        } else {
+            load_path(fin_at(a, base + threadIdx.x), act, e.w);
+        }
         e.len = act ? (int)(e.w[0] & 255u) : 0;
         e.live = lv[t];
         const bool tail = e.len == a.tail_level;
