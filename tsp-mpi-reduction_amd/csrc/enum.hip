@@ -331,11 +331,10 @@ __device__ __forceinline__ int path_byte(const uint32_t (&w)[8], int l)
 // TL! completions; `act` false = a lane with nothing to do (wave-uniform code).
 // (A wave with only a few prefixes takes tail_wide below instead.)
 template <typename V, int TL>
-__device__ __forceinline__ void tail_one(const SearchArgs &a, const V *dl, const V *am, uint32_t full, uint32_t idx,
-                                         bool act, unsigned long long &lanes, TieCache &tcache)
+__device__ __forceinline__ void tail_one(const SearchArgs &a, const V *dl, const V *am, uint32_t full,
+                                         const uint32_t (&w)[8], bool act, unsigned long long &lanes,
+                                         TieCache &tcache)
 {
-    uint32_t w[8];
-    load_path(a.ftail + idx, act, w);
     const int len = act ? (int)(w[0] & 255u) : 1;
     // ---- the prefix 0, t1..t(len-1): the reference's left fold
     V cp = 0;
@@ -506,12 +505,11 @@ __device__ __forceinline__ T sel44(const T (&m)[4][4], int i, int j)
 // straight-line `complete` — and the tours within the incumbent are recorded
 // and offered to the tie rule exactly as in tail_one (TL = 6 only).
 template <typename V, int TL>
-__device__ __forceinline__ void tail_wide(const SearchArgs &a, const V *dl, const V *am, uint32_t full, uint32_t idx,
-                                          bool act, unsigned long long &lanes, TieCache &tcache)
+__device__ __forceinline__ void tail_wide(const SearchArgs &a, const V *dl, const V *am, uint32_t full,
+                                          const uint32_t (&w)[8], bool act, unsigned long long &lanes,
+                                          TieCache &tcache)
 {
     static_assert(TL == 6, "tail_wide: six tail cities");
-    uint32_t w[8];
-    load_path(a.ftail + idx, act, w);
     const int len = act ? (int)(w[0] & 255u) : 1;
     V cp = 0;
     int prev = 0;
@@ -692,7 +690,7 @@ __global__ __launch_bounds__(256) void tail_kernel(SearchArgs a)
 {
     __shared__ V dl[kSearchMaxN * kTRow];
     __shared__ V am[kSearchMaxN];
-    __shared__ uint32_t wq[4][128];
+    __shared__ uint4 wq[4][128][2];  // queued prefixes' words (read once, in the queue pass)
     const int n = a.n;
     const V *gd = static_cast<const V *>(a.dist);
     const V *ga = static_cast<const V *>(a.amin);
@@ -711,7 +709,7 @@ __global__ __launch_bounds__(256) void tail_kernel(SearchArgs a)
 
     const uint32_t full = (uint32_t)((1ull << n) - 1ull) & ~1u;
     const int lane = __lane_id();
-    uint32_t *q = wq[threadIdx.x >> 6];
+    uint4 (*q)[2] = wq[threadIdx.x >> 6];
     uint32_t qn = 0;               // wave-uniform: live slots queued
     unsigned long long lanes = 0;  // wave-uniform
     TieCache tcache;
@@ -720,9 +718,16 @@ __global__ __launch_bounds__(256) void tail_kernel(SearchArgs a)
         const bool more = base < count;
         if (more) {
             const uint32_t idx = base + lane;
-            const bool live = idx < count && a.ftail[idx].b[0] != 0;
+            const bool in = idx < count;
+            const uint4 lo = in ? reinterpret_cast<const uint4 *>(a.ftail + idx)[0] : make_uint4(0, 0, 0, 0);
+            const uint4 hi = in ? reinterpret_cast<const uint4 *>(a.ftail + idx)[1] : make_uint4(0, 0, 0, 0);
+            const bool live = in && (lo.x & 255u) != 0;
             const unsigned long long m = __ballot(live);
-            if (live) q[qn + __popcll(m & ((1ull << lane) - 1ull))] = idx;
+            if (live) {
+                const uint32_t pos = qn + __popcll(m & ((1ull << lane) - 1ull));
+                q[pos][0] = lo;
+                q[pos][1] = hi;
+            }
             qn += (uint32_t)__popcll(m);
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
@@ -731,16 +736,22 @@ __global__ __launch_bounds__(256) void tail_kernel(SearchArgs a)
         while (qn >= 64u || (!more && qn > 0u)) {
             const uint32_t take = qn < 64u ? qn : 64u;
             const bool act = (uint32_t)lane < take;
-            const uint32_t idx = act ? q[qn - take + lane] : 0u;
+            uint32_t w[8];
+            {
+                const uint4 lo = act ? q[qn - take + lane][0] : make_uint4(0, 0, 0, 0);
+                const uint4 hi = act ? q[qn - take + lane][1] : make_uint4(0, 0, 0, 0);
+                w[0] = lo.x, w[1] = lo.y, w[2] = lo.z, w[3] = lo.w;
+                w[4] = hi.x, w[5] = hi.y, w[6] = hi.z, w[7] = hi.w;
+            }
             __builtin_amdgcn_wave_barrier();
             qn -= take;
             if constexpr (TL == 6) {
                 if (take <= kTailWide) {
-                    tail_wide<V, TL>(a, dl, am, full, idx, act, lanes, tcache);
+                    tail_wide<V, TL>(a, dl, am, full, w, act, lanes, tcache);
                     continue;
                 }
             }
-            tail_one<V, TL>(a, dl, am, full, idx, act, lanes, tcache);
+            tail_one<V, TL>(a, dl, am, full, w, act, lanes, tcache);
         }
         if (!more) break;
     }
