@@ -1118,6 +1118,14 @@ __device__ __forceinline__ double tree_bound(const double *dm, const double *pim
 //   B1 (symmetric matrices): e[j] + sum over rem \ j of b + e[0];
 //   H  (the child has a.hs_len cities left): min over x in rem \ j of
 //       d[j][x] + H[rem \ j][x], the exact cheapest completion up to rounding.
+#ifndef TSPGPU_REM_GROUP
+#define TSPGPU_REM_GROUP 4
+#endif
+#ifndef TSPGPU_CHILD_GROUP
+#define TSPGPU_CHILD_GROUP 2
+#endif
+constexpr int kRemGroup = TSPGPU_REM_GROUP;      // remaining cities whose table reads are in flight together
+constexpr int kChildGroup = TSPGPU_CHILD_GROUP;  // children likewise
 template <typename V, int TL>
 __device__ __forceinline__ Expand<V> expand_eval(const SearchArgs &a, const V *dl, const V *am, const V *b2,
                                                  const uint32_t (*bn)[8], const double *dm, uint32_t full,
@@ -1139,19 +1147,19 @@ __device__ __forceinline__ Expand<V> expand_eval(const SearchArgs &a, const V *d
     e.rem = act ? (full & ~mem) : 0u;
     V remA = am[0];  // every city still to be entered: its cheapest incoming edge (exact sums)
     V remB = 0;      // B1: the rem cities' half sums (exact sums)
-    // eight cities' table reads in flight before their adds (ascending order kept)
+    // kRemGroup cities' table reads in flight before their adds (ascending order kept)
     for (uint32_t x = e.rem; x;) {
-        V va[8], vb[8];
+        V va[kRemGroup], vb[kRemGroup];
         uint32_t y = x;
 #pragma unroll
-        for (int q = 0; q < 8; ++q) {
+        for (int q = 0; q < kRemGroup; ++q) {
             const int t = __builtin_ctz(y | 0x80000000u) & 31;
             va[q] = am[t];
             vb[q] = a.sym ? b2[2 * t] : V(0);
             y &= y - 1u;
         }
 #pragma unroll
-        for (int q = 0; q < 8; ++q) {
+        for (int q = 0; q < kRemGroup; ++q) {
             if (x) {
                 remA += va[q];
                 if (a.sym) remB += vb[q];
@@ -1168,13 +1176,13 @@ __device__ __forceinline__ Expand<V> expand_eval(const SearchArgs &a, const V *d
         e.hnodes = act ? (uint32_t)((TL + 1) * TL) : 0u;
         return e;
     }
-    // children four at a time, their table reads in flight together
+    // children kChildGroup at a time, their table reads in flight together
     for (uint32_t x = e.rem; x;) {
-        V vd[4], va[4], vb0[4], vb1[4];
-        int jj[4];
+        V vd[kChildGroup], va[kChildGroup], vb0[kChildGroup], vb1[kChildGroup];
+        int jj[kChildGroup];
         uint32_t y = x;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
+        for (int q = 0; q < kChildGroup; ++q) {
             const int j = __builtin_ctz(y | 0x80000000u) & 31;
             jj[q] = j;
             vd[q] = dl[k * kTRow + j];
@@ -1184,7 +1192,7 @@ __device__ __forceinline__ Expand<V> expand_eval(const SearchArgs &a, const V *d
             y &= y - 1u;
         }
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
+        for (int q = 0; q < kChildGroup; ++q) {
             if (x) {
                 const V cj = c + vd[q];
                 bool ok = a.noprune || !(cj + (remA - va[q]) > thr);
@@ -1446,6 +1454,8 @@ __device__ __forceinline__ void seed_expand_body(const SearchArgs &a, uint32_t b
     __shared__ uint32_t wtot[4];
     __shared__ uint32_t bbase, bskip;
     __shared__ typename SeedNum<V>::Wide aall_s;
+    __shared__ uint4 sq[256][2];  // the round's live seeds, compacted
+    __shared__ uint32_t nlive_s;
     const int n = a.n, N = n - 1, D = a.depth;
     const V *gd = static_cast<const V *>(a.dist);
     const V *ga = static_cast<const V *>(a.amin);
@@ -1507,8 +1517,41 @@ __device__ __forceinline__ void seed_expand_body(const SearchArgs &a, uint32_t b
             if (!a.noprune && SeedNum<V>::pruned((W)c + ra, inc)) live = false;
         }
         w[0] |= (uint32_t)(D + 1);
+        // the round's live seeds compacted to the first threads (most seeds
+        // fail their bound: the evaluation below then runs on full waves only)
+        {
+            const unsigned long long lm = __ballot(live);
+            if (lane == 0) wtot[wv] = (uint32_t)__popcll(lm);
+            __syncthreads();
+            uint32_t off = 0;
+#pragma unroll
+            for (int u = 0; u < 4; ++u) off += u < wv ? wtot[u] : 0u;
+            if (live) {
+                const uint32_t pos = off + (uint32_t)__popcll(lm & ((1ull << lane) - 1ull));
+                sq[pos][0] = make_uint4(w[0], w[1], w[2], w[3]);
+                sq[pos][1] = make_uint4(w[4], w[5], w[6], w[7]);
+            }
+            if (t == 0) nlive_s = wtot[0] + wtot[1] + wtot[2] + wtot[3];
+            __syncthreads();
+        }
+        const uint32_t nlive = nlive_s;
+        const bool mine = (uint32_t)t < nlive;
+        {
+            const uint4 lo = mine ? sq[t][0] : make_uint4(0, 0, 0, 0);
+            const uint4 hi = mine ? sq[t][1] : make_uint4(0, 0, 0, 0);
+            w[0] = lo.x, w[1] = lo.y, w[2] = lo.z, w[3] = lo.w;
+            w[4] = hi.x, w[5] = hi.y, w[6] = hi.z, w[7] = hi.w;
+        }
         // its children (expand_kernel's bounds; no tail children at this level)
-        const Expand<V> e = expand_eval<V, TL>(a, dl, am, b2, bn, dm, full, live ? 0u : 1u, 1u, thr, w);
+        Expand<V> e;
+        e.len = 0;
+        e.rem = 0;
+        e.live = 0;
+        e.hnodes = 0;
+#pragma unroll
+        for (int b = 0; b < 8; ++b) e.w[b] = 0u;
+        if ((uint32_t)(wv * 64) < nlive)  // (wave-uniform: a wave without seeds skips the evaluation)
+            e = expand_eval<V, TL>(a, dl, am, b2, bn, dm, full, mine ? 0u : 1u, 1u, thr, w);
         nodes += (unsigned long long)__builtin_popcount(e.rem) + e.hnodes;
         const uint32_t cnt = (uint32_t)__builtin_popcount(e.live);
         uint32_t incl = cnt;
