@@ -1,11 +1,11 @@
 #!/bin/bash
-# Round-6 final check 2 (the fused first level):
+# Round-6 final check 5 (compacted fused level):
 # rocprofv3 kernel trace, a plain bench.py line, and a kernel trace of the
 # 16-city K2 chain.
 set -u
 cd "$(dirname "$0")/.."
 ROOT=$PWD
-OUT=$ROOT/gpurun_out/r06/final2
+OUT=$ROOT/gpurun_out/r06/final5
 mkdir -p $OUT
 timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $OUT/smoke.log 2>&1
 rc=$?; echo "smoke rc=$rc"; tail -2 $OUT/smoke.log; [ $rc -eq 0 ] || exit $rc
